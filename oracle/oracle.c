@@ -1,0 +1,1357 @@
+/*
+ * oracle.c -- CPU restatement of Shadow's network plane (routing table +
+ * per-round packet hand-off).  TEST INFRASTRUCTURE ONLY: the product in
+ * shadow_amd/ never links or calls this file.  See oracle.h for the pinning
+ * of each part.  Citations are file:line into /root/reference/src/main.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off; no fast-math so every
+ * fp64 operation is the one the reference performs).
+ */
+#include "oracle.h"
+
+#include <arpa/inet.h>
+#include <ctype.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ======================================================================= */
+/* units: core/support/units.rs                                            */
+/* ======================================================================= */
+
+/* Rust str::trim / regex \s on the ASCII subset. */
+static int orc_isspace(int c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
+
+/* Splits "<value> <unit>" per the regex ^([+-]?[0-9\.]*)\s*(.*)$ of
+ * units.rs:420 and trims both parts (units.rs:422-425).  Returns 0 on match. */
+static int split_value_unit(const char* s, char* val, size_t vcap, char* unit, size_t ucap) {
+    const char* p = s;
+    const char* v0 = p;
+    if (*p == '+' || *p == '-') p++;
+    while ((*p >= '0' && *p <= '9') || *p == '.') p++;
+    const char* v1 = p;
+    while (orc_isspace((unsigned char)*p)) p++;
+    const char* u0 = p;
+    /* (.*)$ : '.' does not match '\n', so the rest must be newline-free */
+    for (const char* q = u0; *q; q++)
+        if (*q == '\n') return -1;
+    const char* u1 = u0 + strlen(u0);
+    while (v0 < v1 && orc_isspace((unsigned char)*v0)) v0++;
+    while (v1 > v0 && orc_isspace((unsigned char)v1[-1])) v1--;
+    while (u0 < u1 && orc_isspace((unsigned char)*u0)) u0++;
+    while (u1 > u0 && orc_isspace((unsigned char)u1[-1])) u1--;
+    if ((size_t)(v1 - v0) >= vcap || (size_t)(u1 - u0) >= ucap) return -1;
+    memcpy(val, v0, (size_t)(v1 - v0));
+    val[v1 - v0] = 0;
+    memcpy(unit, u0, (size_t)(u1 - u0));
+    unit[u1 - u0] = 0;
+    return 0;
+}
+
+/* Rust u64::from_str: optional '+', at least one ASCII digit, no overflow. */
+static int parse_u64_rust(const char* s, uint64_t* out) {
+    const char* p = s;
+    if (*p == '+') p++;
+    if (!*p) return -1;
+    uint64_t v = 0;
+    for (; *p; p++) {
+        if (*p < '0' || *p > '9') return -1;
+        uint64_t d = (uint64_t)(*p - '0');
+        if (v > (UINT64_MAX - d) / 10) return -1;
+        v = v * 10 + d;
+    }
+    *out = v;
+    return 0;
+}
+
+/* parse_time_nanosec (units.rs:809-837) over Time<TimePrefix>
+ * (units.rs:233-279, unit_impl! from_str :404-437, suffixes [""] :547). */
+int64_t orc_parse_time_ns(const char* s) {
+    if (!s) return -1;
+    char val[128], unit[128];
+    if (split_value_unit(s, val, sizeof val, unit, sizeof unit) != 0) return -1;
+    uint64_t factor;
+    if (unit[0] == 0) factor = 1000000000ull; /* TimePrefix default = Sec (units.rs:227-231) */
+    else if (!strcmp(unit, "ns") || !strcmp(unit, "nanosecond") || !strcmp(unit, "nanoseconds")) factor = 1ull;
+    else if (!strcmp(unit, "us") || !strcmp(unit, "\xce\xbcs") || !strcmp(unit, "microsecond") ||
+             !strcmp(unit, "microseconds")) factor = 1000ull;
+    else if (!strcmp(unit, "ms") || !strcmp(unit, "millisecond") || !strcmp(unit, "milliseconds")) factor = 1000000ull;
+    else if (!strcmp(unit, "s") || !strcmp(unit, "sec") || !strcmp(unit, "secs") || !strcmp(unit, "second") ||
+             !strcmp(unit, "seconds")) factor = 1000000000ull;
+    else if (!strcmp(unit, "m") || !strcmp(unit, "min") || !strcmp(unit, "mins") || !strcmp(unit, "minute") ||
+             !strcmp(unit, "minutes")) factor = 60000000000ull;
+    else if (!strcmp(unit, "h") || !strcmp(unit, "hr") || !strcmp(unit, "hrs") || !strcmp(unit, "hour") ||
+             !strcmp(unit, "hours")) factor = 3600000000000ull;
+    else return -1;
+    uint64_t v;
+    if (parse_u64_rust(val, &v) != 0) return -1;
+    if (v != 0 && v > UINT64_MAX / factor) return -1; /* checked_mul (units.rs:371-378) */
+    uint64_t ns = v * factor;
+    if (ns > (uint64_t)INT64_MAX) return -1; /* try_into i64 (units.rs:828-834) */
+    return (int64_t)ns;
+}
+
+/* parse_bandwidth (units.rs:777-807) over BitsPerSec<SiPrefixUpper>
+ * (suffixes ["bit","bits"] units.rs:577, prefixes :141-216). */
+int64_t orc_parse_bandwidth_bits(const char* s) {
+    if (!s) return -1;
+    char val[128], unit[128];
+    if (split_value_unit(s, val, sizeof val, unit, sizeof unit) != 0) return -1;
+    /* try removing suffixes in order (units.rs:427-433) */
+    size_t ul = strlen(unit);
+    if (ul >= 3 && !strcmp(unit + ul - 3, "bit")) unit[ul - 3] = 0;
+    else if (ul >= 4 && !strcmp(unit + ul - 4, "bits")) unit[ul - 4] = 0;
+    uint64_t factor;
+    if (unit[0] == 0) factor = 1;
+    else if (!strcmp(unit, "K") || !strcmp(unit, "kilo")) factor = 1000ull;
+    else if (!strcmp(unit, "Ki") || !strcmp(unit, "kibi")) factor = 1024ull;
+    else if (!strcmp(unit, "M") || !strcmp(unit, "mega")) factor = 1000000ull;
+    else if (!strcmp(unit, "Mi") || !strcmp(unit, "mebi")) factor = 1048576ull;
+    else if (!strcmp(unit, "G") || !strcmp(unit, "giga")) factor = 1000000000ull;
+    else if (!strcmp(unit, "Gi") || !strcmp(unit, "gibi")) factor = 1073741824ull;
+    else if (!strcmp(unit, "T") || !strcmp(unit, "tera")) factor = 1000000000000ull;
+    else if (!strcmp(unit, "Ti") || !strcmp(unit, "tebi")) factor = 1099511627776ull;
+    else return -1;
+    uint64_t v;
+    if (parse_u64_rust(val, &v) != 0) return -1;
+    if (v != 0 && v > UINT64_MAX / factor) return -1;
+    uint64_t b = v * factor;
+    if (b > (uint64_t)INT64_MAX) return -1;
+    return (int64_t)b;
+}
+
+/* ======================================================================= */
+/* rand_r streams: utility/random.c:32-51 over glibc rand_r                 */
+/* ======================================================================= */
+
+/* glibc stdlib/rand_r.c (the libc the reference links; published algorithm). */
+int orc_rand_r(uint32_t* state) {
+    uint32_t next = *state;
+    int result;
+    next *= 1103515245u;
+    next += 12345u;
+    result = (int)((next / 65536u) % 2048u);
+    next *= 1103515245u;
+    next += 12345u;
+    result <<= 10;
+    result ^= (int)((next / 65536u) % 1024u);
+    next *= 1103515245u;
+    next += 12345u;
+    result <<= 10;
+    result ^= (int)((next / 65536u) % 1024u);
+    *state = next;
+    return result;
+}
+
+/* random_nextDouble (random.c:39-43): r / RAND_MAX */
+double orc_next_double(uint32_t* state) { return (double)orc_rand_r(state) / 2147483647.0; }
+
+/* random_nextUInt (random.c:45-51) */
+uint32_t orc_next_uint(uint32_t* state) {
+    double f = orc_next_double(state);
+    return (uint32_t)(f * 4294967295.0);
+}
+
+/* ======================================================================= */
+/* GML reader: igraph_read_graph_gml subset (topology.c:326-360 -> igraph)  */
+/* ======================================================================= */
+
+typedef enum { GV_INT, GV_REAL, GV_STR, GV_LIST } GvType;
+typedef struct GItem GItem;
+typedef struct GList {
+    GItem* items;
+    int n, cap;
+} GList;
+struct GItem {
+    char* key;
+    GvType type;
+    long long ival;
+    double rval;
+    char* sval;
+    GList list;
+};
+
+typedef struct {
+    const char* p;
+    int line;
+    int err;
+} GLex;
+
+static void glist_push(GList* l, GItem it) {
+    if (l->n == l->cap) {
+        l->cap = l->cap ? l->cap * 2 : 8;
+        l->items = (GItem*)realloc(l->items, sizeof(GItem) * (size_t)l->cap);
+    }
+    l->items[l->n++] = it;
+}
+
+static void glist_free(GList* l) {
+    for (int i = 0; i < l->n; i++) {
+        free(l->items[i].key);
+        free(l->items[i].sval);
+        if (l->items[i].type == GV_LIST) glist_free(&l->items[i].list);
+    }
+    free(l->items);
+    l->items = NULL;
+    l->n = l->cap = 0;
+}
+
+static void glex_skip(GLex* L) {
+    for (;;) {
+        while (*L->p && (orc_isspace((unsigned char)*L->p))) L->p++;
+        if (*L->p == '#') { /* comment to end of line */
+            while (*L->p && *L->p != '\n') L->p++;
+            continue;
+        }
+        break;
+    }
+}
+
+/* Parses "key value" pairs until ']' (nested) or end of text (top). */
+static int gparse_list(GLex* L, GList* out, int nested) {
+    for (;;) {
+        glex_skip(L);
+        if (!*L->p) return nested ? -1 : 0;
+        if (*L->p == ']') {
+            if (!nested) return -1;
+            L->p++;
+            return 0;
+        }
+        if (!(isalpha((unsigned char)*L->p) || *L->p == '_')) return -1;
+        const char* k0 = L->p;
+        while (isalnum((unsigned char)*L->p) || *L->p == '_') L->p++;
+        GItem it;
+        memset(&it, 0, sizeof it);
+        it.key = strndup(k0, (size_t)(L->p - k0));
+        glex_skip(L);
+        const char* p = L->p;
+        if (*p == '[') {
+            L->p++;
+            it.type = GV_LIST;
+            if (gparse_list(L, &it.list, 1) != 0) {
+                free(it.key);
+                glist_free(&it.list);
+                return -1;
+            }
+        } else if (*p == '"') {
+            const char* s0 = ++L->p;
+            while (*L->p && *L->p != '"') L->p++;
+            if (*L->p != '"') {
+                free(it.key);
+                return -1;
+            }
+            it.type = GV_STR;
+            it.sval = strndup(s0, (size_t)(L->p - s0));
+            L->p++;
+        } else if (*p == '-' || (*p >= '0' && *p <= '9')) {
+            const char* n0 = L->p;
+            if (*L->p == '-') L->p++;
+            if (!(*L->p >= '0' && *L->p <= '9')) {
+                free(it.key);
+                return -1;
+            }
+            while (*L->p >= '0' && *L->p <= '9') L->p++;
+            int real = 0;
+            if (*L->p == '.' && L->p[1] >= '0' && L->p[1] <= '9') {
+                real = 1;
+                L->p++;
+                while (*L->p >= '0' && *L->p <= '9') L->p++;
+            }
+            if ((*L->p == 'e' || *L->p == 'E') &&
+                ((L->p[1] >= '0' && L->p[1] <= '9') ||
+                 ((L->p[1] == '+' || L->p[1] == '-') && L->p[2] >= '0' && L->p[2] <= '9'))) {
+                real = 1;
+                L->p += 2;
+                while (*L->p >= '0' && *L->p <= '9') L->p++;
+            }
+            char* tok = strndup(n0, (size_t)(L->p - n0));
+            if (real) {
+                it.type = GV_REAL;
+                it.rval = strtod(tok, NULL);
+            } else {
+                it.type = GV_INT;
+                it.ival = strtoll(tok, NULL, 10);
+            }
+            free(tok);
+        } else {
+            free(it.key);
+            return -1;
+        }
+        glist_push(out, it);
+    }
+}
+
+/* ======================================================================= */
+/* Graph + attribute tables (what igraph's C attribute handler holds)       */
+/* ======================================================================= */
+
+typedef struct {
+    char* name;
+    int is_string; /* IGRAPH_ATTRIBUTE_STRING vs NUMERIC */
+    double* num;   /* NaN when absent */
+    char** str;    /* "" when absent */
+} Attr;
+
+typedef struct {
+    int n;
+    Attr* a;
+} AttrSet;
+
+static Attr* attr_find(AttrSet* s, const char* name) {
+    for (int i = 0; i < s->n; i++)
+        if (!strcmp(s->a[i].name, name)) return &s->a[i];
+    return NULL;
+}
+
+static void attrset_free(AttrSet* s) {
+    for (int i = 0; i < s->n; i++) {
+        free(s->a[i].name);
+        free(s->a[i].num);
+        if (s->a[i].str) {
+            free(s->a[i].str); /* strings are owned by the GML tree */
+        }
+    }
+    free(s->a);
+}
+
+/* Fill attribute table over a sequence of GML blocks (igraph: type is
+ * NUMERIC unless any occurrence is a string; missing -> NaN / ""). */
+static void attrs_build(AttrSet* s, GItem** blocks, int nb, int skip_src_tgt) {
+    s->n = 0;
+    s->a = NULL;
+    for (int b = 0; b < nb; b++) {
+        GList* l = &blocks[b]->list;
+        for (int j = 0; j < l->n; j++) {
+            GItem* it = &l->items[j];
+            if (it->type == GV_LIST) continue; /* composite attributes ignored */
+            if (skip_src_tgt && (!strcmp(it->key, "source") || !strcmp(it->key, "target"))) continue;
+            Attr* a = attr_find(s, it->key);
+            if (!a) {
+                s->a = (Attr*)realloc(s->a, sizeof(Attr) * (size_t)(s->n + 1));
+                a = &s->a[s->n++];
+                memset(a, 0, sizeof *a);
+                a->name = strdup(it->key);
+                a->is_string = (it->type == GV_STR);
+            } else if (it->type == GV_STR) {
+                a->is_string = 1;
+            }
+        }
+    }
+    static char empty[1] = {0};
+    for (int i = 0; i < s->n; i++) {
+        Attr* a = &s->a[i];
+        if (a->is_string) {
+            a->str = (char**)malloc(sizeof(char*) * (size_t)(nb ? nb : 1));
+            for (int b = 0; b < nb; b++) a->str[b] = empty;
+        } else {
+            a->num = (double*)malloc(sizeof(double) * (size_t)(nb ? nb : 1));
+            for (int b = 0; b < nb; b++) a->num[b] = NAN;
+        }
+    }
+    for (int b = 0; b < nb; b++) {
+        GList* l = &blocks[b]->list;
+        for (int j = 0; j < l->n; j++) {
+            GItem* it = &l->items[j];
+            if (it->type == GV_LIST) continue;
+            if (skip_src_tgt && (!strcmp(it->key, "source") || !strcmp(it->key, "target"))) continue;
+            Attr* a = attr_find(s, it->key);
+            if (a->is_string) {
+                if (it->type == GV_STR) a->str[b] = it->sval;
+                else {
+                    /* numeric value in a string attribute: printed (unpinned corner) */
+                    char buf[64];
+                    if (it->type == GV_INT) snprintf(buf, sizeof buf, "%lld", it->ival);
+                    else snprintf(buf, sizeof buf, "%.17g", it->rval);
+                    free(it->sval);
+                    it->sval = strdup(buf);
+                    a->str[b] = it->sval;
+                }
+            } else {
+                a->num[b] = (it->type == GV_INT) ? (double)it->ival : it->rval;
+            }
+        }
+    }
+}
+
+typedef struct {
+    int eid;
+    int nbr;
+} Inc;
+
+struct OrcTopo {
+    GList tree;
+    int directed;
+    int V, E;
+    int* efrom; /* igraph storage: directed as given; undirected from=max to=min */
+    int* eto;
+    AttrSet va, ea;
+    /* incidence (igraph_incident mode OUT): CSR */
+    int* inc_off;
+    Inc* inc;
+    double* weight_ms; /* _topology_extractEdgeWeights (topology.c:1065-1122) */
+    double* edge_rel;  /* 1.0 - packet_loss (topology.c:396) */
+    int is_complete;
+    int use_sp;
+    /* attach state */
+    int nip, capip;
+    uint32_t* ip_keys;
+    int* ip_vertex;
+    unsigned char* v_attached;
+    /* path cache: row per source vertex, allocated lazily */
+    struct PathE {
+        unsigned char present, is_direct;
+        double lat, rel;
+        uint64_t pkts;
+    }** cache;
+    double min_lat;
+    int min_updates;
+    uint64_t next_min_jump_ns;
+};
+typedef struct PathE PathE;
+
+static int cmp_inc(const void* a, const void* b) {
+    const Inc* x = (const Inc*)a;
+    const Inc* y = (const Inc*)b;
+    if (x->nbr != y->nbr) return x->nbr < y->nbr ? -1 : 1;
+    /* igraph_vector_order leaves parallel edges in descending id order */
+    return x->eid > y->eid ? -1 : (x->eid < y->eid);
+}
+
+/* igraph_incident(graph, v, IGRAPH_OUT): directed -> out-edges sorted by
+ * head; undirected -> ALL: out-part (from==v, by to) then in-part (to==v, by
+ * from), i.e. ascending neighbour, undirected loops listed twice. */
+static void build_incidence(OrcTopo* t) {
+    int V = t->V, E = t->E;
+    int* deg = (int*)calloc((size_t)V + 1, sizeof(int));
+    for (int e = 0; e < E; e++) {
+        deg[t->efrom[e]]++;
+        if (!t->directed) deg[t->eto[e]]++;
+    }
+    t->inc_off = (int*)malloc(sizeof(int) * ((size_t)V + 1));
+    t->inc_off[0] = 0;
+    for (int v = 0; v < V; v++) t->inc_off[v + 1] = t->inc_off[v] + deg[v];
+    t->inc = (Inc*)malloc(sizeof(Inc) * (size_t)(t->inc_off[V] ? t->inc_off[V] : 1));
+    int* fill = (int*)calloc((size_t)V, sizeof(int));
+    for (int e = 0; e < E; e++) {
+        int f = t->efrom[e], g = t->eto[e];
+        t->inc[t->inc_off[f] + fill[f]++] = (Inc){e, g};
+        if (!t->directed) t->inc[t->inc_off[g] + fill[g]++] = (Inc){e, f};
+    }
+    for (int v = 0; v < V; v++) {
+        /* out-part entries have nbr <= v, in-part nbr >= v: a single sort by
+         * (nbr, eid desc) reproduces the concatenation except that the two
+         * copies of an undirected loop must stay adjacent (they do: equal nbr). */
+        qsort(t->inc + t->inc_off[v], (size_t)deg[v], sizeof(Inc), cmp_inc);
+    }
+    free(deg);
+    free(fill);
+}
+
+/* igraph_get_eid(from,to,directed): first edge in incidence order (simple
+ * graphs have exactly one; parallel-edge choice is unpinned). -1 if none. */
+static int get_eid(const OrcTopo* t, int from, int to) {
+    for (int k = t->inc_off[from]; k < t->inc_off[from + 1]; k++)
+        if (t->inc[k].nbr == to) return t->inc[k].eid;
+    return -1;
+}
+
+static const char* vas(const OrcTopo* t, const char* name, int v) {
+    Attr* a = attr_find((AttrSet*)&t->va, name);
+    if (!a || !a->is_string) return NULL;
+    const char* s = a->str[v];
+    return (s && s[0]) ? s : NULL;
+}
+
+/* _topology_findVertexAttributeStringBandwidth (topology.c:210-233) */
+static int vertex_bw(const OrcTopo* t, int v, const char* name, uint64_t* out) {
+    const char* s = vas(t, name, v);
+    if (!s) return 0;
+    int64_t b = orc_parse_bandwidth_bits(s);
+    if (b < 0) return 0;
+    b /= 8 * 1024;
+    *out = (uint64_t)b;
+    return 1;
+}
+
+/* _topology_findEdgeAttributeStringTimeMs (topology.c:280-302) */
+static int edge_time_ms(const OrcTopo* t, int e, const char* name, double* out) {
+    Attr* a = attr_find((AttrSet*)&t->ea, name);
+    if (!a || !a->is_string) return 0;
+    const char* s = a->str[e];
+    if (!s || !s[0]) return 0;
+    int64_t ns = orc_parse_time_ns(s);
+    if (ns < 0) return 0;
+    *out = (double)ns / 1000000.0;
+    return 1;
+}
+
+static int edge_num(const OrcTopo* t, int e, const char* name, double* out) {
+    Attr* a = attr_find((AttrSet*)&t->ea, name);
+    if (!a || a->is_string) return 0;
+    if (isnan(a->num[e])) return 0;
+    *out = a->num[e];
+    return 1;
+}
+
+/* g_ascii_strncasecmp(attrName, expected, strlen(expected)) == 0 */
+static int key_is(const char* name, const char* expected) {
+    return strncasecmp(name, expected, strlen(expected)) == 0;
+}
+
+/* _topology_checkGraphAttributes (topology.c:525-657) */
+static int check_attributes(OrcTopo* t) {
+    int ok = 1;
+    for (int i = 0; i < t->va.n; i++) {
+        Attr* a = &t->va.a[i];
+        if (key_is(a->name, "id")) ok = ok && !a->is_string;
+        else if (key_is(a->name, "ip_address") || key_is(a->name, "city_code") ||
+                 key_is(a->name, "country_code") || key_is(a->name, "bandwidth_down") ||
+                 key_is(a->name, "bandwidth_up") || key_is(a->name, "label"))
+            ok = ok && a->is_string;
+        else ok = 0;
+    }
+    if (!attr_find(&t->va, "id") || !attr_find(&t->va, "bandwidth_down") || !attr_find(&t->va, "bandwidth_up"))
+        ok = 0;
+    for (int i = 0; i < t->ea.n; i++) {
+        Attr* a = &t->ea.a[i];
+        if (key_is(a->name, "latency") || key_is(a->name, "jitter") || key_is(a->name, "label"))
+            ok = ok && a->is_string;
+        else if (key_is(a->name, "packet_loss")) ok = ok && !a->is_string;
+        else ok = 0;
+    }
+    if (!attr_find(&t->ea, "latency") || !attr_find(&t->ea, "packet_loss")) ok = 0;
+    return ok;
+}
+
+/* igraph_is_connected(IGRAPH_STRONG) && clusters == 1 (topology.c:674-713) */
+static int strongly_connected(const OrcTopo* t) {
+    int V = t->V;
+    if (V == 0) return 0;
+    int* seen = (int*)calloc((size_t)V, sizeof(int));
+    int* stack = (int*)malloc(sizeof(int) * (size_t)V);
+    /* reverse adjacency for the backward pass of a directed graph */
+    int* roff = (int*)calloc((size_t)V + 1, sizeof(int));
+    int* radj = (int*)malloc(sizeof(int) * (size_t)(t->E + 1));
+    for (int e = 0; e < t->E; e++) roff[t->eto[e] + 1]++;
+    for (int v = 0; v < V; v++) roff[v + 1] += roff[v];
+    int* rf = (int*)calloc((size_t)V, sizeof(int));
+    for (int e = 0; e < t->E; e++) radj[roff[t->eto[e]] + rf[t->eto[e]]++] = t->efrom[e];
+    int ok = 1;
+    for (int pass = 0; pass < (t->directed ? 2 : 1) && ok; pass++) {
+        memset(seen, 0, sizeof(int) * (size_t)V);
+        int sp = 0, cnt = 1;
+        stack[sp++] = 0;
+        seen[0] = 1;
+        while (sp) {
+            int u = stack[--sp];
+            int k0 = pass == 0 ? t->inc_off[u] : roff[u];
+            int k1 = pass == 0 ? t->inc_off[u + 1] : roff[u + 1];
+            for (int k = k0; k < k1; k++) {
+                int w = pass == 0 ? t->inc[k].nbr : radj[k];
+                if (!seen[w]) {
+                    seen[w] = 1;
+                    cnt++;
+                    stack[sp++] = w;
+                }
+            }
+        }
+        if (cnt != V) ok = 0;
+    }
+    free(seen);
+    free(stack);
+    free(roff);
+    free(radj);
+    free(rf);
+    return ok;
+}
+
+/* _topology_isComplete (topology.c:409-511) */
+static int is_complete(const OrcTopo* t) {
+    for (int v = 0; v < t->V; v++) {
+        int ecount = t->inc_off[v + 1] - t->inc_off[v];
+        if (!t->directed && get_eid(t, v, v) >= 0) ecount -= 1;
+        if (ecount < t->V) return 0;
+    }
+    return 1;
+}
+
+/* _topology_checkGraphVerticesHelperHook (topology.c:718-829) */
+static int check_vertices(const OrcTopo* t) {
+    Attr* id = attr_find((AttrSet*)&t->va, "id");
+    int ok = 1;
+    for (int v = 0; v < t->V; v++) {
+        if (!id || id->is_string || isnan(id->num[v])) ok = 0;
+        uint64_t bw;
+        if (!(vertex_bw(t, v, "bandwidth_down", &bw) && bw > 0)) ok = 0;
+        if (!(vertex_bw(t, v, "bandwidth_up", &bw) && bw > 0)) ok = 0;
+    }
+    return ok;
+}
+
+/* _topology_checkGraphEdgesHelperHook (topology.c:892-977) */
+static int check_edges(const OrcTopo* t) {
+    int ok = 1;
+    for (int e = 0; e < t->E; e++) {
+        double lat, loss, jit;
+        if (!(edge_time_ms(t, e, "latency", &lat) && lat > 0.0)) ok = 0;
+        if (!(edge_num(t, e, "packet_loss", &loss) && loss >= 0.0f && loss <= 1.0f)) ok = 0;
+        if (attr_find((AttrSet*)&t->ea, "jitter") && edge_time_ms(t, e, "jitter", &jit) && !(jit >= 0.0f)) ok = 0;
+    }
+    return ok;
+}
+
+void orc_topology_free(OrcTopo* t) {
+    if (!t) return;
+    attrset_free(&t->va);
+    attrset_free(&t->ea);
+    glist_free(&t->tree);
+    free(t->efrom);
+    free(t->eto);
+    free(t->inc_off);
+    free(t->inc);
+    free(t->weight_ms);
+    free(t->edge_rel);
+    free(t->ip_keys);
+    free(t->ip_vertex);
+    free(t->v_attached);
+    if (t->cache) {
+        for (int v = 0; v < t->V; v++) free(t->cache[v]);
+        free(t->cache);
+    }
+    free(t);
+}
+
+/* topology_new (topology.c:2328-2354): load, check, extract weights. */
+OrcTopo* orc_topology_new(const char* text, int use_shortest_path) {
+    OrcTopo* t = (OrcTopo*)calloc(1, sizeof(OrcTopo));
+    t->use_sp = use_shortest_path ? 1 : 0;
+    GLex L = {text, 1, 0};
+    if (!text || gparse_list(&L, &t->tree, 0) != 0) goto fail;
+    GItem* graph = NULL;
+    for (int i = 0; i < t->tree.n; i++)
+        if (!strcmp(t->tree.items[i].key, "graph") && t->tree.items[i].type == GV_LIST) {
+            graph = &t->tree.items[i];
+            break;
+        }
+    if (!graph) goto fail;
+    int nn = 0, ne = 0;
+    for (int i = 0; i < graph->list.n; i++) {
+        GItem* it = &graph->list.items[i];
+        if (!strcmp(it->key, "node")) {
+            if (it->type != GV_LIST) goto fail;
+            nn++;
+        } else if (!strcmp(it->key, "edge")) {
+            if (it->type != GV_LIST) goto fail;
+            ne++;
+        } else if (!strcmp(it->key, "directed") && it->type == GV_INT) {
+            t->directed = (it->ival == 1);
+        }
+    }
+    GItem** nodes = (GItem**)malloc(sizeof(GItem*) * (size_t)(nn + 1));
+    GItem** edges = (GItem**)malloc(sizeof(GItem*) * (size_t)(ne + 1));
+    nn = ne = 0;
+    for (int i = 0; i < graph->list.n; i++) {
+        GItem* it = &graph->list.items[i];
+        if (!strcmp(it->key, "node")) nodes[nn++] = it;
+        else if (!strcmp(it->key, "edge")) edges[ne++] = it;
+    }
+    t->V = nn;
+    t->E = ne;
+    /* node ids: integer, unique; vertex index = order of node blocks */
+    long long* ids = (long long*)malloc(sizeof(long long) * (size_t)(nn + 1));
+    int bad = 0;
+    for (int v = 0; v < nn; v++) {
+        int has = 0;
+        for (int j = 0; j < nodes[v]->list.n; j++) {
+            GItem* it = &nodes[v]->list.items[j];
+            if (!strcmp(it->key, "id")) {
+                if (it->type != GV_INT) bad = 1;
+                ids[v] = it->ival;
+                has = 1;
+                break;
+            }
+        }
+        if (!has) bad = 1;
+    }
+    for (int v = 0; v < nn && !bad; v++)
+        for (int w = v + 1; w < nn; w++)
+            if (ids[v] == ids[w]) bad = 1;
+    t->efrom = (int*)malloc(sizeof(int) * (size_t)(ne + 1));
+    t->eto = (int*)malloc(sizeof(int) * (size_t)(ne + 1));
+    for (int e = 0; e < ne && !bad; e++) {
+        long long s = 0, g = 0;
+        int hs = 0, hg = 0;
+        for (int j = 0; j < edges[e]->list.n; j++) {
+            GItem* it = &edges[e]->list.items[j];
+            if (!strcmp(it->key, "source")) {
+                if (it->type != GV_INT) bad = 1;
+                s = it->ival;
+                hs = 1;
+            } else if (!strcmp(it->key, "target")) {
+                if (it->type != GV_INT) bad = 1;
+                g = it->ival;
+                hg = 1;
+            }
+        }
+        if (!hs || !hg) {
+            bad = 1;
+            break;
+        }
+        int sv = -1, gv = -1;
+        for (int v = 0; v < nn; v++) {
+            if (ids[v] == s) sv = v;
+            if (ids[v] == g) gv = v;
+        }
+        if (sv < 0 || gv < 0) {
+            bad = 1;
+            break;
+        }
+        if (t->directed || sv > gv) {
+            t->efrom[e] = sv;
+            t->eto[e] = gv;
+        } else {
+            t->efrom[e] = gv;
+            t->eto[e] = sv;
+        }
+    }
+    free(ids);
+    if (bad) {
+        free(nodes);
+        free(edges);
+        goto fail;
+    }
+    attrs_build(&t->va, nodes, nn, 0);
+    attrs_build(&t->ea, edges, ne, 1);
+    free(nodes);
+    free(edges);
+    build_incidence(t);
+
+    /* _topology_checkGraph (topology.c:1040-1063) */
+    if (!check_attributes(t)) goto fail;
+    if (!strongly_connected(t)) goto fail;
+    t->is_complete = is_complete(t);
+    if (!t->is_complete && !t->use_sp) goto fail;
+    if (!check_vertices(t) || !check_edges(t)) goto fail;
+
+    /* _topology_extractEdgeWeights + reliabilities */
+    t->weight_ms = (double*)malloc(sizeof(double) * (size_t)(ne + 1));
+    t->edge_rel = (double*)malloc(sizeof(double) * (size_t)(ne + 1));
+    for (int e = 0; e < ne; e++) {
+        double loss = 0;
+        edge_time_ms(t, e, "latency", &t->weight_ms[e]);
+        edge_num(t, e, "packet_loss", &loss);
+        t->edge_rel[e] = 1.0f - loss;
+    }
+    t->v_attached = (unsigned char*)calloc((size_t)t->V, 1);
+    t->cache = (PathE**)calloc((size_t)t->V, sizeof(PathE*));
+    return t;
+fail:
+    orc_topology_free(t);
+    return NULL;
+}
+
+int orc_topology_vertex_count(const OrcTopo* t) { return t->V; }
+int orc_topology_edge_count(const OrcTopo* t) { return t->E; }
+int orc_topology_is_directed(const OrcTopo* t) { return t->directed; }
+int orc_topology_is_complete(const OrcTopo* t) { return t->is_complete; }
+
+/* ======================================================================= */
+/* attach: topology.c:2024-2272                                            */
+/* ======================================================================= */
+
+/* address_stringToIP (address.c:145-152): inet_pton, INADDR_NONE on failure */
+static uint32_t str_to_ip(const char* s) {
+    struct in_addr a;
+    if (s && inet_pton(AF_INET, s, &a) == 1) return a.s_addr;
+    return 0xffffffffu;
+}
+
+/* INADDR_* compared against network-order values, as the reference does */
+static int ip_usable(uint32_t ip) { return ip != 0xffffffffu && ip != 0u && ip != 0x7f000001u; }
+
+typedef struct {
+    int* v;
+    int n;
+} Queue;
+
+static void q_push(Queue* q, int v, int cap) {
+    (void)cap;
+    q->v[q->n++] = v;
+}
+
+static void ip_map_set(OrcTopo* t, uint32_t ip, int v) {
+    for (int i = 0; i < t->nip; i++)
+        if (t->ip_keys[i] == ip) {
+            t->ip_vertex[i] = v;
+            return;
+        }
+    if (t->nip == t->capip) {
+        t->capip = t->capip ? t->capip * 2 : 64;
+        t->ip_keys = (uint32_t*)realloc(t->ip_keys, sizeof(uint32_t) * (size_t)t->capip);
+        t->ip_vertex = (int*)realloc(t->ip_vertex, sizeof(int) * (size_t)t->capip);
+    }
+    t->ip_keys[t->nip] = ip;
+    t->ip_vertex[t->nip] = v;
+    t->nip++;
+}
+
+int orc_vertex_of_ip(OrcTopo* t, uint32_t ip) {
+    for (int i = 0; i < t->nip; i++)
+        if (t->ip_keys[i] == ip) return t->ip_vertex[i];
+    return -1;
+}
+
+int orc_topology_attach(OrcTopo* t, uint32_t ip_net, uint32_t* rng_state, const char* ip_hint,
+                        const char* city_hint, const char* country_hint, uint64_t* bw_down,
+                        uint64_t* bw_up) {
+    (void)ip_net;
+    int V = t->V;
+    Queue city = {(int*)malloc(sizeof(int) * (size_t)V), 0};
+    Queue country = {(int*)malloc(sizeof(int) * (size_t)V), 0};
+    Queue all = {(int*)malloc(sizeof(int) * (size_t)V), 0};
+    unsigned nIPsCity = 0, nIPsCountry = 0, nIPsAll = 0;
+    int requestedUsable = 0, exact = 0;
+    uint32_t requested = 0;
+    if (ip_hint) {
+        uint32_t ip = str_to_ip(ip_hint);
+        if (ip_usable(ip)) {
+            requestedUsable = 1;
+            requested = ip;
+        }
+    }
+    /* _topology_findAttachmentVertexHelperHook over all vertices (:2024-2100) */
+    for (int v = 0; v < V; v++) {
+        const char* ipStr = vas(t, "ip_address", v);
+        const char* cc = vas(t, "city_code", v);
+        const char* co = vas(t, "country_code", v);
+        int cityMatch = cc && city_hint && !strcasecmp(cc, city_hint);
+        int countryMatch = co && country_hint && !strcasecmp(co, country_hint);
+        int vUsable = 0;
+        uint32_t vip = 0xffffffffu;
+        if (ipStr) {
+            uint32_t ip = str_to_ip(ipStr);
+            if (ip_usable(ip)) {
+                vUsable = 1;
+                vip = ip;
+            }
+        }
+        if (requestedUsable && vUsable && vip == requested) {
+            if (!exact) {
+                city.n = country.n = all.n = 0;
+            }
+            exact = 1;
+            q_push(&all, v, V);
+            nIPsAll++;
+        }
+        if (exact) continue;
+        q_push(&all, v, V);
+        if (vUsable) nIPsAll++;
+        if (cityMatch) {
+            q_push(&city, v, V);
+            if (vUsable) nIPsCity++;
+        }
+        if (countryMatch) {
+            q_push(&country, v, V);
+            if (vUsable) nIPsCountry++;
+        }
+    }
+    Queue* cand;
+    int useLPM;
+    if (city.n > 0) {
+        cand = &city;
+        useLPM = requestedUsable && nIPsCity > 0;
+    } else if (country.n > 0) {
+        cand = &country;
+        useLPM = requestedUsable && nIPsCountry > 0;
+    } else {
+        cand = &all;
+        useLPM = (ip_hint != NULL) && nIPsAll > 0;
+    }
+    int chosen = -1;
+    if (cand->n > 0) {
+        if (useLPM && !exact) {
+            /* _topology_getLongestPrefixMatch (:2102-2130) */
+            uint32_t best = 0;
+            for (int i = 0; i < cand->n; i++) {
+                const char* s = vas(t, "ip_address", cand->v[i]);
+                uint32_t vip = str_to_ip(s ? s : "");
+                uint32_t match = ~(vip ^ requested);
+                if (match > best || best == 0) {
+                    best = match;
+                    chosen = cand->v[i];
+                }
+            }
+        } else {
+            double r = orc_next_double(rng_state);
+            int range = cand->n - 1;
+            int idx = (int)round((double)(range * r));
+            chosen = cand->v[idx];
+        }
+    }
+    free(city.v);
+    free(country.v);
+    free(all.v);
+    if (chosen < 0) return -1;
+    ip_map_set(t, ip_net, chosen);
+    t->v_attached[chosen] = 1;
+    if (bw_up) vertex_bw(t, chosen, "bandwidth_up", bw_up);
+    if (bw_down) vertex_bw(t, chosen, "bandwidth_down", bw_down);
+    return chosen;
+}
+
+/* topology_detach (topology.c:2274-2281): removes the IP only */
+void orc_topology_detach(OrcTopo* t, uint32_t ip) {
+    for (int i = 0; i < t->nip; i++)
+        if (t->ip_keys[i] == ip) {
+            t->ip_keys[i] = t->ip_keys[t->nip - 1];
+            t->ip_vertex[i] = t->ip_vertex[t->nip - 1];
+            t->nip--;
+            return;
+        }
+}
+
+/* ======================================================================= */
+/* igraph_2wheap (igraph 0.8 src/core/indheap.c) -- max-heap on -dist      */
+/* ======================================================================= */
+
+typedef struct {
+    double* data;
+    int* index;  /* heap position -> vertex */
+    int* index2; /* vertex -> position + 2 (0 = absent) */
+    int size;
+} Wheap;
+
+#define WH_PARENT(x) ((((x) + 1) / 2) - 1)
+#define WH_LEFT(x) (((x) + 1) * 2 - 1)
+#define WH_RIGHT(x) (((x) + 1) * 2)
+
+static void wh_switch(Wheap* h, int e1, int e2) {
+    if (e1 != e2) {
+        double tmp = h->data[e1];
+        h->data[e1] = h->data[e2];
+        h->data[e2] = tmp;
+        int t1 = h->index[e1], t2 = h->index[e2];
+        h->index2[t1] = e2 + 2;
+        h->index2[t2] = e1 + 2;
+        h->index[e1] = t2;
+        h->index[e2] = t1;
+    }
+}
+
+static void wh_shift_up(Wheap* h, int e) {
+    while (!(e == 0 || h->data[e] < h->data[WH_PARENT(e)])) {
+        wh_switch(h, e, WH_PARENT(e));
+        e = WH_PARENT(e);
+    }
+}
+
+static void wh_sink(Wheap* h, int head) {
+    for (;;) {
+        int size = h->size;
+        if (WH_LEFT(head) >= size) return;
+        if (WH_RIGHT(head) == size || h->data[WH_LEFT(head)] >= h->data[WH_RIGHT(head)]) {
+            if (h->data[head] < h->data[WH_LEFT(head)]) {
+                wh_switch(h, head, WH_LEFT(head));
+                head = WH_LEFT(head);
+            } else return;
+        } else {
+            if (h->data[head] < h->data[WH_RIGHT(head)]) {
+                wh_switch(h, head, WH_RIGHT(head));
+                head = WH_RIGHT(head);
+            } else return;
+        }
+    }
+}
+
+static void wh_push(Wheap* h, int idx, double elem) {
+    int size = h->size++;
+    h->data[size] = elem;
+    h->index[size] = idx;
+    h->index2[idx] = size + 2;
+    wh_shift_up(h, size);
+}
+
+static double wh_delete_max(Wheap* h, int* idx) {
+    double tmp = h->data[0];
+    *idx = h->index[0];
+    wh_switch(h, 0, h->size - 1);
+    h->size--;
+    h->index2[*idx] = 0;
+    wh_sink(h, 0);
+    return tmp;
+}
+
+static void wh_modify(Wheap* h, int idx, double elem) {
+    int pos = h->index2[idx] - 2;
+    h->data[pos] = elem;
+    wh_sink(h, pos);
+    wh_shift_up(h, pos);
+}
+
+/* igraph_get_shortest_paths_dijkstra (igraph 0.8 structural_properties.c),
+ * mode OUT, weights = weight_ms, early exit once every target is popped.
+ * Fills dist/rel (reliability folded left-to-right along the parent chain,
+ * exactly _topology_computePathProperties' product, topology.c:1308-1365). */
+static void dijkstra(const OrcTopo* t, int src, const unsigned char* is_target_in, int ntargets,
+                     double* dist, double* rel) {
+    int V = t->V;
+    Wheap h;
+    h.data = (double*)malloc(sizeof(double) * (size_t)V);
+    h.index = (int*)malloc(sizeof(int) * (size_t)V);
+    h.index2 = (int*)calloc((size_t)V, sizeof(int));
+    h.size = 0;
+    unsigned char* is_target = (unsigned char*)malloc((size_t)V);
+    memcpy(is_target, is_target_in, (size_t)V);
+    for (int v = 0; v < V; v++) {
+        dist[v] = -1.0;
+        rel[v] = 0.0;
+    }
+    int to_reach = ntargets;
+    dist[src] = 0.0;
+    rel[src] = 1.0;
+    wh_push(&h, src, 0.0);
+    while (h.size > 0 && to_reach > 0) {
+        int u;
+        double mindist = -wh_delete_max(&h, &u);
+        if (is_target[u]) {
+            is_target[u] = 0;
+            to_reach--;
+        }
+        double ru = rel[u];
+        for (int k = t->inc_off[u]; k < t->inc_off[u + 1]; k++) {
+            int e = t->inc[k].eid, v = t->inc[k].nbr;
+            double alt = mindist + t->weight_ms[e];
+            double cur = dist[v];
+            if (cur < 0) {
+                dist[v] = alt;
+                rel[v] = ru * t->edge_rel[e];
+                wh_push(&h, v, -alt);
+            } else if (alt < cur) {
+                dist[v] = alt;
+                rel[v] = ru * t->edge_rel[e];
+                wh_modify(&h, v, -alt);
+            }
+        }
+    }
+    free(h.data);
+    free(h.index);
+    free(h.index2);
+    free(is_target);
+}
+
+/* _topology_computeShortestPathToSelf (topology.c:1431-1576) */
+static void self_path(const OrcTopo* t, int v, double* lat_out, double* rel_out, int* direct_out) {
+    double minLatency = -1.0f, relMin = 0.0f;
+    int isDirect = 0;
+    for (int k = t->inc_off[v]; k < t->inc_off[v + 1]; k++) {
+        int e = t->inc[k].eid;
+        double lat = t->weight_ms[e];
+        int edgeIsDirect = (t->inc[k].nbr == v);
+        if (!edgeIsDirect) lat *= 2.0f;
+        if (minLatency == -1 || lat < minLatency) {
+            minLatency = lat;
+            relMin = t->edge_rel[e];
+            isDirect = edgeIsDirect;
+        }
+    }
+    if (minLatency == -1) {
+        minLatency = 0;
+        isDirect = 1;
+    }
+    double r = relMin;
+    if (!isDirect) r = r * r;
+    *lat_out = minLatency;
+    *rel_out = r;
+    *direct_out = isDirect;
+}
+
+int orc_direct_path(OrcTopo* t, int s, int d, double* lat, double* rel) {
+    int e = get_eid(t, s, d);
+    if (e < 0) return -1;
+    double tl = 0.0, tr = 1.0;
+    tl += t->weight_ms[e];
+    tr *= t->edge_rel[e];
+    *lat = tl;
+    *rel = tr;
+    return 0;
+}
+
+int orc_compute_row(OrcTopo* t, int src, const int* targets, int ntargets, double* lat, double* rel) {
+    int V = t->V;
+    unsigned char* is_t = (unsigned char*)calloc((size_t)V, 1);
+    int distinct = 0;
+    for (int i = 0; i < ntargets; i++)
+        if (!is_t[targets[i]]) {
+            is_t[targets[i]] = 1;
+            distinct++;
+        }
+    double* dist = (double*)malloc(sizeof(double) * (size_t)V);
+    double* r = (double*)malloc(sizeof(double) * (size_t)V);
+    dijkstra(t, src, is_t, distinct, dist, r);
+    for (int i = 0; i < ntargets; i++) {
+        int v = targets[i];
+        if (v == src) {
+            int dd;
+            self_path(t, src, &lat[i], &rel[i], &dd);
+        } else {
+            double l = dist[v];
+            if (l == 0) l = 1; /* topology.c:1787-1791 */
+            lat[i] = l;
+            rel[i] = r[v];
+        }
+    }
+    free(is_t);
+    free(dist);
+    free(r);
+    return 0;
+}
+
+/* ======================================================================= */
+/* path cache + lookups: topology.c:1166-1265, 1900-2022                    */
+/* ======================================================================= */
+
+static PathE* cache_get(OrcTopo* t, int s, int d) {
+    if (!t->cache[s]) return NULL;
+    PathE* p = &t->cache[s][d];
+    return p->present ? p : NULL;
+}
+
+/* controller_updateMinTimeJump (controller.c:141-153) */
+static void controller_update(OrcTopo* t, double minMs) {
+    if (t->next_min_jump_ns == 0 || minMs < (double)t->next_min_jump_ns)
+        t->next_min_jump_ns = ((uint64_t)minMs) * 1000000ull;
+}
+
+/* _topology_shouldStorePath + _topology_storePathInCache (:1189-1265) */
+static void cache_store(OrcTopo* t, int isDirect, int s, int d, double lat, double rel) {
+    if (cache_get(t, s, d) || cache_get(t, d, s)) return;
+    if (!isDirect && !t->use_sp && get_eid(t, s, d) >= 0) return;
+    if (!t->cache[s]) t->cache[s] = (PathE*)calloc((size_t)t->V, sizeof(PathE));
+    PathE* p = &t->cache[s][d];
+    p->present = 1;
+    p->is_direct = (unsigned char)isDirect;
+    p->lat = lat;
+    p->rel = rel;
+    p->pkts = 0;
+    if (t->min_lat == 0 || lat < t->min_lat) {
+        t->min_lat = lat;
+        t->min_updates++;
+        controller_update(t, t->min_lat);
+    }
+}
+
+/* _topology_computeSourcePaths (:1578-1814) incl. the self case */
+static int compute_source_paths(OrcTopo* t, int s, int d) {
+    if (s == d) {
+        double l, r;
+        int dir;
+        self_path(t, s, &l, &r, &dir);
+        cache_store(t, dir, s, s, l, r);
+        return 1;
+    }
+    int V = t->V, n = 0;
+    int* targets = (int*)malloc(sizeof(int) * (size_t)V);
+    for (int v = 0; v < V; v++)
+        if (t->v_attached[v]) targets[n++] = v;
+    unsigned char* is_t = (unsigned char*)calloc((size_t)V, 1);
+    for (int i = 0; i < n; i++) is_t[targets[i]] = 1;
+    double* dist = (double*)malloc(sizeof(double) * (size_t)V);
+    double* r = (double*)malloc(sizeof(double) * (size_t)V);
+    dijkstra(t, s, is_t, n, dist, r);
+    for (int i = 0; i < n; i++) {
+        int v = targets[i];
+        if (v == s || dist[v] < 0) continue;
+        double l = dist[v];
+        if (l == 0) l = 1;
+        cache_store(t, 0, s, v, l, r[v]);
+    }
+    free(targets);
+    free(is_t);
+    free(dist);
+    free(r);
+    return 1;
+}
+
+static PathE* get_path_entry(OrcTopo* t, uint32_t sip, uint32_t dip) {
+    int s = orc_vertex_of_ip(t, sip);
+    if (s < 0) return NULL;
+    int d = orc_vertex_of_ip(t, dip);
+    if (d < 0) return NULL;
+    PathE* p = cache_get(t, s, d);
+    if (!p && !t->directed) p = cache_get(t, d, s);
+    if (!p) {
+        int ok;
+        if (!t->use_sp) {
+            double l, r;
+            ok = orc_direct_path(t, s, d, &l, &r) == 0;
+            if (ok) cache_store(t, 1, s, d, l, r);
+        } else {
+            ok = compute_source_paths(t, s, d);
+        }
+        if (ok) {
+            p = cache_get(t, s, d);
+            if (!p) p = cache_get(t, d, s);
+        }
+    }
+    return p; /* NULL here is utility_panic in the reference (:1970-1976) */
+}
+
+double orc_topology_get_latency(OrcTopo* t, uint32_t s, uint32_t d) {
+    PathE* p = get_path_entry(t, s, d);
+    return p ? p->lat : -1.0;
+}
+
+double orc_topology_get_reliability(OrcTopo* t, uint32_t s, uint32_t d) {
+    PathE* p = get_path_entry(t, s, d);
+    return p ? p->rel : -1.0;
+}
+
+int orc_topology_is_routable(OrcTopo* t, uint32_t s, uint32_t d) {
+    return orc_topology_get_latency(t, s, d) > -1 ? 1 : 0;
+}
+
+void orc_topology_increment_path_packet_counter(OrcTopo* t, uint32_t s, uint32_t d) {
+    PathE* p = get_path_entry(t, s, d);
+    if (p) p->pkts++;
+}
+
+uint64_t orc_topology_path_packet_count(OrcTopo* t, uint32_t s, uint32_t d) {
+    int sv = orc_vertex_of_ip(t, s), dv = orc_vertex_of_ip(t, d);
+    if (sv < 0 || dv < 0) return 0;
+    PathE* p = cache_get(t, sv, dv);
+    if (!p) p = cache_get(t, dv, sv);
+    return p ? p->pkts : 0;
+}
+
+double orc_topology_min_path_latency(const OrcTopo* t) { return t->min_lat; }
+int orc_topology_min_jump_updates(const OrcTopo* t) { return t->min_updates; }
+uint64_t orc_controller_next_min_jump_ns(const OrcTopo* t) { return t->next_min_jump_ns; }
+
+int orc_topology_preload_table(OrcTopo* t, const int* slots, int nslots, const double* lat, const double* rel) {
+    for (int i = 0; i < nslots; i++) {
+        int s = slots[i];
+        for (int j = 0; j < nslots; j++) {
+            int d = slots[j];
+            if (i == j) {
+                cache_store(t, 1, s, s, lat[(size_t)i * nslots + j], rel[(size_t)i * nslots + j]);
+            } else {
+                cache_store(t, 0, s, d, lat[(size_t)i * nslots + j], rel[(size_t)i * nslots + j]);
+            }
+        }
+    }
+    return 0;
+}
+
+/* ======================================================================= */
+/* event order: utility/priority_queue.c:91-175 with event_compare          */
+/* (core/work/event.c:109-152; host_compare host.c:407-413 = id order)      */
+/* ======================================================================= */
+
+static int ev_cmp(const OrcEvKey* a, const OrcEvKey* b) {
+    if (a->time != b->time) return a->time > b->time ? 1 : -1;
+    if (a->dst != b->dst) return a->dst > b->dst ? 1 : -1;
+    if (a->src != b->src) return a->src > b->src ? 1 : -1;
+    if (a->seq != b->seq) return a->seq > b->seq ? 1 : -1;
+    return 0;
+}
+
+typedef struct {
+    uint32_t* heap; /* indices into keys */
+    size_t size, cap;
+    const OrcEvKey* keys;
+} Pq;
+
+static int pq_smaller(Pq* q, size_t i, size_t j) { return ev_cmp(&q->keys[q->heap[i]], &q->keys[q->heap[j]]) < 0; }
+
+static void pq_swap(Pq* q, size_t i, size_t j) {
+    uint32_t x = q->heap[i];
+    q->heap[i] = q->heap[j];
+    q->heap[j] = x;
+}
+
+static void pq_push(Pq* q, uint32_t idx) {
+    if (q->size == q->cap) {
+        q->cap = q->cap ? q->cap * 2 : 100;
+        q->heap = (uint32_t*)realloc(q->heap, sizeof(uint32_t) * q->cap);
+    }
+    size_t i = q->size++;
+    q->heap[i] = idx;
+    while (i > 0 && pq_smaller(q, i, (i - 1) / 2)) {
+        pq_swap(q, i, (i - 1) / 2);
+        i = (i - 1) / 2;
+    }
+}
+
+static uint32_t pq_pop(Pq* q) {
+    uint32_t top = q->heap[0];
+    pq_swap(q, 0, q->size - 1);
+    q->size--;
+    size_t i = 0, c;
+    while ((c = 2 * i + 1) < q->size) {
+        if (c + 1 < q->size && pq_smaller(q, c + 1, c)) c = c + 1;
+        if (pq_smaller(q, c, i)) {
+            pq_swap(q, i, c);
+            i = c;
+        } else break;
+    }
+    return top;
+}
+
+void orc_pq_order(const OrcEvKey* keys, size_t n, uint32_t* order) {
+    Pq q = {NULL, 0, 0, keys};
+    for (size_t i = 0; i < n; i++) pq_push(&q, (uint32_t)i);
+    for (size_t i = 0; i < n; i++) order[i] = pq_pop(&q);
+    free(q.heap);
+}
+
+/* ======================================================================= */
+/* packet hand-off: worker_sendPacket (worker.c:517-576) -> scheduler_push  */
+/* (scheduler.c:232-255) -> host-single push (policy_host_single.c:174-220) */
+/* ======================================================================= */
+
+size_t orc_round(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint64_t barrier, uint64_t end_time,
+                 uint64_t bootstrap_end, const OrcPkt* pkts, size_t n, OrcDeliv* out, uint8_t* status,
+                 uint64_t* min_time) {
+    OrcEvKey* keys = (OrcEvKey*)malloc(sizeof(OrcEvKey) * (n ? n : 1));
+    Pq* qs = (Pq*)calloc(nhosts ? nhosts : 1, sizeof(Pq));
+    for (uint32_t h = 0; h < nhosts; h++) qs[h].keys = keys;
+    uint64_t mn = UINT64_MAX;
+    for (size_t i = 0; i < n; i++) {
+        const OrcPkt* p = &pkts[i];
+        uint32_t sip = host_ips[p->src_host], dip = host_ips[p->dst_host];
+        int boot = p->now < bootstrap_end;
+        double rel = orc_topology_get_reliability(t, sip, dip);
+        uint32_t st = p->rng_state;
+        double chance = orc_next_double(&st);
+        if (boot || chance <= rel || p->payload_len == 0) {
+            double lat = orc_topology_get_latency(t, sip, dip);
+            uint64_t delay = (uint64_t)ceil(lat * 1000000.0);
+            uint64_t tm = p->now + delay;
+            orc_topology_increment_path_packet_counter(t, sip, dip);
+            if (tm >= end_time) {
+                status[i] = ORC_DROP_END;
+                continue;
+            }
+            if (p->src_host != p->dst_host && tm < barrier) tm = barrier;
+            keys[i] = (OrcEvKey){tm, p->dst_host, p->src_host, p->seq};
+            pq_push(&qs[p->dst_host], (uint32_t)i);
+            if (tm >= barrier && tm < mn) mn = tm; /* worker.c:350-363 */
+            status[i] = ORC_DELIVERED;
+        } else {
+            status[i] = ORC_DROP_LOSS;
+        }
+    }
+    size_t k = 0;
+    for (uint32_t h = 0; h < nhosts; h++) {
+        while (qs[h].size) {
+            uint32_t i = pq_pop(&qs[h]);
+            out[k++] = (OrcDeliv){keys[i].time, keys[i].seq, keys[i].src, keys[i].dst, i, 0};
+        }
+        free(qs[h].heap);
+    }
+    free(qs);
+    free(keys);
+    if (min_time) *min_time = mn;
+    return k;
+}

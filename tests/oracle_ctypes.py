@@ -1,0 +1,202 @@
+"""ctypes binding of oracle/liboracle.so (the CPU restatement).
+
+TEST INFRASTRUCTURE: imported only by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.  The product (shadow_amd/) never imports it.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+
+def _build():
+    if not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(
+            os.path.join(ROOT, "oracle", "oracle.c")):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"])
+
+
+_build()
+lib = C.CDLL(LIB_PATH)
+
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+
+lib.orc_parse_time_ns.restype = C.c_int64
+lib.orc_parse_time_ns.argtypes = [C.c_char_p]
+lib.orc_parse_bandwidth_bits.restype = C.c_int64
+lib.orc_parse_bandwidth_bits.argtypes = [C.c_char_p]
+lib.orc_rand_r.restype = C.c_int
+lib.orc_rand_r.argtypes = [u32p]
+lib.orc_next_double.restype = C.c_double
+lib.orc_next_double.argtypes = [u32p]
+lib.orc_next_uint.restype = C.c_uint32
+lib.orc_next_uint.argtypes = [u32p]
+lib.orc_topology_new.restype = C.c_void_p
+lib.orc_topology_new.argtypes = [C.c_char_p, C.c_int]
+lib.orc_topology_free.argtypes = [C.c_void_p]
+for fn in ("orc_topology_vertex_count", "orc_topology_edge_count", "orc_topology_is_directed",
+           "orc_topology_is_complete", "orc_topology_min_jump_updates"):
+    getattr(lib, fn).restype = C.c_int
+    getattr(lib, fn).argtypes = [C.c_void_p]
+lib.orc_topology_attach.restype = C.c_int
+lib.orc_topology_attach.argtypes = [C.c_void_p, C.c_uint32, u32p, C.c_char_p, C.c_char_p, C.c_char_p, u64p, u64p]
+lib.orc_topology_detach.argtypes = [C.c_void_p, C.c_uint32]
+for fn in ("orc_topology_get_latency", "orc_topology_get_reliability"):
+    getattr(lib, fn).restype = C.c_double
+    getattr(lib, fn).argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+lib.orc_topology_is_routable.restype = C.c_int
+lib.orc_topology_is_routable.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+lib.orc_topology_increment_path_packet_counter.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+lib.orc_topology_path_packet_count.restype = C.c_uint64
+lib.orc_topology_path_packet_count.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+lib.orc_topology_min_path_latency.restype = C.c_double
+lib.orc_topology_min_path_latency.argtypes = [C.c_void_p]
+lib.orc_controller_next_min_jump_ns.restype = C.c_uint64
+lib.orc_controller_next_min_jump_ns.argtypes = [C.c_void_p]
+lib.orc_compute_row.restype = C.c_int
+lib.orc_compute_row.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+lib.orc_direct_path.restype = C.c_int
+lib.orc_direct_path.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+lib.orc_vertex_of_ip.restype = C.c_int
+lib.orc_vertex_of_ip.argtypes = [C.c_void_p, C.c_uint32]
+lib.orc_topology_preload_table.restype = C.c_int
+lib.orc_topology_preload_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+lib.orc_round.restype = C.c_size_t
+lib.orc_round.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
+                          C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, u64p]
+lib.orc_pq_order.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+
+
+def _s(x):
+    return None if x is None else x.encode()
+
+
+class OracleTopology:
+    """Mirror of topology.h's API over the oracle (addresses are network-order IPs)."""
+
+    def __init__(self, gml: str, use_shortest_path: bool = True):
+        self.h = lib.orc_topology_new(gml.encode(), 1 if use_shortest_path else 0)
+        if not self.h:
+            raise ValueError("invalid topology")
+
+    def close(self):
+        if self.h:
+            lib.orc_topology_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    @property
+    def V(self):
+        return lib.orc_topology_vertex_count(self.h)
+
+    @property
+    def directed(self):
+        return bool(lib.orc_topology_is_directed(self.h))
+
+    @property
+    def complete(self):
+        return bool(lib.orc_topology_is_complete(self.h))
+
+    def attach(self, ip, rng_state, ip_hint=None, city=None, country=None):
+        st = C.c_uint32(rng_state)
+        dn, up = C.c_uint64(0), C.c_uint64(0)
+        v = lib.orc_topology_attach(self.h, ip, C.byref(st), _s(ip_hint), _s(city), _s(country), C.byref(dn),
+                                    C.byref(up))
+        return v, st.value, dn.value, up.value
+
+    def detach(self, ip):
+        lib.orc_topology_detach(self.h, ip)
+
+    def latency(self, s, d):
+        return lib.orc_topology_get_latency(self.h, s, d)
+
+    def reliability(self, s, d):
+        return lib.orc_topology_get_reliability(self.h, s, d)
+
+    def routable(self, s, d):
+        return bool(lib.orc_topology_is_routable(self.h, s, d))
+
+    def increment(self, s, d):
+        lib.orc_topology_increment_path_packet_counter(self.h, s, d)
+
+    def packet_count(self, s, d):
+        return lib.orc_topology_path_packet_count(self.h, s, d)
+
+    def min_path_latency(self):
+        return lib.orc_topology_min_path_latency(self.h)
+
+    def min_jump_updates(self):
+        return lib.orc_topology_min_jump_updates(self.h)
+
+    def next_min_jump_ns(self):
+        return lib.orc_controller_next_min_jump_ns(self.h)
+
+    def vertex_of_ip(self, ip):
+        return lib.orc_vertex_of_ip(self.h, ip)
+
+    def row(self, src, targets):
+        targets = np.ascontiguousarray(targets, dtype=np.int32)
+        lat = np.empty(len(targets), dtype=np.float64)
+        rel = np.empty(len(targets), dtype=np.float64)
+        lib.orc_compute_row(self.h, int(src), targets.ctypes.data, len(targets), lat.ctypes.data, rel.ctypes.data)
+        return lat, rel
+
+    def direct(self, s, d):
+        lat, rel = C.c_double(), C.c_double()
+        rc = lib.orc_direct_path(self.h, s, d, C.byref(lat), C.byref(rel))
+        return (lat.value, rel.value) if rc == 0 else (None, None)
+
+    def preload(self, slots, lat, rel):
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        lat = np.ascontiguousarray(lat, dtype=np.float64)
+        rel = np.ascontiguousarray(rel, dtype=np.float64)
+        lib.orc_topology_preload_table(self.h, slots.ctypes.data, len(slots), lat.ctypes.data, rel.ctypes.data)
+
+    def round(self, host_ips, pkts, barrier, end_time, bootstrap_end=0):
+        from shadow_amd.synth import DELIV_DTYPE
+        host_ips = np.ascontiguousarray(host_ips, dtype=np.uint32)
+        pkts = np.ascontiguousarray(pkts)
+        n = len(pkts)
+        out = np.zeros(n, dtype=DELIV_DTYPE)
+        status = np.zeros(n, dtype=np.uint8)
+        mt = C.c_uint64(0)
+        k = lib.orc_round(self.h, host_ips.ctypes.data, len(host_ips), barrier, end_time, bootstrap_end,
+                          pkts.ctypes.data, n, out.ctypes.data, status.ctypes.data, C.byref(mt))
+        return out[:k], status, mt.value
+
+
+def parse_time_ns(s):
+    return lib.orc_parse_time_ns(s.encode())
+
+
+def parse_bandwidth_bits(s):
+    return lib.orc_parse_bandwidth_bits(s.encode())
+
+
+def rand_stream(seed, n, kind="double"):
+    st = C.c_uint32(seed)
+    f = {"double": lib.orc_next_double, "uint": lib.orc_next_uint, "rand": lib.orc_rand_r}[kind]
+    return [f(C.byref(st)) for _ in range(n)]
+
+
+def seed_chain(seed, nhosts):
+    st = C.c_uint32(seed)
+    m = lib.orc_next_uint(C.byref(st))
+    ms = C.c_uint32(m)
+    sched = lib.orc_next_uint(C.byref(ms))
+    hosts = [lib.orc_next_uint(C.byref(ms)) for _ in range(nhosts)]
+    return m, sched, hosts
+
+
+def pq_order(keys):
+    arr = np.zeros(len(keys), dtype=np.dtype([("time", "<u8"), ("dst", "<u4"), ("src", "<u4"), ("seq", "<u8")]))
+    for i, (t, d, s, q) in enumerate(keys):
+        arr[i] = (t, d, s, q)
+    order = np.zeros(len(keys), dtype=np.uint32)
+    lib.orc_pq_order(arr.ctypes.data, len(keys), order.ctypes.data)
+    return order.tolist()
