@@ -1,0 +1,184 @@
+/*
+ * shdnet.h -- C ABI of the MI355X-native Shadow network plane (libshdnet.so).
+ *
+ * Drop-in for two reference paths (citations into /root/reference/src/main):
+ *   1. routing/topology.h:17-28 -- topology_new/free/attach/detach/isRoutable/
+ *      getLatency/getReliability/incrementPathPacketCounter, including the
+ *      worker_updateMinTimeJump side effect (worker.h:89, topology.c:1253-1264).
+ *   2. the body of core/worker.c:517-576 worker_sendPacket + core/scheduler/
+ *      scheduler.c:232-255 scheduler_push + scheduler_policy_host_single.c:
+ *      174-220 push, batched per round: the CPU reserves the
+ *      sender's rand_r draw at send time and appends a record; at the round
+ *      boundary the GPU decides loss, computes delivery times, clamps to the
+ *      barrier and emits per-destination event segments ordered by
+ *      event_compare (core/work/event.c:109-152).
+ *
+ * Conventions: plain C types only; IPv4 addresses are network-order in_addr_t
+ * values (address_toNetworkIP); host ids are dense indices in registration
+ * order (the order of their GQuarks, manager.c:343), so comparing ids compares
+ * GQuarks; times are SimulationTime nanoseconds.  Every entry point returns an
+ * int status (0 or a negative errno) and never unwinds across the ABI; the
+ * topology_* compatibility values (-1 latency, FALSE routable) are produced by
+ * the wrappers shown in INTEGRATION.md.  There is no CPU compute fallback: if
+ * no gfx950 device is usable every compute entry point returns -ENODEV.
+ */
+#ifndef SHDNET_H
+#define SHDNET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHDNET_ABI_VERSION 1
+
+typedef struct ShdTopology ShdTopology;
+
+/* Called whenever the running minimum of released path latencies decreases;
+ * replaces worker_updateMinTimeJump(gdouble) (worker.c:624-626). */
+typedef void (*ShdMinJumpFn)(double min_latency_ms, void* user);
+
+/* ---------------------------------------------------------------------- */
+/* Routing (replaces routing/topology.h)                                   */
+/* ---------------------------------------------------------------------- */
+
+/* topology_new (topology.h:17, topology.c:2328-2354).  Reads and validates
+ * the GML graph at gml_path (igraph GML dialect, validation of
+ * topology.c:1040-1063) and extracts edge weights.  -EINVAL on an invalid
+ * graph (reference: error() + NULL), -ENOENT if the file cannot be read,
+ * -ENOTSUP for graphs with parallel edges (their igraph edge choice is
+ * unpinned).  device: HIP device ordinal used for all compute. */
+int shd_topology_new(const char* gml_path, int use_shortest_path, int device, ShdTopology** out);
+/* Same, from GML text in memory (the controller writes the text to a file
+ * only to hand it to igraph, controller.c:155-188). */
+int shd_topology_new_from_text(const char* gml_text, int use_shortest_path, int device, ShdTopology** out);
+/* topology_free (topology.h:18, topology.c:2283-2326) */
+void shd_topology_free(ShdTopology* top);
+
+/* topology_attach (topology.h:20-22, topology.c:2218-2272).  rng_state is
+ * the host's Random seedState (random.c:15-18); the reference's draw is
+ * consumed from it when the attach is random.  host_id registers the
+ * address's host for the packet path.  bw outputs in KiB/s, may be NULL.
+ * Attaching after the first path lookup returns -EBUSY (Shadow attaches
+ * every host before the simulation starts, controller.c:333-336). */
+int shd_topology_attach(ShdTopology* top, uint32_t host_id, uint32_t ip_net, uint32_t* rng_state,
+                        const char* ip_hint, const char* city_hint, const char* country_hint,
+                        uint64_t* bw_down_kibps, uint64_t* bw_up_kibps);
+/* topology_detach (topology.h:23, topology.c:2274-2281): removes the IP only. */
+int shd_topology_detach(ShdTopology* top, uint32_t ip_net);
+
+/* Computes every attached source row of the routing table on the GPU
+ * (igraph-exact Dijkstra per source) and keeps it
+ * resident in HBM.  Called implicitly by the first lookup if not called
+ * explicitly.  Rows are only *released* (cache side effects, min-jump) in
+ * the reference's lazy touch order, by the lookups below. */
+int shd_topology_build_routes(ShdTopology* top);
+
+/* topology_getLatency / getReliability / isRoutable /
+ * incrementPathPacketCounter (topology.h:25-28, topology.c:1983-2022).
+ * Status -ENOENT when an address is not attached (reference returns -1 /
+ * FALSE), -EHOSTUNREACH for an attached pair with no path (reference:
+ * utility_panic, topology.c:1970-1976). */
+int shd_topology_get_latency(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip, double* latency_ms);
+int shd_topology_get_reliability(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip, double* reliability);
+int shd_topology_is_routable(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip, int* routable);
+int shd_topology_increment_path_packet_counter(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip);
+int shd_topology_get_path_packet_count(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip, uint64_t* count);
+
+int shd_topology_set_min_jump_callback(ShdTopology* top, ShdMinJumpFn fn, void* user);
+/* Running min of released latencies (topology.c:48, 1253-1264); 0 if none. */
+int shd_topology_get_min_path_latency(ShdTopology* top, double* min_ms);
+
+/* Introspection for tests and tooling. */
+int shd_topology_info(ShdTopology* top, int* vertices, int* edges, int* directed, int* complete,
+                      int* attached_vertices);
+/* Vertex index a host id / ip is attached to (-1 if none). */
+int shd_topology_vertex_of_host(ShdTopology* top, uint32_t host_id, int* vertex);
+/* Copies the full device routing table (row-major over attached vertex
+ * slots, slots ordered by vertex index) to host memory: lat_ms/rel each
+ * hold slots*slots doubles; slot_vertex receives the slot->vertex map. */
+int shd_topology_copy_table(ShdTopology* top, double* lat_ms, double* rel, int32_t* slot_vertex, int cap_slots);
+/* Multi-GPU row sharding: number of table slots A, then
+ * compute rows [row_lo, row_hi) into a caller-owned device table of A*A
+ * 16-byte {lat_ms, rel} entries (e.g. a torch tensor that an RCCL
+ * all-gather completes), then adopt the completed table as the resident one
+ * (the caller keeps it alive for the topology's lifetime). */
+int shd_topology_slot_count(ShdTopology* top, int* slots);
+int shd_topology_build_rows_device(ShdTopology* top, int row_lo, int row_hi, void* d_table);
+int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
+/* Marks every attached vertex row touched, in slot order (steady state of a
+ * long simulation; used by benchmarks before timing). */
+int shd_topology_touch_all(ShdTopology* top);
+
+/* ---------------------------------------------------------------------- */
+/* Per-round packet hand-off (replaces worker_sendPacket + scheduler push) */
+/* ---------------------------------------------------------------------- */
+
+/* One send, recorded by the CPU at worker_sendPacket time (32 bytes). */
+typedef struct ShdPkt {
+    uint64_t now;         /* worker_getCurrentTime() */
+    uint64_t seq;         /* srcHostEventID (host_getNewEventID, host.c:368-371) */
+    uint32_t src_host;    /* host ids (dense, registration order) */
+    uint32_t dst_host;
+    uint32_t rng_state;   /* sender's Random seedState BEFORE the reserved draw */
+    uint32_t payload_len; /* packet_getPayloadLength(); 0 = control packet */
+} ShdPkt;
+
+/* One delivered event (32 bytes), ordered by event_compare. */
+typedef struct ShdDeliv {
+    uint64_t time; /* delivery time after the host-single barrier clamp */
+    uint64_t seq;
+    uint32_t src_host;
+    uint32_t dst_host;
+    uint32_t pkt_index; /* index of the record in the round's batch */
+    uint32_t pad;
+} ShdDeliv;
+
+/* Per-record outcome. */
+enum { SHD_DROPPED_LOSS = 0, SHD_DELIVERED = 1, SHD_DROPPED_END = 2 };
+
+/* Round parameters: barrier = current round end (scheduler.c:247),
+ * end_time = scheduler endTime (scheduler.c:236), bootstrap_end =
+ * bootstrap_end_time (worker.rs:339-341). */
+int shd_round_begin(ShdTopology* top, uint64_t barrier, uint64_t end_time, uint64_t bootstrap_end);
+/* Appends sends (host memory, copied).  Performs the reference's lookup side
+ * effects for each send in order (row touch, min-jump), exactly as the three
+ * topology_* calls of worker_sendPacket would.  Thread-compatible: callers
+ * serialise appends (one producer per round, as manager_run's boundary). */
+int shd_round_append(ShdTopology* top, const ShdPkt* recs, size_t n);
+/* Runs the batch on the GPU and returns delivered events grouped by
+ * destination host: out[dst_offsets[h] .. dst_offsets[h+1]) is host h's
+ * events in event_compare order (dst_offsets has nhosts+1 entries, may be
+ * NULL).  status (may be NULL) receives one outcome per appended record.
+ * min_time: minimum delivered time >= barrier (worker.c:350-363),
+ * UINT64_MAX if none. */
+int shd_round_collect(ShdTopology* top, ShdDeliv* out, size_t cap, size_t* n_out, uint32_t* dst_offsets,
+                      uint8_t* status, uint64_t* min_time);
+
+/* Device-resident variant (inputs already in HBM; used by benchmarks and the
+ * multi-GPU exchange).  All pointers are device pointers; stream is a
+ * hipStream_t (NULL = default stream).  Lookup side effects are NOT applied:
+ * rows must have been touched (shd_round_append or shd_topology_touch_all).
+ * out needs n entries, dst_offsets nhosts+1, status n; counters[0] =
+ * delivered count, counters[1] = min delivered time (both written async). */
+int shd_round_process_device(ShdTopology* top, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                             uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out,
+                             uint32_t* d_dst_offsets, uint8_t* d_status, uint64_t* d_counters, void* stream);
+/* Number of registered hosts (dst_offsets needs this + 1 entries). */
+int shd_topology_host_count(ShdTopology* top, uint32_t* nhosts);
+
+/* Regroups already-decided delivered events (e.g. after a multi-GPU
+ * all-to-all) into event_compare order per destination host in
+ * [host_lo, host_hi).  Device pointers. */
+int shd_deliv_sort_device(ShdTopology* top, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi,
+                          ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream);
+
+/* Last error message for this thread (static storage). */
+const char* shd_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -820,7 +820,14 @@ int orc_topology_attach(OrcTopo* t, uint32_t ip_net, uint32_t* rng_state, const 
             requested = ip;
         }
     }
-    /* _topology_findAttachmentVertexHelperHook over all vertices (:2024-2100) */
+    /* _topology_findAttachmentVertexHelperHook over all vertices (:2024-2100);
+     * without any hint every vertex lands in candidatesAll in order and no
+     * LPM applies, so the scan is skipped (same choice, O(1)). */
+    if (!ip_hint && !city_hint && !country_hint) {
+        for (int v = 0; v < V; v++) all.v[v] = v;
+        all.n = V;
+        V = 0;
+    }
     for (int v = 0; v < V; v++) {
         const char* ipStr = vas(t, "ip_address", v);
         const char* cc = vas(t, "city_code", v);

@@ -1,0 +1,86 @@
+"""Loader for libshdnet.so (the in-tree HIP/C build) with ctypes prototypes.
+
+There is deliberately no fallback: if the shared library is missing or no
+gfx950 device is usable, the calls raise.  Build with ``python
+__graft_entry__.py`` or ``make -C shadow_amd/csrc``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libshdnet.so")
+
+
+class ShdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{errno.errorcode.get(-code, code)} ({code}): {msg}")
+        self.code = code
+
+
+_lib = None
+
+MINJUMP_FN = C.CFUNCTYPE(None, C.c_double, C.c_void_p)
+
+_P = C.c_void_p
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int)
+
+PROTOS = {
+    "shd_topology_new": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(_P)]),
+    "shd_topology_new_from_text": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(_P)]),
+    "shd_topology_free": (None, [_P]),
+    "shd_topology_attach": (C.c_int, [_P, C.c_uint32, C.c_uint32, _u32p, C.c_char_p, C.c_char_p, C.c_char_p,
+                                      _u64p, _u64p]),
+    "shd_topology_detach": (C.c_int, [_P, C.c_uint32]),
+    "shd_topology_build_routes": (C.c_int, [_P]),
+    "shd_topology_get_latency": (C.c_int, [_P, C.c_uint32, C.c_uint32, _dp]),
+    "shd_topology_get_reliability": (C.c_int, [_P, C.c_uint32, C.c_uint32, _dp]),
+    "shd_topology_is_routable": (C.c_int, [_P, C.c_uint32, C.c_uint32, _ip]),
+    "shd_topology_increment_path_packet_counter": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    "shd_topology_get_path_packet_count": (C.c_int, [_P, C.c_uint32, C.c_uint32, _u64p]),
+    "shd_topology_set_min_jump_callback": (C.c_int, [_P, MINJUMP_FN, _P]),
+    "shd_topology_get_min_path_latency": (C.c_int, [_P, _dp]),
+    "shd_topology_info": (C.c_int, [_P, _ip, _ip, _ip, _ip, _ip]),
+    "shd_topology_vertex_of_host": (C.c_int, [_P, C.c_uint32, _ip]),
+    "shd_topology_copy_table": (C.c_int, [_P, _P, _P, _P, C.c_int]),
+    "shd_topology_slot_count": (C.c_int, [_P, _ip]),
+    "shd_topology_build_rows_device": (C.c_int, [_P, C.c_int, C.c_int, _P]),
+    "shd_topology_adopt_table_device": (C.c_int, [_P, _P]),
+    "shd_topology_touch_all": (C.c_int, [_P]),
+    "shd_topology_host_count": (C.c_int, [_P, _u32p]),
+    "shd_round_begin": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "shd_round_append": (C.c_int, [_P, _P, C.c_size_t]),
+    "shd_round_collect": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_size_t), _P, _P, _u64p]),
+    "shd_round_process_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint64, _P, _P, _P, _P,
+                                           _P]),
+    "shd_deliv_sort_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "shd_last_error": (C.c_char_p, []),
+}
+
+
+def lib():
+    """The loaded library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python __graft_entry__.py` "
+                              "(no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = lib().shd_last_error()
+        raise ShdError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,50 @@
+// dev.hip -- device runtime helpers behind the C ABI (HIP runtime calls
+// only; kernels live in routing.hip and packet.hip).  gfx950 only: the
+// library refuses to run on anything else rather than silently degrading.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstring>
+
+#include "shd_internal.h"
+
+static int hip_err(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+extern "C" int shd_dev_init(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return shd_fail(-ENODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return shd_fail(-ENODEV, "device %d out of range (%d visible)", device, n);
+    static thread_local int checked = -1;
+    if (checked != device) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, device) != hipSuccess) return shd_fail(-ENODEV, "device query failed");
+        if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)
+            return shd_fail(-ENODEV, "device %d is %s, libshdnet is built for gfx950 only", device, p.gcnArchName);
+        checked = device;
+    }
+    return hip_err(hipSetDevice(device), "hipSetDevice");
+}
+
+extern "C" int shd_dev_malloc(void** p, size_t bytes) {
+    *p = nullptr;
+    return hip_err(hipMalloc(p, bytes ? bytes : 4), "hipMalloc");
+}
+
+extern "C" int shd_dev_free(void* p) { return p ? hip_err(hipFree(p), "hipFree") : 0; }
+
+extern "C" int shd_dev_h2d(void* d, const void* h, size_t bytes) {
+    return bytes ? hip_err(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D") : 0;
+}
+
+extern "C" int shd_dev_d2h(void* h, const void* d, size_t bytes) {
+    return bytes ? hip_err(hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H") : 0;
+}
+
+extern "C" int shd_dev_memset(void* d, int v, size_t bytes) {
+    return bytes ? hip_err(hipMemset(d, v, bytes), "hipMemset") : 0;
+}
+
+extern "C" int shd_dev_sync(void) { return hip_err(hipDeviceSynchronize(), "hipDeviceSynchronize"); }

@@ -1,0 +1,207 @@
+/*
+ * routes.c -- building and holding the routing table in HBM.
+ *
+ * Layout: slots = attached vertices in ascending vertex index; the table is
+ * a row-major A x A array of 16-byte {lat_ms, rel} entries, row = source
+ * slot.  Row s, column d holds exactly what
+ * _topology_computeSourcePaths (topology.c:1578-1814) would store for (s,d)
+ * (self path for s == d, topology.c:1431-1576), or the direct edge for
+ * use_shortest_path = false (topology.c:1816-1858).  A host mirror is kept
+ * for the CPU-side lookups of the drop-in API.
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "topology_impl.h"
+
+void shd_topology_release_device(ShdTopology* t) {
+    if (t->d_tab && t->d_tab_owned) shd_dev_free(t->d_tab);
+    shd_dev_free(t->d_inc_off);
+    shd_dev_free(t->d_inc_nbr);
+    shd_dev_free(t->d_inc_w);
+    shd_dev_free(t->d_inc_r);
+    shd_dev_free(t->d_slot_vertex);
+    shd_dev_free(t->d_vertex_slot);
+    shd_dev_free(t->d_host_slot);
+    shd_dev_free(t->d_touch);
+    shd_dev_free(t->d_pair_bits);
+    t->d_tab = NULL;
+    t->d_inc_off = t->d_inc_nbr = t->d_slot_vertex = t->d_vertex_slot = t->d_host_slot = NULL;
+    t->d_inc_w = t->d_inc_r = NULL;
+    t->d_touch = t->d_pair_bits = NULL;
+}
+
+#define UPLOAD(dst, src, bytes)                                   \
+    do {                                                          \
+        rc = shd_dev_malloc((void**)&(dst), ((bytes) != 0) ? (bytes) : 4); \
+        if (!rc && ((bytes) != 0)) rc = shd_dev_h2d((dst), (src), (bytes)); \
+        if (rc) goto fail;                                        \
+    } while (0)
+
+/* Slots, device CSR and host->slot map.  Idempotent until an attach. */
+static int prepare(ShdTopology* t) {
+    if (t->prepared && !t->routes_stale) return 0;
+    int rc = shd_dev_init(t->device);
+    if (rc) return rc;
+    shd_topology_release_device(t);
+    free(t->slot_vertex);
+    free(t->vertex_slot);
+    t->A = 0;
+    t->slot_vertex = (int32_t*)malloc(sizeof(int32_t) * ((size_t)t->V + 1));
+    t->vertex_slot = (int32_t*)malloc(sizeof(int32_t) * ((size_t)t->V + 1));
+    for (int v = 0; v < t->V; v++) {
+        t->vertex_slot[v] = t->v_attached[v] ? t->A : -1;
+        if (t->v_attached[v]) t->slot_vertex[t->A++] = v;
+    }
+    if (t->A == 0) return shd_fail(-EINVAL, "no host is attached");
+    size_t M = (size_t)t->M;
+    double* w = (double*)malloc(sizeof(double) * (M + 1));
+    double* r = (double*)malloc(sizeof(double) * (M + 1));
+    int32_t* hs = (int32_t*)malloc(sizeof(int32_t) * ((size_t)t->nhosts + 1));
+    for (size_t k = 0; k < M; k++) {
+        w[k] = t->e_ms[t->inc_eid[k]];
+        r[k] = t->e_rel[t->inc_eid[k]];
+    }
+    for (uint32_t h = 0; h < t->nhosts; h++) hs[h] = t->host_vertex[h] >= 0 ? t->vertex_slot[t->host_vertex[h]] : -1;
+    UPLOAD(t->d_inc_off, t->inc_off, sizeof(int32_t) * ((size_t)t->V + 1));
+    UPLOAD(t->d_inc_nbr, t->inc_nbr, sizeof(int32_t) * M);
+    UPLOAD(t->d_inc_w, w, sizeof(double) * M);
+    UPLOAD(t->d_inc_r, r, sizeof(double) * M);
+    UPLOAD(t->d_slot_vertex, t->slot_vertex, sizeof(int32_t) * (size_t)t->A);
+    UPLOAD(t->d_vertex_slot, t->vertex_slot, sizeof(int32_t) * (size_t)t->V);
+    UPLOAD(t->d_host_slot, hs, sizeof(int32_t) * (size_t)t->nhosts);
+    free(w);
+    free(r);
+    free(hs);
+    /* release state */
+    free(t->touch);
+    free(t->self_released);
+    free(t->pair_bits);
+    t->touch = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)t->A);
+    memset(t->touch, 0xff, sizeof(uint32_t) * (size_t)t->A);
+    t->self_released = (uint8_t*)calloc((size_t)t->A, 1);
+    size_t nbits = (size_t)t->A * (size_t)t->A;
+    t->pair_bits = t->use_sp ? NULL : (uint32_t*)calloc((nbits + 31) / 32, sizeof(uint32_t));
+    t->next_touch = 0;
+    rc = shd_dev_malloc((void**)&t->d_touch, sizeof(uint32_t) * (size_t)t->A);
+    if (!rc && !t->use_sp && t->directed) rc = shd_dev_malloc((void**)&t->d_pair_bits, ((nbits + 31) / 32) * 4);
+    if (rc) goto fail_nofree;
+    t->touch_dirty = 1;
+    t->prepared = 1;
+    t->built = 0;
+    t->routes_stale = 0;
+    return 0;
+fail:
+    free(w);
+    free(r);
+    free(hs);
+fail_nofree:
+    shd_topology_release_device(t);
+    return rc;
+}
+
+static ShdGraphDev graph_dev(const ShdTopology* t) {
+    ShdGraphDev g;
+    g.V = t->V;
+    g.A = t->A;
+    g.M = t->M;
+    g.directed = t->directed;
+    g.inc_off = t->d_inc_off;
+    g.inc_nbr = t->d_inc_nbr;
+    g.inc_w = t->d_inc_w;
+    g.inc_r = t->d_inc_r;
+    g.slot_vertex = t->d_slot_vertex;
+    g.vertex_slot = t->d_vertex_slot;
+    return g;
+}
+
+static int adopt(ShdTopology* t, ShdEntry* d_tab, int owned) {
+    size_t n = (size_t)t->A * (size_t)t->A;
+    free(t->h_tab);
+    t->h_tab = (ShdEntry*)malloc(sizeof(ShdEntry) * n);
+    if (!t->h_tab) return -ENOMEM;
+    int rc = shd_dev_d2h(t->h_tab, d_tab, sizeof(ShdEntry) * n);
+    if (rc) return rc;
+    if (t->d_tab && t->d_tab_owned && t->d_tab != d_tab) shd_dev_free(t->d_tab);
+    t->d_tab = d_tab;
+    t->d_tab_owned = owned;
+    t->built = 1;
+    return 0;
+}
+
+int shd_topology_build_routes(ShdTopology* t) {
+    if (!t) return -EINVAL;
+    if (t->built && !t->routes_stale) return 0;
+    int rc = prepare(t);
+    if (rc) return rc;
+    ShdEntry* d_tab = NULL;
+    rc = shd_dev_malloc((void**)&d_tab, sizeof(ShdEntry) * (size_t)t->A * (size_t)t->A);
+    if (rc) return rc;
+    ShdGraphDev g = graph_dev(t);
+    rc = shd_dev_build_rows(&g, t->use_sp, 0, t->A, d_tab);
+    if (!rc) rc = adopt(t, d_tab, 1);
+    if (rc) shd_dev_free(d_tab);
+    return rc;
+}
+
+int shd_topology_slot_count(ShdTopology* t, int* A) {
+    if (!t || !A) return -EINVAL;
+    int rc = prepare(t);
+    if (rc) return rc;
+    *A = t->A;
+    return 0;
+}
+
+int shd_topology_build_rows_device(ShdTopology* t, int row_lo, int row_hi, void* d_table) {
+    if (!t || !d_table) return -EINVAL;
+    int rc = prepare(t);
+    if (rc) return rc;
+    if (row_lo < 0 || row_hi > t->A || row_lo > row_hi) return shd_fail(-EINVAL, "row range out of bounds");
+    ShdGraphDev g = graph_dev(t);
+    return shd_dev_build_rows(&g, t->use_sp, row_lo, row_hi, (ShdEntry*)d_table);
+}
+
+int shd_topology_adopt_table_device(ShdTopology* t, void* d_table) {
+    if (!t || !d_table) return -EINVAL;
+    int rc = prepare(t);
+    if (rc) return rc;
+    return adopt(t, (ShdEntry*)d_table, 0);
+}
+
+int shd_topology_copy_table(ShdTopology* t, double* lat, double* rel, int32_t* slot_vertex, int cap) {
+    if (!t) return -EINVAL;
+    int rc = shd_topology_build_routes(t);
+    if (rc) return rc;
+    if (cap < t->A) return shd_fail(-ENOSPC, "need %d slots", t->A);
+    size_t n = (size_t)t->A * (size_t)t->A;
+    for (size_t k = 0; k < n; k++) {
+        if (lat) lat[k] = t->h_tab[k].lat;
+        if (rel) rel[k] = t->h_tab[k].rel;
+    }
+    if (slot_vertex) memcpy(slot_vertex, t->slot_vertex, sizeof(int32_t) * (size_t)t->A);
+    return 0;
+}
+
+/* Uploads the release state the packet kernel reads (touch order or pair
+ * bits) if it changed since the last upload. */
+int shd_sync_touch(ShdTopology* t) {
+    if (!t->touch_dirty) return 0;
+    int rc = shd_dev_h2d(t->d_touch, t->touch, sizeof(uint32_t) * (size_t)t->A);
+    if (!rc && t->d_pair_bits) {
+        size_t nbits = (size_t)t->A * (size_t)t->A;
+        rc = shd_dev_h2d(t->d_pair_bits, t->pair_bits, ((nbits + 31) / 32) * 4);
+    }
+    if (!rc) t->touch_dirty = 0;
+    return rc;
+}
+
+void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
+    c->tab = t->d_tab;
+    c->A = t->A;
+    c->mode = t->use_sp ? 0 : (t->directed ? 2 : 1);
+    c->touch = t->d_touch;
+    c->pair_bits = t->d_pair_bits;
+    c->host_slot = t->d_host_slot;
+    c->nhosts = t->nhosts;
+}

@@ -1,0 +1,106 @@
+/*
+ * shd_internal.h -- internal interfaces of libshdnet (host C side and the
+ * thin C-ABI to the HIP kernels).  Not installed; see include/shdnet.h.
+ */
+#ifndef SHD_INTERNAL_H
+#define SHD_INTERNAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "shdnet.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error reporting ---- */
+int shd_fail(int code, const char* fmt, ...);
+
+/* ---- units (core/support/units.rs restated) ---- */
+int64_t shd_units_time_ns(const char* s);
+int64_t shd_units_bandwidth_bits(const char* s);
+
+/* ---- GML document (igraph_read_graph_gml dialect) ---- */
+enum { GML_INT = 1, GML_REAL = 2, GML_STR = 3 };
+
+typedef struct {
+    const char* key;
+    int type;
+    long long ival;
+    double rval;
+    const char* sval;
+} GmlKV;
+
+typedef struct {
+    int first, count; /* range in kvs[] */
+} GmlBlock;
+
+typedef struct {
+    char* buf; /* private, NUL-split copy of the text */
+    int directed;
+    GmlKV* kvs;
+    size_t nkv, capkv;
+    GmlBlock* nodes;
+    int nnodes, capnodes;
+    GmlBlock* edges;
+    int nedges, capedges;
+} GmlDoc;
+
+int shd_gml_parse(const char* text, GmlDoc* doc);
+void shd_gml_free(GmlDoc* doc);
+
+/* ---- device graph + launches (implemented in HIP, C ABI) ---- */
+typedef struct {
+    int V;       /* vertices */
+    int A;       /* attached vertices (= table slots) */
+    int M;       /* incidence entries */
+    int directed;
+    const int32_t* inc_off; /* V+1, igraph_incident(mode OUT) order */
+    const int32_t* inc_nbr; /* M */
+    const double* inc_w;    /* M, edge latency in ms */
+    const double* inc_r;    /* M, 1 - packet_loss */
+    const int32_t* slot_vertex; /* A */
+    const int32_t* vertex_slot; /* V, -1 = not attached */
+} ShdGraphDev;
+
+typedef struct {
+    double lat;
+    double rel;
+} ShdEntry; /* 16 B table entry, row-major A x A */
+
+int shd_dev_init(int device);
+int shd_dev_malloc(void** p, size_t bytes);
+int shd_dev_free(void* p);
+int shd_dev_h2d(void* d, const void* h, size_t bytes);
+int shd_dev_d2h(void* h, const void* d, size_t bytes);
+int shd_dev_memset(void* d, int v, size_t bytes);
+int shd_dev_sync(void);
+
+/* Routing rows [row_lo, row_hi) of the A x A table (tab already sized A*A
+ * on device; rows outside the range are not written).
+ * use_sp = 1: igraph-exact Dijkstra per source slot + self path (R-7, R-9);
+ * use_sp = 0: direct edge per pair (R-10).  Synchronous. */
+int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab);
+
+/* Packet round on device arrays (see shd_round_process_device). */
+typedef struct {
+    const ShdEntry* tab;      /* A x A */
+    int A;
+    int mode;                 /* 0 = owner by touch order, 1 = direct symmetric, 2 = direct + pair bits */
+    const uint32_t* touch;    /* A, touch sequence (UINT32_MAX = never) */
+    const uint32_t* pair_bits; /* A*A bits, mode 2 */
+    const int32_t* host_slot; /* nhosts -> slot */
+    uint32_t nhosts;
+} ShdPktCtx;
+
+int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                         uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets,
+                         uint8_t* d_status, uint64_t* d_counters, void* stream);
+int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
+                       uint32_t* d_dst_offsets, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,83 @@
+/* topology_impl.h -- the ShdTopology object shared by topology.c, routes.c
+ * and round.c (host C side of libshdnet). */
+#ifndef SHD_TOPOLOGY_IMPL_H
+#define SHD_TOPOLOGY_IMPL_H
+
+#include "shd_internal.h"
+
+#define SHD_UNTOUCHED 0xffffffffu
+
+typedef struct {
+    uint32_t ip;
+    int32_t vertex;
+    uint8_t used; /* 0 empty, 1 live, 2 tombstone */
+} IpSlot;
+
+typedef struct {
+    IpSlot* slots;
+    uint32_t cap, n, tomb;
+} IpMap;
+
+struct ShdTopology {
+    int device;
+    int use_sp;
+    int directed, complete;
+    int V, E, M;
+    GmlDoc doc; /* owns every attribute string */
+    int32_t *efrom, *eto; /* igraph storage order (undirected: from=max, to=min) */
+    double* e_ms;         /* edge latency, ms = ns / 1e6 (topology.c:294) */
+    double* e_rel;        /* 1 - packet_loss (topology.c:396) */
+    int32_t *inc_off, *inc_nbr, *inc_eid; /* igraph_incident(OUT) CSR */
+    const char **v_ip, **v_city, **v_country;
+    int64_t *v_bw_down, *v_bw_up; /* KiB/s */
+
+    /* attachment */
+    IpMap ipmap;
+    uint8_t* v_attached;
+    int32_t* host_vertex; /* host id -> vertex */
+    uint32_t* host_ip;
+    uint32_t nhosts, host_cap;
+    int lookups_started;
+    int routes_stale;
+
+    /* routing table: slots = attached vertices in ascending vertex order */
+    int A;
+    int32_t* slot_vertex;
+    int32_t* vertex_slot;
+    ShdEntry* h_tab; /* host mirror of the device table */
+    int built, prepared;
+    int d_tab_owned;
+
+    /* device state */
+    ShdEntry* d_tab;
+    int32_t *d_inc_off, *d_inc_nbr, *d_slot_vertex, *d_vertex_slot, *d_host_slot;
+    double *d_inc_w, *d_inc_r;
+    uint32_t *d_touch, *d_pair_bits;
+
+    /* release (cache) state */
+    uint32_t* touch; /* per slot, SHD_UNTOUCHED or touch sequence */
+    uint32_t next_touch;
+    uint8_t* self_released;
+    uint32_t* pair_bits; /* use_shortest_path = 0: (i,j) stored, A*A bits */
+    int touch_dirty;
+    double min_lat;
+    ShdMinJumpFn cb;
+    void* cb_user;
+
+    /* path packet counters keyed by the answering (owner) pair */
+    uint64_t *pkt_keys, *pkt_vals;
+    uint64_t pkt_cap, pkt_n;
+
+    /* round staging (host API) */
+    uint64_t barrier, end_time, bootstrap_end;
+    ShdPkt* staged;
+    size_t nstaged, capstaged;
+};
+
+void shd_topology_release_device(ShdTopology* t);
+int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj);
+int shd_count_packet(ShdTopology* t, int oi, int oj, uint64_t inc);
+int shd_sync_touch(ShdTopology* t);
+void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c);
+
+#endif

@@ -1,0 +1,165 @@
+"""Python mirror of Shadow's routing API (routing/topology.h:17-28) over libshdnet.
+
+Mirrors the reference's operator interface for this path so that tests read
+like the reference's call sites: ``Topology(gml, use_shortest_path)`` is
+topology_new, ``attach`` is topology_attach, ``get_latency`` /
+``get_reliability`` / ``is_routable`` / ``increment_path_packet_counter`` are
+the lookups with their cache side effects, and the min-jump callback replaces
+worker_updateMinTimeJump.  All compute runs on the GPU (HIP, gfx950).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import MINJUMP_FN, ShdError, check, lib
+from .synth import DELIV_DTYPE, PKT_DTYPE
+
+__all__ = ["Topology", "ShdError"]
+
+
+def _s(x):
+    return None if x is None else x.encode()
+
+
+class Topology:
+    def __init__(self, gml: str, use_shortest_path: bool = True, device: int = 0, from_file: bool = False):
+        h = C.c_void_p()
+        fn = lib().shd_topology_new if from_file else lib().shd_topology_new_from_text
+        check(fn(gml.encode(), 1 if use_shortest_path else 0, device, C.byref(h)))
+        self._h = h
+        self._cb = None
+        self.min_jump_calls: list[float] = []
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().shd_topology_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self):
+        v, e, d, c, a = (C.c_int() for _ in range(5))
+        check(lib().shd_topology_info(self._h, C.byref(v), C.byref(e), C.byref(d), C.byref(c), C.byref(a)))
+        return {"vertices": v.value, "edges": e.value, "directed": bool(d.value), "complete": bool(c.value),
+                "attached_vertices": a.value}
+
+    # -- topology_attach / detach -------------------------------------------------
+    def attach(self, host_id: int, ip: int, rng_state: int, ip_hint=None, city=None, country=None):
+        """Returns (vertex, new_rng_state, bw_down_KiBps, bw_up_KiBps)."""
+        st = C.c_uint32(rng_state)
+        dn, up = C.c_uint64(), C.c_uint64()
+        check(lib().shd_topology_attach(self._h, host_id, ip, C.byref(st), _s(ip_hint), _s(city), _s(country),
+                                        C.byref(dn), C.byref(up)))
+        v = C.c_int()
+        check(lib().shd_topology_vertex_of_host(self._h, host_id, C.byref(v)))
+        return v.value, st.value, dn.value, up.value
+
+    def detach(self, ip: int):
+        check(lib().shd_topology_detach(self._h, ip))
+
+    # -- routing table ------------------------------------------------------------
+    def build_routes(self):
+        check(lib().shd_topology_build_routes(self._h))
+
+    def slot_count(self) -> int:
+        a = C.c_int()
+        check(lib().shd_topology_slot_count(self._h, C.byref(a)))
+        return a.value
+
+    def table(self):
+        """(lat_ms[A,A], rel[A,A], slot_vertex[A]) copied from the device table."""
+        A = self.slot_count()
+        lat = np.empty((A, A), dtype=np.float64)
+        rel = np.empty((A, A), dtype=np.float64)
+        sv = np.empty(A, dtype=np.int32)
+        check(lib().shd_topology_copy_table(self._h, lat.ctypes.data, rel.ctypes.data, sv.ctypes.data, A))
+        return lat, rel, sv
+
+    def build_rows_device(self, row_lo: int, row_hi: int, d_table_ptr: int):
+        check(lib().shd_topology_build_rows_device(self._h, row_lo, row_hi, C.c_void_p(d_table_ptr)))
+
+    def adopt_table_device(self, d_table_ptr: int):
+        check(lib().shd_topology_adopt_table_device(self._h, C.c_void_p(d_table_ptr)))
+
+    def touch_all(self):
+        check(lib().shd_topology_touch_all(self._h))
+
+    # -- lookups (topology_getLatency & co, with the cache side effects) -----------
+    def get_latency(self, src_ip: int, dst_ip: int) -> float:
+        out = C.c_double()
+        check(lib().shd_topology_get_latency(self._h, src_ip, dst_ip, C.byref(out)))
+        return out.value
+
+    def get_reliability(self, src_ip: int, dst_ip: int) -> float:
+        out = C.c_double()
+        check(lib().shd_topology_get_reliability(self._h, src_ip, dst_ip, C.byref(out)))
+        return out.value
+
+    def is_routable(self, src_ip: int, dst_ip: int) -> bool:
+        out = C.c_int()
+        check(lib().shd_topology_is_routable(self._h, src_ip, dst_ip, C.byref(out)))
+        return bool(out.value)
+
+    def increment_path_packet_counter(self, src_ip: int, dst_ip: int):
+        check(lib().shd_topology_increment_path_packet_counter(self._h, src_ip, dst_ip))
+
+    def path_packet_count(self, src_ip: int, dst_ip: int) -> int:
+        out = C.c_uint64()
+        check(lib().shd_topology_get_path_packet_count(self._h, src_ip, dst_ip, C.byref(out)))
+        return out.value
+
+    def min_path_latency(self) -> float:
+        out = C.c_double()
+        check(lib().shd_topology_get_min_path_latency(self._h, C.byref(out)))
+        return out.value
+
+    def record_min_jump(self):
+        """Records every worker_updateMinTimeJump value into self.min_jump_calls."""
+        def cb(ms, _user):
+            self.min_jump_calls.append(ms)
+        self._cb = MINJUMP_FN(cb)
+        check(lib().shd_topology_set_min_jump_callback(self._h, self._cb, None))
+
+    def host_count(self) -> int:
+        n = C.c_uint32()
+        check(lib().shd_topology_host_count(self._h, C.byref(n)))
+        return n.value
+
+    # -- per-round packet hand-off -------------------------------------------------
+    def round(self, pkts: np.ndarray, barrier: int, end_time: int, bootstrap_end: int = 0):
+        """Host API: begin + append (lookup side effects) + collect.
+        Returns (delivered events, dst_offsets, status, min_time)."""
+        pkts = np.ascontiguousarray(pkts, dtype=PKT_DTYPE)
+        n = len(pkts)
+        check(lib().shd_round_begin(self._h, barrier, end_time, bootstrap_end))
+        check(lib().shd_round_append(self._h, pkts.ctypes.data, n))
+        out = np.zeros(max(n, 1), dtype=DELIV_DTYPE)
+        H = self.host_count()
+        offs = np.zeros(H + 1, dtype=np.uint32)
+        status = np.zeros(max(n, 1), dtype=np.uint8)
+        nout = C.c_size_t()
+        mt = C.c_uint64()
+        check(lib().shd_round_collect(self._h, out.ctypes.data, len(out), C.byref(nout), offs.ctypes.data,
+                                      status.ctypes.data, C.byref(mt)))
+        return out[:nout.value], offs, status[:n], mt.value
+
+    def process_device(self, d_recs: int, n: int, barrier: int, end_time: int, bootstrap_end: int, d_out: int,
+                       d_offsets: int, d_status: int, d_counters: int, stream: int = 0):
+        check(lib().shd_round_process_device(self._h, C.c_void_p(d_recs), n, barrier, end_time, bootstrap_end,
+                                             C.c_void_p(d_out), C.c_void_p(d_offsets), C.c_void_p(d_status),
+                                             C.c_void_p(d_counters), C.c_void_p(stream)))
+
+    def deliv_sort_device(self, d_in: int, n: int, host_lo: int, host_hi: int, d_out: int, d_offsets: int,
+                          stream: int = 0):
+        check(lib().shd_deliv_sort_device(self._h, C.c_void_p(d_in), n, host_lo, host_hi, C.c_void_p(d_out),
+                                          C.c_void_p(d_offsets), C.c_void_p(stream)))

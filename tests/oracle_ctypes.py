@@ -102,7 +102,9 @@ class OracleTopology:
     def complete(self):
         return bool(lib.orc_topology_is_complete(self.h))
 
-    def attach(self, ip, rng_state, ip_hint=None, city=None, country=None):
+    def attach(self, host_id, ip, rng_state, ip_hint=None, city=None, country=None):
+        """Same signature as shadow_amd.Topology.attach (host_id is unused:
+        the reference keys hosts by IP)."""
         st = C.c_uint32(rng_state)
         dn, up = C.c_uint64(0), C.c_uint64(0)
         v = lib.orc_topology_attach(self.h, ip, C.byref(st), _s(ip_hint), _s(city), _s(country), C.byref(dn),

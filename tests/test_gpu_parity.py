@@ -1,0 +1,231 @@
+"""GPU parity: libshdnet (HIP, gfx950) against the CPU oracle, through the C ABI.
+
+Bar: bit-exact for latencies, reliabilities (the oracle reproduces igraph's
+tie-breaking, so products along the same path are bitwise equal; north_star's
+1e-12 relative tolerance is therefore met with margin 0), delivery status,
+delivery times, per-destination order and the min delivered time.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+from shadow_amd import Topology, scenario, synth
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-12  # north_star tolerance for reliability products (we assert bitwise)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, dtype=np.float64).view(np.uint64)
+
+
+def make_pair(gml, H, use_sp=True, seed=1):
+    top = Topology(gml, use_shortest_path=use_sp)
+    ips, st, verts = scenario.register_hosts(top, H, seed)
+    orc = O.OracleTopology(gml, use_sp)
+    ips2, st2, verts2 = scenario.register_hosts(orc, H, seed)
+    assert (verts == verts2).all() and (st == st2).all()
+    return top, orc, ips, st
+
+
+GRAPHS = {
+    "1_gbit_switch": (synth.ONE_GBIT_SWITCH_GML, 4),
+    "complete30_ms": (synth.complete_graph_gml(30, 0x5EED0001), 90),
+    "complete40_ns": (synth.complete_graph_gml(40, 0x5EED0011, ns_variant=True), 120),
+    "complete25_dir": (synth.complete_graph_gml(25, 0x5EED0031, directed=True), 80),
+    "sparse300_ms": (synth.sparse_graph_gml(300, 0x5EED0002), 400),
+    "sparse300_ns": (synth.sparse_graph_gml(300, 0x5EED0012, ns_variant=True), 400),
+    "sparse200_dir_ns": (synth.sparse_graph_gml(200, 0x5EED0022, ns_variant=True, directed=True), 300),
+    "sparse5000_hbm": (synth.sparse_graph_gml(5000, 0x5EED0042), 200),  # V > 4096: HBM-slab kernel
+}
+
+
+@pytest.mark.parametrize("name", list(GRAPHS))
+def test_routing_table_bit_exact(name):
+    gml, H = GRAPHS[name]
+    top, orc, _, _ = make_pair(gml, H)
+    lat, rel, sv = top.table()
+    for i, s in enumerate(sv):
+        ol, orl = orc.row(int(s), sv)
+        assert np.array_equal(bits(lat[i]), bits(ol)), (name, i)
+        assert np.array_equal(bits(rel[i]), bits(orl)), (name, i)
+        nz = orl != 0
+        assert np.all(np.abs(rel[i][nz] - orl[nz]) <= REL_TOL * np.abs(orl[nz]))
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_direct_paths_bit_exact(directed):
+    gml = synth.complete_graph_gml(20, 0x5EED0051, directed=directed)
+    top, orc, _, _ = make_pair(gml, 60, use_sp=False)
+    lat, rel, sv = top.table()
+    for i, s in enumerate(sv):
+        for j, d in enumerate(sv):
+            ol, orl = orc.direct(int(s), int(d))
+            assert bits(lat[i, j]) == bits(ol) and bits(rel[i, j]) == bits(orl)
+
+
+@pytest.mark.parametrize("name,use_sp", [("complete30_ms", True), ("sparse300_ns", True),
+                                         ("sparse200_dir_ns", True), ("complete25_dir", True),
+                                         ("complete25_dir", False)])
+def test_lookup_side_effects_match_reference(name, use_sp):
+    """Random lookup sequences: values, the lazy touch/direction quirk and the
+    running min that feeds worker_updateMinTimeJump."""
+    gml, H = GRAPHS[name]
+    top, orc, ips, _ = make_pair(gml, H, use_sp)
+    rng = np.random.default_rng(7)
+    for _ in range(600):
+        a, b = (int(x) for x in rng.integers(0, H, 2))
+        s, d = int(ips[a]), int(ips[b])
+        assert bits(top.get_reliability(s, d)) == bits(orc.reliability(s, d))
+        assert bits(top.get_latency(s, d)) == bits(orc.latency(s, d))
+        assert top.is_routable(s, d) == orc.routable(s, d)
+        assert bits(top.min_path_latency()) == bits(orc.min_path_latency())
+
+
+def test_unattached_address():
+    top, orc, ips, _ = make_pair(synth.complete_graph_gml(5, 3), 5)
+    from shadow_amd import ShdError
+    with pytest.raises(ShdError):
+        top.get_latency(int(ips[0]), 0x01020304)
+    assert orc.latency(int(ips[0]), 0x01020304) == -1
+    assert top.is_routable(int(ips[0]), 0x01020304) is False
+
+
+ROUND_CASES = [
+    # name, barrier, end_time, bootstrap_end, p_payload
+    ("complete30_ms", 110_000_000, 10**15, 0, 0.9),
+    ("complete40_ns", 110_000_000, 10**15, 0, 0.9),
+    ("sparse300_ms", 110_000_000, 200_000_000, 0, 0.9),   # end-time drops
+    ("sparse300_ns", 110_000_000, 10**15, 105_000_000, 0.5),  # bootstrap half the window
+    ("sparse200_dir_ns", 110_000_000, 10**15, 0, 0.9),
+    ("complete25_dir", 110_000_000, 10**15, 0, 1.0),
+    ("1_gbit_switch", 110_000_000, 10**15, 0, 0.9),
+]
+
+
+@pytest.mark.parametrize("case", ROUND_CASES, ids=lambda c: c[0])
+def test_packet_round_host_api_bit_exact(case):
+    name, barrier, end, boot, pp = case
+    gml, H = GRAPHS[name]
+    top, orc, ips, st = make_pair(gml, H)
+    pk = synth.packet_batch(20000, H, 0x5EED0003, 100_000_000, 10_000_000, st, p_payload=pp)
+    out, offs, status, mt = top.round(pk, barrier, end, boot)
+    oout, ostatus, omt = orc.round(ips, pk, barrier, end, boot)
+    assert np.array_equal(status, ostatus)
+    assert mt == omt
+    assert np.array_equal(out, oout)
+    # segments: out[offs[h]:offs[h+1]] all go to h
+    for h in range(H):
+        assert (out["dst_host"][offs[h]:offs[h + 1]] == h).all()
+    assert offs[-1] == len(out)
+    # path packet counters (topology_incrementPathPacketCounter per kept packet)
+    for a in range(0, H, max(1, H // 7)):
+        for b in range(0, H, max(1, H // 5)):
+            assert top.path_packet_count(int(ips[a]), int(ips[b])) == orc.packet_count(int(ips[a]), int(ips[b]))
+
+
+def test_multi_round_state_carries():
+    gml, H = GRAPHS["sparse300_ns"]
+    top, orc, ips, st = make_pair(gml, H)
+    states = st.copy()
+    for r in range(3):
+        pk = synth.packet_batch(5000, H, 0x5EED0100 + r, 100_000_000 * (r + 1), 10_000_000, states)
+        out, _, status, mt = top.round(pk, 100_000_000 * (r + 1) + 10_000_000, 10**15)
+        oout, ostatus, omt = orc.round(ips, pk, 100_000_000 * (r + 1) + 10_000_000, 10**15)
+        assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+        # advance each host's stream by the draws it made
+        cnt = np.bincount(pk["src_host"], minlength=H)
+        for h in range(H):
+            for _ in range(cnt[h]):
+                from shadow_amd.scenario import _rand_r
+                _, states[h] = _rand_r(int(states[h]))
+    assert bits(top.min_path_latency()) == bits(orc.min_path_latency())
+
+
+def test_big_segments_bitonic_path():
+    """All packets to a few destinations: segments far above the LDS rank-sort
+    size take the bitonic network."""
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    pk = synth.packet_batch(12000, H, 0x5EED0200, 100_000_000, 10_000_000, st)
+    pk["dst_host"] = np.where(pk["src_host"] % 3 == 0, 1, 2).astype(np.uint32)
+    pk["dst_host"] = np.where(pk["dst_host"] == pk["src_host"], 0, pk["dst_host"]).astype(np.uint32)
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert np.diff(offs).max() > 1024
+
+
+def test_device_api_matches_oracle_after_touch_all():
+    import torch
+    gml, H = GRAPHS["sparse300_ns"]
+    top, orc, ips, st = make_pair(gml, H)
+    top.touch_all()
+    lat, rel, sv = top.table()
+    orc.preload(sv, lat, rel)  # same rows released in slot order
+    pk = synth.packet_batch(50000, H, 0x5EED0300, 100_000_000, 10_000_000, st)
+    n = len(pk)
+    d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                       d_status.data_ptr(), d_cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    cnt = d_cnt.cpu().numpy().view(np.uint64)
+    out = d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]]
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(d_status.cpu().numpy(), ostatus)
+    assert cnt[1] == omt
+    assert np.array_equal(out, oout)
+
+
+def test_deliv_sort_device_against_lexsort():
+    import torch
+    top, _, _, _ = make_pair(synth.complete_graph_gml(5, 3), 5)
+    rng = np.random.default_rng(3)
+    n, lo, hi = 200000, 1000, 3000
+    ev = np.zeros(n, dtype=synth.DELIV_DTYPE)
+    ev["time"] = rng.integers(0, 50, n)
+    ev["dst_host"] = rng.integers(lo, hi, n)
+    ev["src_host"] = rng.integers(0, 5000, n)
+    ev["seq"] = np.arange(n) * 7 % 100003 + rng.integers(0, 3, n) * 1000000
+    ev["pkt_index"] = np.arange(n)
+    ev["dst_host"][:5000] = lo + 7  # one big segment
+    d_in = torch.from_numpy(ev.view(np.uint8)).cuda()
+    d_out = torch.empty_like(d_in)
+    d_off = torch.empty(hi - lo + 1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    top.deliv_sort_device(d_in.data_ptr(), n, lo, hi, d_out.data_ptr(), d_off.data_ptr(), 0)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy().view(synth.DELIV_DTYPE)
+    order = np.lexsort((ev["pkt_index"], ev["seq"], ev["src_host"], ev["time"], ev["dst_host"]))
+    want = ev[order]
+    # (time, src, seq) ties are broken arbitrarily by construction here; compare keys
+    for k in ("dst_host", "time", "src_host", "seq"):
+        assert np.array_equal(got[k], want[k]), k
+    offs = d_off.cpu().numpy()
+    assert offs[-1] == n and np.array_equal(np.diff(offs), np.bincount(ev["dst_host"] - lo, minlength=hi - lo))
+
+
+def test_multi_gpu_row_shards_assemble():
+    """Rows built in shards into a caller-owned (torch) table == one-shot build."""
+    import torch
+    gml, H = GRAPHS["sparse300_ns"]
+    top, _, _, _ = make_pair(gml, H)
+    lat, rel, sv = top.table()
+    top2 = Topology(gml)
+    scenario.register_hosts(top2, H, 1)
+    A = top2.slot_count()
+    tab = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
+    for lo in range(0, A, 97):
+        top2.build_rows_device(lo, min(A, lo + 97), tab.data_ptr())
+    torch.cuda.synchronize()
+    top2.adopt_table_device(tab.data_ptr())
+    lat2, rel2, _ = top2.table()
+    assert np.array_equal(bits(lat), bits(lat2)) and np.array_equal(bits(rel), bits(rel2))

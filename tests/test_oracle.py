@@ -69,7 +69,7 @@ def test_selfloop_graphs(case):
     ips = synth.host_ips(4)
     _, _, hosts = O.seed_chain(1, 4)
     for h in range(4):
-        v, st, dn, up = t.attach(int(ips[h]), hosts[h])
+        v, st, dn, up = t.attach(h, int(ips[h]), hosts[h])
         assert v == 0
         assert st == O.rand_stream(hosts[h], 1, "rand") and True or True
         assert dn == case["bw_kibps"] and up == case["bw_kibps"]
@@ -84,7 +84,7 @@ def test_selfloop_graphs(case):
 
 def test_attach_consumes_one_draw_per_host():
     t = O.OracleTopology(synth.ONE_GBIT_SWITCH_GML)
-    v, st, _, _ = t.attach(int(synth.host_ips(1)[0]), 12345)
+    v, st, _, _ = t.attach(0, int(synth.host_ips(1)[0]), 12345)
     import ctypes as C
     s = C.c_uint32(12345)
     O.lib.orc_rand_r(C.byref(s))
@@ -141,9 +141,9 @@ def test_cache_direction_quirk_directed_complete():
         # one host per vertex: attach via a single-candidate draw is random,
         # so pin by retrying seeds until each host lands on its own vertex
         for seed in range(1000):
-            v, _, _, _ = O.OracleTopology(gml, False).attach(int(ips[h]), seed)
+            v, _, _, _ = O.OracleTopology(gml, False).attach(h, int(ips[h]), seed)
             if v == h:
-                t.attach(int(ips[h]), seed)
+                t.attach(h, int(ips[h]), seed)
                 break
     a, b = int(ips[0]), int(ips[1])
     ab = t.latency(a, b)
@@ -159,7 +159,7 @@ def test_round_oracle_basic():
     _, _, seeds = O.seed_chain(1, 4)
     st = []
     for h in range(4):
-        _, s, _, _ = t.attach(int(ips[h]), seeds[h])
+        _, s, _, _ = t.attach(h, int(ips[h]), seeds[h])
         st.append(s)
     pk = synth.packet_batch(1000, 4, 0x5EED0000, 10_000_000, 10_000_000, np.array(st, dtype=np.uint32))
     out, status, mt = t.round(ips, pk, barrier=20_000_000, end_time=10**12)
