@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X network plane (BASELINE.json metric:
+"routed host-pairs/sec (APSP) + inter-host packets/sec per round").
+
+`value` = inter-host packets/s per round on the C3 workload (10M synthetic
+packets per round and per GPU over 100k hosts attached to the C2 sparse graph,
+V=20k), whole-job aggregate over all ranks, inputs resident in HBM when the
+timed region starts.  One step = one round: the packet-scatter kernel
+(decision + gathers), the per-destination scan/place and the event_compare
+segment sort; at N > 1 also the RCCL all-to-all of delivered events to their
+destination's owner and the local regrouping there (weak scaling: 10M packets
+per GPU).  The routing-table build is reported beside it ("routing": C1, the
+1,000-vertex complete graph with 5,000 hosts; routed host-pairs/s = H^2 / t).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: torchrun --nproc-per-node N bench.py --gpus N ...)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "routed host-pairs/sec (APSP) + inter-host packets/sec per round, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec (6.29 measured float4 copy)
+# algorithmic bytes: per packet the scatter kernel reads the
+# 32 B record, 2 x 4 B host->vertex slots and the 16 B table entry and
+# writes the 32 B event; place/segsort move the 32 B event in and out.
+BYTES_SCATTER_PER_PKT = 32 + 2 * 4 + 16 + 32
+BYTES_MOVE_PER_EVENT = 32 + 32
+STAGES = ["packet_scatter", "scan", "place", "segment_sort"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--packets", type=int, default=10_000_000, help="packets per round per GPU")
+    ap.add_argument("--hosts", type=int, default=100_000)
+    ap.add_argument("--vertices", type=int, default=20_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-routing", action="store_true")
+    ap.add_argument("--traffic", default=None, help="JSON with PMC-measured HBM bytes per launch")
+    return ap.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from shadow_amd import Topology, _lib, scenario, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ------------------------------------------------------------------ C3 setup
+    H, V, P = args.hosts, args.vertices, args.packets
+    t0 = time.perf_counter()
+    gml = synth.sparse_graph_gml(V, 0x5EED0002)
+    top = Topology(gml, device=local)
+    ips, states, verts = scenario.register_hosts(top, H, seed=1)
+    A = top.slot_count()
+    log(f"C2 graph V={V} H={H} A={A} ready in {time.perf_counter() - t0:.1f}s")
+
+    # routing rows sharded by source slot, assembled by RCCL all-gather (§8e)
+    rows_per = (A + world - 1) // world
+    full = torch.empty(rows_per * world * A * 2, dtype=torch.float64, device=dev)
+    shard = full.narrow(0, rank * rows_per * A * 2, rows_per * A * 2)
+    lo, hi = min(A, rank * rows_per), min(A, (rank + 1) * rows_per)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if hi > lo:
+        # rows are written at their absolute offsets inside `full`
+        top.build_rows_device(lo, hi, full.data_ptr())
+    torch.cuda.synchronize(dev)
+    t_rows_c2 = time.perf_counter() - t0
+    if world > 1:
+        dist.all_gather_into_tensor(full, shard.clone())
+        torch.cuda.synchronize(dev)
+    top.adopt_table_device(full.data_ptr())
+    top.touch_all()  # steady state: every row released (slot order)
+    log(f"C2 table {A}x{A} rows {lo}:{hi} in {t_rows_c2:.2f}s; touched")
+
+    # this rank's packets: senders are its src-shard hosts
+    hlo, hhi = rank * H // world, (rank + 1) * H // world
+    pk = synth.packet_batch(P, H, 0x5EED0003 + rank, 100_000_000, 10_000_000, states, hosts_lo=hlo, hosts_hi=hhi)
+    barrier_t, end_t = 110_000_000, 10**15
+    d_recs = torch.from_numpy(pk.view(np.uint8)).to(dev)
+    d_out = torch.empty(P * 32, dtype=torch.uint8, device=dev)
+    d_off = torch.empty(H + 1, dtype=torch.int32, device=dev)
+    d_status = torch.empty(P, dtype=torch.uint8, device=dev)
+    d_cnt = torch.empty(2, dtype=torch.int64, device=dev)
+    own_lo = [r * H // world for r in range(world + 1)]
+    my_lo, my_hi = own_lo[rank], own_lo[rank + 1]
+    d_final = torch.empty(P * 32 * (2 if world > 1 else 1), dtype=torch.uint8, device=dev)
+    d_final_off = torch.empty(my_hi - my_lo + 1, dtype=torch.int32, device=dev)
+    bounds = torch.tensor(own_lo, dtype=torch.int64, device=dev)
+    sptr = stream.cuda_stream
+    last = {}
+
+    def step():
+        top.process_device(d_recs.data_ptr(), P, barrier_t, end_t, 0, d_out.data_ptr(), d_off.data_ptr(),
+                           d_status.data_ptr(), d_cnt.data_ptr(), sptr)
+        if world == 1:
+            return
+        # exchange delivered events to their destination owner (RCCL all-to-all)
+        cuts = d_off.to(torch.int64)[bounds]
+        send = (cuts[1:] - cuts[:-1])
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send)
+        sc, rc = send.cpu().tolist(), recv.cpu().tolist()
+        nrecv = sum(rc)
+        rbuf = torch.empty(max(nrecv, 1) * 32, dtype=torch.uint8, device=dev)
+        dist.all_to_all_single(rbuf[:nrecv * 32], d_out[:sum(sc) * 32], [c * 32 for c in rc], [c * 32 for c in sc])
+        top.deliv_sort_device(rbuf.data_ptr(), nrecv, my_lo, my_hi, d_final.data_ptr(), d_final_off.data_ptr(), sptr)
+        last["nrecv"] = nrecv
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    lib = _lib.lib()
+    _lib.check(lib.shd_round_timing_enable(1))
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    stage_ms = (C.c_double * 4)()
+    nl = C.c_int()
+    _lib.check(lib.shd_round_timing_read(stage_ms, 4, C.byref(nl)))
+    _lib.check(lib.shd_round_timing_enable(0))
+    cnt = d_cnt.cpu().numpy().view(np.uint64)
+    delivered = int(cnt[0])
+    launches = max(nl.value, 1)
+    per_launch_ms = [stage_ms[k] / launches for k in range(4)]
+    # each rank's stage times; the roofline uses rank 0's live numbers
+    dom = int(np.argmax(per_launch_ms[:1] + [per_launch_ms[1], per_launch_ms[2], per_launch_ms[3]]))
+    alg_bytes = [BYTES_SCATTER_PER_PKT * P, 4.0 * 3 * H, BYTES_MOVE_PER_EVENT * delivered + P,
+                 BYTES_MOVE_PER_EVENT * delivered]
+    achieved = [alg_bytes[k] / (per_launch_ms[k] * 1e-3) / 1e9 if per_launch_ms[k] > 0 else 0.0 for k in range(4)]
+    total_pkts = P * world * args.steps
+    value = total_pkts / dt
+    traffic = None
+    if args.traffic and os.path.exists(args.traffic):
+        with open(args.traffic) as f:
+            traffic = json.load(f).get(STAGES[dom])
+
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "packets/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64+f64",
+        "data": "synthetic (seeded splitmix64 graph, hosts, packets; no datasets)",
+        "config": {
+            "workload": "C3 per-round packet hand-off: 10M packets/round/GPU over 100k hosts on the C2 sparse "
+                        "graph (V=20k); dst-sharded with RCCL all-to-all at N>1",
+            "packets_per_round_per_gpu": P, "hosts": H, "vertices": V, "attached_vertices": A,
+            "delivered_per_round_rank0": delivered, "parallelism": f"dst-shard x{world}",
+        },
+        "roofline": {
+            "kernel": STAGES[dom], "bound": "hbm", "achieved": achieved[dom], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved[dom] / HBM_PEAK_GBS, "traffic": traffic,
+            "per_stage_ms": dict(zip(STAGES, per_launch_ms)),
+            "per_stage_GBps": dict(zip(STAGES, achieved)),
+            "alg_bytes_per_launch": dict(zip(STAGES, alg_bytes)),
+            "timing": "HIP events on the launch stream, averaged over the timed steps",
+        },
+    }
+
+    # ------------------------------------------------------------ C1 routing
+    if not args.no_routing:
+        g1 = synth.complete_graph_gml(1000, 0x5EED0001)
+        t1 = Topology(g1, device=local)
+        scenario.register_hosts(t1, 5000, seed=1)
+        A1 = t1.slot_count()
+        tab1 = torch.empty(A1 * A1 * 2, dtype=torch.float64, device=dev)
+        per1 = (A1 + world - 1) // world
+        l1, h1 = min(A1, rank * per1), min(A1, (rank + 1) * per1)
+        t1.build_rows_device(l1, h1, tab1.data_ptr())  # warm
+        reps = 5
+        barrier()
+        torch.cuda.synchronize(dev)
+        s0 = time.perf_counter()
+        for _ in range(reps):
+            t1.build_rows_device(l1, h1, tab1.data_ptr())
+        torch.cuda.synchronize(dev)
+        barrier()
+        tr = max_over_ranks((time.perf_counter() - s0) / reps)
+        result["routing"] = {
+            "config": "C1 complete graph V=1000 (E=500,500 incl. self-loops), H=5000 hosts, A=%d attached" % A1,
+            "value": 5000.0 ** 2 / tr, "unit": "routed host-pairs/s", "vertex_pairs_per_s": A1 * A1 / tr,
+            "ms_per_table": tr * 1e3, "kernel": "k_sssp_rows<lds> (igraph-exact Dijkstra, 1 wave/source)",
+            "c2_rows_s": t_rows_c2, "c2_host_pairs_per_s": (H * H) / max(max_over_ranks(t_rows_c2), 1e-9),
+        }
+
+    # ------------------------------------------------------- CPU baseline (N=1)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(gml, H, states, top, result)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(gml, H, states, top, result):
+    """The oracle (C restatement of worker_sendPacket + per-destination binary
+    heaps) timed on this host, one core, on a bounded sample of the C3 workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ctypes as O  # checker/baseline only
+    from shadow_amd import scenario, synth
+
+    orc = O.OracleTopology(gml)
+    ips, st2, verts = scenario.register_hosts(orc, H, seed=1)
+    lat, rel, sv = top.table()
+    nslot = 1000
+    sub_slots = np.arange(nslot)
+    sub_vert = sv[sub_slots]
+    hosts = np.flatnonzero(np.isin(verts, sub_vert)).astype(np.uint32)
+    orc.preload(sub_vert, lat[np.ix_(sub_slots, sub_slots)], rel[np.ix_(sub_slots, sub_slots)])
+    n = 20_000_000
+    pk = synth.packet_batch(n, H, 0x5EED0007, 100_000_000, 10_000_000, st2, hosts=hosts)
+    t0 = time.perf_counter()
+    out, status, mt = orc.round(ips, pk, 110_000_000, 10**15)
+    dt = time.perf_counter() - t0
+    base = {"value": n / dt, "unit": "packets/s", "cores": 1, "kind": "port",
+            "sample": f"{n} packets among the {len(hosts)} hosts attached to {nslot} of the C2 graph's attached "
+                      f"vertices; rows preloaded (routing excluded, as in the GPU timed region); {dt:.1f}s"}
+    # routing baseline: oracle Dijkstra rows of C1 (1 core, the reference holds a global graphLock)
+    g1 = synth.complete_graph_gml(1000, 0x5EED0001)
+    o1 = O.OracleTopology(g1)
+    _, _, v1 = scenario.register_hosts(o1, 5000, seed=1)
+    targets = np.unique(v1).astype(np.int32)
+    k = 100
+    t0 = time.perf_counter()
+    for s in targets[:k]:
+        o1.row(int(s), targets)
+    per_row = (time.perf_counter() - t0) / k
+    full = per_row * len(targets)
+    base["routing"] = {"value": 5000.0 ** 2 / full, "unit": "routed host-pairs/s", "cores": 1, "kind": "port",
+                       "sample": f"{k} of {len(targets)} C1 source rows (igraph-0.8 Dijkstra restatement), "
+                                 f"extrapolated to the full table: {full:.2f}s"}
+    return base
+
+
+if __name__ == "__main__":
+    main()

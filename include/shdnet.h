@@ -175,6 +175,13 @@ int shd_topology_host_count(ShdTopology* top, uint32_t* nhosts);
 int shd_deliv_sort_device(ShdTopology* top, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi,
                           ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream);
 
+/* Device timing of the round pipeline with HIP events recorded on the launch
+ * stream (for benchmarks): stages 0 packet-scatter (decision + gathers +
+ * per-destination count), 1 scan, 2 place, 3 segment sort.  enable resets
+ * the record; read sums the elapsed ms per stage over recorded launches. */
+int shd_round_timing_enable(int enable);
+int shd_round_timing_read(double* stage_ms, int nstages, int* launches);
+
 /* Last error message for this thread (static storage). */
 const char* shd_last_error(void);
 

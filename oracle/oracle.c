@@ -780,25 +780,52 @@ static void q_push(Queue* q, int v, int cap) {
     q->v[q->n++] = v;
 }
 
+/* virtualIP hash table (topology.c:40, GHashTable) as linear probing over
+ * capip slots; ip_vertex < 0 marks an empty slot, -2 a removed one. */
+static uint32_t ip_slot(const OrcTopo* t, uint32_t ip) {
+    /* full-avalanche mix: network-order IPs differ only in their high bytes */
+    ip ^= ip >> 16;
+    ip *= 0x85ebca6bu;
+    ip ^= ip >> 13;
+    ip *= 0xc2b2ae35u;
+    ip ^= ip >> 16;
+    return ip & (uint32_t)(t->capip - 1);
+}
+
+static void ip_map_set(OrcTopo* t, uint32_t ip, int v);
+
+static void ip_map_grow(OrcTopo* t) {
+    int oc = t->capip;
+    uint32_t* ok = t->ip_keys;
+    int* ov = t->ip_vertex;
+    t->capip = oc ? oc * 2 : 1024;
+    t->ip_keys = (uint32_t*)calloc((size_t)t->capip, sizeof(uint32_t));
+    t->ip_vertex = (int*)malloc(sizeof(int) * (size_t)t->capip);
+    for (int i = 0; i < t->capip; i++) t->ip_vertex[i] = -1;
+    t->nip = 0;
+    for (int i = 0; i < oc; i++)
+        if (ov[i] >= 0) ip_map_set(t, ok[i], ov[i]);
+    free(ok);
+    free(ov);
+}
+
 static void ip_map_set(OrcTopo* t, uint32_t ip, int v) {
-    for (int i = 0; i < t->nip; i++)
-        if (t->ip_keys[i] == ip) {
-            t->ip_vertex[i] = v;
-            return;
-        }
-    if (t->nip == t->capip) {
-        t->capip = t->capip ? t->capip * 2 : 64;
-        t->ip_keys = (uint32_t*)realloc(t->ip_keys, sizeof(uint32_t) * (size_t)t->capip);
-        t->ip_vertex = (int*)realloc(t->ip_vertex, sizeof(int) * (size_t)t->capip);
-    }
-    t->ip_keys[t->nip] = ip;
-    t->ip_vertex[t->nip] = v;
-    t->nip++;
+    if ((t->nip + 1) * 2 > t->capip) ip_map_grow(t);
+    uint32_t h = ip_slot(t, ip);
+    while (t->ip_vertex[h] != -1 && !(t->ip_vertex[h] >= 0 && t->ip_keys[h] == ip))
+        h = (h + 1) & (uint32_t)(t->capip - 1);
+    if (t->ip_vertex[h] == -1) t->nip++;
+    t->ip_keys[h] = ip;
+    t->ip_vertex[h] = v;
 }
 
 int orc_vertex_of_ip(OrcTopo* t, uint32_t ip) {
-    for (int i = 0; i < t->nip; i++)
-        if (t->ip_keys[i] == ip) return t->ip_vertex[i];
+    if (!t->capip) return -1;
+    uint32_t h = ip_slot(t, ip);
+    while (t->ip_vertex[h] != -1) {
+        if (t->ip_vertex[h] >= 0 && t->ip_keys[h] == ip) return t->ip_vertex[h];
+        h = (h + 1) & (uint32_t)(t->capip - 1);
+    }
     return -1;
 }
 
@@ -824,9 +851,16 @@ int orc_topology_attach(OrcTopo* t, uint32_t ip_net, uint32_t* rng_state, const 
      * without any hint every vertex lands in candidatesAll in order and no
      * LPM applies, so the scan is skipped (same choice, O(1)). */
     if (!ip_hint && !city_hint && !country_hint) {
-        for (int v = 0; v < V; v++) all.v[v] = v;
-        all.n = V;
-        V = 0;
+        double r = orc_next_double(rng_state);
+        int chosen = (int)round((double)((V - 1) * r));
+        free(city.v);
+        free(country.v);
+        free(all.v);
+        ip_map_set(t, ip_net, chosen);
+        t->v_attached[chosen] = 1;
+        if (bw_up) vertex_bw(t, chosen, "bandwidth_up", bw_up);
+        if (bw_down) vertex_bw(t, chosen, "bandwidth_down", bw_down);
+        return chosen;
     }
     for (int v = 0; v < V; v++) {
         const char* ipStr = vas(t, "ip_address", v);
@@ -909,13 +943,15 @@ int orc_topology_attach(OrcTopo* t, uint32_t ip_net, uint32_t* rng_state, const 
 
 /* topology_detach (topology.c:2274-2281): removes the IP only */
 void orc_topology_detach(OrcTopo* t, uint32_t ip) {
-    for (int i = 0; i < t->nip; i++)
-        if (t->ip_keys[i] == ip) {
-            t->ip_keys[i] = t->ip_keys[t->nip - 1];
-            t->ip_vertex[i] = t->ip_vertex[t->nip - 1];
-            t->nip--;
+    if (!t->capip) return;
+    uint32_t h = ip_slot(t, ip);
+    while (t->ip_vertex[h] != -1) {
+        if (t->ip_vertex[h] >= 0 && t->ip_keys[h] == ip) {
+            t->ip_vertex[h] = -2; /* tombstone keeps probe chains intact */
             return;
         }
+        h = (h + 1) & (uint32_t)(t->capip - 1);
+    }
 }
 
 /* ======================================================================= */

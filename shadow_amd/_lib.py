@@ -59,6 +59,8 @@ PROTOS = {
     "shd_round_process_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint64, _P, _P, _P, _P,
                                            _P]),
     "shd_deliv_sort_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P, _P]),
+    "shd_round_timing_enable": (C.c_int, [C.c_int]),
+    "shd_round_timing_read": (C.c_int, [_dp, C.c_int, _ip]),
     "shd_last_error": (C.c_char_p, []),
 }
 
@@ -67,6 +69,13 @@ def lib():
     """The loaded library (raises if it has not been built)."""
     global _lib
     if _lib is None:
+        # PyTorch-ROCm bundles its own libamdhip64.so.7.  Two HIP runtimes in
+        # one process do not coexist, so when torch is present it is loaded
+        # first and libshdnet binds to the same runtime (soname match).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `python __graft_entry__.py` "
                               "(no CPU fallback exists)")

@@ -29,7 +29,7 @@
 namespace {
 
 constexpr int kScanTile = 4096; // 256 threads x 16
-constexpr int kSmallSeg = 1024;
+constexpr int kSmallSeg = 512; // wave register sort up to 8 events per lane
 
 __device__ __forceinline__ int glibc_rand_r(uint32_t* state) {
     uint32_t next = *state;
@@ -210,21 +210,97 @@ __device__ __forceinline__ bool ev_less(const ShdDeliv& a, const ShdDeliv& b) {
     return a.seq < b.seq;
 }
 
-__global__ __launch_bounds__(64) void k_segsort_small(const ShdDeliv* __restrict__ scr, const uint32_t* __restrict__ off,
-                                                      uint32_t H, ShdDeliv* __restrict__ out) {
-    __shared__ ShdDeliv s[kSmallSeg];
-    for (uint32_t d = blockIdx.x; d < H; d += gridDim.x) {
-        const uint32_t b = off[d], n = off[d + 1] - b;
-        if (n == 0 || n > (uint32_t)kSmallSeg) continue;
-        for (uint32_t k = threadIdx.x; k < n; k += 64) s[k] = scr[b + k];
-        __syncthreads();
-        for (uint32_t a = threadIdx.x; a < n; a += 64) {
-            const ShdDeliv x = s[a];
-            uint32_t rank = 0;
-            for (uint32_t k = 0; k < n; k++) rank += ev_less(s[k], x) ? 1u : 0u;
-            out[b + rank] = x;
+// Sort key + payload of one event inside a destination segment.
+struct Ev {
+    unsigned long long t, q; // time, srcHostEventID
+    unsigned s, ix;          // src host, packet index
+};
+
+__device__ __forceinline__ bool ev_lt(const Ev& a, const Ev& b) {
+    if (a.t != b.t) return a.t < b.t;
+    if (a.s != b.s) return a.s < b.s;
+    return a.q < b.q;
+}
+
+__device__ __forceinline__ Ev ev_shfl_xor(const Ev& e, int m) {
+    Ev o;
+    o.t = __shfl_xor(e.t, m);
+    o.q = __shfl_xor(e.q, m);
+    o.s = (unsigned)__shfl_xor((int)e.s, m);
+    o.ix = (unsigned)__shfl_xor((int)e.ix, m);
+    return o;
+}
+
+// One wave sorts one segment of n <= 64*E events held in registers
+// (element i = e*64 + lane), bitonic network over 64*E slots with +inf
+// padding; partner distances < 64 cross lanes by shuffle, >= 64 stay in-lane.
+template <int E>
+__device__ void wave_sort_segment(const ShdDeliv* __restrict__ scr, uint32_t b, uint32_t n, uint32_t d,
+                                  ShdDeliv* __restrict__ out, int lane) {
+    Ev v[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        if (i < n) {
+            const ShdDeliv r = scr[b + i];
+            v[e] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
+        } else {
+            v[e] = Ev{~0ull, ~0ull, ~0u, ~0u};
         }
-        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int p = e ^ (j >> 6);
+                    if (p > e) {
+                        const bool up = (((e * 64 + lane) & k) == 0);
+                        const bool sw = up ? ev_lt(v[p], v[e]) : ev_lt(v[e], v[p]);
+                        if (sw) {
+                            const Ev tmp = v[e];
+                            v[e] = v[p];
+                            v[p] = tmp;
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const Ev o = ev_shfl_xor(v[e], j);
+                    const bool up = (((e * 64 + lane) & k) == 0);
+                    const bool lower = (lane & j) == 0;
+                    const bool o_lt = ev_lt(o, v[e]);
+                    // the lower slot keeps the min when ascending, the max when descending
+                    const bool take_o = (lower == up) ? o_lt : ev_lt(v[e], o);
+                    if (take_o) v[e] = o;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        if (i < n) out[b + i] = ShdDeliv{v[e].t, v[e].q, v[e].s, d, v[e].ix, 0u};
+    }
+}
+
+// Segments of up to kSmallSeg events, one wave each.
+__global__ __launch_bounds__(256) void k_segsort_wave(const ShdDeliv* __restrict__ scr, const uint32_t* __restrict__ off,
+                                                      uint32_t H, uint32_t host_lo, ShdDeliv* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t d = wave; d < H; d += nwaves) {
+        const uint32_t b = off[d], n = off[d + 1] - b;
+        const uint32_t dh = d + host_lo;
+        if (n == 0) continue;
+        if (n <= 64) wave_sort_segment<1>(scr, b, n, dh, out, lane);
+        else if (n <= 128) wave_sort_segment<2>(scr, b, n, dh, out, lane);
+        else if (n <= 256) wave_sort_segment<4>(scr, b, n, dh, out, lane);
+        else if (n <= (uint32_t)kSmallSeg) wave_sort_segment<8>(scr, b, n, dh, out, lane);
     }
 }
 
@@ -329,6 +405,21 @@ unsigned grid_for(size_t n, unsigned block, unsigned cap) {
     return (unsigned)(g > cap ? cap : g);
 }
 
+// ---- optional per-stage timing with HIP events on the launch stream ----
+constexpr int kStages = 4; // 0 packet-scatter, 1 scan, 2 place, 3 segment sort
+constexpr int kMaxTimed = 1024;
+struct Timing {
+    bool on = false;
+    int n = 0;
+    hipEvent_t ev[kMaxTimed][kStages + 1];
+    bool created = false;
+};
+Timing g_tm;
+
+void mark(int stage, hipStream_t s) {
+    if (g_tm.on && g_tm.n < kMaxTimed) (void)hipEventRecord(g_tm.ev[g_tm.n][stage], s);
+}
+
 // scan + place + segment sort, shared by both entry points
 int group_and_sort(const ShdDeliv* tmp, const uint8_t* status, size_t n, uint32_t host_lo, uint32_t H, ShdDeliv* out,
                    uint32_t* offsets, unsigned long long* counters, hipStream_t s) {
@@ -337,11 +428,15 @@ int group_and_sort(const ShdDeliv* tmp, const uint8_t* status, size_t n, uint32_
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g_ws.bsum, nb);
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(H + 1, 256, 1u << 30)), dim3(256), 0, s, offsets, g_ws.cnt, H,
                        g_ws.bsum, nb, g_ws.cur, g_ws.big, g_ws.nbig, counters);
+    mark(2, s);
     hipLaunchKernelGGL(k_place, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, tmp, status, n, host_lo, H, offsets,
                        g_ws.cur, g_ws.scr);
-    hipLaunchKernelGGL(k_segsort_small, dim3(H < 65536u ? (H ? H : 1) : 65536u), dim3(64), 0, s, g_ws.scr, offsets,
-                       H, out);
+    mark(3, s);
+    hipLaunchKernelGGL(k_segsort_wave, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.scr, offsets, H, host_lo,
+                       out);
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.scr, offsets, g_ws.big, g_ws.nbig, out);
+    mark(4, s);
+    if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort launch");
 }
 
@@ -359,13 +454,43 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
         (rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 4, s), "memset nbig")) ||
         (rc = hip_status(hipMemsetAsync(counters, 0xff, 16, s), "memset counters")))
         return rc;
+    mark(0, s);
     if (n)
         hipLaunchKernelGGL(k_pkt_scatter, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, *c, d_recs, n, barrier,
                            end_time, bootstrap_end, g_ws.tmp, d_status, g_ws.cnt, counters);
+    mark(1, s);
     if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
     rc = group_and_sort(g_ws.tmp, d_status, n, 0, H, d_out, d_dst_offsets, counters, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "packet round");
+}
+
+extern "C" int shd_round_timing_enable(int enable) {
+    if (enable && !g_tm.created) {
+        for (int i = 0; i < kMaxTimed; i++)
+            for (int k = 0; k <= kStages; k++)
+                if (hipEventCreate(&g_tm.ev[i][k]) != hipSuccess) return shd_fail(-EIO, "hipEventCreate");
+        g_tm.created = true;
+    }
+    g_tm.on = enable != 0;
+    g_tm.n = 0;
+    return 0;
+}
+
+extern "C" int shd_round_timing_read(double* stage_ms, int nstages, int* launches) {
+    if (nstages > kStages) nstages = kStages;
+    for (int k = 0; k < nstages; k++) stage_ms[k] = 0.0;
+    for (int i = 0; i < g_tm.n; i++) {
+        if (hipEventSynchronize(g_tm.ev[i][kStages]) != hipSuccess) return shd_fail(-EIO, "hipEventSynchronize");
+        for (int k = 0; k < nstages; k++) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, g_tm.ev[i][k], g_tm.ev[i][k + 1]) != hipSuccess)
+                return shd_fail(-EIO, "hipEventElapsedTime");
+            stage_ms[k] += ms;
+        }
+    }
+    if (launches) *launches = g_tm.n;
+    return 0;
 }
 
 extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
@@ -377,8 +502,10 @@ extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_
     if ((rc = hip_status(hipMemsetAsync(g_ws.cnt, 0, 4ull * (H + 1), s), "memset cnt")) ||
         (rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 4, s), "memset nbig")))
         return rc;
+    mark(0, s);
     if (n)
         hipLaunchKernelGGL(k_hist_deliv, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, d_in, n, host_lo, H, g_ws.cnt);
+    mark(1, s);
     rc = group_and_sort(d_in, nullptr, n, host_lo, H, d_out, d_dst_offsets, nullptr, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "deliv sort");

@@ -165,24 +165,34 @@ DELIV_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("src_host", "<u4"), ("
 
 def packet_batch(n: int, nhosts: int, seed: int, window_start: int, window_ns: int,
                  host_seeds: np.ndarray, zipf: bool = False, p_payload: float = 0.9,
-                 hosts_lo: int = 0, hosts_hi: int | None = None) -> np.ndarray:
+                 hosts_lo: int = 0, hosts_hi: int | None = None, hosts: np.ndarray | None = None) -> np.ndarray:
     """C3: one round's packet records.  src uniform over [hosts_lo, hosts_hi)
-    (or Zipf s=1.1), dst uniform != src, now uniform in the window, payload
-    1448 B with prob p_payload else 0.  rng_state = the src host's real
-    rand_r state advanced once per earlier packet of that host in this batch
-    (the CPU reserves one draw per send); seq = per-src ordinal."""
-    hi = nhosts if hosts_hi is None else hosts_hi
+    (or Zipf s=1.1), dst uniform != src over all hosts, now uniform in the
+    window, payload 1448 B with prob p_payload else 0.  With `hosts` given,
+    src and dst are both drawn from that host list instead (bounded samples).
+    rng_state = the src host's real rand_r state advanced once per earlier
+    packet of that host in this batch (the CPU reserves one draw per send);
+    seq = per-src ordinal."""
     rng = SplitMix64(seed)
     r = rng.array(4 * n)
-    span = hi - hosts_lo
-    if zipf:
-        u = (r[0::4] >> np.uint64(11)).astype(np.float64) / float(1 << 53)
-        ranks = np.floor(np.power(span, u) ** 1.0).astype(np.int64)  # log-uniform ~ Zipf(1)
-        src = (hosts_lo + np.clip(ranks - 1, 0, span - 1)).astype(np.uint32)
+    if hosts is not None:
+        hosts = np.asarray(hosts, dtype=np.uint32)
+        m = len(hosts)
+        si = (r[0::4] % np.uint64(m)).astype(np.int64)
+        di = (r[1::4] % np.uint64(m - 1)).astype(np.int64)
+        di = np.where(di >= si, di + 1, di)
+        src, dst = hosts[si], hosts[di]
     else:
-        src = (hosts_lo + (r[0::4] % np.uint64(span))).astype(np.uint32)
-    dst = (r[1::4] % np.uint64(nhosts - 1)).astype(np.uint32)
-    dst = np.where(dst >= src, dst + 1, dst).astype(np.uint32)
+        hi = nhosts if hosts_hi is None else hosts_hi
+        span = hi - hosts_lo
+        if zipf:
+            u = (r[0::4] >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+            ranks = np.floor(np.power(span, u)).astype(np.int64)  # log-uniform ~ Zipf(1)
+            src = (hosts_lo + np.clip(ranks - 1, 0, span - 1)).astype(np.uint32)
+        else:
+            src = (hosts_lo + (r[0::4] % np.uint64(span))).astype(np.uint32)
+        dst = (r[1::4] % np.uint64(nhosts - 1)).astype(np.uint32)
+        dst = np.where(dst >= src, dst + 1, dst).astype(np.uint32)
     now = np.uint64(window_start) + (r[2::4] % np.uint64(window_ns))
     payload = np.where((r[3::4] % np.uint64(1000)) < np.uint64(int(p_payload * 1000)), 1448, 0).astype(np.uint32)
     # per-src ordinal (stable in batch order)
