@@ -85,8 +85,10 @@ __global__ __launch_bounds__(256) void k_pkt_scatter(ShdPktCtx c, const ShdPkt* 
                 } else {
                     if (p.src_host != p.dst_host && t < barrier) t = barrier; // host_single.c:187-192
                     st = SHD_DELIVERED;
-                    tmp[i] = ShdDeliv{t, p.seq, p.src_host, p.dst_host, (uint32_t)i, 0u};
-                    atomicAdd(&cnt[p.dst_host], 1u);
+                    // the count's old value is this event's slot in its
+                    // destination segment (carried in pad; order fixed by the sort)
+                    const uint32_t rank = atomicAdd(&cnt[p.dst_host], 1u);
+                    tmp[i] = ShdDeliv{t, p.seq, p.src_host, p.dst_host, (uint32_t)i, rank};
                     if (t >= barrier && t < mn) mn = t; // worker.c:350-363
                 }
             }
@@ -105,10 +107,11 @@ __global__ __launch_bounds__(256) void k_pkt_scatter(ShdPktCtx c, const ShdPkt* 
 }
 
 __global__ __launch_bounds__(256) void k_hist_deliv(const ShdDeliv* __restrict__ in, size_t n, uint32_t host_lo,
-                                                    uint32_t H, uint32_t* __restrict__ cnt) {
+                                                    uint32_t H, uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ rank) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t d = in[i].dst_host - host_lo; // out-of-range events are dropped
-        if (d < H) atomicAdd(&cnt[d], 1u);
+        rank[i] = d < H ? atomicAdd(&cnt[d], 1u) : ~0u;
     }
 }
 
@@ -191,15 +194,19 @@ __global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ off, co
     }
 }
 
+// Atomic-free placement: every event already holds its slot inside its
+// destination segment (returned by the counting atomic), in pad (packet
+// path) or in rank[] (regroup path).
 __global__ __launch_bounds__(256) void k_place(const ShdDeliv* __restrict__ tmp, const uint8_t* __restrict__ status,
-                                               size_t n, uint32_t host_lo, uint32_t H, const uint32_t* __restrict__ off,
-                                               uint32_t* __restrict__ cur, ShdDeliv* __restrict__ scr) {
+                                               const uint32_t* __restrict__ rank, size_t n, uint32_t host_lo,
+                                               uint32_t H, const uint32_t* __restrict__ off,
+                                               ShdDeliv* __restrict__ scr) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         if (status && status[i] != SHD_DELIVERED) continue;
         const ShdDeliv r = tmp[i];
         const uint32_t d = r.dst_host - host_lo;
         if (d >= H) continue;
-        scr[off[d] + atomicAdd(&cur[d], 1u)] = r;
+        scr[off[d] + (rank ? rank[i] : r.pad)] = r;
     }
 }
 
@@ -323,7 +330,11 @@ __global__ __launch_bounds__(256) void k_segsort_big(const ShdDeliv* __restrict_
         const uint32_t d = big[q];
         const uint32_t b = off[d], n = off[d + 1] - b;
         ShdDeliv* v = out + b;
-        for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) v[k] = scr[b + k];
+        for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+            ShdDeliv r = scr[b + k];
+            r.pad = 0; // drop the placement rank carried in pad
+            v[k] = r;
+        }
         __syncthreads();
         uint32_t N = 1;
         while (N < n) N <<= 1;
@@ -421,16 +432,16 @@ void mark(int stage, hipStream_t s) {
 }
 
 // scan + place + segment sort, shared by both entry points
-int group_and_sort(const ShdDeliv* tmp, const uint8_t* status, size_t n, uint32_t host_lo, uint32_t H, ShdDeliv* out,
-                   uint32_t* offsets, unsigned long long* counters, hipStream_t s) {
+int group_and_sort(const ShdDeliv* tmp, const uint8_t* status, const uint32_t* rank, size_t n, uint32_t host_lo,
+                   uint32_t H, ShdDeliv* out, uint32_t* offsets, unsigned long long* counters, hipStream_t s) {
     const uint32_t nb = (H + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, g_ws.cnt, H, offsets, g_ws.bsum);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g_ws.bsum, nb);
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(H + 1, 256, 1u << 30)), dim3(256), 0, s, offsets, g_ws.cnt, H,
                        g_ws.bsum, nb, g_ws.cur, g_ws.big, g_ws.nbig, counters);
     mark(2, s);
-    hipLaunchKernelGGL(k_place, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, tmp, status, n, host_lo, H, offsets,
-                       g_ws.cur, g_ws.scr);
+    hipLaunchKernelGGL(k_place, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, tmp, status, rank, n, host_lo, H,
+                       offsets, g_ws.scr);
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_wave, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.scr, offsets, H, host_lo,
                        out);
@@ -460,7 +471,7 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
                            end_time, bootstrap_end, g_ws.tmp, d_status, g_ws.cnt, counters);
     mark(1, s);
     if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
-    rc = group_and_sort(g_ws.tmp, d_status, n, 0, H, d_out, d_dst_offsets, counters, s);
+    rc = group_and_sort(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "packet round");
 }
@@ -504,9 +515,11 @@ extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_
         return rc;
     mark(0, s);
     if (n)
-        hipLaunchKernelGGL(k_hist_deliv, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, d_in, n, host_lo, H, g_ws.cnt);
+        hipLaunchKernelGGL(k_hist_deliv, dim3(grid_for(n, 256, 8192)), dim3(256), 0, s, d_in, n, host_lo, H, g_ws.cnt,
+                           reinterpret_cast<uint32_t*>(g_ws.tmp)); // tmp is free here: ranks
     mark(1, s);
-    rc = group_and_sort(d_in, nullptr, n, host_lo, H, d_out, d_dst_offsets, nullptr, s);
+    rc = group_and_sort(d_in, nullptr, reinterpret_cast<const uint32_t*>(g_ws.tmp), n, host_lo, H, d_out,
+                        d_dst_offsets, nullptr, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "deliv sort");
 }
