@@ -63,13 +63,24 @@ def main():
 
     from shadow_amd import Topology, _lib, scenario, synth
 
+    from shadow_amd import exchange
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (the driver's runs use neither): all ranks on GPU 0, and
+    # gloo instead of RCCL, for checking the N>1 logic on a one-GPU box
+    if os.environ.get("SHD_BENCH_SHARE_GPU") == "1":
+        local = 0
+    backend = os.environ.get("SHD_BENCH_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where collectives run
     stream = torch.cuda.current_stream(dev)
 
     def barrier():
@@ -79,7 +90,7 @@ def main():
     def max_over_ranks(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -105,7 +116,12 @@ def main():
     torch.cuda.synchronize(dev)
     t_rows_c2 = time.perf_counter() - t0
     if world > 1:
-        dist.all_gather_into_tensor(full, shard.clone())
+        if cdev == dev:
+            dist.all_gather_into_tensor(full, shard.clone())
+        else:
+            host = full.cpu()
+            dist.all_gather_into_tensor(host, host.narrow(0, rank * rows_per * A * 2, rows_per * A * 2).clone())
+            full.copy_(host)
         torch.cuda.synchronize(dev)
     top.adopt_table_device(full.data_ptr())
     top.touch_all()  # steady state: every row released (slot order)
@@ -120,11 +136,10 @@ def main():
     d_off = torch.empty(H + 1, dtype=torch.int32, device=dev)
     d_status = torch.empty(P, dtype=torch.uint8, device=dev)
     d_cnt = torch.empty(2, dtype=torch.int64, device=dev)
-    own_lo = [r * H // world for r in range(world + 1)]
+    own_lo = exchange.owner_bounds(H, world)
     my_lo, my_hi = own_lo[rank], own_lo[rank + 1]
     d_final = torch.empty(P * 32 * (2 if world > 1 else 1), dtype=torch.uint8, device=dev)
     d_final_off = torch.empty(my_hi - my_lo + 1, dtype=torch.int32, device=dev)
-    bounds = torch.tensor(own_lo, dtype=torch.int64, device=dev)
     sptr = stream.cuda_stream
     last = {}
 
@@ -133,15 +148,12 @@ def main():
                            d_status.data_ptr(), d_cnt.data_ptr(), sptr)
         if world == 1:
             return
-        # exchange delivered events to their destination owner (RCCL all-to-all)
-        cuts = d_off.to(torch.int64)[bounds]
-        send = (cuts[1:] - cuts[:-1])
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send)
-        sc, rc = send.cpu().tolist(), recv.cpu().tolist()
-        nrecv = sum(rc)
-        rbuf = torch.empty(max(nrecv, 1) * 32, dtype=torch.uint8, device=dev)
-        dist.all_to_all_single(rbuf[:nrecv * 32], d_out[:sum(sc) * 32], [c * 32 for c in rc], [c * 32 for c in sc])
+        # destination-owner exchange (RCCL all-to-all over xGMI), then regroup
+        if cdev == dev:
+            rbuf, nrecv, _ = exchange.exchange_events(d_out, d_off, own_lo)
+        else:
+            h, n, _ = exchange.exchange_events(d_out.cpu(), d_off.cpu(), own_lo)
+            rbuf, nrecv = h.to(dev), n
         top.deliv_sort_device(rbuf.data_ptr(), nrecv, my_lo, my_hi, d_final.data_ptr(), d_final_off.data_ptr(), sptr)
         last["nrecv"] = nrecv
 
