@@ -23,11 +23,12 @@ void shd_topology_release_device(ShdTopology* t) {
     shd_dev_free(t->d_inc_r);
     shd_dev_free(t->d_slot_vertex);
     shd_dev_free(t->d_vertex_slot);
-    shd_dev_free(t->d_host_slot);
+    shd_dev_free(t->d_host_info);
     shd_dev_free(t->d_touch);
     shd_dev_free(t->d_pair_bits);
     t->d_tab = NULL;
-    t->d_inc_off = t->d_inc_nbr = t->d_slot_vertex = t->d_vertex_slot = t->d_host_slot = NULL;
+    t->d_host_info = NULL;
+    t->d_inc_off = t->d_inc_nbr = t->d_slot_vertex = t->d_vertex_slot = NULL;
     t->d_inc_w = t->d_inc_r = NULL;
     t->d_touch = t->d_pair_bits = NULL;
 }
@@ -58,22 +59,26 @@ static int prepare(ShdTopology* t) {
     size_t M = (size_t)t->M;
     double* w = (double*)malloc(sizeof(double) * (M + 1));
     double* r = (double*)malloc(sizeof(double) * (M + 1));
-    int32_t* hs = (int32_t*)malloc(sizeof(int32_t) * ((size_t)t->nhosts + 1));
+    free(t->h_host_info);
+    uint32_t* hs = t->h_host_info = (uint32_t*)malloc(sizeof(uint32_t) * 2 * ((size_t)t->nhosts + 1));
     for (size_t k = 0; k < M; k++) {
         w[k] = t->e_ms[t->inc_eid[k]];
         r[k] = t->e_rel[t->inc_eid[k]];
     }
-    for (uint32_t h = 0; h < t->nhosts; h++) hs[h] = t->host_vertex[h] >= 0 ? t->vertex_slot[t->host_vertex[h]] : -1;
+    for (uint32_t h = 0; h < t->nhosts; h++) {
+        hs[2 * h] = t->host_vertex[h] >= 0 ? (uint32_t)t->vertex_slot[t->host_vertex[h]] : SHD_UNTOUCHED;
+        hs[2 * h + 1] = SHD_UNTOUCHED;
+    }
     UPLOAD(t->d_inc_off, t->inc_off, sizeof(int32_t) * ((size_t)t->V + 1));
     UPLOAD(t->d_inc_nbr, t->inc_nbr, sizeof(int32_t) * M);
     UPLOAD(t->d_inc_w, w, sizeof(double) * M);
     UPLOAD(t->d_inc_r, r, sizeof(double) * M);
     UPLOAD(t->d_slot_vertex, t->slot_vertex, sizeof(int32_t) * (size_t)t->A);
     UPLOAD(t->d_vertex_slot, t->vertex_slot, sizeof(int32_t) * (size_t)t->V);
-    UPLOAD(t->d_host_slot, hs, sizeof(int32_t) * (size_t)t->nhosts);
+    UPLOAD(t->d_host_info, hs, sizeof(uint32_t) * 2 * (size_t)t->nhosts);
     free(w);
     free(r);
-    free(hs);
+    hs = NULL;
     /* release state */
     free(t->touch);
     free(t->self_released);
@@ -95,7 +100,6 @@ static int prepare(ShdTopology* t) {
 fail:
     free(w);
     free(r);
-    free(hs);
 fail_nofree:
     shd_topology_release_device(t);
     return rc;
@@ -188,6 +192,11 @@ int shd_topology_copy_table(ShdTopology* t, double* lat, double* rel, int32_t* s
 int shd_sync_touch(ShdTopology* t) {
     if (!t->touch_dirty) return 0;
     int rc = shd_dev_h2d(t->d_touch, t->touch, sizeof(uint32_t) * (size_t)t->A);
+    /* per-host {slot, touch[slot]} records: one 8-byte gather per endpoint */
+    uint32_t* hs = t->h_host_info;
+    for (uint32_t h = 0; h < t->nhosts; h++)
+        hs[2 * h + 1] = hs[2 * h] != SHD_UNTOUCHED ? t->touch[hs[2 * h]] : SHD_UNTOUCHED;
+    if (!rc) rc = shd_dev_h2d(t->d_host_info, hs, sizeof(uint32_t) * 2 * (size_t)t->nhosts);
     if (!rc && t->d_pair_bits) {
         size_t nbits = (size_t)t->A * (size_t)t->A;
         rc = shd_dev_h2d(t->d_pair_bits, t->pair_bits, ((nbits + 31) / 32) * 4);
@@ -202,6 +211,6 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->mode = t->use_sp ? 0 : (t->directed ? 2 : 1);
     c->touch = t->d_touch;
     c->pair_bits = t->d_pair_bits;
-    c->host_slot = t->d_host_slot;
+    c->host_info = t->d_host_info;
     c->nhosts = t->nhosts;
 }

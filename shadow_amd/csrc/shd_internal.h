@@ -90,7 +90,7 @@ typedef struct {
     int mode;                 /* 0 = owner by touch order, 1 = direct symmetric, 2 = direct + pair bits */
     const uint32_t* touch;    /* A, touch sequence (UINT32_MAX = never) */
     const uint32_t* pair_bits; /* A*A bits, mode 2 */
-    const int32_t* host_slot; /* nhosts -> slot */
+    const uint32_t* host_info; /* nhosts x {slot (UINT32_MAX = unattached), touch[slot]}: one 8-B gather */
     uint32_t nhosts;
 } ShdPktCtx;
 

@@ -514,6 +514,7 @@ void shd_topology_free(ShdTopology* t) {
     free(t->pkt_keys);
     free(t->pkt_vals);
     free(t->staged);
+    free(t->h_host_info);
     free(t);
 }
 

@@ -50,7 +50,9 @@ struct ShdTopology {
 
     /* device state */
     ShdEntry* d_tab;
-    int32_t *d_inc_off, *d_inc_nbr, *d_slot_vertex, *d_vertex_slot, *d_host_slot;
+    int32_t *d_inc_off, *d_inc_nbr, *d_slot_vertex, *d_vertex_slot;
+    uint32_t* d_host_info; /* nhosts x {slot, touch[slot]} for the packet kernel */
+    uint32_t* h_host_info;
     double *d_inc_w, *d_inc_r;
     uint32_t *d_touch, *d_pair_bits;
 
