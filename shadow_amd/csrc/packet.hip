@@ -37,16 +37,16 @@
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kItems = 16;
-constexpr int kBatch = 4; // records per thread in flight through the gather chain
-constexpr int kTile = kBlock * kItems; // records per workgroup in the tile kernels
-constexpr int kMaxBuckets = 1024;      // level-1 buckets (LDS histogram size)
-constexpr int kScanTile = 4096;        // 256 threads x 16
-constexpr int kSmallSeg = 256;         // wave register sort up to 4 events per lane
-constexpr int kSortBlock = 512;        // k_part2_sort workgroup (8 waves)
-constexpr int kStream = 8;             // loads in flight per thread in the streaming passes
-constexpr int kGroup = 8;              // scatter tiles per k_part1 workgroup
-constexpr int kPartBlock = 1024;
+constexpr int kBatch = 4;          // records per thread in flight through the gather chain
+constexpr int kChunks = 1024;      // scatter workgroups per launch (columns of the count matrix)
+constexpr int kMaxBuckets = 4096;  // destination buckets (LDS histogram size)
+constexpr int kScanTile = 4096;    // 256 threads x 16
+constexpr int kSmallSeg = 256;     // wave register sort up to 4 events per lane
+constexpr int kSortBlock = 1024;   // k_bucket_sort workgroup (16 waves)
+constexpr int kMaxPerBucket = 2 * kSortBlock; // destinations per bucket (LDS scan width)
+constexpr int kBucketCap = 16384;  // events per bucket on the LDS path (3 x u16 each)
+constexpr int kStream = 8;         // loads in flight per thread in the streaming passes
+constexpr int kPlaceBlock = 256;
 
 __device__ __forceinline__ int glibc_rand_r(uint32_t* state) {
     uint32_t next = *state;
@@ -69,19 +69,42 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
     return v;
 }
 
+// Partition geometry of one launch.  The batch is cut into `ntiles`
+// contiguous chunks of `chunk` records, one scatter workgroup each; the
+// destination range [host_lo, host_lo + H) into `nb` buckets of 2^shift
+// hosts.  cnt1 / off1 are the bucket-major nb x ntiles count matrix and its
+// exclusive scan: bucket b's region of the partitioned array (and of the
+// output) starts at off1[b * ntiles].
 struct Bucketing {
     uint32_t host_lo; // first host id of the range
     uint32_t H;       // hosts in range
     uint32_t shift;   // bucket = (dst - host_lo) >> shift
     uint32_t nb;      // number of buckets
-    uint32_t ntiles;
+    uint32_t ntiles;  // scatter workgroups (matrix columns)
+    uint32_t chunk;   // records per scatter workgroup
+    uint32_t xcd;     // 1: XCD-grouped column order (see col_of)
+    uint32_t rsort;   // segment sort: 1 rank (default), 0 bitonic (see sort_segment)
 };
 
+// Matrix column of chunk g.  Workgroups are dealt to the 8 XCDs round-robin
+// (g % 8, for speed only -- correctness never depends on it), so with the
+// columns of one XCD's chunks adjacent, a bucket's consecutive runs are
+// written through ONE XCD's L2 and its partly written lines fill up there
+// instead of being written back piecewise from eight L2s.  A bijection of
+// [0, ntiles) either way.
+__device__ __forceinline__ uint32_t col_of(const Bucketing& bk, uint32_t g) {
+    if (!bk.xcd) return g;
+    const uint32_t q = bk.ntiles >> 3, r = bk.ntiles & 7, x = g & 7;
+    return x * q + (x < r ? x : r) + (g >> 3);
+}
+
 // kRank = true ("rank" pipeline): each delivered event takes its slot in its
-// destination segment from a per-destination counter (the counter's old
-// value, carried in pad); cnt1 is then the per-destination count array.
-// kRank = false ("bucket" pipeline): LDS histogram over destination buckets
-// per tile; cnt1 is the bucket x tile matrix.
+// destination segment from a per-destination global counter (the counter's
+// old value, carried in pad); cnt1 is then the per-destination count array.
+// kRank = false ("bucket" pipeline, default): the slot inside the
+// (workgroup, bucket) run comes from the workgroup's LDS histogram (old
+// value of an LDS atomic, carried in pad) -- no global atomics per event;
+// cnt1 is the bucket x tile matrix.
 template <bool kRank>
 __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
                                                         uint64_t barrier, uint64_t end_time, uint64_t boot_end,
@@ -95,20 +118,21 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
     __syncthreads();
     unsigned long long mn = ~0ull;
     const size_t A = (size_t)c.A;
-    const size_t base = (size_t)blockIdx.x * kTile;
+    const size_t beg = (size_t)blockIdx.x * bk.chunk;
+    const size_t end = beg + bk.chunk < n ? beg + bk.chunk : n;
     const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
     const ShdEntry* __restrict__ tab = c.tab;
     // kBatch records per thread go through each gather level together, so a
     // wave keeps kBatch x 64 independent requests in flight per level
-    for (int it0 = 0; it0 < kItems; it0 += kBatch) {
+    for (size_t b0 = beg; b0 < end; b0 += (size_t)kBlock * kBatch) {
         ShdPkt p[kBatch];
         int si[kBatch], di[kBatch];
         size_t idx[kBatch];
         bool live[kBatch];
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
-            idx[k] = base + (size_t)(it0 + k) * kBlock + threadIdx.x;
-            live[k] = idx[k] < n;
+            idx[k] = b0 + (size_t)k * kBlock + threadIdx.x;
+            live[k] = idx[k] < end;
             if (live[k]) p[k] = recs[idx[k]];
         }
         uint32_t ts[kBatch], td[kBatch];
@@ -156,9 +180,9 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
                     } else {
                         if (p[k].src_host != p[k].dst_host && t < barrier) t = barrier; // host_single.c:187-192
                         st = SHD_DELIVERED;
-                        uint32_t rank = 0;
+                        uint32_t rank;
                         if (kRank) rank = atomicAdd(&cnt1[p[k].dst_host], 1u);
-                        else atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
+                        else rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
                         tmp[idx[k]] = ShdDeliv{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
                         if (t >= barrier && t < mn) mn = t; // worker.c:350-363
                     }
@@ -171,7 +195,8 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
     if ((threadIdx.x & 63) == 0) wmin[threadIdx.x >> 6] = mn;
     __syncthreads();
     if (!kRank)
-        for (uint32_t b = threadIdx.x; b < bk.nb; b += kBlock) cnt1[(size_t)b * bk.ntiles + blockIdx.x] = hist[b];
+        for (uint32_t b = threadIdx.x; b < bk.nb; b += kBlock)
+            cnt1[(size_t)b * bk.ntiles + col_of(bk, blockIdx.x)] = hist[b];
     if (threadIdx.x == 0) {
         unsigned long long m = wmin[0];
         for (int k = 1; k < kBlock / 64; k++) m = wmin[k] < m ? wmin[k] : m;
@@ -179,21 +204,22 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
     }
 }
 
-// Regroup path (events already decided, e.g. after the multi-GPU exchange).
+// Regroup path (events already decided, e.g. after the multi-GPU exchange):
+// per-chunk bucket histogram; rank[i] = the event's slot in its
+// (chunk, bucket) run, ~0u for events outside the host range.
 __global__ __launch_bounds__(kBlock) void k_hist_tiles(const ShdDeliv* __restrict__ in, size_t n, Bucketing bk,
-                                                       uint32_t* __restrict__ cnt1) {
+                                                       uint32_t* __restrict__ cnt1, uint32_t* __restrict__ rank) {
     __shared__ uint32_t hist[kMaxBuckets];
     for (uint32_t b = threadIdx.x; b < bk.nb; b += kBlock) hist[b] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * kTile;
-    for (int it = 0; it < kItems; it++) {
-        const size_t i = base + (size_t)it * kBlock + threadIdx.x;
-        if (i >= n) break;
+    const size_t beg = (size_t)blockIdx.x * bk.chunk;
+    const size_t end = beg + bk.chunk < n ? beg + bk.chunk : n;
+    for (size_t i = beg + threadIdx.x; i < end; i += kBlock) {
         const uint32_t d = in[i].dst_host - bk.host_lo;
-        if (d < bk.H) atomicAdd(&hist[d >> bk.shift], 1u);
+        rank[i] = d < bk.H ? atomicAdd(&hist[d >> bk.shift], 1u) : ~0u;
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < bk.nb; b += kBlock) cnt1[(size_t)b * bk.ntiles + blockIdx.x] = hist[b];
+    for (uint32_t b = threadIdx.x; b < bk.nb; b += kBlock) cnt1[(size_t)b * bk.ntiles + col_of(bk, blockIdx.x)] = hist[b];
 }
 
 // ---- exclusive scan of u32 counts: out[k] = sum(in[0..k)), out[len] = total ----
@@ -270,44 +296,42 @@ __global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, si
     }
 }
 
-// ---- level 1: tile -> bucket regions (LDS ranks, no global atomics) ----
-// One workgroup covers kGroup consecutive scatter tiles: a bucket's offsets
-// are contiguous across consecutive tiles of the (bucket-major) scan, so the
-// first tile's offset is the group's base and runs get kGroup x longer.
-__global__ __launch_bounds__(kPartBlock) void k_part1(const ShdDeliv* __restrict__ in,
-                                                      const uint8_t* __restrict__ status, size_t n, Bucketing bk,
-                                                      const uint32_t* __restrict__ off1,
-                                                      ShdDeliv* __restrict__ stage) {
-    __shared__ uint32_t base[kMaxBuckets];
-    __shared__ uint32_t cur[kMaxBuckets];
-    const uint32_t t0 = blockIdx.x * kGroup;
-    for (uint32_t b = threadIdx.x; b < bk.nb; b += kPartBlock) {
-        base[b] = off1[(size_t)b * bk.ntiles + t0];
-        cur[b] = 0;
-    }
+// ---- bucket placement: one workgroup per scatter chunk, atomic-free ----
+// The chunk's column of off1 (its run start in every bucket) is staged in
+// LDS; every event goes to col[bucket] + its rank, a pure streaming pass.
+__global__ __launch_bounds__(kPlaceBlock) void k_place_bucket(const ShdDeliv* __restrict__ in,
+                                                              const uint8_t* __restrict__ status,
+                                                              const uint32_t* __restrict__ rank, size_t n,
+                                                              Bucketing bk, const uint32_t* __restrict__ off1,
+                                                              ShdDeliv* __restrict__ stage) {
+    __shared__ uint32_t col[kMaxBuckets];
+    const uint32_t c = col_of(bk, blockIdx.x);
+    for (uint32_t b = threadIdx.x; b < bk.nb; b += kPlaceBlock) col[b] = off1[(size_t)b * bk.ntiles + c];
     __syncthreads();
-    const size_t tb = (size_t)t0 * kTile;
-    constexpr int kPartItems = kGroup * kTile / kPartBlock;
-    for (int it0 = 0; it0 < kPartItems; it0 += kBatch) {
-        ShdDeliv r[kBatch];
-        bool ok[kBatch];
+    const size_t beg = (size_t)blockIdx.x * bk.chunk;
+    const size_t end = beg + bk.chunk < n ? beg + bk.chunk : n;
+    for (size_t i0 = beg + threadIdx.x; i0 < end; i0 += (size_t)kPlaceBlock * kStream) {
+        ShdDeliv r[kStream];
+        uint32_t rk[kStream];
+        bool ok[kStream];
 #pragma unroll
-        for (int k = 0; k < kBatch; k++) {
-            const size_t i = tb + (size_t)(it0 + k) * kPartBlock + threadIdx.x;
-            ok[k] = i < n && (!status || status[i] == SHD_DELIVERED);
-            if (ok[k]) r[k] = in[i];
+        for (int k = 0; k < kStream; k++) {
+            const size_t i = i0 + (size_t)k * kPlaceBlock;
+            ok[k] = i < end && (!status || status[i] == SHD_DELIVERED);
+            if (ok[k]) {
+                r[k] = in[i];
+                rk[k] = rank ? rank[i] : r[k].pad;
+            }
         }
 #pragma unroll
-        for (int k = 0; k < kBatch; k++) {
+        for (int k = 0; k < kStream; k++) {
             const uint32_t d = r[k].dst_host - bk.host_lo;
-            if (!ok[k] || d >= bk.H) continue;
-            const uint32_t b = d >> bk.shift;
-            stage[base[b] + atomicAdd(&cur[b], 1u)] = r[k];
+            if (ok[k] && d < bk.H) stage[col[d >> bk.shift] + rk[k]] = r[k];
         }
     }
 }
 
-// ---- level 2 + segment sort ----
+// ---- per-destination segment sort ----
 
 struct Ev {
     unsigned long long t, q; // time, srcHostEventID
@@ -329,18 +353,95 @@ __device__ __forceinline__ Ev ev_shfl_xor(const Ev& e, int m) {
     return o;
 }
 
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// One wave sorts one segment of n <= 64*E events held in registers
+// (element i = e*64 + lane) by RANK: event_compare is a total order on
+// distinct events ((src host, srcHostEventID) is unique), so the final slot of
+// an event is the number of segment events that precede it.  Every element is
+// broadcast once to the wave with v_readlane (scalar registers, no LDS, no
+// shuffles) and compared with the lane's E elements; each event is then
+// stored straight to out[o + rank] (the segment's lines are all written by
+// this wave, back to back).  Element i is read from src[b + i], or from
+// src[b + perm[i]] when perm (an LDS index list) is given.
+template <int E>
+__device__ void wave_rank_segment(const ShdDeliv* __restrict__ src, uint32_t b, const uint16_t* perm, uint32_t n,
+                                  uint32_t d, ShdDeliv* __restrict__ out, uint32_t o, int lane) {
+    Ev v[E];
+    uint32_t rank[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        rank[e] = 0;
+        if (i < n) {
+            const ShdDeliv r = src[b + (perm ? (uint32_t)perm[i] : i)];
+            v[e] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
+        } else {
+            v[e] = Ev{~0ull, ~0ull, ~0u, ~0u};
+        }
+    }
+    // pass 1: delivery times only (one 64-bit compare per pair), counting
+    // equal times to detect ties (every element equals itself once)
+    uint32_t eq[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) eq[e] = 0;
+#pragma unroll
+    for (int ej = 0; ej < E; ej++) {
+        const int lim = (int)n - ej * 64 < 64 ? (int)n - ej * 64 : 64; // wave-uniform
+        for (int l = 0; l < lim; l++) {
+            const unsigned long long tj = readlane_u64(v[ej].t, l);
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                rank[e] += (uint32_t)(tj < v[e].t);
+                eq[e] += (uint32_t)(tj == v[e].t);
+            }
+        }
+    }
+    bool tie = false;
+#pragma unroll
+    for (int e = 0; e < E; e++) tie |= (e * 64 + lane < (int)n) && eq[e] > 1;
+    if (__ballot(tie)) {
+        // pass 2 (segments with equal delivery times only): rank among the
+        // events of equal time by (src host, srcHostEventID), branch-free
+#pragma unroll
+        for (int ej = 0; ej < E; ej++) {
+            const int lim = (int)n - ej * 64 < 64 ? (int)n - ej * 64 : 64;
+            for (int l = 0; l < lim; l++) {
+                const unsigned long long tj = readlane_u64(v[ej].t, l);
+                const unsigned long long qj = readlane_u64(v[ej].q, l);
+                const unsigned sj = (unsigned)__builtin_amdgcn_readlane((int)v[ej].s, l);
+#pragma unroll
+                for (int e = 0; e < E; e++)
+                    rank[e] += (uint32_t)((tj == v[e].t) & ((sj < v[e].s) | ((sj == v[e].s) & (qj < v[e].q))));
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        if (i < n) out[o + rank[e]] = ShdDeliv{v[e].t, v[e].q, v[e].s, d, v[e].ix, 0u};
+    }
+}
+
 // One wave sorts one segment of n <= 64*E events held in registers
 // (element i = e*64 + lane), bitonic network over 64*E slots with +inf
 // padding; partner distances < 64 cross lanes by shuffle, >= 64 stay in-lane.
+// Element i is read from src[b + i], or from src[b + perm[i]] when perm
+// (an LDS index list) is given; it is written to out[o + i].  (Kept as the
+// SHD_SEGSORT=bitonic alternative of wave_rank_segment.)
 template <int E>
-__device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, uint32_t n, uint32_t d,
-                                  ShdDeliv* __restrict__ out, int lane) {
+__device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, const uint16_t* perm, uint32_t n,
+                                  uint32_t d, ShdDeliv* __restrict__ out, uint32_t o, int lane) {
     Ev v[E];
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)(e * 64 + lane);
         if (i < n) {
-            const ShdDeliv r = src[b + i];
+            const ShdDeliv r = src[b + (perm ? (uint32_t)perm[i] : i)];
             v[e] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
         } else {
             v[e] = Ev{~0ull, ~0ull, ~0u, ~0u};
@@ -380,45 +481,83 @@ __device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, 
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)(e * 64 + lane);
-        if (i < n) out[b + i] = ShdDeliv{v[e].t, v[e].q, v[e].s, d, v[e].ix, 0u};
+        if (i < n) out[o + i] = ShdDeliv{v[e].t, v[e].q, v[e].s, d, v[e].ix, 0u};
     }
 }
 
-// One workgroup per level-1 bucket (<= kMaxBuckets destinations): per-
-// destination histogram and offsets in LDS, LDS-ranked placement into
-// stage2 (the bucket's region, L2/MALL-resident), then the segments are
-// sorted by the workgroup's waves straight into the output.
-__global__ __launch_bounds__(kSortBlock) void k_part2_sort(const ShdDeliv* __restrict__ stage1,
-                                                           ShdDeliv* __restrict__ stage2, Bucketing bk,
-                                                           const uint32_t* __restrict__ off1,
-                                                           uint32_t* __restrict__ offsets,
-                                                           ShdDeliv* __restrict__ out, uint32_t* __restrict__ big,
-                                                           uint32_t* __restrict__ nbig) {
-    __shared__ uint32_t cnt[kMaxBuckets];
-    __shared__ uint32_t loc[kMaxBuckets];
-    __shared__ uint32_t cur[kMaxBuckets];
+// Sorts one destination segment of n <= kSmallSeg events with one wave.
+// algo: 1 rank sort, 0 bitonic network, 2 copy without sorting (a
+// benchmark probe of the memory side only; never selected by the library).
+__device__ __forceinline__ void sort_segment(uint32_t algo, const ShdDeliv* __restrict__ src, uint32_t b,
+                                             const uint16_t* perm, uint32_t n, uint32_t d,
+                                             ShdDeliv* __restrict__ out, uint32_t o, int lane) {
+    if (algo == 2) {
+        for (uint32_t i = lane; i < n; i += 64) {
+            ShdDeliv r = src[b + (perm ? (uint32_t)perm[i] : i)];
+            r.pad = 0;
+            out[o + i] = r;
+        }
+    } else if (algo == 1) {
+        if (n <= 64) wave_rank_segment<1>(src, b, perm, n, d, out, o, lane);
+        else if (n <= 128) wave_rank_segment<2>(src, b, perm, n, d, out, o, lane);
+        else wave_rank_segment<4>(src, b, perm, n, d, out, o, lane);
+    } else {
+        if (n <= 64) wave_sort_segment<1>(src, b, perm, n, d, out, o, lane);
+        else if (n <= 128) wave_sort_segment<2>(src, b, perm, n, d, out, o, lane);
+        else wave_sort_segment<4>(src, b, perm, n, d, out, o, lane);
+    }
+}
+
+// One workgroup per bucket (2^shift destinations, at most kBucketCap events
+// on the LDS path).  The bucket's events are read once for their
+// destination (LDS histogram, rank = old value of the LDS atomic), the
+// per-destination offsets are scanned in LDS, an LDS index list orders the
+// events by destination, and each wave sorts whole destination segments by
+// (time, src host, srcHostEventID), gathering the events through the index
+// list (the bucket region was just read: L2 / Infinity-Cache resident) and
+// writing each segment contiguously to its final place.  Segments above
+// kSmallSeg events, and every segment of a bucket above kBucketCap events,
+// are copied unsorted to their final place and listed for k_segsort_big.
+__global__ __launch_bounds__(kSortBlock) void k_bucket_sort(const ShdDeliv* __restrict__ stage, Bucketing bk,
+                                                            const uint32_t* __restrict__ off1,
+                                                            uint32_t* __restrict__ offsets,
+                                                            ShdDeliv* __restrict__ out, uint32_t* __restrict__ big,
+                                                            uint32_t* __restrict__ nbig) {
+    __shared__ uint32_t cnt[kMaxPerBucket];
+    __shared__ uint32_t loc[kMaxPerBucket];
     __shared__ uint32_t wsum[kSortBlock / 64];
+    __shared__ uint16_t rk[kBucketCap];
+    __shared__ uint16_t dd[kBucketCap];
+    __shared__ uint16_t perm[kBucketCap];
     const uint32_t b = blockIdx.x;
-    const uint32_t per = 1u << bk.shift;
-    const uint32_t d0 = b << bk.shift;                   // first destination (range-relative)
-    const uint32_t nd = min(per, bk.H - d0);             // destinations in this bucket
-    const uint32_t s = off1[(size_t)b * bk.ntiles];      // bucket region [s, e)
+    const uint32_t d0 = b << bk.shift;                           // first destination (range-relative)
+    const uint32_t nd = min(1u << bk.shift, bk.H - d0);          // destinations in this bucket
+    const uint32_t s = off1[(size_t)b * bk.ntiles];              // bucket region [s, e)
     const uint32_t e = off1[(size_t)(b + 1) * bk.ntiles];
-    for (uint32_t j = threadIdx.x; j < nd; j += kSortBlock) cnt[j] = 0, cur[j] = 0;
+    const uint32_t ne = e - s;
+    const bool fits = ne <= (uint32_t)kBucketCap;
+    for (uint32_t j = threadIdx.x; j < nd; j += kSortBlock) cnt[j] = 0;
     __syncthreads();
-    for (uint32_t k0 = s + threadIdx.x; k0 < e; k0 += kSortBlock * kStream) {
-        uint32_t dd[kStream];
+    for (uint32_t i0 = threadIdx.x; i0 < ne; i0 += kSortBlock * kStream) {
+        uint32_t dq[kStream];
 #pragma unroll
         for (int q = 0; q < kStream; q++) {
-            const uint32_t k = k0 + (uint32_t)q * kSortBlock;
-            dd[q] = k < e ? stage1[k].dst_host : ~0u;
+            const uint32_t i = i0 + (uint32_t)q * kSortBlock;
+            dq[q] = i < ne ? stage[s + i].dst_host - bk.host_lo - d0 : ~0u;
         }
 #pragma unroll
-        for (int q = 0; q < kStream; q++)
-            if (dd[q] != ~0u) atomicAdd(&cnt[dd[q] - bk.host_lo - d0], 1u);
+        for (int q = 0; q < kStream; q++) {
+            if (dq[q] == ~0u) continue;
+            const uint32_t r = atomicAdd(&cnt[dq[q]], 1u);
+            if (fits) {
+                const uint32_t i = i0 + (uint32_t)q * kSortBlock;
+                rk[i] = (uint16_t)r;
+                dd[i] = (uint16_t)dq[q];
+            }
+        }
     }
     __syncthreads();
-    // exclusive scan of cnt[0..nd) (nd <= 1024): two values per thread
+    // exclusive scan of cnt[0..nd) (nd <= kMaxPerBucket = 2 * kSortBlock)
     {
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         const uint32_t j0 = 2 * threadIdx.x, j1 = j0 + 1;
@@ -435,29 +574,37 @@ __global__ __launch_bounds__(kSortBlock) void k_part2_sort(const ShdDeliv* __res
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nd; j += kSortBlock) offsets[d0 + j] = s + loc[j];
     if (b == gridDim.x - 1 && threadIdx.x == 0) offsets[bk.H] = e;
-    for (uint32_t k0 = s + threadIdx.x; k0 < e; k0 += kSortBlock * kStream) {
-        ShdDeliv r[kStream];
-#pragma unroll
-        for (int q = 0; q < kStream; q++) {
-            const uint32_t k = k0 + (uint32_t)q * kSortBlock;
-            if (k < e) r[q] = stage1[k];
-        }
-#pragma unroll
-        for (int q = 0; q < kStream; q++) {
-            if (k0 + (uint32_t)q * kSortBlock >= e) break;
-            const uint32_t j = r[q].dst_host - bk.host_lo - d0;
-            stage2[s + loc[j] + atomicAdd(&cur[j], 1u)] = r[q];
-        }
-    }
-    __syncthreads(); // workgroup-scope release/acquire: stage2 writes visible to the sorting waves
     const int lane = threadIdx.x & 63;
-    for (uint32_t j = threadIdx.x >> 6; j < nd; j += kSortBlock / 64) {
-        const uint32_t n = cnt[j], o = s + loc[j], dh = bk.host_lo + d0 + j;
-        if (n == 0) continue;
-        if (n <= 64) wave_sort_segment<1>(stage2, o, n, dh, out, lane);
-        else if (n <= 128) wave_sort_segment<2>(stage2, o, n, dh, out, lane);
-        else if (n <= (uint32_t)kSmallSeg) wave_sort_segment<4>(stage2, o, n, dh, out, lane);
-        else if (lane == 0) big[atomicAdd(nbig, 1u)] = d0 + j;
+    if (fits) {
+        for (uint32_t i = threadIdx.x; i < ne; i += kSortBlock) perm[loc[dd[i]] + rk[i]] = (uint16_t)i;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x >> 6; j < nd; j += kSortBlock / 64) {
+            const uint32_t n = cnt[j], o = loc[j], dh = bk.host_lo + d0 + j;
+            if (n == 0) continue;
+            if (n <= (uint32_t)kSmallSeg) sort_segment(bk.rsort, stage, s, perm + o, n, dh, out, s + o, lane);
+            else {
+                for (uint32_t i = lane; i < n; i += 64) {
+                    ShdDeliv r = stage[s + perm[o + i]];
+                    r.pad = 0;
+                    out[s + o + i] = r;
+                }
+                if (lane == 0) big[atomicAdd(nbig, 1u)] = d0 + j;
+            }
+        }
+    } else {
+        // oversized bucket (skewed destinations): unsorted placement through
+        // LDS cursors, every segment sorted in place by k_segsort_big
+        for (uint32_t j = threadIdx.x; j < nd; j += kSortBlock)
+            if (cnt[j] > 0) big[atomicAdd(nbig, 1u)] = d0 + j;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < nd; j += kSortBlock) cnt[j] = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < ne; i += kSortBlock) {
+            ShdDeliv r = stage[s + i];
+            r.pad = 0;
+            const uint32_t j = r.dst_host - bk.host_lo - d0;
+            out[s + loc[j] + atomicAdd(&cnt[j], 1u)] = r;
+        }
     }
 }
 
@@ -475,22 +622,25 @@ __device__ __forceinline__ void cmpx(ShdDeliv* v, uint32_t a, uint32_t b) {
     }
 }
 
-// Segments above kSmallSeg events: copy, then an all-ascending bitonic
-// network over the next power of two with virtual +inf padding (pairs that
-// touch the padding are skipped, which is exact for this network form).
-__global__ __launch_bounds__(256) void k_segsort_big(const ShdDeliv* __restrict__ stage2,
+// Segments above kSmallSeg events: copy (skipped when sorting in place),
+// then an all-ascending bitonic network over the next power of two with
+// virtual +inf padding (pairs that touch the padding are skipped, which is
+// exact for this network form).
+__global__ __launch_bounds__(256) void k_segsort_big(const ShdDeliv* stage2,
                                                      const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig,
-                                                     ShdDeliv* __restrict__ out) {
+                                                     ShdDeliv* out) {
     const uint32_t nb = *nbig;
     for (uint32_t q = blockIdx.x; q < nb; q += gridDim.x) {
         const uint32_t d = big[q];
         const uint32_t b = off[d], n = off[d + 1] - b;
         ShdDeliv* v = out + b;
-        for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
-            ShdDeliv r = stage2[b + k];
-            r.pad = 0;
-            v[k] = r;
+        if (stage2 != out) {
+            for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
+                ShdDeliv r = stage2[b + k];
+                r.pad = 0;
+                v[k] = r;
+            }
         }
         __syncthreads();
         uint32_t N = 1;
@@ -558,7 +708,8 @@ __global__ __launch_bounds__(256) void k_place_rank(const ShdDeliv* __restrict__
 // to the bitonic-in-HBM list.
 __global__ __launch_bounds__(256) void k_segsort_dst(const ShdDeliv* __restrict__ scr, const uint32_t* __restrict__ off,
                                                      uint32_t H, uint32_t host_lo, ShdDeliv* __restrict__ out,
-                                                     uint32_t* __restrict__ big, uint32_t* __restrict__ nbig) {
+                                                     uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
+                                                     uint32_t rsort) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
@@ -566,9 +717,7 @@ __global__ __launch_bounds__(256) void k_segsort_dst(const ShdDeliv* __restrict_
         const uint32_t b = off[d], n = off[d + 1] - b;
         const uint32_t dh = d + host_lo;
         if (n == 0) continue;
-        if (n <= 64) wave_sort_segment<1>(scr, b, n, dh, out, lane);
-        else if (n <= 128) wave_sort_segment<2>(scr, b, n, dh, out, lane);
-        else if (n <= (uint32_t)kSmallSeg) wave_sort_segment<4>(scr, b, n, dh, out, lane);
+        if (n <= (uint32_t)kSmallSeg) sort_segment(rsort, scr, b, nullptr, n, dh, out, b, lane);
         else if (lane == 0) big[atomicAdd(nbig, 1u)] = d;
     }
 }
@@ -576,17 +725,16 @@ __global__ __launch_bounds__(256) void k_segsort_dst(const ShdDeliv* __restrict_
 // ---- workspace (grow-only, per process / device) ----
 struct Ws {
     size_t cap_n = 0;
-    ShdDeliv* tmp = nullptr;
-    ShdDeliv* st1 = nullptr;
-    ShdDeliv* st2 = nullptr;
-    size_t cap_m = 0; // bucket x tile matrix
+    ShdDeliv* tmp = nullptr; // decided events in record order
+    ShdDeliv* st1 = nullptr; // events partitioned by bucket (bucket) / destination (rank)
+    uint32_t* rnk = nullptr; // per-event rank, regroup path
+    size_t cap_m = 0;        // count matrix (bucket) / per-destination counts (rank)
     uint32_t* cnt1 = nullptr;
     uint32_t* off1 = nullptr;
     uint32_t* bsum = nullptr;
     uint32_t cap_h = 0;
     uint32_t* big = nullptr;
     uint32_t* nbig = nullptr;
-    uint32_t* rnk = nullptr; // per-event rank, regroup path of the rank pipeline
 };
 Ws g_ws;
 
@@ -600,15 +748,13 @@ int ws_reserve(size_t n, size_t m, uint32_t H) {
     if (n > g_ws.cap_n) {
         (void)hipFree(g_ws.tmp);
         (void)hipFree(g_ws.st1);
-        (void)hipFree(g_ws.st2);
         (void)hipFree(g_ws.rnk);
-        g_ws.tmp = g_ws.st1 = g_ws.st2 = nullptr;
+        g_ws.tmp = g_ws.st1 = nullptr;
         g_ws.rnk = nullptr;
         g_ws.cap_n = 0;
         const size_t cap = n + n / 8 + 1024;
         if ((rc = hip_status(hipMalloc((void**)&g_ws.tmp, sizeof(ShdDeliv) * cap), "hipMalloc ws.tmp")) ||
             (rc = hip_status(hipMalloc((void**)&g_ws.st1, sizeof(ShdDeliv) * cap), "hipMalloc ws.st1")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.st2, sizeof(ShdDeliv) * cap), "hipMalloc ws.st2")) ||
             (rc = hip_status(hipMalloc((void**)&g_ws.rnk, sizeof(uint32_t) * cap), "hipMalloc ws.rnk")))
             return rc;
         g_ws.cap_n = cap;
@@ -638,27 +784,53 @@ int ws_reserve(size_t n, size_t m, uint32_t H) {
     return 0;
 }
 
-Bucketing make_bucketing(uint32_t host_lo, uint32_t H, size_t n) {
-    Bucketing bk;
-    bk.host_lo = host_lo;
-    bk.H = H;
-    bk.shift = 7; // 128 destinations per bucket, up to kMaxBuckets buckets
-    while (((size_t)H + (1u << bk.shift) - 1) >> bk.shift > (size_t)kMaxBuckets) bk.shift++;
-    bk.nb = (uint32_t)(((size_t)H + (1u << bk.shift) - 1) >> bk.shift);
-    if (bk.nb == 0) bk.nb = 1;
-    bk.ntiles = (uint32_t)((n + kTile - 1) / kTile);
-    if (bk.ntiles == 0) bk.ntiles = 1;
-    return bk;
-}
-
 unsigned grid_for(size_t n, unsigned block, unsigned cap) {
     size_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
     return (unsigned)(g > cap ? cap : g);
 }
 
+// SHD_SEGSORT=bitonic selects the bitonic segment network, else rank sort
+// (SHD_SEGSORT=probe-copy: no sorting at all, a benchmark probe only).
+uint32_t rank_sort() {
+    const char* v = getenv("SHD_SEGSORT");
+    if (v && strcmp(v, "bitonic") == 0) return 0;
+    if (v && strcmp(v, "probe-copy") == 0) return 2;
+    return 1;
+}
+
+constexpr uint32_t kMaxShift = 11; // 2^11 = kMaxPerBucket destinations per bucket
+
+// Buckets: the fewest (widest) that keep a uniform batch's expected events
+// per bucket within half the LDS capacity of k_bucket_sort; chunks: about
+// kChunks scatter workgroups, each a multiple of one batch of records.
+int make_bucketing(uint32_t host_lo, uint32_t H, size_t n, Bucketing* out) {
+    Bucketing bk;
+    bk.host_lo = host_lo;
+    bk.H = H;
+    bk.shift = 0;
+    while ((((size_t)H + (1u << bk.shift) - 1) >> bk.shift) > (size_t)kMaxBuckets) bk.shift++;
+    if (bk.shift > kMaxShift) return shd_fail(-E2BIG, "%u destination hosts exceed the partition limit", H);
+    while (bk.shift < kMaxShift && H > 0 && (double)n * (double)(2u << bk.shift) / (double)H <= kBucketCap / 2.0)
+        bk.shift++;
+    bk.nb = (uint32_t)(((size_t)H + (1u << bk.shift) - 1) >> bk.shift);
+    if (bk.nb == 0) bk.nb = 1;
+    const size_t unit = (size_t)kBlock * kBatch;
+    size_t chunk = (n + kChunks - 1) / kChunks;
+    chunk = (chunk + unit - 1) / unit * unit;
+    if (chunk < unit) chunk = unit;
+    bk.chunk = (uint32_t)chunk;
+    bk.ntiles = (uint32_t)((n + chunk - 1) / chunk);
+    if (bk.ntiles == 0) bk.ntiles = 1;
+    const char* x = getenv("SHD_XCD_COLS");
+    bk.xcd = !(x && strcmp(x, "0") == 0);
+    bk.rsort = rank_sort();
+    *out = bk;
+    return 0;
+}
+
 // ---- optional per-stage timing with HIP events on the launch stream ----
-constexpr int kStages = 4; // 0 packet-scatter, 1 scan, 2 level-1 partition, 3 level-2 + segment sort
+constexpr int kStages = 4; // 0 packet-scatter, 1 scan, 2 placement, 3 per-bucket / per-destination sort
 constexpr int kMaxTimed = 1024;
 struct Timing {
     bool on = false;
@@ -672,9 +844,10 @@ void mark(int stage, hipStream_t s) {
     if (g_tm.on && g_tm.n < kMaxTimed) (void)hipEventRecord(g_tm.ev[g_tm.n][stage], s);
 }
 
-// scan + partition + segment sort, shared by both entry points
-int group_and_sort(const ShdDeliv* in, const uint8_t* status, size_t n, const Bucketing& bk, ShdDeliv* out,
-                   uint32_t* offsets, unsigned long long* counters, hipStream_t s) {
+// scan of the count matrix, atomic-free placement into bucket regions,
+// per-bucket LDS sort (shared by both entry points)
+int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n, const Bucketing& bk,
+                   ShdDeliv* out, uint32_t* offsets, unsigned long long* counters, hipStream_t s) {
     const size_t m = (size_t)bk.nb * bk.ntiles;
     const uint32_t nb = (uint32_t)((m + kScanTile - 1) / kScanTile);
     hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, g_ws.cnt1, m, g_ws.off1, g_ws.bsum);
@@ -682,12 +855,12 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, size_t n, const Bu
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m + 1, 256, 1u << 30)), dim3(256), 0, s, g_ws.off1, m, g_ws.bsum,
                        nb, counters);
     mark(2, s);
-    hipLaunchKernelGGL(k_part1, dim3((bk.ntiles + kGroup - 1) / kGroup), dim3(kPartBlock), 0, s, in, status, n, bk,
-                       g_ws.off1, g_ws.st1);
+    hipLaunchKernelGGL(k_place_bucket, dim3(bk.ntiles), dim3(kPlaceBlock), 0, s, in, status, rank, n, bk, g_ws.off1,
+                       g_ws.st1);
     mark(3, s);
-    hipLaunchKernelGGL(k_part2_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, g_ws.st1, g_ws.st2, bk, g_ws.off1,
-                       offsets, out, g_ws.big, g_ws.nbig);
-    hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.st2, offsets, g_ws.big, g_ws.nbig, out);
+    hipLaunchKernelGGL(k_bucket_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, g_ws.st1, bk, g_ws.off1, offsets, out,
+                       g_ws.big, g_ws.nbig);
+    hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort launch");
@@ -709,18 +882,18 @@ int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_
                            n, host_lo, H, offsets, g_ws.st1);
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.st1, offsets, H, host_lo,
-                       out, g_ws.big, g_ws.nbig);
+                       out, g_ws.big, g_ws.nbig, rank_sort());
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort_rank launch");
 }
 
-// SHD_PACKET_PIPELINE=bucket selects the two-level bucket partition;
-// anything else the per-destination rank pipeline.
+// SHD_PACKET_PIPELINE=rank selects the per-destination-counter pipeline;
+// anything else the bucket pipeline (default).
 bool use_rank_pipeline() {
     const char* v = getenv("SHD_PACKET_PIPELINE");
-    return !(v && strcmp(v, "bucket") == 0);
+    return v && strcmp(v, "rank") == 0;
 }
 
 } // namespace
@@ -731,10 +904,11 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     hipStream_t s = (hipStream_t)stream;
     const uint32_t H = c->nhosts;
     const bool rk = use_rank_pipeline();
-    const Bucketing bk = make_bucketing(0, H, n);
-    const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
-    int rc = ws_reserve(n, m, H);
+    Bucketing bk;
+    int rc = make_bucketing(0, H, n, &bk);
     if (rc) return rc;
+    const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
+    if ((rc = ws_reserve(n, m, H))) return rc;
     unsigned long long* counters = (unsigned long long*)d_counters;
     if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 4, s), "memset nbig")) ||
         (rc = hip_status(hipMemsetAsync(counters, 0xff, 16, s), "memset counters")))
@@ -754,7 +928,7 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     mark(1, s);
     if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
     rc = rk ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s)
-            : group_and_sort(g_ws.tmp, d_status, n, bk, d_out, d_dst_offsets, counters, s);
+            : group_and_sort(g_ws.tmp, d_status, nullptr, n, bk, d_out, d_dst_offsets, counters, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "packet round");
 }
@@ -792,10 +966,11 @@ extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_
     hipStream_t s = (hipStream_t)stream;
     const uint32_t H = host_hi - host_lo;
     const bool rk = use_rank_pipeline();
-    const Bucketing bk = make_bucketing(host_lo, H, n);
-    const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
-    int rc = ws_reserve(n, m, H);
+    Bucketing bk;
+    int rc = make_bucketing(host_lo, H, n, &bk);
     if (rc) return rc;
+    const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
+    if ((rc = ws_reserve(n, m, H))) return rc;
     if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 4, s), "memset nbig"))) return rc;
     if ((rk || !n) && (rc = hip_status(hipMemsetAsync(g_ws.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
     mark(0, s);
@@ -804,11 +979,11 @@ extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_
             hipLaunchKernelGGL(k_hist_rank, dim3(grid_for(n, 256, 1u << 20)), dim3(256), 0, s, d_in, n, host_lo, H,
                                g_ws.cnt1, g_ws.rnk);
         else
-            hipLaunchKernelGGL(k_hist_tiles, dim3(bk.ntiles), dim3(kBlock), 0, s, d_in, n, bk, g_ws.cnt1);
+            hipLaunchKernelGGL(k_hist_tiles, dim3(bk.ntiles), dim3(kBlock), 0, s, d_in, n, bk, g_ws.cnt1, g_ws.rnk);
     }
     mark(1, s);
     rc = rk ? group_and_sort_rank(d_in, nullptr, g_ws.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s)
-            : group_and_sort(d_in, nullptr, n, bk, d_out, d_dst_offsets, nullptr, s);
+            : group_and_sort(d_in, nullptr, g_ws.rnk, n, bk, d_out, d_dst_offsets, nullptr, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "deliv sort");
 }

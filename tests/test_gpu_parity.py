@@ -94,6 +94,13 @@ def test_unattached_address():
     assert top.is_routable(int(ips[0]), 0x01020304) is False
 
 
+@pytest.fixture(params=["bucket", "rank"])
+def pipeline(request, monkeypatch):
+    """Both grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, read per launch)."""
+    monkeypatch.setenv("SHD_PACKET_PIPELINE", request.param)
+    return request.param
+
+
 ROUND_CASES = [
     # name, barrier, end_time, bootstrap_end, p_payload
     ("complete30_ms", 110_000_000, 10**15, 0, 0.9),
@@ -107,7 +114,7 @@ ROUND_CASES = [
 
 
 @pytest.mark.parametrize("case", ROUND_CASES, ids=lambda c: c[0])
-def test_packet_round_host_api_bit_exact(case):
+def test_packet_round_host_api_bit_exact(case, pipeline):
     name, barrier, end, boot, pp = case
     gml, H = GRAPHS[name]
     top, orc, ips, st = make_pair(gml, H)
@@ -145,7 +152,7 @@ def test_multi_round_state_carries():
     assert bits(top.min_path_latency()) == bits(orc.min_path_latency())
 
 
-def test_big_segments_bitonic_path():
+def test_big_segments_bitonic_path(pipeline):
     """All packets to a few destinations: segments far above the LDS rank-sort
     size take the bitonic network."""
     gml, H = GRAPHS["complete30_ms"]
@@ -159,7 +166,21 @@ def test_big_segments_bitonic_path():
     assert np.diff(offs).max() > 1024
 
 
-def test_device_api_matches_oracle_after_touch_all():
+def test_oversized_bucket_fallback(pipeline):
+    """Skewed destinations: one partition bucket far above the LDS capacity of
+    the per-bucket sort (16384 events) takes the in-place fallback."""
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    pk = synth.packet_batch(60000, H, 0x5EED0210, 100_000_000, 10_000_000, st)
+    hot = (pk["seq"] % 10) != 0  # 90 % of the packets go to host 1 (or 2 from host 1)
+    pk["dst_host"] = np.where(hot, np.where(pk["src_host"] == 1, 2, 1), pk["dst_host"]).astype(np.uint32)
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert offs[2] - offs[1] > 16384
+
+
+def test_device_api_matches_oracle_after_touch_all(pipeline):
     import torch
     gml, H = GRAPHS["sparse300_ns"]
     top, orc, ips, st = make_pair(gml, H)
@@ -185,7 +206,7 @@ def test_device_api_matches_oracle_after_touch_all():
     assert np.array_equal(out, oout)
 
 
-def test_deliv_sort_device_against_lexsort():
+def test_deliv_sort_device_against_lexsort(pipeline):
     import torch
     top, _, _, _ = make_pair(synth.complete_graph_gml(5, 3), 5)
     rng = np.random.default_rng(3)
@@ -229,3 +250,50 @@ def test_multi_gpu_row_shards_assemble():
     top2.adopt_table_device(tab.data_ptr())
     lat2, rel2, _ = top2.table()
     assert np.array_equal(bits(lat), bits(lat2)) and np.array_equal(bits(rel), bits(rel2))
+
+
+def test_full_size_c3_round_bit_exact():
+    """BASELINE configs[3] at full size: 10M packets over 100k hosts on the
+    V=20k sparse graph (the whole 19,870 x 19,870 table resident), device API.
+    Senders and receivers are the hosts attached to the first 1,000 table
+    slots so that the oracle's preloaded rows stay small; every packet still
+    goes through the full-size kernels, host map and partition geometry."""
+    import torch
+    H, V = 100_000, 20_000
+    gml = synth.sparse_graph_gml(V, 0x5EED0002)
+    top = Topology(gml)
+    ips, st, verts = scenario.register_hosts(top, H, seed=1)
+    A = top.slot_count()
+    sv = np.unique(verts).astype(np.int32)  # slots = attached vertices, ascending
+    assert len(sv) == A
+    full = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
+    top.build_rows_device(0, A, full.data_ptr())
+    torch.cuda.synchronize()
+    top.adopt_table_device(full.data_ptr())
+    top.touch_all()
+    k = 1000
+    blk = full.view(A, A, 2)[:k, :k].cpu().numpy()
+    orc = O.OracleTopology(gml)
+    ips_o, st_o, verts_o = scenario.register_hosts(orc, H, seed=1)
+    assert (verts == verts_o).all()
+    orc.preload(sv[:k], np.ascontiguousarray(blk[:, :, 0]), np.ascontiguousarray(blk[:, :, 1]))
+    hosts = np.flatnonzero(np.isin(verts, sv[:k])).astype(np.uint32)
+    n = 10_000_000
+    pk = synth.packet_batch(n, H, 0x5EED0400, 100_000_000, 10_000_000, st, hosts=hosts)
+    d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                       d_status.data_ptr(), d_cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    cnt = d_cnt.cpu().numpy().view(np.uint64)
+    out = d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]]
+    oout, ostatus, omt = orc.round(ips_o, pk, 110_000_000, 10**15)
+    assert np.array_equal(d_status.cpu().numpy(), ostatus)
+    assert cnt[1] == omt
+    assert np.array_equal(out, oout)
+    offs = d_off.cpu().numpy().astype(np.int64)
+    assert offs[-1] == len(out) and np.array_equal(np.diff(offs), np.bincount(out["dst_host"], minlength=H))
