@@ -216,7 +216,7 @@ def main():
             "per_stage_GBps": dict(zip(STAGES, achieved)),
             "alg_bytes_per_launch": dict(zip(STAGES, alg_bytes)),
             "timing": "HIP events on the launch stream, averaged over the timed steps",
-            "pipeline": "rank" if os.environ.get("SHD_PACKET_PIPELINE") == "rank" else "bucket",
+            "pipeline": "bucket" if os.environ.get("SHD_PACKET_PIPELINE") == "bucket" else "rank",
         },
     }
 

@@ -14,109 +14,119 @@
 // already final because u was popped.  Results are therefore bit-identical
 // to the reference, ties included, with no CPU fallback.
 //
-// Parallel structure: sources are independent (one wave each, all of the
-// chip's waves in flight); within a pop the wave relaxes 64 incident edges
-// per step (coalesced CSR reads, gathered dist reads), a ballot collects
-// the improving lanes and the wave applies their heap operations in
-// incidence order (the order igraph applies them) with uniform control
-// flow.  Small graphs keep dist/rel/heap (32 B per vertex) in LDS; large
-// graphs use a per-wave slab in HBM.
+// Parallel structure: sources are independent (one wave each, as many in
+// flight as the CUs hold); within a pop the wave relaxes 64 incident edges
+// per step (coalesced CSR reads, gathered dist reads), a ballot collects the
+// improving lanes and the wave applies their updates in incidence order (the
+// order igraph applies them) with uniform control flow.  Every heap,
+// distance and reliability store inside the pop loop is made by all 64 lanes
+// with the same address and value, so each lane reads back its own writes in
+// program order and the loop needs no barrier.
+//
+// Storage: 16-B heap nodes {key = -dist, vertex} plus igraph's index2 (pos).
+//  * V <= kLdsMaxV: everything in LDS (36 B per vertex), one wave per block.
+//  * larger graphs: a private HBM slab per wave (heap, dist, rel, pos), with
+//    heap positions [0, kTop) -- the levels every pop walks through -- kept in
+//    LDS; kSlabWaves independent waves per block, up to kWavesPerCU per CU,
+//    persistent over rows.  A row is bound by its chain of dependent heap
+//    loads, not by bandwidth, so the kernel keeps as many rows in flight as
+//    the CUs hold.
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
+#include <cstdlib>
 
 #include "shd_internal.h"
 
 namespace {
 
-struct Heap {
-    double* d; // heap keys (= -dist), position order
-    int* ix;   // position -> vertex
-    int* pos;  // vertex -> position + 2 (igraph index2)
-    int n;
+constexpr int kTop = 256;       // heap positions in LDS for the slab kernel (levels 0..7)
+constexpr int kSlabWaves = 4;   // independent waves per slab-kernel block
+constexpr int kWavesPerCU = 32; // gfx950: resident waves per CU
+constexpr int kLdsMaxV = 4096;  // 36 B per vertex -> 144 KiB of the 160 KiB LDS
+
+struct __attribute__((aligned(16))) HNode {
+    double key; // -dist
+    int v;
+    int pad;
 };
 
-__device__ __forceinline__ void heap_shift_up(Heap& h, int e) {
-    const double x = h.d[e];
-    const int xi = h.ix[e];
-    while (e > 0) {
-        const int p = ((e + 1) >> 1) - 1;
-        const double dp = h.d[p];
-        if (x < dp) break; // igraph: stop iff data[elem] < data[parent]
-        const int pi = h.ix[p];
-        h.d[e] = dp;
-        h.ix[e] = pi;
-        h.pos[pi] = e + 2;
-        e = p;
-    }
-    h.d[e] = x;
-    h.ix[e] = xi;
-    h.pos[xi] = e + 2;
-}
+// igraph_2wheap over split storage.  kAll: every position in LDS (top).
+// Else positions < kTop in LDS and position p >= kTop at rest[p + 1], which
+// puts each child pair (2e+1, 2e+2) in one 32-B sector.
+template <bool kAll>
+struct Heap {
+    HNode* top;
+    HNode* rest;
+    int* pos; // vertex -> position + 2 (igraph index2; 0 once popped)
+    int n;
 
-__device__ __forceinline__ void heap_sink(Heap& h, int e) {
-    const double x = h.d[e];
-    const int xi = h.ix[e];
-    for (;;) {
-        const int l = 2 * e + 1;
-        if (l >= h.n) break;
-        const int r = l + 1;
-        const double dl = h.d[l];
-        int c = l;
-        double dc = dl;
-        if (r != h.n) {
-            const double dr = h.d[r];
-            if (!(dl >= dr)) c = r, dc = dr; // left when left >= right
+    __device__ __forceinline__ HNode ld(int p) const { return (kAll || p < kTop) ? top[p] : rest[p + 1]; }
+    __device__ __forceinline__ void st(int p, const HNode& x) {
+        if (kAll || p < kTop) top[p] = x;
+        else rest[p + 1] = x;
+        pos[x.v] = p + 2;
+    }
+    // climb while !(x < parent)
+    __device__ __forceinline__ void shift_up(int e, const HNode& x) {
+        while (e > 0) {
+            const int p = ((e + 1) >> 1) - 1;
+            const HNode pn = ld(p);
+            if (x.key < pn.key) break;
+            st(e, pn);
+            e = p;
         }
-        if (!(x < dc)) break;
-        const int ci = h.ix[c];
-        h.d[e] = dc;
-        h.ix[e] = ci;
-        h.pos[ci] = e + 2;
-        e = c;
+        st(e, x);
     }
-    h.d[e] = x;
-    h.ix[e] = xi;
-    h.pos[xi] = e + 2;
-}
-
-__device__ __forceinline__ void heap_push(Heap& h, int idx, double key) {
-    const int s = h.n++;
-    h.d[s] = key;
-    h.ix[s] = idx;
-    h.pos[idx] = s + 2;
-    heap_shift_up(h, s);
-}
-
-__device__ __forceinline__ int heap_delete_max(Heap& h, double* key) {
-    const double top = h.d[0];
-    const int ti = h.ix[0];
-    const int last = h.n - 1;
-    if (last > 0) {
-        const int li = h.ix[last];
-        h.d[0] = h.d[last];
-        h.ix[0] = li;
-        h.pos[li] = 2;
+    // descend towards the larger child (the left one when left >= right)
+    // while x < child; both children are loaded before either is compared
+    // (position l + 1 <= V is inside the storage even when l + 1 == n)
+    __device__ __forceinline__ void sink(int e, const HNode& x) {
+        for (;;) {
+            const int l = 2 * e + 1;
+            if (l >= n) break;
+            HNode c = ld(l);
+            const HNode r = ld(l + 1);
+            int ci = l;
+            if (l + 1 < n && !(c.key >= r.key)) c = r, ci = l + 1;
+            if (!(x.key < c.key)) break;
+            st(e, c);
+            e = ci;
+        }
+        st(e, x);
     }
-    h.n = last;
-    h.pos[ti] = 0;
-    if (h.n > 0) heap_sink(h, 0);
-    *key = top;
-    return ti;
-}
-
-__device__ __forceinline__ void heap_modify(Heap& h, int idx, double key) {
-    const int p = h.pos[idx] - 2;
-    h.d[p] = key;
-    heap_sink(h, p);
-    heap_shift_up(h, p);
-}
+    __device__ __forceinline__ void push(int v, double key) {
+        const int e = n++;
+        shift_up(e, HNode{key, v, 0});
+    }
+    // delete_max: the last node takes the root and sinks
+    __device__ __forceinline__ int pop(double* key) {
+        const HNode t = ld(0);
+        const int last = --n;
+        pos[t.v] = 0;
+        if (last > 0) sink(0, ld(last));
+        *key = t.key;
+        return t.v;
+    }
+    // igraph_2wheap_modify with a larger key (Dijkstra only lowers a
+    // distance, strictly): its sink step cannot move the node -- the heap
+    // keeps parent >= child, so every child is <= the old key < the new key --
+    // which leaves the shift-up at the node's position.
+    __device__ __forceinline__ void raise(int v, double key) { shift_up(pos[v] - 2, HNode{key, v, 0}); }
+};
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const long long b = __double_as_longlong(v);
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// orders one wave's per-lane accesses before its uniform ones (and back)
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // _topology_computeShortestPathToSelf (topology.c:1431-1576): first strict
@@ -151,31 +161,32 @@ __device__ void self_entry(const ShdGraphDev& g, int u, ShdEntry* out, int lane)
     }
 }
 
-template <bool kLds>
-__global__ __launch_bounds__(64) void k_sssp_rows(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab,
-                                                  char* __restrict__ slab, size_t slab_stride) {
+template <bool kAll>
+__global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, int row_lo, int row_hi,
+                                                              ShdEntry* __restrict__ tab, char* __restrict__ slab,
+                                                              size_t slab_stride) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int gw = (int)blockIdx.x * wpb + w, nw = (int)gridDim.x * wpb;
     const int V = g.V, A = g.A;
-    char* base = kLds ? smem : slab + (size_t)blockIdx.x * slab_stride;
-    double* dist = reinterpret_cast<double*>(base);
+    HNode* top = reinterpret_cast<HNode*>(smem) + (kAll ? 0 : w * kTop);
+    HNode* rest = kAll ? nullptr : reinterpret_cast<HNode*>(slab + (size_t)gw * slab_stride);
+    double* dist = reinterpret_cast<double*>(kAll ? top + V + 1 : rest + V + 2);
     double* rel = dist + V;
-    double* hd = rel + V;
-    int* hix = reinterpret_cast<int*>(hd + V);
-    int* hpos = hix + V;
+    int* pos = reinterpret_cast<int*>(rel + V);
 
-    for (int row = row_lo + (int)blockIdx.x; row < row_hi; row += (int)gridDim.x) {
+    for (int row = row_lo + gw; row < row_hi; row += nw) {
         const int src = g.slot_vertex[row];
         for (int v = lane; v < V; v += 64) dist[v] = -1.0;
-        __syncthreads();
-        Heap h{hd, hix, hpos, 0};
+        wave_fence();
+        Heap<kAll> h{top, rest, pos, 0};
         dist[src] = 0.0;
         rel[src] = 1.0;
-        heap_push(h, src, 0.0);
+        h.push(src, 0.0);
         int to_reach = A;
         while (h.n > 0 && to_reach > 0) {
             double key;
-            const int u = heap_delete_max(h, &key);
+            const int u = h.pop(&key);
             const double mindist = -key;
             if (g.vertex_slot[u] >= 0) --to_reach;
             const double ru = rel[u];
@@ -183,32 +194,32 @@ __global__ __launch_bounds__(64) void k_sssp_rows(ShdGraphDev g, int row_lo, int
             for (int b = k0; b < k1; b += 64) {
                 const int k = b + lane;
                 int v = 0;
-                double alt = 0.0;
+                double alt = 0.0, rv = 0.0;
                 bool imp = false, fresh = false;
                 if (k < k1) {
                     v = g.inc_nbr[k];
                     alt = mindist + g.inc_w[k];
+                    rv = ru * g.inc_r[k];
                     const double cur = dist[v];
                     fresh = cur < 0;
                     imp = fresh || alt < cur;
-                    if (imp) {
-                        dist[v] = alt;
-                        rel[v] = ru * g.inc_r[k];
-                    }
                 }
+                // (parallel edges are rejected at load, so the lanes' v differ)
                 unsigned long long m = __ballot(imp);
                 const unsigned long long fm = __ballot(fresh);
-                while (m) { // heap ops in incidence order, uniform across the wave
+                while (m) {
                     const int l = __builtin_ctzll(m);
                     m &= m - 1;
                     const int vv = __builtin_amdgcn_readlane(v, l);
                     const double aa = readlane_d(alt, l);
-                    if ((fm >> l) & 1ull) heap_push(h, vv, -aa);
-                    else heap_modify(h, vv, -aa);
+                    dist[vv] = aa;
+                    rel[vv] = readlane_d(rv, l);
+                    if ((fm >> l) & 1ull) h.push(vv, -aa);
+                    else h.raise(vv, -aa);
                 }
             }
-            __syncthreads();
         }
+        wave_fence();
         ShdEntry* out = tab + (size_t)row * (size_t)A;
         for (int j = lane; j < A; j += 64) {
             if (j == row) continue;
@@ -225,7 +236,7 @@ __global__ __launch_bounds__(64) void k_sssp_rows(ShdGraphDev g, int row_lo, int
             out[j] = e;
         }
         self_entry(g, src, out + row, lane);
-        __syncthreads();
+        wave_fence();
     }
 }
 
@@ -250,8 +261,6 @@ int hip_status(hipError_t e, const char* what) {
     return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
 }
 
-constexpr int kLdsMaxV = 4096; // 32 B per vertex -> 128 KiB of the 160 KiB LDS
-
 } // namespace
 
 extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo, int row_hi, ShdEntry* tab) {
@@ -265,9 +274,8 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         if ((rc = hip_status(hipGetLastError(), "k_direct_rows launch"))) return rc;
         return hip_status(hipDeviceSynchronize(), "k_direct_rows");
     }
-    const size_t per_vertex = 3 * sizeof(double) + 2 * sizeof(int);
     if (g.V <= kLdsMaxV) {
-        const size_t lds = per_vertex * (size_t)g.V;
+        const size_t lds = sizeof(HNode) * ((size_t)g.V + 1) + 20 * (size_t)g.V;
         if (lds > 65536 &&
             (rc = hip_status(hipFuncSetAttribute((const void*)k_sssp_rows<true>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
@@ -278,16 +286,29 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         if ((rc = hip_status(hipGetLastError(), "k_sssp_rows<lds> launch"))) return rc;
         return hip_status(hipDeviceSynchronize(), "k_sssp_rows<lds>");
     }
-    // large graphs: one HBM slab per resident wave, persistent over rows
-    const size_t stride = (per_vertex * (size_t)g.V + 255) & ~(size_t)255;
-    int grid = rows < 2048 ? rows : 2048;
+    // large graphs: persistent waves, one HBM slab each (heap V+2 nodes,
+    // dist, rel, pos); SHD_SSSP_WAVES overrides the wave count
+    const size_t stride = (sizeof(HNode) * ((size_t)g.V + 2) + 20 * (size_t)g.V + 255) & ~(size_t)255;
+    int dev = 0, cus = 0;
+    if ((rc = hip_status(hipGetDevice(&dev), "hipGetDevice")) ||
+        (rc = hip_status(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
+                         "hipDeviceGetAttribute")))
+        return rc;
+    long waves = (long)cus * kWavesPerCU;
+    if (const char* e = getenv("SHD_SSSP_WAVES")) {
+        const long x = atol(e);
+        if (x > 0) waves = x;
+    }
+    if (waves > rows) waves = rows;
+    int grid = (int)((waves + kSlabWaves - 1) / kSlabWaves);
     char* slab = nullptr;
-    while (hipMalloc((void**)&slab, stride * (size_t)grid) != hipSuccess) {
+    while (hipMalloc((void**)&slab, stride * kSlabWaves * (size_t)grid) != hipSuccess) {
         (void)hipGetLastError();
-        if (grid <= 64) return shd_fail(-ENOMEM, "cannot allocate SSSP workspace");
+        if (grid <= 16) return shd_fail(-ENOMEM, "cannot allocate SSSP workspace");
         grid /= 2;
     }
-    hipLaunchKernelGGL(k_sssp_rows<false>, dim3(grid), dim3(64), 0, nullptr, g, row_lo, row_hi, tab, slab, stride);
+    hipLaunchKernelGGL(k_sssp_rows<false>, dim3(grid), dim3(64 * kSlabWaves), sizeof(HNode) * kTop * kSlabWaves,
+                       nullptr, g, row_lo, row_hi, tab, slab, stride);
     rc = hip_status(hipGetLastError(), "k_sssp_rows<hbm> launch");
     if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_rows<hbm>");
     (void)hipFree(slab);

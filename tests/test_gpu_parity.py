@@ -40,6 +40,7 @@ GRAPHS = {
     "sparse300_ns": (synth.sparse_graph_gml(300, 0x5EED0012, ns_variant=True), 400),
     "sparse200_dir_ns": (synth.sparse_graph_gml(200, 0x5EED0022, ns_variant=True, directed=True), 300),
     "sparse5000_hbm": (synth.sparse_graph_gml(5000, 0x5EED0042), 200),  # V > 4096: HBM-slab kernel
+    "sparse4500_dir_ns_hbm": (synth.sparse_graph_gml(4500, 0x5EED0052, ns_variant=True, directed=True), 150),
 }
 
 
@@ -54,6 +55,35 @@ def test_routing_table_bit_exact(name):
         assert np.array_equal(bits(rel[i]), bits(orl)), (name, i)
         nz = orl != 0
         assert np.all(np.abs(rel[i][nz] - orl[nz]) <= REL_TOL * np.abs(orl[nz]))
+
+
+@pytest.mark.parametrize("waves", [1, 6])
+def test_slab_kernel_persistent_rows(waves, monkeypatch):
+    """Fewer slab waves than rows (SHD_SSSP_WAVES): each wave reuses its slab
+    and LDS heap top for many sources; 6 waves = one partly idle block."""
+    monkeypatch.setenv("SHD_SSSP_WAVES", str(waves))
+    gml, H = GRAPHS["sparse5000_hbm"]
+    top, orc, _, _ = make_pair(gml, H)
+    lat, rel, sv = top.table()
+    for i, s in enumerate(sv):
+        ol, orl = orc.row(int(s), sv)
+        assert np.array_equal(bits(lat[i]), bits(ol)), i
+        assert np.array_equal(bits(rel[i]), bits(orl)), i
+
+
+def test_reference_converter_fixture_graph():
+    """The reference's own GML fixture (src/test/config/convert/
+    topology.expected.gml, kept as data in tests/golden/): directed graph, one
+    vertex, "50 ms" self-loop, loss 0."""
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "convert_topology_expected.gml")) as f:
+        gml = f.read()
+    top, orc, ips, _ = make_pair(gml, 3)
+    for a in range(3):
+        for b in range(3):
+            assert top.get_latency(int(ips[a]), int(ips[b])) == 50.0
+            assert top.get_reliability(int(ips[a]), int(ips[b])) == 1.0
+            assert orc.latency(int(ips[a]), int(ips[b])) == 50.0
 
 
 @pytest.mark.parametrize("directed", [False, True])
@@ -276,6 +306,10 @@ def test_full_size_c3_round_bit_exact():
     orc = O.OracleTopology(gml)
     ips_o, st_o, verts_o = scenario.register_hosts(orc, H, seed=1)
     assert (verts == verts_o).all()
+    for i in (0, 1, A // 2, A - 1):  # full-length rows of the slab kernel vs the oracle's Dijkstra
+        ol, orl = orc.row(int(sv[i]), sv)
+        row = full.view(A, A, 2)[i].cpu().numpy()
+        assert np.array_equal(bits(row[:, 0]), bits(ol)) and np.array_equal(bits(row[:, 1]), bits(orl)), i
     orc.preload(sv[:k], np.ascontiguousarray(blk[:, :, 0]), np.ascontiguousarray(blk[:, :, 1]))
     hosts = np.flatnonzero(np.isin(verts, sv[:k])).astype(np.uint32)
     n = 10_000_000

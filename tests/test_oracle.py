@@ -82,6 +82,20 @@ def test_selfloop_graphs(case):
     assert t.next_min_jump_ns() == int(case["latency_ms"]) * 1_000_000
 
 
+def test_reference_converter_fixture_graph():
+    """The reference's own GML fixture (src/test/config/convert/
+    topology.expected.gml, kept as data): directed, one vertex with label and
+    country_code, "81920 Kibit" bandwidths, "50 ms" self-loop, loss 0.0."""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "convert_topology_expected.gml")) as f:
+        t = O.OracleTopology(f.read())
+    ips = synth.host_ips(2)
+    for h in range(2):
+        v, _, dn, up = t.attach(h, int(ips[h]), 7 + h)
+        assert v == 0 and dn == up == 81920 * 1024 // (8 * 1024)  # KiB/s (topology.c:220-225)
+    assert t.latency(int(ips[0]), int(ips[1])) == 50.0 and t.reliability(int(ips[0]), int(ips[1])) == 1.0
+    assert t.next_min_jump_ns() == 50_000_000
+
+
 def test_attach_consumes_one_draw_per_host():
     t = O.OracleTopology(synth.ONE_GBIT_SWITCH_GML)
     v, st, _, _ = t.attach(0, int(synth.host_ips(1)[0]), 12345)
