@@ -169,6 +169,10 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int gw = (int)blockIdx.x * wpb + w, nw = (int)gridDim.x * wpb;
     const int V = g.V, A = g.A;
+    // dense graphs (LDS kernel): 4 batches in flight; sparse ones rarely
+    // have a second batch, and the slab kernel keeps its registers for
+    // occupancy
+    constexpr int kRelax = kAll ? 4 : 1;
     HNode* top = reinterpret_cast<HNode*>(smem) + (kAll ? 0 : w * kTop);
     HNode* rest = kAll ? nullptr : reinterpret_cast<HNode*>(slab + (size_t)gw * slab_stride);
     double* dist = reinterpret_cast<double*>(kAll ? top + V + 1 : rest + V + 2);
@@ -191,31 +195,45 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
             if (g.vertex_slot[u] >= 0) --to_reach;
             const double ru = rel[u];
             const int k0 = g.inc_off[u], k1 = g.inc_off[u + 1];
-            for (int b = k0; b < k1; b += 64) {
-                const int k = b + lane;
-                int v = 0;
-                double alt = 0.0, rv = 0.0;
-                bool imp = false, fresh = false;
-                if (k < k1) {
-                    v = g.inc_nbr[k];
-                    alt = mindist + g.inc_w[k];
-                    rv = ru * g.inc_r[k];
-                    const double cur = dist[v];
-                    fresh = cur < 0;
-                    imp = fresh || alt < cur;
+            // kRelax batches of 64 incident edges are loaded together (CSR
+            // loads, then the dist gathers) before their updates are applied:
+            // an update only writes the dist of its own neighbour, and a
+            // neighbour occurs once per incidence list (parallel edges are
+            // rejected at load; a loop never improves), so the early gathers
+            // read exactly what one-at-a-time relaxation would.
+            for (int b0 = k0; b0 < k1; b0 += 64 * kRelax) {
+                int v[kRelax];
+                double alt[kRelax], rv[kRelax];
+                bool imp[kRelax], fresh[kRelax];
+#pragma unroll
+                for (int q = 0; q < kRelax; q++) {
+                    const int k = b0 + q * 64 + lane;
+                    const int kk = k < k1 ? k : k1 - 1; // branch-free: clamp, then mask
+                    v[q] = g.inc_nbr[kk];
+                    alt[q] = mindist + g.inc_w[kk];
+                    rv[q] = ru * g.inc_r[kk];
                 }
-                // (parallel edges are rejected at load, so the lanes' v differ)
-                unsigned long long m = __ballot(imp);
-                const unsigned long long fm = __ballot(fresh);
-                while (m) {
-                    const int l = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const int vv = __builtin_amdgcn_readlane(v, l);
-                    const double aa = readlane_d(alt, l);
-                    dist[vv] = aa;
-                    rel[vv] = readlane_d(rv, l);
-                    if ((fm >> l) & 1ull) h.push(vv, -aa);
-                    else h.raise(vv, -aa);
+#pragma unroll
+                for (int q = 0; q < kRelax; q++) {
+                    const double cur = dist[v[q]];
+                    const bool ok = b0 + q * 64 + lane < k1;
+                    fresh[q] = ok && cur < 0;
+                    imp[q] = ok && (cur < 0 || alt[q] < cur);
+                }
+#pragma unroll
+                for (int q = 0; q < kRelax; q++) {
+                    unsigned long long m = __ballot(imp[q]);
+                    const unsigned long long fm = __ballot(fresh[q]);
+                    while (m) { // igraph's order: incidence order, one edge at a time
+                        const int l = __builtin_ctzll(m);
+                        m &= m - 1;
+                        const int vv = __builtin_amdgcn_readlane(v[q], l);
+                        const double aa = readlane_d(alt[q], l);
+                        dist[vv] = aa;
+                        rel[vv] = readlane_d(rv[q], l);
+                        if ((fm >> l) & 1ull) h.push(vv, -aa);
+                        else h.raise(vv, -aa);
+                    }
                 }
             }
         }
