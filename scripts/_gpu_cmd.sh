@@ -1,9 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-T=s3b
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -k "routing or slab or direct or lookup or full_size or shards or fixture" --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || { tail -30 gpurun_out/${T}_pytest.log; exit 1; }
+T=s4e
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -k "routing or slab" --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || { tail -30 gpurun_out/${T}_pytest.log; exit 1; }
 tail -1 gpurun_out/${T}_pytest.log
-for v in "X=1"; do
-  env $v timeout -k 10 200 python bench.py --steps 10 --no-cpu-baseline > gpurun_out/${T}_b.json 2>/dev/null || exit 1
-  echo "$v $(python -c "import json;d=json.load(open('gpurun_out/${T}_b.json'));r=d['routing'];print(round(d['ms_per_step'],4), {k:round(v,4) for k,v in d['roofline']['per_stage_ms'].items()}, 'C1 ms', round(r['ms_per_table'],3), 'C2 s', round(r['c2_rows_s'],3))")"
-done
+timeout -k 10 200 python bench.py --steps 10 --no-cpu-baseline > gpurun_out/${T}_b.json 2>/dev/null || exit 1
+python -c "import json;d=json.load(open('gpurun_out/${T}_b.json'));r=d['routing'];print(round(d['ms_per_step'],4), {k:round(v,4) for k,v in d['roofline']['per_stage_ms'].items()}, 'C1 ms', round(r['ms_per_table'],3), 'C2 s', round(r['c2_rows_s'],3))"

@@ -51,6 +51,14 @@ struct __attribute__((aligned(16))) HNode {
     int pad;
 };
 
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ double uni_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // igraph_2wheap over split storage.  kAll: every position in LDS (top).
 // Else positions < kTop in LDS and position p >= kTop at rest[p + 1], which
 // puts each child pair (2e+1, 2e+2) in one 32-B sector.
@@ -61,10 +69,31 @@ struct Heap {
     int* pos; // vertex -> position + 2 (igraph index2; 0 once popped)
     int n;
 
-    __device__ __forceinline__ HNode ld(int p) const { return (kAll || p < kTop) ? top[p] : rest[p + 1]; }
+    // every heap operand is wave-uniform: readfirstlane tells the compiler
+    // so, and the heap then runs on scalar branches with LDS- or
+    // global-specific accesses (not exec-masked flat ones)
+    __device__ __forceinline__ HNode ld(int p) const {
+        HNode x;
+        // (distinct asm markers after each access keep the compiler from
+        // sinking the LDS and the global access into one flat access)
+        if (kAll || p < kTop) {
+            x = top[p];
+            if (!kAll) __asm__ volatile("; heap lds" ::: "memory");
+        } else {
+            x = rest[p + 1];
+            __asm__ volatile("; heap hbm" ::: "memory");
+        }
+        if (kAll) return x; // (the LDS kernel is faster without the readfirstlanes)
+        return HNode{uni_d(x.key), uni(x.v), 0};
+    }
     __device__ __forceinline__ void st(int p, const HNode& x) {
-        if (kAll || p < kTop) top[p] = x;
-        else rest[p + 1] = x;
+        if (kAll || p < kTop) {
+            top[p] = x;
+            if (!kAll) __asm__ volatile("; heap lds st" ::: "memory");
+        } else {
+            rest[p + 1] = x;
+            __asm__ volatile("; heap hbm st" ::: "memory");
+        }
         pos[x.v] = p + 2;
     }
     // climb while !(x < parent)
@@ -99,20 +128,19 @@ struct Heap {
         const int e = n++;
         shift_up(e, HNode{key, v, 0});
     }
-    // delete_max: the last node takes the root and sinks
-    __device__ __forceinline__ int pop(double* key) {
-        const HNode t = ld(0);
+    // delete_max in two halves: the root is read first (top), then removed
+    // (the last node takes the root and sinks)
+    __device__ __forceinline__ HNode top_node() const { return ld(0); }
+    __device__ __forceinline__ void pop_top(int v) {
         const int last = --n;
-        pos[t.v] = 0;
+        pos[v] = 0;
         if (last > 0) sink(0, ld(last));
-        *key = t.key;
-        return t.v;
     }
     // igraph_2wheap_modify with a larger key (Dijkstra only lowers a
     // distance, strictly): its sink step cannot move the node -- the heap
     // keeps parent >= child, so every child is <= the old key < the new key --
     // which leaves the shift-up at the node's position.
-    __device__ __forceinline__ void raise(int v, double key) { shift_up(pos[v] - 2, HNode{key, v, 0}); }
+    __device__ __forceinline__ void raise(int v, double key) { shift_up((kAll ? pos[v] : uni(pos[v])) - 2, HNode{key, v, 0}); }
 };
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -189,12 +217,18 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
         h.push(src, 0.0);
         int to_reach = A;
         while (h.n > 0 && to_reach > 0) {
-            double key;
-            const int u = h.pop(&key);
-            const double mindist = -key;
-            if (g.vertex_slot[u] >= 0) --to_reach;
-            const double ru = rel[u];
-            const int k0 = g.inc_off[u], k1 = g.inc_off[u + 1];
+            // the loads that relaxing u needs (CSR range, rel[u], its slot)
+            // are issued before the root is removed: the sink touches heap
+            // nodes and positions only, so their latency overlaps it
+            const HNode t = h.top_node();
+            const int u = t.v;
+            const double mindist = -t.key;
+            int k0 = g.inc_off[u], k1 = g.inc_off[u + 1];
+            double ru = rel[u];
+            int uslot = g.vertex_slot[u];
+            if (!kAll) k0 = uni(k0), k1 = uni(k1), ru = uni_d(ru), uslot = uni(uslot);
+            h.pop_top(u);
+            if (uslot >= 0) --to_reach;
             // kRelax batches of 64 incident edges are loaded together (CSR
             // loads, then the dist gathers) before their updates are applied:
             // an update only writes the dist of its own neighbour, and a

@@ -41,6 +41,9 @@ GRAPHS = {
     "sparse200_dir_ns": (synth.sparse_graph_gml(200, 0x5EED0022, ns_variant=True, directed=True), 300),
     "sparse5000_hbm": (synth.sparse_graph_gml(5000, 0x5EED0042), 200),  # V > 4096: HBM-slab kernel
     "sparse4500_dir_ns_hbm": (synth.sparse_graph_gml(4500, 0x5EED0052, ns_variant=True, directed=True), 150),
+    # dense enough that Dijkstra's heap holds thousands of vertices: the
+    # block-loaded sink and parallel shift-up cross from LDS into the slab
+    "dense4400_hbm": (synth.sparse_graph_gml(4400, 0x5EED0062, avg_degree=60.0), 120),
 }
 
 
