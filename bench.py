@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--vertices", type=int, default=20_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-routing", action="store_true")
+    ap.add_argument("--c4", type=int, default=1, help="1: also time the C4 routing build (V=100k, H=200k)")
+    ap.add_argument("--c4-vertices", type=int, default=100_000)
+    ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--traffic", default=None, help="JSON with PMC-measured HBM bytes per launch")
     return ap.parse_args()
 
@@ -245,6 +248,39 @@ def main():
             "ms_per_table": tr * 1e3, "kernel": "k_sssp_rows<lds> (igraph-exact Dijkstra, 1 wave/source)",
             "c2_rows_s": t_rows_c2, "c2_host_pairs_per_s": (H * H) / max(max_over_ranks(t_rows_c2), 1e-9),
         }
+
+    # ------------------------------------------------- C4 routing-table build
+    # configs[4]: V=100k sparse graph, 200k hosts; rows sharded by source slot
+    # across ranks (no collective: the full matrix is not requested, §8e)
+    if not args.no_routing and args.c4:
+        t0 = time.perf_counter()
+        g4 = synth.sparse_graph_gml(args.c4_vertices, 0x5EED0004)
+        t4 = Topology(g4, device=local)
+        scenario.register_hosts(t4, args.c4_hosts, seed=1)
+        A4 = t4.slot_count()
+        log(f"C4 graph V={args.c4_vertices} H={args.c4_hosts} A={A4} ready in {time.perf_counter() - t0:.1f}s")
+        per4 = (A4 + world - 1) // world
+        l4, h4 = min(A4, rank * per4), min(A4, (rank + 1) * per4)
+        shard4 = torch.empty(max(h4 - l4, 1) * A4 * 2, dtype=torch.float64, device=dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        s0 = time.perf_counter()
+        if h4 > l4:
+            # rows land at absolute offsets from the base: base = shard - l4 rows
+            t4.build_rows_device(l4, h4, shard4.data_ptr() - l4 * A4 * 16)
+        torch.cuda.synchronize(dev)
+        barrier()
+        tr4 = max_over_ranks(time.perf_counter() - s0)
+        log(f"C4 rows {l4}:{h4} of {A4} in {tr4:.2f}s")
+        result.setdefault("routing", {})["c4"] = {
+            "config": "C4 sparse graph V=%d, H=%d hosts, A=%d attached; rows sharded over %d GPU(s)"
+                      % (args.c4_vertices, args.c4_hosts, A4, world),
+            "value": float(args.c4_hosts) ** 2 / tr4, "unit": "routed host-pairs/s",
+            "vertex_pairs_per_s": float(A4) * A4 / tr4, "build_s": tr4,
+            "kernel": "k_sssp_rows<slab> (igraph-exact Dijkstra, 1 wave/source, persistent)",
+        }
+        del shard4, t4
+        torch.cuda.empty_cache()
 
     # ------------------------------------------------------- CPU baseline (N=1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -51,6 +51,12 @@ struct __attribute__((aligned(16))) HNode {
     int pad;
 };
 
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ double uni_d(double v) {
     const long long b = __double_as_longlong(v);
@@ -68,6 +74,7 @@ struct Heap {
     HNode* rest;
     int* pos; // vertex -> position + 2 (igraph index2; 0 once popped)
     int n;
+    int lane;
 
     // every heap operand is wave-uniform: readfirstlane tells the compiler
     // so, and the heap then runs on scalar branches with LDS- or
@@ -114,6 +121,10 @@ struct Heap {
         for (;;) {
             const int l = 2 * e + 1;
             if (l >= n) break;
+            if (!kAll && l >= kTop - 1) { // children in the HBM slab
+                sink_blocks(e, x);
+                return;
+            }
             HNode c = ld(l);
             const HNode r = ld(l + 1);
             int ci = l;
@@ -121,6 +132,50 @@ struct Heap {
             if (!(x.key < c.key)) break;
             st(e, c);
             e = ci;
+        }
+        st(e, x);
+    }
+    // The part of a sink below the LDS levels: every level there costs an
+    // HBM round trip, so the wave loads the 62 nodes of the next 5 levels at
+    // once (lane t: level j = log2(t + 2), index t + 2 - 2^j under e, only
+    // positions < n) and makes the same comparisons and moves on readlane'd
+    // copies, reloading every 5 levels.  Moved nodes are stored above the
+    // next block, so a block never reads a position this sink has written.
+    __device__ __forceinline__ void sink_blocks(int e, const HNode& x) {
+        const int j = 31 - __builtin_clz((unsigned)lane + 2);
+        const int bi = lane + 2 - (1 << j);
+        for (;;) {
+            if (2 * e + 1 >= n) break;
+            const int p = (e + 1) * (1 << j) - 1 + bi;
+            double ck_l = 0.0;
+            int cv_l = 0;
+            if (lane < 62 && p < n) {
+                const HNode c = p < kTop ? top[p] : rest[p + 1];
+                ck_l = c.key;
+                cv_l = c.v;
+            }
+            int lv = 0, li = 0; // block level and index of e
+            for (; lv < 5; lv++) {
+                const int l = 2 * e + 1;
+                if (l >= n) break;
+                const int cl = (2 << lv) - 2 + 2 * li; // lane of the left child
+                double ck = readlane_d(ck_l, cl);
+                int cv = __builtin_amdgcn_readlane(cv_l, cl);
+                int ci = l;
+                if (l + 1 < n) {
+                    const double rk = readlane_d(ck_l, cl + 1);
+                    if (!(ck >= rk)) {
+                        ck = rk;
+                        cv = __builtin_amdgcn_readlane(cv_l, cl + 1);
+                        ci = l + 1;
+                    }
+                }
+                if (!(x.key < ck)) break;
+                st(e, HNode{ck, cv, 0});
+                li = 2 * li + (ci - l);
+                e = ci;
+            }
+            if (lv < 5) break;
         }
         st(e, x);
     }
@@ -143,12 +198,6 @@ struct Heap {
     __device__ __forceinline__ void raise(int v, double key) { shift_up((kAll ? pos[v] : uni(pos[v])) - 2, HNode{key, v, 0}); }
 };
 
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
 
 // orders one wave's per-lane accesses before its uniform ones (and back)
 __device__ __forceinline__ void wave_fence() {
@@ -200,7 +249,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
     // dense graphs (LDS kernel): 4 batches in flight; sparse ones rarely
     // have a second batch, and the slab kernel keeps its registers for
     // occupancy
-    constexpr int kRelax = kAll ? 4 : 1;
+    constexpr int kRelax = kAll ? 16 : 1;
     HNode* top = reinterpret_cast<HNode*>(smem) + (kAll ? 0 : w * kTop);
     HNode* rest = kAll ? nullptr : reinterpret_cast<HNode*>(slab + (size_t)gw * slab_stride);
     double* dist = reinterpret_cast<double*>(kAll ? top + V + 1 : rest + V + 2);
@@ -211,7 +260,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
         const int src = g.slot_vertex[row];
         for (int v = lane; v < V; v += 64) dist[v] = -1.0;
         wave_fence();
-        Heap<kAll> h{top, rest, pos, 0};
+        Heap<kAll> h{top, rest, pos, 0, lane};
         dist[src] = 0.0;
         rel[src] = 1.0;
         h.push(src, 0.0);
