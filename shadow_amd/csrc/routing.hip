@@ -254,17 +254,23 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
     constexpr int kRelax = kAll ? 16 : 1;
     HNode* top = reinterpret_cast<HNode*>(smem) + (kAll ? 0 : w * kTop);
     HNode* rest = kAll ? nullptr : reinterpret_cast<HNode*>(slab + (size_t)gw * slab_stride);
-    double* dist = reinterpret_cast<double*>(kAll ? top + V + 1 : rest + V + 2);
-    double* rel = dist + V;
-    int* pos = reinterpret_cast<int*>(rel + V);
+    // per-vertex distance and reliability: separate LDS arrays in the LDS
+    // kernel; in the slab one 16-B record {dist, rel} per vertex, so the
+    // stores after an improvement and the rel[u] read at its pop fall on the
+    // line the distance gather already fetched (the slab kernel is bound by
+    // random HBM line requests)
+    double* dr = reinterpret_cast<double*>(kAll ? top + V + 1 : rest + V + 2);
+    int* pos = reinterpret_cast<int*>(dr + 2 * (size_t)V);
+    auto DI = [&](int x) -> double& { return kAll ? dr[x] : dr[2 * (size_t)x]; };
+    auto RI = [&](int x) -> double& { return kAll ? dr[V + x] : dr[2 * (size_t)x + 1]; };
 
     for (int row = row_lo + gw; row < row_hi; row += nw) {
         const int src = g.slot_vertex[row];
-        for (int v = lane; v < V; v += 64) dist[v] = -1.0;
+        for (int v = lane; v < V; v += 64) DI(v) = -1.0;
         wave_fence();
         Heap<kAll> h{top, rest, pos, 0, lane};
-        dist[src] = 0.0;
-        rel[src] = 1.0;
+        DI(src) = 0.0;
+        RI(src) = 1.0;
         h.push(src, 0.0);
         int to_reach = A;
         while (h.n > 0 && to_reach > 0) {
@@ -275,7 +281,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
             const int u = t.v;
             const double mindist = -t.key;
             int k0 = g.inc_off[u], k1 = g.inc_off[u + 1];
-            double ru = rel[u];
+            double ru = RI(u);
             int uslot = g.vertex_slot[u];
             if (!kAll) k0 = uni(k0), k1 = uni(k1), ru = uni_d(ru), uslot = uni(uslot);
             h.pop_top(u);
@@ -300,7 +306,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
                 }
 #pragma unroll
                 for (int q = 0; q < kRelax; q++) {
-                    const double cur = dist[v[q]];
+                    const double cur = DI(v[q]);
                     const bool ok = b0 + q * 64 + lane < k1;
                     fresh[q] = ok && cur < 0;
                     imp[q] = ok && (cur < 0 || alt[q] < cur);
@@ -314,8 +320,8 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
                         m &= m - 1;
                         const int vv = __builtin_amdgcn_readlane(v[q], l);
                         const double aa = readlane_d(alt[q], l);
-                        dist[vv] = aa;
-                        rel[vv] = readlane_d(rv[q], l);
+                        DI(vv) = aa;
+                        RI(vv) = readlane_d(rv[q], l);
                         if ((fm >> l) & 1ull) h.push(vv, -aa);
                         else h.raise(vv, -aa);
                     }
@@ -327,14 +333,14 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
         for (int j = lane; j < A; j += 64) {
             if (j == row) continue;
             const int v = g.slot_vertex[j];
-            const double l = dist[v];
+            const double l = DI(v);
             ShdEntry e;
             if (l < 0) {
                 e.lat = -1.0; // unreachable: impossible on a validated (strongly connected) graph
                 e.rel = 0.0;
             } else {
                 e.lat = (l == 0) ? 1.0 : l; // topology.c:1787-1791
-                e.rel = rel[v];
+                e.rel = RI(v);
             }
             out[j] = e;
         }
