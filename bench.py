@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--c4", type=int, default=1, help="1: also time the C4 routing build (V=100k, H=200k)")
     ap.add_argument("--c4-vertices", type=int, default=100_000)
     ap.add_argument("--c4-hosts", type=int, default=200_000)
-    ap.add_argument("--traffic", default=None, help="JSON with PMC-measured HBM bytes per launch")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
+                    help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
 
@@ -188,10 +189,13 @@ def main():
     achieved = [alg_bytes[k] / (per_launch_ms[k] * 1e-3) / 1e9 if per_launch_ms[k] > 0 else 0.0 for k in range(4)]
     total_pkts = P * world * args.steps
     value = total_pkts / dt
-    traffic = None
+    traffic, traffic_src = None, None
     if args.traffic and os.path.exists(args.traffic):
         with open(args.traffic) as f:
-            traffic = json.load(f).get(STAGES[dom])
+            tj = json.load(f)
+        if STAGES[dom] in tj:
+            traffic = tj[STAGES[dom]]["bytes"]
+            traffic_src = os.path.relpath(args.traffic, ROOT) + ": " + tj.get("_source", "")
 
     result = {
         "metric": METRIC,
@@ -214,7 +218,8 @@ def main():
         },
         "roofline": {
             "kernel": STAGES[dom], "bound": "hbm", "achieved": achieved[dom], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved[dom] / HBM_PEAK_GBS, "traffic": traffic,
+            "frac": achieved[dom] / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "traffic_GBps": (traffic / (per_launch_ms[dom] * 1e-3) / 1e9) if traffic else None,
             "per_stage_ms": dict(zip(STAGES, per_launch_ms)),
             "per_stage_GBps": dict(zip(STAGES, achieved)),
             "alg_bytes_per_launch": dict(zip(STAGES, alg_bytes)),

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Folds rocprofv3 PMC passes into per-launch HBM traffic (bytes) per bench
+stage, as MI355X_MICROARCH.md §HBM prescribes for gfx950: FETCH_SIZE counts
+64 B per TCC_EA0_RDREQ while the requests are 128-B lines (x2 correction,
+cross-checked against TCC_EA0_RDREQ_sum in the third pass); WRITE_SIZE is
+taken as is (it equals 64 B x WRREQ_64B + 32 B x the other write requests).
+Usage: scripts/traffic.py OUT.json PASS_CSV...   (profiles/r01_s5a_pmc_p*.csv)"""
+import csv
+import json
+import re
+import sys
+
+STAGE = {"k_pkt_scatter": "packet_scatter", "k_place_rank": "place", "k_place_bucket": "place",
+         "k_segsort_dst": "segment_sort", "k_sssp_rows<false>": "routing_slab", "k_sssp_rows<true>": "routing_lds"}
+
+
+def kname(n):
+    m = re.search(r"(k_\w+(?:<\w+>)?)", n)
+    return m.group(1) if m else n
+
+
+def main():
+    out, files = sys.argv[1], sys.argv[2:]
+    agg = {}
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            k = kname(r["Kernel_Name"])
+            k = "k_pkt_scatter" if k.startswith("k_pkt_scatter") else k
+            agg.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+    res = {}
+    for k, st in STAGE.items():
+        f, w = agg.get((k, "FETCH_SIZE")), agg.get((k, "WRITE_SIZE"))
+        if not f or not w:
+            continue
+        rd = 2 * 1024 * sum(f) / len(f)
+        wr = 1024 * sum(w) / len(w)
+        rq = agg.get((k, "TCC_EA0_RDREQ_sum"))
+        wq = agg.get((k, "TCC_EA0_WRREQ_sum"))
+        res[st] = {"bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                   "rd_requests": sum(rq) / len(rq) if rq else None,
+                   "wr_requests": sum(wq) / len(wq) if wq else None}
+    res["_source"] = "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | TCC_EA0_*REQ (separate passes) over " \
+                     "`bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline`; FETCH_SIZE x2 (gfx950)"
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
