@@ -334,3 +334,74 @@ def test_full_size_c3_round_bit_exact():
     assert np.array_equal(out, oout)
     offs = d_off.cpu().numpy().astype(np.int64)
     assert offs[-1] == len(out) and np.array_equal(np.diff(offs), np.bincount(out["dst_host"], minlength=H))
+
+
+# ---- edge cases of the hand-off (empty / single / all dropped / bad ids) ----
+
+def test_empty_and_single_packet_rounds(pipeline):
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    pk = synth.packet_batch(1, H, 0x5EED0400, 100_000_000, 10_000_000, st)
+    for batch in (pk[:0], pk):
+        out, offs, status, mt = top.round(batch, 110_000_000, 10**15)
+        oout, ostatus, omt = orc.round(ips, batch, 110_000_000, 10**15)
+        assert len(status) == len(batch)
+        assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+        assert offs[-1] == len(out)
+    assert mt != 2**64 - 1  # the single packet was delivered
+
+
+def test_every_packet_dropped(pipeline):
+    """Loss 1.0 on every edge (reliability 0): only draws of exactly 0 keep a
+    packet with payload; then an end time before the window drops the rest."""
+    import re
+    gml = re.sub(r"packet_loss [0-9.eE+-]+", "packet_loss 1.0", synth.complete_graph_gml(20, 0x5EED0071))
+    top, orc, ips, st = make_pair(gml, 60)
+    pk = synth.packet_batch(30000, 60, 0x5EED0410, 100_000_000, 10_000_000, st, p_payload=1.0)
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    DELIVERED, LOSS = 1, 0  # shdnet.h: SHD_DROPPED_LOSS = 0, SHD_DELIVERED = 1, SHD_DROPPED_END = 2
+    assert len(out) == (status == DELIVERED).sum() < 10 and (status == LOSS).sum() >= len(pk) - 10
+    top2, orc2, ips2, st2 = make_pair(GRAPHS["complete30_ms"][0], 90)
+    pk2 = synth.packet_batch(30000, 90, 0x5EED0411, 100_000_000, 10_000_000, st2, p_payload=0.5)
+    out, offs, status, mt = top2.round(pk2, 110_000_000, 100_000_000)  # end time = window start
+    oout, ostatus, omt = orc2.round(ips2, pk2, 110_000_000, 100_000_000)
+    assert np.array_equal(status, ostatus) and mt == omt == 2**64 - 1 and len(out) == len(oout) == 0
+    assert offs[-1] == 0
+
+
+def test_device_api_unknown_hosts_not_delivered(pipeline):
+    """Records naming host ids outside the registered range get status 0xff and
+    no event; every other record is decided exactly as the oracle does."""
+    import torch
+    gml, H = GRAPHS["sparse300_ns"]
+    top, orc, ips, st = make_pair(gml, H)
+    top.touch_all()
+    lat, rel, sv = top.table()
+    orc.preload(sv, lat, rel)
+    pk = synth.packet_batch(20000, H, 0x5EED0420, 100_000_000, 10_000_000, st)
+    bad = np.zeros(len(pk), dtype=bool)
+    bad[::97] = True
+    pk["dst_host"][::194] = H + 5
+    pk["src_host"][97::194] = 0xFFFFFFF0
+    n = len(pk)
+    d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                       d_status.data_ptr(), d_cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    status = d_status.cpu().numpy()
+    cnt = d_cnt.cpu().numpy().view(np.uint64)
+    out = d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]].copy()
+    assert (status[bad] == 0xFF).all()
+    good = np.flatnonzero(~bad)
+    oout, ostatus, omt = orc.round(ips, pk[good], 110_000_000, 10**15)
+    oout = oout.copy()
+    oout["pkt_index"] = good[oout["pkt_index"]]
+    assert np.array_equal(status[good], ostatus) and cnt[1] == omt
+    assert np.array_equal(out, oout)
