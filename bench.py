@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--c4", type=int, default=1, help="1: also time the C4 routing build (V=100k, H=200k)")
     ap.add_argument("--c4-vertices", type=int, default=100_000)
     ap.add_argument("--c4-hosts", type=int, default=200_000)
+    ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
+    ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
@@ -224,7 +226,7 @@ def main():
             "per_stage_GBps": dict(zip(STAGES, achieved)),
             "alg_bytes_per_launch": dict(zip(STAGES, alg_bytes)),
             "timing": "HIP events on the launch stream, averaged over the timed steps",
-            "pipeline": "bucket" if os.environ.get("SHD_PACKET_PIPELINE") == "bucket" else "rank",
+            "pipeline": os.environ.get("SHD_PACKET_PIPELINE") or "slab",
         },
     }
 
@@ -261,7 +263,7 @@ def main():
         t0 = time.perf_counter()
         g4 = synth.sparse_graph_gml(args.c4_vertices, 0x5EED0004)
         t4 = Topology(g4, device=local)
-        scenario.register_hosts(t4, args.c4_hosts, seed=1)
+        _, states4, _ = scenario.register_hosts(t4, args.c4_hosts, seed=1)
         A4 = t4.slot_count()
         log(f"C4 graph V={args.c4_vertices} H={args.c4_hosts} A={A4} ready in {time.perf_counter() - t0:.1f}s")
         per4 = (A4 + world - 1) // world
@@ -284,6 +286,42 @@ def main():
             "vertex_pairs_per_s": float(A4) * A4 / tr4, "build_s": tr4,
             "kernel": "k_sssp_rows<slab> (igraph-exact Dijkstra, 1 wave/source, persistent)",
         }
+        # C4 packet delivery: 1,000 rounds of packets on the full 100k-vertex
+        # table.  At N=1 the table is resident (A4^2 x 16 B = 120 GB of the
+        # 288 GB); at N>1 the rows stay sharded (no full matrix requested), so
+        # the rounds leg runs on one GPU only.
+        if world == 1 and args.c4_rounds > 0:
+            t4.adopt_table_device_resident(shard4.data_ptr())  # no 120 GB host mirror
+            P4 = args.c4_packets
+            pk4 = synth.packet_batch(P4, args.c4_hosts, 0x5EED0008, 100_000_000, 10_000_000, states4)
+            r_recs = torch.from_numpy(pk4.view(np.uint8)).to(dev)
+            r_out = torch.empty(P4 * 32, dtype=torch.uint8, device=dev)
+            r_off = torch.empty(args.c4_hosts + 1, dtype=torch.int32, device=dev)
+            r_status = torch.empty(P4, dtype=torch.uint8, device=dev)
+            r_cnt = torch.empty(2, dtype=torch.int64, device=dev)
+
+            def round4():
+                t4.process_device(r_recs.data_ptr(), P4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
+                                  r_status.data_ptr(), r_cnt.data_ptr(), sptr)
+
+            for _ in range(3):
+                round4()
+            torch.cuda.synchronize(dev)
+            s0 = time.perf_counter()
+            for _ in range(args.c4_rounds):
+                round4()
+            torch.cuda.synchronize(dev)
+            tp4 = time.perf_counter() - s0
+            c4 = result["routing"]["c4"]
+            c4["rounds"] = {
+                "rounds": args.c4_rounds, "packets_per_round": P4, "seconds": tp4,
+                "packets_per_s": P4 * args.c4_rounds / tp4, "ms_per_round": tp4 / args.c4_rounds * 1e3,
+                "delivered_per_round": int(r_cnt.cpu().numpy().view(np.uint64)[0]),
+                "input": "one synthetic batch (uniform src/dst over the 200k hosts, reserved rand_r pre-states) "
+                         "replayed every round, resident in HBM; full 120 GB table resident",
+            }
+            log(f"C4 {args.c4_rounds} rounds x {P4} packets in {tp4:.2f}s")
+            del r_recs, r_out, r_status
         del shard4, t4
         torch.cuda.empty_cache()
 

@@ -108,6 +108,13 @@ int shd_topology_copy_table(ShdTopology* top, double* lat_ms, double* rel, int32
 int shd_topology_slot_count(ShdTopology* top, int* slots);
 int shd_topology_build_rows_device(ShdTopology* top, int row_lo, int row_hi, void* d_table);
 int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
+/* Adopts a device table WITHOUT a host mirror (tables larger than host RAM
+ * wants: A = 86k slots is 120 GB) and releases every row in slot order (the
+ * touch_all steady state).  Host lookups then read single entries from the
+ * device.  use_shortest_path graphs only (-ENOTSUP), before any row was
+ * released (-EBUSY).  Replaces nothing in the reference: topology.c keeps
+ * its paths in host hash tables (topology.c:1217-1265). */
+int shd_topology_adopt_table_device_resident(ShdTopology* top, void* d_table);
 /* Marks every attached vertex row touched, in slot order (steady state of a
  * long simulation; used by benchmarks before timing). */
 int shd_topology_touch_all(ShdTopology* top);

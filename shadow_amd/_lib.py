@@ -51,6 +51,7 @@ PROTOS = {
     "shd_topology_slot_count": (C.c_int, [_P, _ip]),
     "shd_topology_build_rows_device": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "shd_topology_adopt_table_device": (C.c_int, [_P, _P]),
+    "shd_topology_adopt_table_device_resident": (C.c_int, [_P, _P]),
     "shd_topology_touch_all": (C.c_int, [_P]),
     "shd_topology_host_count": (C.c_int, [_P, _u32p]),
     "shd_round_begin": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64]),

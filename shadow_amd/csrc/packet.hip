@@ -42,6 +42,7 @@ constexpr int kChunks = 1024;      // scatter workgroups per launch (columns of 
 constexpr int kMaxBuckets = 4096;  // destination buckets (LDS histogram size)
 constexpr int kScanTile = 4096;    // 256 threads x 16
 constexpr int kSmallSeg = 256;     // wave register sort up to 4 events per lane
+constexpr uint32_t kSlab = kSmallSeg; // "slab" pipeline: event slots reserved per destination
 constexpr int kSortBlock = 1024;   // k_bucket_sort workgroup (16 waves)
 constexpr int kMaxPerBucket = 2 * kSortBlock; // destinations per bucket (LDS scan width)
 constexpr int kBucketCap = 4096;   // events per bucket staged in LDS by k_bucket_sort (30 B each)
@@ -137,19 +138,26 @@ __device__ __forceinline__ uint32_t col_of(const Bucketing& bk, uint32_t g) {
     return x * q + (x < r ? x : r) + (g >> 3);
 }
 
-// kRank = true ("rank" pipeline): each delivered event takes its slot in its
+// kMode 1 ("rank" pipeline): each delivered event takes its slot in its
 // destination segment from a per-destination global counter (the counter's
 // old value, carried in pad); cnt1 is then the per-destination count array.
-// kRank = false ("bucket" pipeline, default): the slot inside the
-// (workgroup, bucket) run comes from the workgroup's LDS histogram (old
-// value of an LDS atomic, carried in pad) -- no global atomics per event;
-// cnt1 is the bucket x tile matrix.
-template <bool kRank>
+// kMode 2 ("slab" pipeline, default): the same counter, but the event is
+// written straight into its destination's slab of kSlab slots,
+// tmp[dst * kSlab + slot]; slots >= kSlab go to the overflow list ovf
+// (novf = its length), placed later by k_place_ovf.  No record-order copy
+// and no placement pass over the whole batch.
+// kMode 0 ("bucket" pipeline): the slot inside the (workgroup, bucket) run
+// comes from the workgroup's LDS histogram (old value of an LDS atomic,
+// carried in pad) -- no global atomics per event; cnt1 is the bucket x tile
+// matrix.
+template <int kMode>
 __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
                                                         uint64_t barrier, uint64_t end_time, uint64_t boot_end,
                                                         Bucketing bk, ShdDeliv* __restrict__ tmp,
                                                         uint8_t* __restrict__ status, uint32_t* __restrict__ cnt1,
-                                                        unsigned long long* counters) {
+                                                        unsigned long long* counters, ShdDeliv* __restrict__ ovf,
+                                                        uint32_t* __restrict__ novf) {
+    constexpr bool kRank = kMode != 0;
     __shared__ uint32_t hist[kRank ? 1 : kMaxBuckets];
     __shared__ unsigned long long wmin[kBlock / 64];
     if (!kRank)
@@ -222,7 +230,10 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
                         uint32_t rank;
                         if (kRank) rank = atomicAdd(&cnt1[p[k].dst_host], 1u);
                         else rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
-                        st_ev(&tmp[idx[k]], ShdDeliv{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank});
+                        const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
+                        if (kMode != 2) st_ev(&tmp[idx[k]], ev);
+                        else if (rank < kSlab) st_ev(&tmp[(size_t)p[k].dst_host * kSlab + rank], ev);
+                        else st_ev(&ovf[atomicAdd(novf, 1u)], ev); // rare: segments above kSlab
                         if (t >= barrier && t < mn) mn = t; // worker.c:350-363
                     }
                 }
@@ -946,12 +957,28 @@ __global__ __launch_bounds__(256) void k_place_rank(const ShdDeliv* __restrict__
     }
 }
 
+// "slab" pipeline: the overflow events (slot >= kSlab of a destination with
+// more than kSlab events) go to off[dst] + slot of the staging array, where
+// k_segsort_dst has put the first kSlab slots.  Grid-stride over the device
+// count, so the launch costs nothing when no segment overflowed.
+__global__ __launch_bounds__(256) void k_place_ovf(const ShdDeliv* __restrict__ ovf, const uint32_t* __restrict__ novf,
+                                                   const uint32_t* __restrict__ off, ShdDeliv* __restrict__ scr) {
+    const uint32_t m = *novf;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const ShdDeliv r = ld_ev(&ovf[i]);
+        st_ev(&scr[off[r.dst_host] + r.pad], r);
+    }
+}
+
 // One wave per destination segment of up to kSmallSeg events; larger ones go
-// to the bitonic-in-HBM list.
-__global__ __launch_bounds__(256) void k_segsort_dst(const ShdDeliv* __restrict__ scr, const uint32_t* __restrict__ off,
+// to the bitonic-in-HBM list.  With a slab (the "slab" pipeline) segment d's
+// events are read from slab[d * kSlab ...]; a larger segment first copies its
+// kSlab slab slots to the front of its staging range scr[off[d] ...].
+__global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr, const uint32_t* __restrict__ off,
                                                      uint32_t H, uint32_t host_lo, ShdDeliv* __restrict__ out,
                                                      uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
-                                                     uint32_t rsort, uint32_t flo, uint32_t fhi) {
+                                                     uint32_t rsort, uint32_t flo, uint32_t fhi,
+                                                     const ShdDeliv* __restrict__ slab) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
@@ -959,8 +986,18 @@ __global__ __launch_bounds__(256) void k_segsort_dst(const ShdDeliv* __restrict_
         const uint32_t b = off[d], n = off[d + 1] - b;
         const uint32_t dh = d + host_lo;
         if (n == 0) continue;
-        if (n <= (uint32_t)kSmallSeg) sort_segment(rsort, scr, b, nullptr, n, dh, out, b, lane);
-        else if (lane == 0) big[atomicAdd(nbig, 1u)] = d;
+        if (slab) {
+            if (n <= kSlab) {
+                sort_segment(rsort, slab, d * kSlab, nullptr, n, dh, out, b, lane);
+            } else {
+                for (uint32_t i = lane; i < kSlab; i += 64) st_ev(&scr[b + i], ld_ev(&slab[(size_t)d * kSlab + i]));
+                if (lane == 0) big[atomicAdd(nbig, 1u)] = d;
+            }
+        } else if (n <= (uint32_t)kSmallSeg) {
+            sort_segment(rsort, scr, b, nullptr, n, dh, out, b, lane);
+        } else if (lane == 0) {
+            big[atomicAdd(nbig, 1u)] = d;
+        }
     }
 }
 
@@ -979,7 +1016,9 @@ struct Ws {
     uint32_t* bsum = nullptr;
     uint32_t cap_h = 0;
     uint32_t* big = nullptr;
-    uint32_t* nbig = nullptr;
+    uint32_t* nbig = nullptr; // [0] big segments, [1] slab overflow events
+    size_t cap_slab = 0;      // slab pipeline: H x kSlab event slots
+    ShdDeliv* slab = nullptr;
 };
 Ws g_ws;
 
@@ -1033,6 +1072,17 @@ int ws_reserve(size_t n, size_t m, uint32_t H) {
         g_ws.cap_h = cap;
     }
     return 0;
+}
+
+int slab_reserve(uint32_t H) {
+    const size_t need = (size_t)H * kSlab;
+    if (need <= g_ws.cap_slab) return 0;
+    (void)hipFree(g_ws.slab);
+    g_ws.slab = nullptr;
+    g_ws.cap_slab = 0;
+    int rc = hip_status(hipMalloc((void**)&g_ws.slab, sizeof(ShdDeliv) * need), "hipMalloc ws.slab");
+    if (!rc) g_ws.cap_slab = need;
+    return rc;
 }
 
 unsigned grid_for(size_t n, unsigned block, unsigned cap) {
@@ -1140,34 +1190,45 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* ra
 
 // scan of per-destination counts straight into the offsets, atomic-free
 // placement by rank, one wave per destination segment
+// slab: the scatter already wrote each event to its destination's slab (or
+// the overflow list); only overflow events are placed.
 int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n,
                         uint32_t host_lo, uint32_t H, ShdDeliv* out, uint32_t* offsets,
-                        unsigned long long* counters, hipStream_t s) {
+                        unsigned long long* counters, hipStream_t s, const ShdDeliv* slab = nullptr) {
     const uint32_t nb = (uint32_t)((H + kScanTile - 1) / kScanTile);
     hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, g_ws.cnt1, (size_t)H, offsets, g_ws.bsum);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g_ws.bsum, nb);
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for((size_t)H + 1, 256, 1u << 30)), dim3(256), 0, s, offsets, (size_t)H,
                        g_ws.bsum, nb, counters);
     mark(2, s);
-    if (n)
+    if (slab)
+        hipLaunchKernelGGL(k_place_ovf, dim3(512), dim3(256), 0, s, g_ws.st2, g_ws.nbig + 1, offsets, g_ws.st1);
+    else if (n)
         hipLaunchKernelGGL(k_place_rank, dim3(grid_for(n, 256 * kBatch, 1u << 20)), dim3(256), 0, s, in, status, rank,
                            n, host_lo, H, offsets, g_ws.st1, 0u, H);
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.st1, offsets, H, host_lo, out,
-                       g_ws.big, g_ws.nbig, rank_sort(), 0u, H);
+                       g_ws.big, g_ws.nbig, rank_sort(), 0u, H, slab);
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort_rank launch");
 }
 
-// The per-destination-counter pipeline is the default (measured r01: 1.14 vs
-// 1.19 ms per 10M-packet C3 round); SHD_PACKET_PIPELINE=bucket selects the
-// atomic-free bucket partition instead.
-bool use_rank_pipeline() {
+// SHD_PACKET_PIPELINE: "slab" (default for the packet round), "rank"
+// (per-destination counters + a placement pass over the batch) or "bucket"
+// (atomic-free bucket partition).  The slab pipeline needs H x kSlab x 32 B
+// of HBM (100k hosts: 0.8 GB); above kMaxSlabBytes it falls back to rank.
+enum Pipeline { kBucketPipe = 0, kRankPipe = 1, kSlabPipe = 2 };
+constexpr size_t kMaxSlabBytes = 32ull << 30;
+int pipeline_for(uint32_t H, bool slab_ok) {
     const char* v = getenv("SHD_PACKET_PIPELINE");
-    return !(v && strcmp(v, "bucket") == 0);
+    if (v && strcmp(v, "bucket") == 0) return kBucketPipe;
+    if (v && strcmp(v, "rank") == 0) return kRankPipe;
+    if (!slab_ok || (size_t)H * kSlab * sizeof(ShdDeliv) > kMaxSlabBytes) return kRankPipe;
+    return kSlabPipe;
 }
+bool use_rank_pipeline() { return pipeline_for(0, false) != kBucketPipe; }
 
 } // namespace
 
@@ -1176,14 +1237,16 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
                                     uint32_t* d_dst_offsets, uint8_t* d_status, uint64_t* d_counters, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t H = c->nhosts;
-    const bool rk = use_rank_pipeline();
+    const int pipe = pipeline_for(H, true);
+    const bool rk = pipe != kBucketPipe;
     Bucketing bk;
     int rc = make_bucketing(0, H, n, &bk);
     if (rc) return rc;
     const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
     if ((rc = ws_reserve(n, m, H))) return rc;
+    if (pipe == kSlabPipe && (rc = slab_reserve(H))) return rc;
     unsigned long long* counters = (unsigned long long*)d_counters;
-    if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 4, s), "memset nbig")) ||
+    if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 8, s), "memset nbig")) ||
         (rc = hip_status(hipMemsetAsync(counters, 0xff, 16, s), "memset counters")))
         return rc;
     // rank: per-destination counters start at zero; bucket: every tile writes
@@ -1191,17 +1254,25 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     if ((rk || !n) && (rc = hip_status(hipMemsetAsync(g_ws.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
     mark(0, s);
     if (n) {
-        if (rk)
-            hipLaunchKernelGGL(k_pkt_scatter<true>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.tmp, d_status, g_ws.cnt1, counters);
+        if (pipe == kSlabPipe)
+            hipLaunchKernelGGL(k_pkt_scatter<2>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
+                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
+                               g_ws.nbig + 1);
+        else if (rk)
+            hipLaunchKernelGGL(k_pkt_scatter<1>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
+                               end_time, bootstrap_end, bk, g_ws.tmp, d_status, g_ws.cnt1, counters, nullptr,
+                               nullptr);
         else
-            hipLaunchKernelGGL(k_pkt_scatter<false>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.tmp, d_status, g_ws.cnt1, counters);
+            hipLaunchKernelGGL(k_pkt_scatter<0>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
+                               end_time, bootstrap_end, bk, g_ws.tmp, d_status, g_ws.cnt1, counters, nullptr,
+                               nullptr);
     }
     mark(1, s);
     if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
-    rc = rk ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s)
-            : group_and_sort(g_ws.tmp, d_status, nullptr, n, bk, d_out, d_dst_offsets, counters, s);
+    rc = pipe == kSlabPipe
+             ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s, g_ws.slab)
+         : rk ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s)
+              : group_and_sort(g_ws.tmp, d_status, nullptr, n, bk, d_out, d_dst_offsets, counters, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "packet round");
 }

@@ -178,6 +178,7 @@ int shd_topology_copy_table(ShdTopology* t, double* lat, double* rel, int32_t* s
     int rc = shd_topology_build_routes(t);
     if (rc) return rc;
     if (cap < t->A) return shd_fail(-ENOSPC, "need %d slots", t->A);
+    if (!t->h_tab) return shd_fail(-ENOTSUP, "the table is device-resident (no host mirror)");
     size_t n = (size_t)t->A * (size_t)t->A;
     for (size_t k = 0; k < n; k++) {
         if (lat) lat[k] = t->h_tab[k].lat;

@@ -35,6 +35,7 @@
 
 #include <cerrno>
 #include <cstdlib>
+#include <cstring>
 
 #include "shd_internal.h"
 
@@ -365,6 +366,30 @@ __global__ __launch_bounds__(256) void k_direct_rows(ShdGraphDev g, int row_lo, 
     }
 }
 
+// Released minimum of a device-resident table: min lat over (i, j), i < j,
+// lat >= 0 (the pairs touch_all's row-by-row release stores).  Latencies
+// are >= 0 doubles, whose bit patterns order like u64; ~0 = none.  One
+// block per row range; lanes read consecutive entries of a row (coalesced).
+__global__ __launch_bounds__(256) void k_min_upper(const ShdEntry* __restrict__ tab, int A,
+                                                   unsigned long long* __restrict__ out) {
+    unsigned long long m = ~0ull;
+    for (int i = blockIdx.x; i < A; i += gridDim.x) {
+        const ShdEntry* row = tab + (size_t)i * (size_t)A;
+        for (int j = i + 1 + threadIdx.x; j < A; j += blockDim.x) {
+            const double l = row[j].lat;
+            if (l >= 0.0) {
+                const unsigned long long b = (unsigned long long)__double_as_longlong(l);
+                m = b < m ? b : m;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off);
+        m = o < m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(out, m);
+}
+
 int hip_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return 0;
     return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
@@ -421,5 +446,22 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
     rc = hip_status(hipGetLastError(), "k_sssp_rows<hbm> launch");
     if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_rows<hbm>");
     (void)hipFree(slab);
+    return rc;
+}
+
+extern "C" int shd_dev_min_upper(const ShdEntry* tab, int A, double* out) {
+    *out = -1.0;
+    if (A < 2) return 0;
+    unsigned long long* d = nullptr;
+    int rc = hip_status(hipMalloc((void**)&d, sizeof *d), "hipMalloc min");
+    if (rc) return rc;
+    unsigned long long h = ~0ull;
+    if (!(rc = hip_status(hipMemcpy(d, &h, sizeof h, hipMemcpyHostToDevice), "hipMemcpy min"))) {
+        hipLaunchKernelGGL(k_min_upper, dim3(A < 8192 ? A : 8192), dim3(256), 0, nullptr, tab, A, d);
+        rc = hip_status(hipGetLastError(), "k_min_upper launch");
+        if (!rc) rc = hip_status(hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost), "hipMemcpy min");
+    }
+    (void)hipFree(d);
+    if (!rc && h != ~0ull) memcpy(out, &h, sizeof h);
     return rc;
 }

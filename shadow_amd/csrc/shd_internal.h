@@ -82,6 +82,8 @@ int shd_dev_sync(void);
  * use_sp = 1: igraph-exact Dijkstra per source slot + self path (R-7, R-9);
  * use_sp = 0: direct edge per pair (R-10).  Synchronous. */
 int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab);
+/* min latency over the entries (i, j), i < j, lat >= 0 of an A x A table; -1 if none */
+int shd_dev_min_upper(const ShdEntry* tab, int A, double* out);
 
 /* Packet round on device arrays (see shd_round_process_device). */
 typedef struct {

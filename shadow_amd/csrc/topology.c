@@ -728,10 +728,21 @@ static void note_released(ShdTopology* t, double lat) {
     }
 }
 
-/* Releases row i (a touch): every (i, y) with y untouched. */
+/* Entry k of the table: from the host mirror, or one 16-byte read of the
+ * device table when it is device-resident (no mirror). */
+static ShdEntry ent(const ShdTopology* t, size_t k) {
+    if (t->h_tab) return t->h_tab[k];
+    ShdEntry e = {-1.0, 0.0};
+    if (shd_dev_d2h(&e, t->d_tab + k, sizeof e)) e.lat = -1.0;
+    return e;
+}
+
+/* Releases row i (a touch): every (i, y) with y untouched.  Device-resident
+ * tables release every row at adoption, so they never get here. */
 static void touch_row(ShdTopology* t, int i) {
     t->touch[i] = t->next_touch++;
     t->touch_dirty = 1;
+    if (!t->h_tab) return;
     const ShdEntry* row = t->h_tab + (size_t)i * (size_t)t->A;
     double mn = 0;
     int any = 0;
@@ -757,13 +768,12 @@ static void set_pair_bit(ShdTopology* t, int i, int j) {
 /* _topology_getPathEntry (topology.c:1900-1981) for slots (si, di): applies
  * the side effects and returns the slot pair whose entry answers. */
 int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) {
-    const ShdEntry* tab = t->h_tab;
     size_t A = (size_t)t->A;
     if (t->use_sp) {
         if (si == di) {
             if (!t->self_released[si]) {
                 t->self_released[si] = 1;
-                note_released(t, tab[(size_t)si * A + (size_t)si].lat);
+                note_released(t, ent(t, (size_t)si * A + (size_t)si).lat);
             }
             *oi = *oj = si;
         } else {
@@ -777,14 +787,15 @@ int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) {
     } else {
         int hit = pair_bit(t, si, di) || (!t->directed && pair_bit(t, di, si));
         if (!hit && !pair_bit(t, di, si)) {
-            if (tab[(size_t)si * A + (size_t)di].lat < 0) return shd_fail(-EHOSTUNREACH, "no direct edge");
+            const double lat = ent(t, (size_t)si * A + (size_t)di).lat;
+            if (lat < 0) return shd_fail(-EHOSTUNREACH, "no direct edge");
             set_pair_bit(t, si, di);
-            note_released(t, tab[(size_t)si * A + (size_t)di].lat);
+            note_released(t, lat);
         }
         if (pair_bit(t, si, di)) *oi = si, *oj = di;
         else *oi = di, *oj = si;
     }
-    if (tab[(size_t)*oi * A + (size_t)*oj].lat < 0) return shd_fail(-EHOSTUNREACH, "unroutable pair");
+    if (ent(t, (size_t)*oi * A + (size_t)*oj).lat < 0) return shd_fail(-EHOSTUNREACH, "unroutable pair");
     return 0;
 }
 
@@ -799,33 +810,33 @@ static int slots_of(ShdTopology* t, uint32_t sip, uint32_t dip, int* si, int* di
     return 0;
 }
 
-static int entry_of(ShdTopology* t, uint32_t sip, uint32_t dip, const ShdEntry** e, int* oi, int* oj) {
+static int entry_of(ShdTopology* t, uint32_t sip, uint32_t dip, ShdEntry* e, int* oi, int* oj) {
     int si = 0, di = 0;
     int rc = slots_of(t, sip, dip, &si, &di);
     if (rc) return rc;
     rc = shd_resolve(t, si, di, oi, oj);
     if (rc) return rc;
-    *e = t->h_tab + (size_t)*oi * (size_t)t->A + (size_t)*oj;
+    *e = ent(t, (size_t)*oi * (size_t)t->A + (size_t)*oj);
     return 0;
 }
 
 int shd_topology_get_latency(ShdTopology* t, uint32_t s, uint32_t d, double* out) {
-    const ShdEntry* e;
+    ShdEntry e;
     int oi, oj;
     if (!t || !out) return -EINVAL;
     int rc = entry_of(t, s, d, &e, &oi, &oj);
     if (rc) return rc;
-    *out = e->lat;
+    *out = e.lat;
     return 0;
 }
 
 int shd_topology_get_reliability(ShdTopology* t, uint32_t s, uint32_t d, double* out) {
-    const ShdEntry* e;
+    ShdEntry e;
     int oi, oj;
     if (!t || !out) return -EINVAL;
     int rc = entry_of(t, s, d, &e, &oi, &oj);
     if (rc) return rc;
-    *out = e->rel;
+    *out = e.rel;
     return 0;
 }
 
@@ -875,7 +886,7 @@ int shd_count_packet(ShdTopology* t, int oi, int oj, uint64_t inc) {
 }
 
 int shd_topology_increment_path_packet_counter(ShdTopology* t, uint32_t s, uint32_t d) {
-    const ShdEntry* e;
+    ShdEntry e;
     int oi, oj;
     if (!t) return -EINVAL;
     int rc = entry_of(t, s, d, &e, &oi, &oj);
@@ -888,7 +899,7 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
     *out = 0;
     IpSlot* a = ipmap_find(&t->ipmap, s);
     IpSlot* b = ipmap_find(&t->ipmap, d);
-    if (!a || !b || !t->h_tab) return 0;
+    if (!a || !b || !t->built) return 0;
     int si = t->vertex_slot[a->vertex], di = t->vertex_slot[b->vertex];
     for (int pass = 0; pass < 2 && t->pkt_cap; pass++) {
         uint64_t key = pass ? (((uint64_t)(uint32_t)di << 32) | (uint32_t)si) : (((uint64_t)(uint32_t)si << 32) | (uint32_t)di);
@@ -901,6 +912,32 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
             h = (h + 1) & (t->pkt_cap - 1);
         }
     }
+    return 0;
+}
+
+/* Device-resident table (no host mirror; C4's A = 86k table is 120 GB):
+ * adopts d_table and releases every row in slot order, as touch_all does.
+ * The released minimum is one device reduction over the pairs (i < j) that
+ * the row-by-row release would store; the min-jump callback fires once with
+ * the final value instead of once per decreasing row. */
+int shd_topology_adopt_table_device_resident(ShdTopology* t, void* d_table) {
+    int A = 0;
+    if (!t || !d_table) return -EINVAL;
+    int rc = shd_topology_slot_count(t, &A); /* prepares the device graph */
+    if (rc) return rc;
+    if (!t->use_sp) return shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
+    if (t->next_touch) return shd_fail(-EBUSY, "rows were already released");
+    double mn = -1.0;
+    if ((rc = shd_dev_min_upper((const ShdEntry*)d_table, A, &mn))) return rc;
+    free(t->h_tab);
+    t->h_tab = NULL;
+    if (t->d_tab && t->d_tab_owned && t->d_tab != (ShdEntry*)d_table) shd_dev_free(t->d_tab);
+    t->d_tab = (ShdEntry*)d_table;
+    t->d_tab_owned = 0;
+    t->built = 1;
+    for (int i = 0; i < A; i++) t->touch[i] = t->next_touch++;
+    t->touch_dirty = 1;
+    if (mn >= 0) note_released(t, mn);
     return 0;
 }
 

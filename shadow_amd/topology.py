@@ -91,6 +91,10 @@ class Topology:
     def adopt_table_device(self, d_table_ptr: int):
         check(lib().shd_topology_adopt_table_device(self._h, C.c_void_p(d_table_ptr)))
 
+    def adopt_table_device_resident(self, d_table_ptr: int):
+        """Adopt without a host mirror; every row released in slot order."""
+        check(lib().shd_topology_adopt_table_device_resident(self._h, C.c_void_p(d_table_ptr)))
+
     def touch_all(self):
         check(lib().shd_topology_touch_all(self._h))
 

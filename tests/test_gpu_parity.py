@@ -127,9 +127,9 @@ def test_unattached_address():
     assert top.is_routable(int(ips[0]), 0x01020304) is False
 
 
-@pytest.fixture(params=["bucket", "rank"])
+@pytest.fixture(params=["bucket", "rank", "slab"])
 def pipeline(request, monkeypatch):
-    """Both grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, read per launch)."""
+    """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, read per launch)."""
     monkeypatch.setenv("SHD_PACKET_PIPELINE", request.param)
     return request.param
 
@@ -405,3 +405,62 @@ def test_device_api_unknown_hosts_not_delivered(pipeline):
     oout["pkt_index"] = good[oout["pkt_index"]]
     assert np.array_equal(status[good], ostatus) and cnt[1] == omt
     assert np.array_equal(out, oout)
+
+
+@pytest.mark.parametrize("name", ["sparse300_ns", "sparse200_dir_ns", "sparse5000_hbm"])
+def test_device_resident_table_matches_mirrored(name, pipeline):
+    """adopt_table_device_resident (no host mirror, all rows released at
+    adoption) == adopt_table_device + touch_all: same released minimum, same
+    host lookups (single-entry device reads), same device round as the oracle."""
+    import torch
+    from shadow_amd import ShdError
+    gml, H = GRAPHS[name]
+    top, orc, ips, st = make_pair(gml, H)
+    top.touch_all()
+    lat, rel, sv = top.table()
+    orc.preload(sv, lat, rel)
+    top2 = Topology(gml)
+    scenario.register_hosts(top2, H, 1)
+    A = top2.slot_count()
+    tab = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
+    top2.build_rows_device(0, A, tab.data_ptr())
+    torch.cuda.synchronize()
+    top2.adopt_table_device_resident(tab.data_ptr())
+    assert bits(top2.min_path_latency()) == bits(top.min_path_latency())
+    with pytest.raises(ShdError):
+        top2.adopt_table_device_resident(tab.data_ptr())  # rows already released: -EBUSY
+    for a in range(0, H, max(1, H // 9)):
+        for b in range(0, H, max(1, H // 7)):
+            s, d = int(ips[a]), int(ips[b])
+            assert bits(top2.get_latency(s, d)) == bits(top.get_latency(s, d))
+            assert bits(top2.get_reliability(s, d)) == bits(top.get_reliability(s, d))
+    pk = synth.packet_batch(30000, H, 0x5EED0430, 100_000_000, 10_000_000, st)
+    n = len(pk)
+    d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    top2.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                        d_status.data_ptr(), d_cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    cnt = d_cnt.cpu().numpy().view(np.uint64)
+    out = d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]]
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(d_status.cpu().numpy(), ostatus) and cnt[1] == omt
+    assert np.array_equal(out, oout)
+
+
+def test_device_resident_needs_shortest_path():
+    import torch
+    from shadow_amd import ShdError
+    gml, H = GRAPHS["complete30_ms"]
+    top = Topology(gml, use_shortest_path=False)
+    scenario.register_hosts(top, H, 1)
+    A = top.slot_count()
+    tab = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
+    top.build_rows_device(0, A, tab.data_ptr())
+    torch.cuda.synchronize()
+    with pytest.raises(ShdError):
+        top.adopt_table_device_resident(tab.data_ptr())
