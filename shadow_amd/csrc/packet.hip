@@ -88,6 +88,16 @@ __device__ __forceinline__ void st_ev(ShdDeliv* p, const ShdDeliv& r) {
     q[0] = make_uint4((uint32_t)r.time, (uint32_t)(r.time >> 32), (uint32_t)r.seq, (uint32_t)(r.seq >> 32));
     q[1] = make_uint4(r.src_host, r.dst_host, r.pkt_index, r.pad);
 }
+// Streaming store of an event that nothing reads again in this kernel
+// (slab slots): nontemporal, so the partial line is not allocated in L2.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_ev_nt(ShdDeliv* p, const ShdDeliv& r) {
+    u32x4* q = reinterpret_cast<u32x4*>(__builtin_assume_aligned(p, 16));
+    u32x4 a = {(uint32_t)r.time, (uint32_t)(r.time >> 32), (uint32_t)r.seq, (uint32_t)(r.seq >> 32)};
+    u32x4 b = {r.src_host, r.dst_host, r.pkt_index, r.pad};
+    __builtin_nontemporal_store(a, q);
+    __builtin_nontemporal_store(b, q + 1);
+}
 __device__ __forceinline__ ShdPkt ld_pkt(const ShdPkt* p) {
     const uint4* q = reinterpret_cast<const uint4*>(__builtin_assume_aligned(p, 16));
     const uint4 a = q[0], b = q[1];
@@ -133,7 +143,7 @@ struct Bucketing {
 // instead of being written back piecewise from eight L2s.  A bijection of
 // [0, ntiles) either way.
 __device__ __forceinline__ uint32_t col_of(const Bucketing& bk, uint32_t g) {
-    if (!bk.xcd) return g;
+    if (!(bk.xcd & 1)) return g;
     const uint32_t q = bk.ntiles >> 3, r = bk.ntiles & 7, x = g & 7;
     return x * q + (x < r ? x : r) + (g >> 3);
 }
@@ -150,7 +160,7 @@ __device__ __forceinline__ uint32_t col_of(const Bucketing& bk, uint32_t g) {
 // comes from the workgroup's LDS histogram (old value of an LDS atomic,
 // carried in pad) -- no global atomics per event; cnt1 is the bucket x tile
 // matrix.
-template <int kMode>
+template <int kMode, int kB = kBatch>
 __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
                                                         uint64_t barrier, uint64_t end_time, uint64_t boot_end,
                                                         Bucketing bk, ShdDeliv* __restrict__ tmp,
@@ -169,22 +179,22 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
     const size_t end = beg + bk.chunk < n ? beg + bk.chunk : n;
     const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
     const ShdEntry* __restrict__ tab = c.tab;
-    // kBatch records per thread go through each gather level together, so a
-    // wave keeps kBatch x 64 independent requests in flight per level
-    for (size_t b0 = beg; b0 < end; b0 += (size_t)kBlock * kBatch) {
-        ShdPkt p[kBatch];
-        int si[kBatch], di[kBatch];
-        size_t idx[kBatch];
-        bool live[kBatch];
+    // kB records per thread go through each gather level together, so a
+    // wave keeps kB x 64 independent requests in flight per level
+    for (size_t b0 = beg; b0 < end; b0 += (size_t)kBlock * kB) {
+        ShdPkt p[kB];
+        int si[kB], di[kB];
+        size_t idx[kB];
+        bool live[kB];
 #pragma unroll
-        for (int k = 0; k < kBatch; k++) {
+        for (int k = 0; k < kB; k++) {
             idx[k] = b0 + (size_t)k * kBlock + threadIdx.x;
             live[k] = idx[k] < end;
             if (live[k]) p[k] = ld_pkt(&recs[idx[k]]);
         }
-        uint32_t ts[kBatch], td[kBatch];
+        uint32_t ts[kB], td[kB];
 #pragma unroll
-        for (int k = 0; k < kBatch; k++) {
+        for (int k = 0; k < kB; k++) {
             const bool known = live[k] && p[k].src_host < c.nhosts && p[k].dst_host < c.nhosts;
             const uint2 hs = known ? host_info[p[k].src_host] : make_uint2(~0u, ~0u);
             const uint2 hd = known ? host_info[p[k].dst_host] : make_uint2(~0u, ~0u);
@@ -193,9 +203,9 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
             ts[k] = hs.y;
             td[k] = hd.y;
         }
-        size_t ei[kBatch];
+        size_t ei[kB];
 #pragma unroll
-        for (int k = 0; k < kBatch; k++) {
+        for (int k = 0; k < kB; k++) {
             int oi = si[k], oj = di[k];
             if (oi >= 0 && oj >= 0) {
                 if (c.mode == 0) {
@@ -208,12 +218,12 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
             }
             ei[k] = (size_t)(oi < 0 ? 0 : oi) * A + (size_t)(oj < 0 ? 0 : oj);
         }
-        ShdEntry e[kBatch];
+        ShdEntry e[kB];
 #pragma unroll
-        for (int k = 0; k < kBatch; k++)
+        for (int k = 0; k < kB; k++)
             if (si[k] >= 0 && di[k] >= 0) e[k] = tab[ei[k]];
 #pragma unroll
-        for (int k = 0; k < kBatch; k++) {
+        for (int k = 0; k < kB; k++) {
             if (!live[k]) continue;
             uint8_t st = 0xff; // unregistered host: not delivered
             if (si[k] >= 0 && di[k] >= 0) {
@@ -232,7 +242,10 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
                         else rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
                         const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
                         if (kMode != 2) st_ev(&tmp[idx[k]], ev);
-                        else if (rank < kSlab) st_ev(&tmp[(size_t)p[k].dst_host * kSlab + rank], ev);
+                        else if (rank < kSlab) {
+                            if (bk.xcd & 2) st_ev_nt(&tmp[(size_t)p[k].dst_host * kSlab + rank], ev);
+                            else st_ev(&tmp[(size_t)p[k].dst_host * kSlab + rank], ev);
+                        }
                         else st_ev(&ovf[atomicAdd(novf, 1u)], ev); // rare: segments above kSlab
                         if (t >= barrier && t < mn) mn = t; // worker.c:350-363
                     }
@@ -1132,6 +1145,8 @@ int make_bucketing(uint32_t host_lo, uint32_t H, size_t n, Bucketing* out) {
     if (bk.ntiles == 0) bk.ntiles = 1;
     const char* x = getenv("SHD_XCD_COLS");
     bk.xcd = !(x && strcmp(x, "0") == 0);
+    const char* nt = getenv("SHD_SLAB_NT"); // bit 1 of xcd: nontemporal slab stores
+    if (nt && strcmp(nt, "1") == 0) bk.xcd |= 2;
     bk.rsort = rank_sort();
     *out = bk;
     return 0;
@@ -1254,7 +1269,16 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     if ((rk || !n) && (rc = hip_status(hipMemsetAsync(g_ws.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
     mark(0, s);
     if (n) {
-        if (pipe == kSlabPipe)
+        const char* sb = getenv("SHD_SCATTER_BATCH");
+        if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
+            hipLaunchKernelGGL((k_pkt_scatter<2, 8>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
+                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
+                               g_ws.nbig + 1);
+        else if (pipe == kSlabPipe && sb && strcmp(sb, "2") == 0)
+            hipLaunchKernelGGL((k_pkt_scatter<2, 2>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
+                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
+                               g_ws.nbig + 1);
+        else if (pipe == kSlabPipe)
             hipLaunchKernelGGL(k_pkt_scatter<2>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
                                end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
                                g_ws.nbig + 1);
