@@ -1,8 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${1:-s6e}
-for b in 4 8 2 4; do
-  SHD_SCATTER_BATCH=$b timeout -k 10 200 python -u bench.py --no-routing --no-cpu-baseline --steps 40 > gpurun_out/${T}_bench_b$b.json 2> gpurun_out/${T}_bench_b$b.err || { tail -20 gpurun_out/${T}_bench_b$b.err; exit 1; }
-  python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], d['ms_per_step'], r['per_stage_ms'])" gpurun_out/${T}_bench_b$b.json $b
-done
+T=${1:-s6h}
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o prof -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 --no-routing --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log; exit 1; }
+grep -o '"per_stage_ms": {[^}]*}' $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log
