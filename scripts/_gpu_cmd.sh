@@ -1,6 +1,10 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=${1:-s6h}
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/gpurun_out/${T}_prof -o prof -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 --no-routing --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log; exit 1; }
-grep -o '"per_stage_ms": {[^}]*}' $GRAFT_REPO_ROOT/gpurun_out/${T}_prof.log
+T=${1:-s6j}
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 || { tail -40 gpurun_out/${T}_pytest.log; exit 1; }
+tail -1 gpurun_out/${T}_pytest.log
+for k in a b; do
+timeout -k 10 200 python -u bench.py --no-routing --no-cpu-baseline --steps 40 > gpurun_out/${T}_$k.json 2> gpurun_out/${T}_$k.err || { tail -20 gpurun_out/${T}_$k.err; exit 1; }
+python -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(round(d['ms_per_step'],4), {k: round(v,4) for k,v in r['per_stage_ms'].items()})" gpurun_out/${T}_$k.json
+done

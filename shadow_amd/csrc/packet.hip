@@ -629,27 +629,25 @@ __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* _
 #pragma unroll
     for (int e = 0; e < E; e++)
         key[e] = (e * 64 + lane < (int)n) ? (packed ? ((v[e].t - tmin) << 24) | v[e].s : v[e].t) : ~0ull;
-    // pass 1: one 64-bit compare per pair, counting equal keys to detect ties
-    // (every element equals itself once)
-    uint32_t eq[E];
-#pragma unroll
-    for (int e = 0; e < E; e++) eq[e] = 0;
+    // pass 1: one 64-bit compare per pair (rank = number of smaller keys)
 #pragma unroll
     for (int ej = 0; ej < E; ej++) {
         const int lim = (int)n - ej * 64 < 64 ? (int)n - ej * 64 : 64; // wave-uniform
         for (int l = 0; l < lim; l++) {
             const unsigned long long kj = readlane_u64(key[ej], l);
 #pragma unroll
-            for (int e = 0; e < E; e++) {
-                rank[e] += (uint32_t)(kj < key[e]);
-                eq[e] += (uint32_t)(kj == key[e]);
-            }
+            for (int e = 0; e < E; e++) rank[e] += (uint32_t)(kj < key[e]);
         }
     }
-    bool tie = false;
+    // Ties: the ranks are a permutation of [0, n) -- sum n(n-1)/2 -- iff all
+    // keys differ; a group of g equal keys shares its lowest rank, which
+    // lowers the sum.  (Replaces an equality count per pair: pass 1 is the
+    // VALU-bound part of the segment sort.)
+    uint32_t rsum = 0;
 #pragma unroll
-    for (int e = 0; e < E; e++) tie |= (e * 64 + lane < (int)n) && eq[e] > 1;
-    if (__ballot(tie)) {
+    for (int e = 0; e < E; e++) rsum += (e * 64 + lane < (int)n) ? rank[e] : 0u;
+    for (int off = 32; off > 0; off >>= 1) rsum += (uint32_t)__shfl_xor((int)rsum, off);
+    if (rsum != n * (n - 1) / 2) {
         // pass 2 (segments with equal keys only): rank among the events of
         // equal key by event_compare's remaining keys, branch-free
 #pragma unroll
