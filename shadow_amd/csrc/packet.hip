@@ -88,16 +88,6 @@ __device__ __forceinline__ void st_ev(ShdDeliv* p, const ShdDeliv& r) {
     q[0] = make_uint4((uint32_t)r.time, (uint32_t)(r.time >> 32), (uint32_t)r.seq, (uint32_t)(r.seq >> 32));
     q[1] = make_uint4(r.src_host, r.dst_host, r.pkt_index, r.pad);
 }
-// Streaming store of an event that nothing reads again in this kernel
-// (slab slots): nontemporal, so the partial line is not allocated in L2.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_ev_nt(ShdDeliv* p, const ShdDeliv& r) {
-    u32x4* q = reinterpret_cast<u32x4*>(__builtin_assume_aligned(p, 16));
-    u32x4 a = {(uint32_t)r.time, (uint32_t)(r.time >> 32), (uint32_t)r.seq, (uint32_t)(r.seq >> 32)};
-    u32x4 b = {r.src_host, r.dst_host, r.pkt_index, r.pad};
-    __builtin_nontemporal_store(a, q);
-    __builtin_nontemporal_store(b, q + 1);
-}
 __device__ __forceinline__ ShdPkt ld_pkt(const ShdPkt* p) {
     const uint4* q = reinterpret_cast<const uint4*>(__builtin_assume_aligned(p, 16));
     const uint4 a = q[0], b = q[1];
@@ -134,6 +124,7 @@ struct Bucketing {
     uint32_t chunk;   // records per scatter workgroup
     uint32_t xcd;     // 1: XCD-grouped column order (see col_of)
     uint32_t rsort;   // segment sort: 1 rank (default), 0 bitonic (see sort_segment)
+    uint32_t slab_rm; // slab layout: 1 rank-major (slot r of host d at r * H + d), 0 host-major (d * kSlab + r)
 };
 
 // Matrix column of chunk g.  Workgroups are dealt to the 8 XCDs round-robin
@@ -143,7 +134,7 @@ struct Bucketing {
 // instead of being written back piecewise from eight L2s.  A bijection of
 // [0, ntiles) either way.
 __device__ __forceinline__ uint32_t col_of(const Bucketing& bk, uint32_t g) {
-    if (!(bk.xcd & 1)) return g;
+    if (!bk.xcd) return g;
     const uint32_t q = bk.ntiles >> 3, r = bk.ntiles & 7, x = g & 7;
     return x * q + (x < r ? x : r) + (g >> 3);
 }
@@ -238,14 +229,15 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
                         if (p[k].src_host != p[k].dst_host && t < barrier) t = barrier; // host_single.c:187-192
                         st = SHD_DELIVERED;
                         uint32_t rank;
-                        if (kRank) rank = atomicAdd(&cnt1[p[k].dst_host], 1u);
+                        if (kMode == 3) rank = (uint32_t)idx[k] & (kSlab - 1); // probe: no atomic
+                        else if (kRank) rank = atomicAdd(&cnt1[p[k].dst_host], 1u);
                         else rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
                         const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
-                        if (kMode != 2) st_ev(&tmp[idx[k]], ev);
-                        else if (rank < kSlab) {
-                            if (bk.xcd & 2) st_ev_nt(&tmp[(size_t)p[k].dst_host * kSlab + rank], ev);
-                            else st_ev(&tmp[(size_t)p[k].dst_host * kSlab + rank], ev);
-                        }
+                        if (kMode == 4) { if (rank == ~0u) st_ev(&tmp[0], ev); } // probe: no event write
+                        else if (kMode < 2) st_ev(&tmp[idx[k]], ev);
+                        else if (rank < kSlab)
+                            st_ev(&tmp[bk.slab_rm ? (size_t)rank * bk.H + p[k].dst_host
+                                                  : (size_t)p[k].dst_host * kSlab + rank], ev);
                         else st_ev(&ovf[atomicAdd(novf, 1u)], ev); // rare: segments above kSlab
                         if (t >= barrier && t < mn) mn = t; // worker.c:350-363
                     }
@@ -679,14 +671,15 @@ __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* _
 // (an LDS index list) is given; it is written to out[o + i].  (Kept as the
 // SHD_SEGSORT=bitonic alternative of wave_rank_segment.)
 template <int E>
-__device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, const uint16_t* perm, uint32_t n,
+__device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, const uint16_t* perm, uint32_t stride,
+                                  uint32_t n,
                                   uint32_t d, ShdDeliv* __restrict__ out, uint32_t o, int lane) {
     Ev v[E];
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)(e * 64 + lane);
         if (i < n) {
-            const ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i)]);
+            const ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i * stride)]);
             v[e] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
         } else {
             v[e] = Ev{~0ull, ~0ull, ~0u, ~0u};
@@ -733,27 +726,30 @@ __device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, 
 // Sorts one destination segment of n <= kSmallSeg events with one wave.
 // algo: 1 rank sort, 0 bitonic network, 2 copy without sorting (a
 // benchmark probe of the memory side only; never selected by the library).
+// Element i of the segment is src[b + perm[i]] (LDS index list) or
+// src[b + i * stride] (stride 1: contiguous; H: a rank-major slab).
 __device__ __forceinline__ void sort_segment(uint32_t algo, const ShdDeliv* __restrict__ src, uint32_t b,
                                              const uint16_t* perm, uint32_t n, uint32_t d,
-                                             ShdDeliv* __restrict__ out, uint32_t o, int lane) {
+                                             ShdDeliv* __restrict__ out, uint32_t o, int lane,
+                                             uint32_t stride = 1) {
     if (algo == 2) {
         for (uint32_t i = lane; i < n; i += 64) {
-            ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i)]);
+            ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i * stride)]);
             r.pad = 0;
             st_ev(&out[o + i], r);
         }
     } else if (algo == 1) {
         auto load = [&](uint32_t i) {
-            const ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i)]);
+            const ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i * stride)]);
             return Ev{r.time, r.seq, r.src_host, r.pkt_index};
         };
         if (n <= 64) wave_rank_segment<1>(load, n, d, out, o, lane);
         else if (n <= 128) wave_rank_segment<2>(load, n, d, out, o, lane);
         else wave_rank_segment<4>(load, n, d, out, o, lane);
     } else {
-        if (n <= 64) wave_sort_segment<1>(src, b, perm, n, d, out, o, lane);
-        else if (n <= 128) wave_sort_segment<2>(src, b, perm, n, d, out, o, lane);
-        else wave_sort_segment<4>(src, b, perm, n, d, out, o, lane);
+        if (n <= 64) wave_sort_segment<1>(src, b, perm, stride, n, d, out, o, lane);
+        else if (n <= 128) wave_sort_segment<2>(src, b, perm, stride, n, d, out, o, lane);
+        else wave_sort_segment<4>(src, b, perm, stride, n, d, out, o, lane);
     }
 }
 
@@ -989,7 +985,7 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
                                                      uint32_t H, uint32_t host_lo, ShdDeliv* __restrict__ out,
                                                      uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
                                                      uint32_t rsort, uint32_t flo, uint32_t fhi,
-                                                     const ShdDeliv* __restrict__ slab) {
+                                                     const ShdDeliv* __restrict__ slab, uint32_t slab_rm) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
@@ -998,10 +994,11 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
         const uint32_t dh = d + host_lo;
         if (n == 0) continue;
         if (slab) {
+            const uint32_t base = slab_rm ? d : d * kSlab, stride = slab_rm ? H : 1u;
             if (n <= kSlab) {
-                sort_segment(rsort, slab, d * kSlab, nullptr, n, dh, out, b, lane);
+                sort_segment(rsort, slab, base, nullptr, n, dh, out, b, lane, stride);
             } else {
-                for (uint32_t i = lane; i < kSlab; i += 64) st_ev(&scr[b + i], ld_ev(&slab[(size_t)d * kSlab + i]));
+                for (uint32_t i = lane; i < kSlab; i += 64) st_ev(&scr[b + i], ld_ev(&slab[base + (size_t)i * stride]));
                 if (lane == 0) big[atomicAdd(nbig, 1u)] = d;
             }
         } else if (n <= (uint32_t)kSmallSeg) {
@@ -1143,8 +1140,8 @@ int make_bucketing(uint32_t host_lo, uint32_t H, size_t n, Bucketing* out) {
     if (bk.ntiles == 0) bk.ntiles = 1;
     const char* x = getenv("SHD_XCD_COLS");
     bk.xcd = !(x && strcmp(x, "0") == 0);
-    const char* nt = getenv("SHD_SLAB_NT"); // bit 1 of xcd: nontemporal slab stores
-    if (nt && strcmp(nt, "1") == 0) bk.xcd |= 2;
+    const char* sl = getenv("SHD_SLAB_LAYOUT");
+    bk.slab_rm = sl && strcmp(sl, "rank") == 0;
     bk.rsort = rank_sort();
     *out = bk;
     return 0;
@@ -1207,7 +1204,8 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* ra
 // the overflow list); only overflow events are placed.
 int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n,
                         uint32_t host_lo, uint32_t H, ShdDeliv* out, uint32_t* offsets,
-                        unsigned long long* counters, hipStream_t s, const ShdDeliv* slab = nullptr) {
+                        unsigned long long* counters, hipStream_t s, const ShdDeliv* slab = nullptr,
+                        uint32_t slab_rm = 0) {
     const uint32_t nb = (uint32_t)((H + kScanTile - 1) / kScanTile);
     hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, g_ws.cnt1, (size_t)H, offsets, g_ws.bsum);
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g_ws.bsum, nb);
@@ -1221,7 +1219,7 @@ int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_
                            n, host_lo, H, offsets, g_ws.st1, 0u, H);
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.st1, offsets, H, host_lo, out,
-                       g_ws.big, g_ws.nbig, rank_sort(), 0u, H, slab);
+                       g_ws.big, g_ws.nbig, rank_sort(), 0u, H, slab, slab_rm);
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
@@ -1272,6 +1270,14 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
             hipLaunchKernelGGL((k_pkt_scatter<2, 8>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
                                end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
                                g_ws.nbig + 1);
+        else if (pipe == kSlabPipe && sb && strcmp(sb, "probe-noatomic") == 0) // benchmark probes only:
+            hipLaunchKernelGGL((k_pkt_scatter<3>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
+                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
+                               g_ws.nbig + 1);                                  // wrong output by design
+        else if (pipe == kSlabPipe && sb && strcmp(sb, "probe-nowrite") == 0)
+            hipLaunchKernelGGL((k_pkt_scatter<4>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
+                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
+                               g_ws.nbig + 1);
         else if (pipe == kSlabPipe && sb && strcmp(sb, "2") == 0)
             hipLaunchKernelGGL((k_pkt_scatter<2, 2>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
                                end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
@@ -1292,7 +1298,8 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     mark(1, s);
     if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
     rc = pipe == kSlabPipe
-             ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s, g_ws.slab)
+             ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s, g_ws.slab,
+                                   bk.slab_rm)
          : rk ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s)
               : group_and_sort(g_ws.tmp, d_status, nullptr, n, bk, d_out, d_dst_offsets, counters, s);
     if (rc) return rc;

@@ -127,10 +127,12 @@ def test_unattached_address():
     assert top.is_routable(int(ips[0]), 0x01020304) is False
 
 
-@pytest.fixture(params=["bucket", "rank", "slab"])
+@pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor"])
 def pipeline(request, monkeypatch):
-    """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, read per launch)."""
-    monkeypatch.setenv("SHD_PACKET_PIPELINE", request.param)
+    """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, and the slab
+    layout SHD_SLAB_LAYOUT, read per launch)."""
+    monkeypatch.setenv("SHD_PACKET_PIPELINE", request.param.split("_")[0])
+    monkeypatch.setenv("SHD_SLAB_LAYOUT", "rank" if request.param.endswith("rankmajor") else "host")
     return request.param
 
 
