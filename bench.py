@@ -100,6 +100,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    c4_ctx = None
     # ------------------------------------------------------------------ C3 setup
     H, V, P = args.hosts, args.vertices, args.packets
     t0 = time.perf_counter()
@@ -263,7 +264,8 @@ def main():
         t0 = time.perf_counter()
         g4 = synth.sparse_graph_gml(args.c4_vertices, 0x5EED0004)
         t4 = Topology(g4, device=local)
-        _, states4, _ = scenario.register_hosts(t4, args.c4_hosts, seed=1)
+        _, states4, verts4 = scenario.register_hosts(t4, args.c4_hosts, seed=1)
+        c4_ctx = (g4, np.unique(verts4).astype(np.int32))  # slots = attached vertices, ascending
         A4 = t4.slot_count()
         log(f"C4 graph V={args.c4_vertices} H={args.c4_hosts} A={A4} ready in {time.perf_counter() - t0:.1f}s")
         per4 = (A4 + world - 1) // world
@@ -327,7 +329,7 @@ def main():
 
     # ------------------------------------------------------- CPU baseline (N=1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(gml, H, states, top, result)
+        result["cpu_baseline"] = cpu_baseline(gml, H, states, top, result, c4_ctx)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -335,7 +337,18 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(gml, H, states, top, result):
+def cpu_rows_parallel(orc, sources, targets, threads):
+    """Oracle Dijkstra rows on `threads` host threads (ctypes releases the GIL
+    inside orc_compute_row; rows are independent, like the reference's rows
+    without its global graphLock).  Returns seconds per row, amortised."""
+    from concurrent.futures import ThreadPoolExecutor
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda s: orc.row(int(s), targets), sources))
+    return (time.perf_counter() - t0) / len(sources)
+
+
+def cpu_baseline(gml, H, states, top, result, c4_ctx=None):
     """The oracle (C restatement of worker_sendPacket + per-destination binary
     heaps) timed on this host, one core, on a bounded sample of the C3 workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -372,6 +385,28 @@ def cpu_baseline(gml, H, states, top, result):
     base["routing"] = {"value": 5000.0 ** 2 / full, "unit": "routed host-pairs/s", "cores": 1, "kind": "port",
                        "sample": f"{k} of {len(targets)} C1 source rows (igraph-0.8 Dijkstra restatement), "
                                  f"extrapolated to the full table: {full:.2f}s"}
+    # row-parallel oracle on the box's CPU share ("all N host
+    # cores"); the box exposes 16 CPUs to a job, os.cpu_count() shows the host
+    threads = int(os.environ.get("SHD_CPU_THREADS", "16"))
+    per_mt = cpu_rows_parallel(o1, targets, targets, threads)
+    base["routing_mt"] = {"value": 5000.0 ** 2 / (per_mt * len(targets)), "unit": "routed host-pairs/s",
+                          "cores": threads, "kind": "port",
+                          "sample": f"all {len(targets)} C1 source rows, {threads} threads: "
+                                    f"{per_mt * len(targets):.2f}s"}
+    if c4_ctx is not None:
+        g4, sv4 = c4_ctx
+        o4 = O.OracleTopology(g4)
+        k4 = 512
+        per4 = cpu_rows_parallel(o4, sv4[:: max(1, len(sv4) // k4)][:k4], sv4, threads)
+        full4 = per4 * len(sv4)
+        hosts4 = result.get("routing", {}).get("c4", {}).get("config", "")
+        base["routing_c4_mt"] = {"value": None, "unit": "routed host-pairs/s", "cores": threads, "kind": "port",
+                                 "sample": f"{k4} of {len(sv4)} C4 source rows (evenly spaced), {threads} threads, "
+                                           f"extrapolated to the full table: {full4:.1f}s ({hosts4})",
+                                 "build_s_extrapolated": full4}
+        c4 = result.get("routing", {}).get("c4")
+        if c4:
+            base["routing_c4_mt"]["value"] = c4["value"] * c4["build_s"] / full4
     return base
 
 

@@ -622,6 +622,27 @@ void orc_topology_free(OrcTopo* t) {
     free(t);
 }
 
+typedef struct {
+    long long id;
+    int v;
+} IdIdx;
+
+static int cmp_ididx(const void* a, const void* b) {
+    const IdIdx *x = (const IdIdx*)a, *y = (const IdIdx*)b;
+    return x->id < y->id ? -1 : x->id > y->id;
+}
+
+static int find_id(const IdIdx* byid, int n, long long id) {
+    int lo = 0, hi = n - 1;
+    while (lo <= hi) {
+        int mid = lo + (hi - lo) / 2;
+        if (byid[mid].id == id) return byid[mid].v;
+        if (byid[mid].id < id) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return -1;
+}
+
 /* topology_new (topology.c:2328-2354): load, check, extract weights. */
 OrcTopo* orc_topology_new(const char* text, int use_shortest_path) {
     OrcTopo* t = (OrcTopo*)calloc(1, sizeof(OrcTopo));
@@ -674,9 +695,13 @@ OrcTopo* orc_topology_new(const char* text, int use_shortest_path) {
         }
         if (!has) bad = 1;
     }
-    for (int v = 0; v < nn && !bad; v++)
-        for (int w = v + 1; w < nn; w++)
-            if (ids[v] == ids[w]) bad = 1;
+    /* (id, vertex) pairs sorted by id: uniqueness check and endpoint lookup
+     * in O(log V) (ids are unique, so the lookup is the one matching vertex) */
+    IdIdx* byid = (IdIdx*)malloc(sizeof(IdIdx) * (size_t)(nn + 1));
+    for (int v = 0; v < nn; v++) byid[v].id = ids[v], byid[v].v = v;
+    qsort(byid, (size_t)nn, sizeof(IdIdx), cmp_ididx);
+    for (int v = 1; v < nn && !bad; v++)
+        if (byid[v].id == byid[v - 1].id) bad = 1;
     t->efrom = (int*)malloc(sizeof(int) * (size_t)(ne + 1));
     t->eto = (int*)malloc(sizeof(int) * (size_t)(ne + 1));
     for (int e = 0; e < ne && !bad; e++) {
@@ -698,11 +723,7 @@ OrcTopo* orc_topology_new(const char* text, int use_shortest_path) {
             bad = 1;
             break;
         }
-        int sv = -1, gv = -1;
-        for (int v = 0; v < nn; v++) {
-            if (ids[v] == s) sv = v;
-            if (ids[v] == g) gv = v;
-        }
+        int sv = find_id(byid, nn, s), gv = find_id(byid, nn, g);
         if (sv < 0 || gv < 0) {
             bad = 1;
             break;
@@ -716,6 +737,7 @@ OrcTopo* orc_topology_new(const char* text, int use_shortest_path) {
         }
     }
     free(ids);
+    free(byid);
     if (bad) {
         free(nodes);
         free(edges);
