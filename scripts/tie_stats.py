@@ -38,12 +38,13 @@ def parse(gml):
 def main():
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c1"
     ns = int(sys.argv[2]) if len(sys.argv) > 2 else 200
-    gml = synth.complete_graph_gml(1000, 0x5EED0001) if cfg == "c1" else synth.sparse_graph_gml(20000, 0x5EED0002)
+    gml = (synth.complete_graph_gml(1000, 0x5EED0001) if cfg == "c1" else
+           synth.sparse_graph_gml(20000, 0x5EED0002) if cfg == "c2" else synth.sparse_graph_gml(100000, 0x5EED0004))
     V, s, d, w = parse(gml)
     M = csr_matrix((w, (s, d)), shape=(V, V))
     srcs = np.arange(0, V, max(1, V // ns))[:ns]
     D = dijkstra(M, directed=True, indices=srcs)
-    tied_pairs = pairs = tied_rows = 0
+    tied_pairs = pairs = tied_rows = amb_pairs = amb_rows = 0
     for i, so in enumerate(srcs):
         dist = D[i]
         tight = np.isclose(dist[s] + w, dist[d], rtol=0, atol=1e-9)  # exact for integer ms
@@ -53,8 +54,23 @@ def main():
         tied_pairs += t
         pairs += V - 1
         tied_rows += t > 0
+        # igraph's parent = the FIRST POPPED tight predecessor; pop order is by
+        # distance, so only tight predecessors of equal (minimal) distance are
+        # decided by the heap: count those vertices
+        ts, td = s[tight], d[tight]
+        du = dist[ts]
+        mind = np.full(V, np.inf)
+        np.minimum.at(mind, td, du)
+        nmin = np.bincount(td[du == mind[td]], minlength=V)
+        nmin[so] = 0
+        a = int((nmin > 1).sum())
+        amb_pairs += a
+        amb_rows += a > 0
     print(f"{cfg}: V={V}, {len(srcs)} sources: {tied_pairs}/{pairs} = {tied_pairs / pairs:.1%} of (s,d) pairs "
           f"have >1 shortest-path predecessor; {tied_rows}/{len(srcs)} rows contain at least one")
+    print(f"{cfg}: {amb_pairs}/{pairs} = {amb_pairs / pairs:.2%} of vertices have >1 shortest-path predecessor of "
+          f"EQUAL (minimal) distance -- the only ones whose parent needs the heap's pop order; "
+          f"{amb_rows}/{len(srcs)} rows contain at least one")
 
 
 if __name__ == "__main__":
