@@ -969,11 +969,41 @@ __global__ __launch_bounds__(256) void k_place_rank(const ShdDeliv* __restrict__
 // k_segsort_dst has put the first kSlab slots.  Grid-stride over the device
 // count, so the launch costs nothing when no segment overflowed.
 __global__ __launch_bounds__(256) void k_place_ovf(const ShdDeliv* __restrict__ ovf, const uint32_t* __restrict__ novf,
-                                                   const uint32_t* __restrict__ off, ShdDeliv* __restrict__ scr) {
+                                                   const uint32_t* __restrict__ off, uint32_t host_lo,
+                                                   ShdDeliv* __restrict__ scr) {
     const uint32_t m = *novf;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         const ShdDeliv r = ld_ev(&ovf[i]);
-        st_ev(&scr[off[r.dst_host] + r.pad], r);
+        st_ev(&scr[off[r.dst_host - host_lo] + r.pad], r);
+    }
+}
+
+// Regroup path, slab pipeline: each event in the host range takes its slot
+// from its destination's counter and goes straight into the slab (or the
+// overflow list); out-of-range events are dropped.
+__global__ __launch_bounds__(256) void k_hist_slab(const ShdDeliv* __restrict__ in, size_t n, uint32_t host_lo,
+                                                   uint32_t H, uint32_t* __restrict__ cnt, ShdDeliv* __restrict__ slab,
+                                                   uint32_t slab_rm, ShdDeliv* __restrict__ ovf,
+                                                   uint32_t* __restrict__ novf) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * kBatch) {
+        ShdDeliv r[kBatch];
+        bool ok[kBatch];
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const size_t i = i0 + (size_t)k * stride;
+            ok[k] = i < n;
+            if (ok[k]) r[k] = ld_ev(&in[i]);
+        }
+#pragma unroll
+        for (int k = 0; k < kBatch; k++) {
+            const uint32_t d = r[k].dst_host - host_lo;
+            if (!ok[k] || d >= H) continue;
+            const uint32_t rank = atomicAdd(&cnt[d], 1u);
+            r[k].pad = rank;
+            if (rank < kSlab) st_ev(&slab[slab_rm ? (size_t)rank * H + d : (size_t)d * kSlab + rank], r[k]);
+            else st_ev(&ovf[atomicAdd(novf, 1u)], r[k]);
+        }
     }
 }
 
@@ -1213,7 +1243,8 @@ int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_
                        g_ws.bsum, nb, counters);
     mark(2, s);
     if (slab)
-        hipLaunchKernelGGL(k_place_ovf, dim3(512), dim3(256), 0, s, g_ws.st2, g_ws.nbig + 1, offsets, g_ws.st1);
+        hipLaunchKernelGGL(k_place_ovf, dim3(512), dim3(256), 0, s, g_ws.st2, g_ws.nbig + 1, offsets, host_lo,
+                           g_ws.st1);
     else if (n)
         hipLaunchKernelGGL(k_place_rank, dim3(grid_for(n, 256 * kBatch, 1u << 20)), dim3(256), 0, s, in, status, rank,
                            n, host_lo, H, offsets, g_ws.st1, 0u, H);
@@ -1239,7 +1270,7 @@ int pipeline_for(uint32_t H, bool slab_ok) {
     if (!slab_ok || (size_t)H * kSlab * sizeof(ShdDeliv) > kMaxSlabBytes) return kRankPipe;
     return kSlabPipe;
 }
-bool use_rank_pipeline() { return pipeline_for(0, false) != kBucketPipe; }
+
 
 } // namespace
 
@@ -1338,25 +1369,33 @@ extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_
                                   uint32_t* d_dst_offsets, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     const uint32_t H = host_hi - host_lo;
-    const bool rk = use_rank_pipeline();
+    const int pipe = pipeline_for(H, true);
+    const bool rk = pipe != kBucketPipe;
     Bucketing bk;
     int rc = make_bucketing(host_lo, H, n, &bk);
     if (rc) return rc;
     const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
     if ((rc = ws_reserve(n, m, H))) return rc;
-    if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 4, s), "memset nbig"))) return rc;
+    if (pipe == kSlabPipe && (rc = slab_reserve(H))) return rc;
+    if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 8, s), "memset nbig"))) return rc;
     if ((rk || !n) && (rc = hip_status(hipMemsetAsync(g_ws.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
     mark(0, s);
     if (n) {
-        if (rk)
+        if (pipe == kSlabPipe)
+            hipLaunchKernelGGL(k_hist_slab, dim3(grid_for(n, 256 * kBatch, 1u << 20)), dim3(256), 0, s, d_in, n,
+                               host_lo, H, g_ws.cnt1, g_ws.slab, bk.slab_rm, g_ws.st2, g_ws.nbig + 1);
+        else if (rk)
             hipLaunchKernelGGL(k_hist_rank, dim3(grid_for(n, 256, 1u << 20)), dim3(256), 0, s, d_in, n, host_lo, H,
                                g_ws.cnt1, g_ws.rnk);
         else
             hipLaunchKernelGGL(k_hist_tiles, dim3(bk.ntiles), dim3(kBlock), 0, s, d_in, n, bk, g_ws.cnt1, g_ws.rnk);
     }
     mark(1, s);
-    rc = rk ? group_and_sort_rank(d_in, nullptr, g_ws.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s)
-            : group_and_sort(d_in, nullptr, g_ws.rnk, n, bk, d_out, d_dst_offsets, nullptr, s);
+    rc = pipe == kSlabPipe
+             ? group_and_sort_rank(d_in, nullptr, g_ws.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s, g_ws.slab,
+                                   bk.slab_rm)
+         : rk ? group_and_sort_rank(d_in, nullptr, g_ws.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s)
+              : group_and_sort(d_in, nullptr, g_ws.rnk, n, bk, d_out, d_dst_offsets, nullptr, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "deliv sort");
 }
