@@ -466,3 +466,16 @@ def test_device_resident_needs_shortest_path():
     torch.cuda.synchronize()
     with pytest.raises(ShdError):
         top.adopt_table_device_resident(tab.data_ptr())
+
+
+def test_packet_round_zipf_senders(pipeline):
+    """C3's Zipf variant: skewed senders, so a few hosts send
+    most packets (long rand_r advances, many equal-time ties per sender)."""
+    gml, H = GRAPHS["sparse300_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    pk = synth.packet_batch(50000, H, 0x5EED0440, 100_000_000, 10_000_000, st, zipf=True)
+    assert np.bincount(pk["src_host"], minlength=H).max() > 20 * len(pk) / H  # skewed
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert offs[-1] == len(out)
