@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from shadow_amd import Topology, scenario, synth  # noqa: E402
 
-n, lo, hi = 10_000_000, 0, 100_000
+n, lo, hi = 10_000_000, 0, int(os.environ.get("REGROUP_HOSTS", "100000"))
 rng = np.random.default_rng(5)
 ev = np.zeros(n, dtype=synth.DELIV_DTYPE)
 ev["time"] = 110_000_000 + rng.integers(0, 150_000_000, n)
@@ -25,7 +25,7 @@ scenario.register_hosts(top, 5, 1)
 d_in = torch.from_numpy(ev.view(np.uint8)).cuda()
 d_out = torch.empty_like(d_in)
 d_off = torch.empty(hi - lo + 1, dtype=torch.int32, device="cuda")
-for pipe in ("rank", "slab", "rank", "slab"):
+for pipe in os.environ.get("REGROUP_PIPES", "rank,slab,rank,slab").split(","):
     os.environ["SHD_PACKET_PIPELINE"] = pipe
     for _ in range(2):
         top.deliv_sort_device(d_in.data_ptr(), n, lo, hi, d_out.data_ptr(), d_off.data_ptr(), 0)
@@ -35,4 +35,5 @@ for pipe in ("rank", "slab", "rank", "slab"):
     for _ in range(k):
         top.deliv_sort_device(d_in.data_ptr(), n, lo, hi, d_out.data_ptr(), d_off.data_ptr(), 0)
     torch.cuda.synchronize()
-    print(f"{pipe}: {(time.perf_counter() - t0) / k * 1e3:.3f} ms per 10M-event regroup", flush=True)
+    print(f"{pipe}: {(time.perf_counter() - t0) / k * 1e3:.3f} ms per 10M-event regroup over {hi - lo} hosts",
+          flush=True)

@@ -20,7 +20,8 @@
 //                  placement, then one wave per destination sorts the
 //                  segment by event_compare's remaining keys (time, src host,
 //                  srcHostEventID) with a register bitonic network.
-//   k_segsort_big  destinations with more than 512 events in a round:
+//   k_segsort_mid  listed segments up to 2048 events: LDS bitonic, one workgroup each.
+//   k_segsort_big  larger segments:
 //                  padded all-ascending bitonic network in HBM.
 // event_compare is a total order, so per-destination heap pop order
 // (priority_queue.c) equals this sorted order: the output is identical to
@@ -886,6 +887,56 @@ __device__ __forceinline__ void cmpx(ShdDeliv* v, uint32_t a, uint32_t b) {
 // then an all-ascending bitonic network over the next power of two with
 // virtual +inf padding (pairs that touch the padding are skipped, which is
 // exact for this network form).
+// Listed segments of up to kMidSeg events: one workgroup loads the segment
+// into LDS (24 B per event: time, srcHostEventID, src, index), runs a
+// bitonic network over the next power of two with +inf padding (event_compare
+// is total on real events, padding sorts last) and writes the segment back in
+// order -- in place when stage2 == out.  Larger segments stay with
+// k_segsort_big.
+constexpr uint32_t kMidSeg = 2048;
+__global__ __launch_bounds__(1024) void k_segsort_mid(const ShdDeliv* stage2, const uint32_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ big,
+                                                      const uint32_t* __restrict__ nbig, ShdDeliv* out) {
+    __shared__ Ev sv[kMidSeg];
+    const uint32_t nb = *nbig;
+    for (uint32_t q = blockIdx.x; q < nb; q += gridDim.x) {
+        const uint32_t d = big[q];
+        const uint32_t b = off[d], n = off[d + 1] - b;
+        if (n == 0 || n > kMidSeg) continue; // block-uniform
+        const uint32_t dh = stage2[b].dst_host;
+        uint32_t N = 1;
+        while (N < n) N <<= 1;
+        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+            if (i < n) {
+                const ShdDeliv r = ld_ev(&stage2[b + i]);
+                sv[i] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
+            } else {
+                sv[i] = Ev{~0ull, ~0ull, ~0u, ~0u};
+            }
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= N; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const Ev x = sv[i], y = sv[l];
+                        const bool up = (i & k) == 0;
+                        if (up ? ev_lt(y, x) : ev_lt(x, y)) {
+                            sv[i] = y;
+                            sv[l] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+            st_ev(&out[b + i], ShdDeliv{sv[i].t, sv[i].q, sv[i].s, dh, sv[i].ix, 0u});
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_segsort_big(const ShdDeliv* stage2,
                                                      const uint32_t* __restrict__ off,
                                                      const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig,
@@ -894,6 +945,7 @@ __global__ __launch_bounds__(256) void k_segsort_big(const ShdDeliv* stage2,
     for (uint32_t q = blockIdx.x; q < nb; q += gridDim.x) {
         const uint32_t d = big[q];
         const uint32_t b = off[d], n = off[d + 1] - b;
+        if (n <= kMidSeg) continue; // k_segsort_mid
         ShdDeliv* v = out + b;
         if (stage2 != out) {
             for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
@@ -1222,6 +1274,7 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* ra
     mark(3, s);
     hipLaunchKernelGGL(k_bucket_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, g_ws.st1, bk, g_ws.off1, offsets, out,
                        g_ws.big, g_ws.nbig);
+    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
@@ -1251,6 +1304,7 @@ int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.st1, offsets, H, host_lo, out,
                        g_ws.big, g_ws.nbig, rank_sort(), 0u, H, slab, slab_rm);
+    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;

@@ -479,3 +479,20 @@ def test_packet_round_zipf_senders(pipeline):
     oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
     assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
     assert offs[-1] == len(out)
+
+
+def test_medium_segments_lds_path(pipeline):
+    """Destinations with 257..2048 events in a round (a server host receiving
+    from many clients): the LDS bitonic segment sort."""
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    pk = synth.packet_batch(14000, H, 0x5EED0450, 100_000_000, 10_000_000, st)
+    hot = (pk["seq"] % 4) != 0  # 3/4 of the packets go to hosts 1..8
+    d = (1 + (pk["seq"] * 7 + pk["src_host"]) % 8).astype(np.uint32)
+    d = np.where(d == pk["src_host"], 9, d).astype(np.uint32)
+    pk["dst_host"] = np.where(hot, d, pk["dst_host"]).astype(np.uint32)
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    seg = np.diff(offs)
+    assert ((seg > 256) & (seg <= 2048)).sum() >= 4
