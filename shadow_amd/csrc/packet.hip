@@ -20,7 +20,7 @@
 //                  placement, then one wave per destination sorts the
 //                  segment by event_compare's remaining keys (time, src host,
 //                  srcHostEventID) with a register bitonic network.
-//   k_segsort_mid  listed segments up to 2048 events: LDS bitonic, one workgroup each.
+//   k_segsort_mid  listed segments up to 4096 events: LDS bitonic, one workgroup each.
 //   k_segsort_big  larger segments:
 //                  padded all-ascending bitonic network in HBM.
 // event_compare is a total order, so per-destination heap pop order
@@ -893,11 +893,12 @@ __device__ __forceinline__ void cmpx(ShdDeliv* v, uint32_t a, uint32_t b) {
 // is total on real events, padding sorts last) and writes the segment back in
 // order -- in place when stage2 == out.  Larger segments stay with
 // k_segsort_big.
-constexpr uint32_t kMidSeg = 2048;
+constexpr uint32_t kMidSeg = 4096; // 96 KiB of dynamic LDS
 __global__ __launch_bounds__(1024) void k_segsort_mid(const ShdDeliv* stage2, const uint32_t* __restrict__ off,
                                                       const uint32_t* __restrict__ big,
                                                       const uint32_t* __restrict__ nbig, ShdDeliv* out) {
-    __shared__ Ev sv[kMidSeg];
+    extern __shared__ __attribute__((aligned(16))) char mid_smem[];
+    Ev* sv = reinterpret_cast<Ev*>(mid_smem);
     const uint32_t nb = *nbig;
     for (uint32_t q = blockIdx.x; q < nb; q += gridDim.x) {
         const uint32_t d = big[q];
@@ -1175,6 +1176,18 @@ int slab_reserve(uint32_t H) {
     return rc;
 }
 
+// k_segsort_mid's dynamic LDS (above the 64 KiB default), set once per process
+constexpr size_t kMidLds = sizeof(Ev) * kMidSeg;
+int mid_attr() {
+    static bool done = false;
+    if (done) return 0;
+    int rc = hip_status(hipFuncSetAttribute((const void*)k_segsort_mid, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)kMidLds),
+                        "hipFuncSetAttribute k_segsort_mid");
+    done = rc == 0;
+    return rc;
+}
+
 unsigned grid_for(size_t n, unsigned block, unsigned cap) {
     size_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
@@ -1274,7 +1287,8 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* ra
     mark(3, s);
     hipLaunchKernelGGL(k_bucket_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, g_ws.st1, bk, g_ws.off1, offsets, out,
                        g_ws.big, g_ws.nbig);
-    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
+    if (int rc = mid_attr()) return rc;
+    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, out, offsets, g_ws.big, g_ws.nbig, out);
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
@@ -1304,7 +1318,9 @@ int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.st1, offsets, H, host_lo, out,
                        g_ws.big, g_ws.nbig, rank_sort(), 0u, H, slab, slab_rm);
-    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
+    if (int rc = mid_attr()) return rc;
+    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig,
+                       out);
     hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;

@@ -482,7 +482,7 @@ def test_packet_round_zipf_senders(pipeline):
 
 
 def test_medium_segments_lds_path(pipeline):
-    """Destinations with 257..2048 events in a round (a server host receiving
+    """Destinations with 257..4096 events in a round (a server host receiving
     from many clients): the LDS bitonic segment sort."""
     gml, H = GRAPHS["complete30_ms"]
     top, orc, ips, st = make_pair(gml, H)
@@ -495,4 +495,4 @@ def test_medium_segments_lds_path(pipeline):
     oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
     assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
     seg = np.diff(offs)
-    assert ((seg > 256) & (seg <= 2048)).sum() >= 4
+    assert ((seg > 256) & (seg <= 4096)).sum() >= 4
