@@ -1289,7 +1289,7 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* ra
                        g_ws.big, g_ws.nbig);
     if (int rc = mid_attr()) return rc;
     hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, out, offsets, g_ws.big, g_ws.nbig, out);
-    hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
+    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort launch");
@@ -1321,7 +1321,7 @@ int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_
     if (int rc = mid_attr()) return rc;
     hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig,
                        out);
-    hipLaunchKernelGGL(k_segsort_big, dim3(64), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
+    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort_rank launch");
