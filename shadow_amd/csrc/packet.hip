@@ -230,12 +230,10 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
                         if (p[k].src_host != p[k].dst_host && t < barrier) t = barrier; // host_single.c:187-192
                         st = SHD_DELIVERED;
                         uint32_t rank;
-                        if (kMode == 3) rank = (uint32_t)idx[k] & (kSlab - 1); // probe: no atomic
-                        else if (kRank) rank = atomicAdd(&cnt1[p[k].dst_host], 1u);
+                        if (kRank) rank = atomicAdd(&cnt1[p[k].dst_host], 1u);
                         else rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
                         const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
-                        if (kMode == 4) { if (rank == ~0u) st_ev(&tmp[0], ev); } // probe: no event write
-                        else if (kMode < 2) st_ev(&tmp[idx[k]], ev);
+                        if (kMode < 2) st_ev(&tmp[idx[k]], ev);
                         else if (rank < kSlab)
                             st_ev(&tmp[bk.slab_rm ? (size_t)rank * bk.H + p[k].dst_host
                                                   : (size_t)p[k].dst_host * kSlab + rank], ev);
@@ -725,21 +723,14 @@ __device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, 
 }
 
 // Sorts one destination segment of n <= kSmallSeg events with one wave.
-// algo: 1 rank sort, 0 bitonic network, 2 copy without sorting (a
-// benchmark probe of the memory side only; never selected by the library).
+// algo: 1 rank sort, 0 bitonic network.
 // Element i of the segment is src[b + perm[i]] (LDS index list) or
 // src[b + i * stride] (stride 1: contiguous; H: a rank-major slab).
 __device__ __forceinline__ void sort_segment(uint32_t algo, const ShdDeliv* __restrict__ src, uint32_t b,
                                              const uint16_t* perm, uint32_t n, uint32_t d,
                                              ShdDeliv* __restrict__ out, uint32_t o, int lane,
                                              uint32_t stride = 1) {
-    if (algo == 2) {
-        for (uint32_t i = lane; i < n; i += 64) {
-            ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i * stride)]);
-            r.pad = 0;
-            st_ev(&out[o + i], r);
-        }
-    } else if (algo == 1) {
+    if (algo == 1) {
         auto load = [&](uint32_t i) {
             const ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i * stride)]);
             return Ev{r.time, r.seq, r.src_host, r.pkt_index};
@@ -1202,11 +1193,9 @@ bool staged_partition() {
 }
 
 // SHD_SEGSORT=bitonic selects the bitonic segment network, else rank sort
-// (SHD_SEGSORT=probe-copy: no sorting at all, a benchmark probe only).
 uint32_t rank_sort() {
     const char* v = getenv("SHD_SEGSORT");
     if (v && strcmp(v, "bitonic") == 0) return 0;
-    if (v && strcmp(v, "probe-copy") == 0) return 2;
     return 1;
 }
 
@@ -1369,14 +1358,6 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
         const char* sb = getenv("SHD_SCATTER_BATCH");
         if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
             hipLaunchKernelGGL((k_pkt_scatter<2, 8>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
-                               g_ws.nbig + 1);
-        else if (pipe == kSlabPipe && sb && strcmp(sb, "probe-noatomic") == 0) // benchmark probes only:
-            hipLaunchKernelGGL((k_pkt_scatter<3>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
-                               g_ws.nbig + 1);                                  // wrong output by design
-        else if (pipe == kSlabPipe && sb && strcmp(sb, "probe-nowrite") == 0)
-            hipLaunchKernelGGL((k_pkt_scatter<4>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
                                end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
                                g_ws.nbig + 1);
         else if (pipe == kSlabPipe && sb && strcmp(sb, "2") == 0)
