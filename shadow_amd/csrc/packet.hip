@@ -3,26 +3,27 @@
 // core/scheduler/scheduler.c:232-255, scheduler_policy_host_single.c:174-220,
 // core/work/event.c:109-152, utility/random.c:32-43).
 //
-// Pipeline over one round's batch (device-resident, one stream, no global
-// atomics on the event path -- device-scope atomics execute memory-side on
-// gfx950, ~20 G/s for scattered addresses, which bounded the first version):
-//   k_pkt_scatter  tile of 8192 records per workgroup: host->slot gathers,
-//                  owner resolution of the reference cache (touch order /
-//                  pair bits), 16 B table gather, the sender's reserved
-//                  rand_r draw, drop rule, ceil(lat * 1e6) delay, end-time
-//                  drop, barrier clamp; writes the event and counts it in an
-//                  LDS histogram over destination *buckets* (128 hosts each).
-//                  HBM-bound; the roofline is quoted on this kernel.
-//   k_scan_*       exclusive scan of the (bucket x tile) count matrix.
-//   k_part1        per tile: LDS ranks -> event into its bucket's region.
-//   k_part2_sort   per bucket (workgroup): LDS histogram + scan over its
-//                  128 destinations -> per-destination offsets, LDS-ranked
-//                  placement, then one wave per destination sorts the
-//                  segment by event_compare's remaining keys (time, src host,
-//                  srcHostEventID) with a register bitonic network.
+// Pipeline over one round's batch (device-resident, one stream), default
+// "slab" (SHD_PACKET_PIPELINE=slab):
+//   k_pkt_scatter<2> per record: host->slot gathers, owner resolution of the
+//                  reference cache (touch order / pair bits), 16 B table
+//                  gather, the sender's reserved rand_r draw, drop rule,
+//                  ceil(lat * 1e6) delay, end-time drop, barrier clamp; the
+//                  event's slot = old value of its destination's counter, and
+//                  the event goes straight to slab[dst * kSlab + slot] (slots
+//                  >= kSlab to an overflow list).  The roofline is quoted on
+//                  this kernel.
+//   k_scan_*       exclusive scan of the per-destination counts -> offsets.
+//   k_place_ovf    overflow events only (grid-stride over a device count).
+//   k_segsort_dst  one wave per destination: register rank sort of its slab
+//                  by (time, src host, srcHostEventID), written at off[dst].
 //   k_segsort_mid  listed segments up to 4096 events: LDS bitonic, one workgroup each.
-//   k_segsort_big  larger segments:
-//                  padded all-ascending bitonic network in HBM.
+//   k_segsort_big  larger segments: padded all-ascending bitonic network in HBM.
+// Alternatives, all bit-exact and parity-tested: "rank" (events in record
+// order, then k_place_rank over the whole batch) and "bucket" (LDS
+// histograms over destination buckets, k_place_bucket, k_bucket_sort; no
+// global atomics).  The multi-GPU regroup (shd_dev_deliv_sort) uses the same
+// pipelines (k_hist_slab / k_hist_rank / k_hist_tiles).
 // event_compare is a total order, so per-destination heap pop order
 // (priority_queue.c) equals this sorted order: the output is identical to
 // pushing every event into its destination's queue.
