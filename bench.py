@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r01_traffic_slab.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
@@ -60,6 +60,48 @@ def parse():
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def gpu_state(dev_index):
+    """Clocks and compute/memory partition mode of the box (read-only
+    rocm-smi query) plus the device properties, so that run-to-run spreads
+    can be attributed from the bench record alone."""
+    import subprocess
+
+    import torch
+    p = torch.cuda.get_device_properties(dev_index)
+    st = {"name": p.name, "gcn_arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
+          "total_mem_gb": round(p.total_memory / 2**30, 1)}
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--showcomputepartition", "--showmemorypartition",
+                            "--json"], capture_output=True, text=True, timeout=30)
+        js = json.loads(r.stdout) if r.returncode == 0 and r.stdout.strip().startswith("{") else {}
+        keep = {}
+        for card, kv in js.items():
+            if isinstance(kv, dict):
+                keep[card] = {k: v for k, v in kv.items()
+                              if any(w in k.lower() for w in ("sclk", "mclk", "fclk", "socclk", "partition"))}
+        st["rocm_smi"] = keep
+    except Exception as e:  # the record is informational; never fail the bench on it
+        st["rocm_smi_error"] = repr(e)[:200]
+    return st
+
+
+def routing_roofline(A, build_s, csr_bytes, rows, pops_per_row, traffic=None):
+    """Routing build roofline: compulsory bytes = the 16-B {lat, rel} table
+    entries written (16 A x rows) + the CSR read once; the kernel is bound
+    by random memory requests, so the PMC request count per
+    heap pop is reported beside the byte fraction when a PMC record exists."""
+    alg = 16.0 * A * rows + csr_bytes
+    out = {"bound": "hbm (random-request rate)", "alg_bytes": alg, "achieved": alg / build_s / 1e9,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / build_s / 1e9 / HBM_PEAK_GBS,
+           "pops": rows * pops_per_row}
+    if traffic:
+        rq = (traffic.get("rd_requests") or 0) + (traffic.get("wr_requests") or 0)
+        out.update({"traffic": traffic["bytes"], "traffic_GBps": traffic["bytes"] / build_s / 1e9,
+                    "requests": rq, "requests_per_pop": rq / (rows * pops_per_row) if rq else None,
+                    "requests_per_s": rq / build_s if rq else None})
+    return out
 
 
 def main():
@@ -167,6 +209,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    state_before = gpu_state(local) if rank == 0 else None
     lib = _lib.lib()
     _lib.check(lib.shd_round_timing_enable(1))
     barrier()
@@ -192,7 +235,7 @@ def main():
     achieved = [alg_bytes[k] / (per_launch_ms[k] * 1e-3) / 1e9 if per_launch_ms[k] > 0 else 0.0 for k in range(4)]
     total_pkts = P * world * args.steps
     value = total_pkts / dt
-    traffic, traffic_src = None, None
+    traffic, traffic_src, tj = None, None, {}
     if args.traffic and os.path.exists(args.traffic):
         with open(args.traffic) as f:
             tj = json.load(f)
@@ -229,6 +272,7 @@ def main():
             "timing": "HIP events on the launch stream, averaged over the timed steps",
             "pipeline": os.environ.get("SHD_PACKET_PIPELINE") or "slab",
         },
+        "gpu_state": {"before_timed": state_before, "after_timed": gpu_state(local) if rank == 0 else None},
     }
 
     # ------------------------------------------------------------ C1 routing
@@ -250,11 +294,18 @@ def main():
         torch.cuda.synchronize(dev)
         barrier()
         tr = max_over_ranks((time.perf_counter() - s0) / reps)
+        info1 = t1.info()
+        info2 = top.info()
+        t_c2 = max(max_over_ranks(t_rows_c2), 1e-9)
         result["routing"] = {
             "config": "C1 complete graph V=1000 (E=500,500 incl. self-loops), H=5000 hosts, A=%d attached" % A1,
             "value": 5000.0 ** 2 / tr, "unit": "routed host-pairs/s", "vertex_pairs_per_s": A1 * A1 / tr,
             "ms_per_table": tr * 1e3, "kernel": "k_sssp_rows<lds> (igraph-exact Dijkstra, 1 wave/source)",
-            "c2_rows_s": t_rows_c2, "c2_host_pairs_per_s": (H * H) / max(max_over_ranks(t_rows_c2), 1e-9),
+            "roofline": routing_roofline(A1, tr, 20.0 * 2 * info1["edges"] + 4 * 1001, max(h1 - l1, 0), 1000,
+                                         tj.get("routing_lds")),
+            "c2_rows_s": t_rows_c2, "c2_host_pairs_per_s": (H * H) / t_c2,
+            "c2_roofline": routing_roofline(A, t_c2, 20.0 * 2 * info2["edges"] + 4 * (V + 1), max(hi - lo, 0), V,
+                                            tj.get("routing_slab")),
         }
 
     # ------------------------------------------------- C4 routing-table build
@@ -287,6 +338,8 @@ def main():
             "value": float(args.c4_hosts) ** 2 / tr4, "unit": "routed host-pairs/s",
             "vertex_pairs_per_s": float(A4) * A4 / tr4, "build_s": tr4,
             "kernel": "k_sssp_rows<slab> (igraph-exact Dijkstra, 1 wave/source, persistent)",
+            "roofline": routing_roofline(A4, tr4, 20.0 * 2 * t4.info()["edges"] + 4 * (args.c4_vertices + 1),
+                                         max(h4 - l4, 0), args.c4_vertices, tj.get("routing_slab_c4")),
         }
         # C4 packet delivery: 1,000 rounds of packets on the full 100k-vertex
         # table.  At N=1 the table is resident (A4^2 x 16 B = 120 GB of the

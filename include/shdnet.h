@@ -189,6 +189,13 @@ int shd_deliv_sort_device(ShdTopology* top, const ShdDeliv* d_in, size_t n, uint
 int shd_round_timing_enable(int enable);
 int shd_round_timing_read(double* stage_ms, int nstages, int* launches);
 
+/* Unit strings as the GML loader reads them (replace parse_time_nanosec /
+ * parse_bandwidth, bindings.h:279,282, core/support/units.rs:777-837):
+ * "<u64>[ ]<unit>", unit default seconds / bits.  -EINVAL on a malformed
+ * string (e.g. "10.5 ms", units.rs:632). */
+int shd_parse_time_ns(const char* s, uint64_t* ns);
+int shd_parse_bandwidth_bits(const char* s, uint64_t* bits_per_s);
+
 /* Last error message for this thread (static storage). */
 const char* shd_last_error(void);
 

@@ -1294,6 +1294,31 @@ int orc_topology_min_jump_updates(const OrcTopo* t) { return t->min_updates; }
 uint64_t orc_controller_next_min_jump_ns(const OrcTopo* t) { return t->next_min_jump_ns; }
 
 int orc_topology_preload_table(OrcTopo* t, const int* slots, int nslots, const double* lat, const double* rel) {
+    int empty = t->use_sp;
+    for (int v = 0; v < t->V && empty; v++) empty = t->cache[v] == NULL;
+    if (empty) {
+        /* Same stores, same order, without the lookups: on an empty cache
+         * row i's store of (s_i, s_j) succeeds exactly for j >= i (the
+         * reverse (s_j, s_i), j < i, was stored by the earlier row j). */
+        for (int i = 0; i < nslots; i++) {
+            int s = slots[i];
+            if (!t->cache[s]) t->cache[s] = (PathE*)calloc((size_t)t->V, sizeof(PathE));
+            for (int j = i; j < nslots; j++) {
+                PathE* p = &t->cache[s][slots[j]];
+                p->present = 1;
+                p->is_direct = (unsigned char)(i == j);
+                p->lat = lat[(size_t)i * nslots + j];
+                p->rel = rel[(size_t)i * nslots + j];
+                p->pkts = 0;
+                if (t->min_lat == 0 || p->lat < t->min_lat) {
+                    t->min_lat = p->lat;
+                    t->min_updates++;
+                    controller_update(t, t->min_lat);
+                }
+            }
+        }
+        return 0;
+    }
     for (int i = 0; i < nslots; i++) {
         int s = slots[i];
         for (int j = 0; j < nslots; j++) {
@@ -1305,6 +1330,20 @@ int orc_topology_preload_table(OrcTopo* t, const int* slots, int nslots, const d
             }
         }
     }
+    return 0;
+}
+
+/* Rows of a table whose columns are all attached vertices (slot order):
+ * stores (rows[i], cols[j]) in row order, i.e. as if rows[0], rows[1], ...
+ * had been touched first, in that order (the _topology_storePathInCache rule
+ * keeps the first stored direction of a pair).  Used to check a sampled
+ * subset of a table too large for preload_table (C4: 86k x 86k). */
+int orc_topology_preload_rows(OrcTopo* t, const int* rows, int nrows, const int* cols, int ncols, const double* lat,
+                              const double* rel) {
+    for (int i = 0; i < nrows; i++)
+        for (int j = 0; j < ncols; j++)
+            cache_store(t, rows[i] == cols[j], rows[i], cols[j], lat[(size_t)i * ncols + j],
+                        rel[(size_t)i * ncols + j]);
     return 0;
 }
 

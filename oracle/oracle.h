@@ -86,6 +86,10 @@ int orc_vertex_of_ip(OrcTopo* t, uint32_t ip_net);
  * list `slots`.  Entries are inserted as if rows were touched in slot order. */
 int orc_topology_preload_table(OrcTopo* t, const int* slots, int nslots, const double* lat,
                                const double* rel);
+/* Full rows (nrows x ncols, columns = the attached vertices `cols`) inserted
+ * as if rows[0], rows[1], ... were touched first, in that order. */
+int orc_topology_preload_rows(OrcTopo* t, const int* rows, int nrows, const int* cols, int ncols,
+                              const double* lat, const double* rel);
 
 /* ---- packet hand-off (core/worker.c:517-576, scheduler push, event order) ---- */
 typedef struct OrcPkt {

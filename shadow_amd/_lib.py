@@ -62,6 +62,8 @@ PROTOS = {
     "shd_deliv_sort_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "shd_round_timing_enable": (C.c_int, [C.c_int]),
     "shd_round_timing_read": (C.c_int, [_dp, C.c_int, _ip]),
+    "shd_parse_time_ns": (C.c_int, [C.c_char_p, _u64p]),
+    "shd_parse_bandwidth_bits": (C.c_int, [C.c_char_p, _u64p]),
     "shd_last_error": (C.c_char_p, []),
 }
 

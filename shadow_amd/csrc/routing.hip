@@ -122,9 +122,11 @@ struct Heap {
             const int l = 2 * e + 1;
             if (l >= n) break;
             HNode c = ld(l);
-            const HNode r = ld(l + 1);
             int ci = l;
-            if (l + 1 < n && !(c.key >= r.key)) c = r, ci = l + 1;
+            if (l + 1 < n) { // (the right child exists: never read past the heap)
+                const HNode r = ld(l + 1);
+                if (!(c.key >= r.key)) c = r, ci = l + 1;
+            }
             if (!(x.key < c.key)) break;
             st(e, c);
             e = ci;

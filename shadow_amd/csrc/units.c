@@ -7,6 +7,7 @@
  * trimmed, mapped through the prefix table; value * factor checked in u64,
  * then checked into i64.  Any failure -> -1.
  */
+#include <errno.h>
 #include <string.h>
 
 #include "shd_internal.h"
@@ -119,4 +120,19 @@ int64_t shd_units_bandwidth_bits(const char* s) {
     else if (len >= 4 && memcmp(sp.u1 - 4, "bits", 4) == 0) len -= 4;
     if (lookup(kSiUpper, sizeof kSiUpper / sizeof *kSiUpper, sp.u0, len, &f)) return -1;
     return scaled(sp.v0, sp.v1, f);
+}
+
+/* C-ABI exports (include/shdnet.h): the same rules the GML loader applies. */
+int shd_parse_time_ns(const char* s, uint64_t* ns) {
+    const int64_t v = shd_units_time_ns(s);
+    if (v < 0) return shd_fail(-EINVAL, "invalid time string");
+    if (ns) *ns = (uint64_t)v;
+    return 0;
+}
+
+int shd_parse_bandwidth_bits(const char* s, uint64_t* bits) {
+    const int64_t v = shd_units_bandwidth_bits(s);
+    if (v < 0) return shd_fail(-EINVAL, "invalid bandwidth string");
+    if (bits) *bits = (uint64_t)v;
+    return 0;
 }

@@ -165,17 +165,23 @@ DELIV_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("src_host", "<u4"), ("
 
 def packet_batch(n: int, nhosts: int, seed: int, window_start: int, window_ns: int,
                  host_seeds: np.ndarray, zipf: bool = False, p_payload: float = 0.9,
-                 hosts_lo: int = 0, hosts_hi: int | None = None, hosts: np.ndarray | None = None) -> np.ndarray:
+                 hosts_lo: int = 0, hosts_hi: int | None = None, hosts: np.ndarray | None = None,
+                 pairs: tuple[np.ndarray, np.ndarray] | None = None) -> np.ndarray:
     """C3: one round's packet records.  src uniform over [hosts_lo, hosts_hi)
     (or Zipf s=1.1), dst uniform != src over all hosts, now uniform in the
     window, payload 1448 B with prob p_payload else 0.  With `hosts` given,
-    src and dst are both drawn from that host list instead (bounded samples).
+    src and dst are both drawn from that host list instead (bounded samples);
+    with `pairs` = (src, dst) arrays of length n they are taken as given.
     rng_state = the src host's real rand_r state advanced once per earlier
     packet of that host in this batch (the CPU reserves one draw per send);
     seq = per-src ordinal."""
     rng = SplitMix64(seed)
     r = rng.array(4 * n)
-    if hosts is not None:
+    if pairs is not None:
+        src = np.asarray(pairs[0], dtype=np.uint32)
+        dst = np.asarray(pairs[1], dtype=np.uint32)
+        assert len(src) == len(dst) == n
+    elif hosts is not None:
         hosts = np.asarray(hosts, dtype=np.uint32)
         m = len(hosts)
         si = (r[0::4] % np.uint64(m)).astype(np.int64)

@@ -65,6 +65,9 @@ lib.orc_vertex_of_ip.restype = C.c_int
 lib.orc_vertex_of_ip.argtypes = [C.c_void_p, C.c_uint32]
 lib.orc_topology_preload_table.restype = C.c_int
 lib.orc_topology_preload_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+lib.orc_topology_preload_rows.restype = C.c_int
+lib.orc_topology_preload_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                          C.c_void_p]
 lib.orc_round.restype = C.c_size_t
 lib.orc_round.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
                           C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, u64p]
@@ -158,6 +161,25 @@ class OracleTopology:
         lat = np.ascontiguousarray(lat, dtype=np.float64)
         rel = np.ascontiguousarray(rel, dtype=np.float64)
         lib.orc_topology_preload_table(self.h, slots.ctypes.data, len(slots), lat.ctypes.data, rel.ctypes.data)
+
+    def preload_rows(self, rows, cols, lat, rel):
+        """Full rows over the column vertices, stored as if `rows` were touched first, in order."""
+        rows = np.ascontiguousarray(rows, dtype=np.int32)
+        cols = np.ascontiguousarray(cols, dtype=np.int32)
+        lat = np.ascontiguousarray(lat, dtype=np.float64)
+        rel = np.ascontiguousarray(rel, dtype=np.float64)
+        assert lat.shape == rel.shape == (len(rows), len(cols))
+        lib.orc_topology_preload_rows(self.h, rows.ctypes.data, len(rows), cols.ctypes.data, len(cols),
+                                      lat.ctypes.data, rel.ctypes.data)
+
+    def rows_parallel(self, sources, targets, threads=16):
+        """orc.row for many sources on a thread pool (ctypes releases the GIL;
+        rows are independent).  Returns (lat[len(sources), len(targets)], rel)."""
+        from concurrent.futures import ThreadPoolExecutor
+        sources = [int(s) for s in sources]
+        with ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(lambda s: self.row(s, targets), sources))
+        return np.stack([r[0] for r in res]), np.stack([r[1] for r in res])
 
     def round(self, host_ips, pkts, barrier, end_time, bootstrap_end=0):
         from shadow_amd.synth import DELIV_DTYPE

@@ -104,6 +104,24 @@ def test_attach_matches_oracle_with_hints():
         assert a == b, (h, ip_hint, city, country)
 
 
+def test_product_unit_parser_matches_reference_tests():
+    """csrc/units.c (the parser the GML loader uses) against the cases and
+    values the reference's own Rust tests state (units.rs:579-775), the same
+    fixture the oracle is pinned by."""
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "units_cases.json")))
+    lib = _lib.lib()
+    out = C.c_uint64()
+    for fn, key in ((lib.shd_parse_time_ns, "time_ns"), (lib.shd_parse_bandwidth_bits, "bandwidth_bits")):
+        for s, want in g[key]:
+            rc = fn(s.encode(), C.byref(out))
+            if want < 0:
+                assert rc != 0, s
+            else:
+                assert rc == 0 and out.value == want, (s, want, out.value)
+    assert len(g["time_ns"]) >= 10 and any(w < 0 for _, w in g["time_ns"])
+
+
 def test_seed_chain_matches_reference_fixture():
     import json
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "ref_random_pq.json")))

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import oracle_ctypes as O
-from shadow_amd import synth
+from shadow_amd import scenario, synth
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -181,3 +181,22 @@ def test_round_oracle_basic():
     assert mt == 20_000_000  # every delivery clamps to the barrier (now + 1 ms < barrier)
     keys = list(zip(out["dst_host"], out["time"], out["src_host"], out["seq"]))
     assert keys == sorted(keys)
+
+
+def test_preload_fast_path_equals_store_rule():
+    """orc_topology_preload_table's empty-cache fast path stores exactly what
+    the _topology_storePathInCache rule (orc_topology_preload_rows, every
+    store through the cache checks) stores for rows touched in slot order."""
+    gml = synth.sparse_graph_gml(60, 0x5EED0099, ns_variant=True)
+    a, b = O.OracleTopology(gml), O.OracleTopology(gml)
+    ips, _, verts = scenario.register_hosts(a, 90, 1)
+    scenario.register_hosts(b, 90, 1)
+    sv = np.unique(verts).astype(np.int32)
+    lat, rel = a.rows_parallel(sv, sv, 4)
+    a.preload(sv, lat, rel)
+    b.preload_rows(sv, sv, lat, rel)
+    assert a.min_path_latency() == b.min_path_latency() and a.min_jump_updates() == b.min_jump_updates()
+    for s in ips[::7]:
+        for d in ips[::5]:
+            assert a.latency(int(s), int(d)) == b.latency(int(s), int(d))
+            assert a.reliability(int(s), int(d)) == b.reliability(int(s), int(d))
