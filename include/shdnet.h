@@ -118,6 +118,11 @@ int shd_topology_adopt_table_device_resident(ShdTopology* top, void* d_table);
 /* Marks every attached vertex row touched, in slot order (steady state of a
  * long simulation; used by benchmarks before timing). */
 int shd_topology_touch_all(ShdTopology* top);
+/* Release state, for tests and tooling: per table slot, the touch sequence
+ * number of its row (UINT32_MAX = never touched) and whether its self pair
+ * was released; either pointer may be NULL.  The owner of a released pair
+ * {X, Y} is the row with the smaller sequence number. */
+int shd_topology_touch_order(ShdTopology* top, uint32_t* touch_seq, uint8_t* self_released, int cap_slots);
 
 /* ---------------------------------------------------------------------- */
 /* Per-round packet hand-off (replaces worker_sendPacket + scheduler push) */
@@ -150,12 +155,26 @@ enum { SHD_DROPPED_LOSS = 0, SHD_DELIVERED = 1, SHD_DROPPED_END = 2 };
  * end_time = scheduler endTime (scheduler.c:236), bootstrap_end =
  * bootstrap_end_time (worker.rs:339-341). */
 int shd_round_begin(ShdTopology* top, uint64_t barrier, uint64_t end_time, uint64_t bootstrap_end);
-/* Appends sends (host memory, copied).  Performs the reference's lookup side
- * effects for each send in order (row touch, min-jump), exactly as the three
- * topology_* calls of worker_sendPacket would.  Thread-compatible: callers
- * serialise appends (one producer per round, as manager_run's boundary). */
+/* Number of worker threads that append (Shadow's worker pool size,
+ * worker.c:132-185); each gets its own staging buffer.  Default 1.  Only
+ * between rounds (-EBUSY while records are staged). */
+int shd_round_set_workers(ShdTopology* top, int nworkers);
+/* Called by worker `worker` inside worker_sendPacket, at send time: performs
+ * the reference's lookup side effects for each send right away, in send
+ * order (row touch, min-jump -- topology_getReliability at worker.c:539), and
+ * stages the records (host memory, copied) in that worker's own buffer.
+ * Workers append concurrently without locking each other; a worker index is
+ * used by one thread at a time.  The whole batch is validated first: on
+ * -ENOENT (an unattached host) nothing was staged and no side effect ran.
+ * pkt_index in shd_round_collect's output counts records in worker order
+ * (worker 0's records first, each worker's in append order). */
+int shd_round_append_worker(ShdTopology* top, int worker, const ShdPkt* recs, size_t n);
+/* shd_round_append_worker(top, 0, recs, n) (single producer). */
 int shd_round_append(ShdTopology* top, const ShdPkt* recs, size_t n);
-/* Runs the batch on the GPU and returns delivered events grouped by
+/* Records staged for the current round, over all workers. */
+int shd_round_staged(ShdTopology* top, size_t* n);
+/* At the round boundary (workers idle): runs the batch on the GPU and
+ * returns delivered events grouped by
  * destination host: out[dst_offsets[h] .. dst_offsets[h+1]) is host h's
  * events in event_compare order (dst_offsets has nhosts+1 entries, may be
  * NULL).  status (may be NULL) receives one outcome per appended record.

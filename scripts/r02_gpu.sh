@@ -21,6 +21,7 @@ ok_or_assert() { # continue on pytest's "tests failed" (1), stop on anything els
 }
 pmc_passes() { # $1 = out dir, rest = bench args
   local D=$1; shift
+  mkdir -p $D
   local i=0
   while read -r GROUP; do
     [ -z "$GROUP" ] && continue
@@ -32,7 +33,7 @@ pmc_passes() { # $1 = out dir, rest = bench args
 for STEP in "$@"; do
   case $STEP in
     test)
-      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread --durations=15 ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest.log 2>&1
+      timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -v --timeout 600 --timeout-method thread --durations=15 ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest.log 2>&1
       rc=$?; tail -25 $O/pytest.log; ok_or_assert $rc ;;
     bench)
       timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }

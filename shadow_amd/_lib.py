@@ -53,9 +53,13 @@ PROTOS = {
     "shd_topology_adopt_table_device": (C.c_int, [_P, _P]),
     "shd_topology_adopt_table_device_resident": (C.c_int, [_P, _P]),
     "shd_topology_touch_all": (C.c_int, [_P]),
+    "shd_topology_touch_order": (C.c_int, [_P, _P, _P, C.c_int]),
     "shd_topology_host_count": (C.c_int, [_P, _u32p]),
     "shd_round_begin": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "shd_round_set_workers": (C.c_int, [_P, C.c_int]),
+    "shd_round_append_worker": (C.c_int, [_P, C.c_int, _P, C.c_size_t]),
     "shd_round_append": (C.c_int, [_P, _P, C.c_size_t]),
+    "shd_round_staged": (C.c_int, [_P, C.POINTER(C.c_size_t)]),
     "shd_round_collect": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_size_t), _P, _P, _u64p]),
     "shd_round_process_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint64, _P, _P, _P, _P,
                                            _P]),

@@ -13,12 +13,15 @@ static int hip_err(hipError_t e, const char* what) {
     return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
 }
 
+// Selects `device` for the calling thread (HIP's current device is per
+// thread: lookups may come from any worker); the device count and the gfx950
+// check run once per thread and device.
 extern "C" int shd_dev_init(int device) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return shd_fail(-ENODEV, "no HIP device visible");
-    if (device < 0 || device >= n) return shd_fail(-ENODEV, "device %d out of range (%d visible)", device, n);
     static thread_local int checked = -1;
     if (checked != device) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return shd_fail(-ENODEV, "no HIP device visible");
+        if (device < 0 || device >= n) return shd_fail(-ENODEV, "device %d out of range (%d visible)", device, n);
         hipDeviceProp_t p;
         if (hipGetDeviceProperties(&p, device) != hipSuccess) return shd_fail(-ENODEV, "device query failed");
         if (std::strncmp(p.gcnArchName, "gfx950", 6) != 0)

@@ -33,6 +33,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 
 #include "shd_internal.h"
 
@@ -1084,8 +1085,12 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
     }
 }
 
-// ---- workspace (grow-only, per process / device) ----
+// ---- workspace (grow-only, one per topology; see shd_dev_ws_new) ----
 struct Ws {
+    int device = -1;           // device the buffers live on
+    hipEvent_t done = nullptr; // recorded after the last launch that used the buffers
+    hipStream_t last = nullptr;
+    bool used = false;
     size_t cap_n = 0;
     ShdDeliv* tmp = nullptr; // decided events in record order
     ShdDeliv* st1 = nullptr; // events partitioned by bucket (bucket) / destination (rank)
@@ -1103,68 +1108,76 @@ struct Ws {
     size_t cap_slab = 0;      // slab pipeline: H x kSlab event slots
     ShdDeliv* slab = nullptr;
 };
-Ws g_ws;
 
 int hip_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return 0;
     return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
 }
 
-int ws_reserve(size_t n, size_t m, uint32_t H) {
+// Before buffers are freed or regrown, the last launch that used them (on
+// whatever stream) must have finished.
+int ws_quiesce(Ws& w) {
+    if (!w.used) return 0;
+    return hip_status(hipEventSynchronize(w.done), "hipEventSynchronize ws");
+}
+
+int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
     int rc = 0;
-    if (n > g_ws.cap_n) {
-        (void)hipFree(g_ws.tmp);
-        (void)hipFree(g_ws.st1);
-        (void)hipFree(g_ws.rnk);
-        (void)hipFree(g_ws.st2);
-        g_ws.tmp = g_ws.st1 = g_ws.st2 = nullptr;
-        g_ws.rnk = nullptr;
-        g_ws.cap_n = 0;
+    if ((n > w.cap_n || m + 1 > w.cap_m || H + 1 > w.cap_h) && (rc = ws_quiesce(w))) return rc;
+    if (n > w.cap_n) {
+        (void)hipFree(w.tmp);
+        (void)hipFree(w.st1);
+        (void)hipFree(w.rnk);
+        (void)hipFree(w.st2);
+        w.tmp = w.st1 = w.st2 = nullptr;
+        w.rnk = nullptr;
+        w.cap_n = 0;
         const size_t cap = n + n / 8 + 1024;
-        if ((rc = hip_status(hipMalloc((void**)&g_ws.tmp, sizeof(ShdDeliv) * cap), "hipMalloc ws.tmp")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.st1, sizeof(ShdDeliv) * cap), "hipMalloc ws.st1")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.rnk, sizeof(uint32_t) * cap), "hipMalloc ws.rnk")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.st2, sizeof(ShdDeliv) * cap), "hipMalloc ws.st2")))
+        if ((rc = hip_status(hipMalloc((void**)&w.tmp, sizeof(ShdDeliv) * cap), "hipMalloc ws.tmp")) ||
+            (rc = hip_status(hipMalloc((void**)&w.st1, sizeof(ShdDeliv) * cap), "hipMalloc ws.st1")) ||
+            (rc = hip_status(hipMalloc((void**)&w.rnk, sizeof(uint32_t) * cap), "hipMalloc ws.rnk")) ||
+            (rc = hip_status(hipMalloc((void**)&w.st2, sizeof(ShdDeliv) * cap), "hipMalloc ws.st2")))
             return rc;
-        g_ws.cap_n = cap;
+        w.cap_n = cap;
     }
-    if (m + 1 > g_ws.cap_m) {
-        (void)hipFree(g_ws.cnt1);
-        (void)hipFree(g_ws.off1);
-        (void)hipFree(g_ws.bsum);
-        (void)hipFree(g_ws.poff);
-        (void)hipFree(g_ws.cursor);
-        g_ws.cap_m = 0;
+    if (m + 1 > w.cap_m) {
+        (void)hipFree(w.cnt1);
+        (void)hipFree(w.off1);
+        (void)hipFree(w.bsum);
+        (void)hipFree(w.poff);
+        (void)hipFree(w.cursor);
+        w.cap_m = 0;
         const size_t cap = m + 1 + (m >> 3) + 4096;
-        if ((rc = hip_status(hipMalloc((void**)&g_ws.cnt1, 4 * cap), "hipMalloc ws.cnt1")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.off1, 4 * cap), "hipMalloc ws.off1")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.bsum, 4 * (cap / kScanTile + 2)), "hipMalloc ws.bsum")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.poff, 4 * cap), "hipMalloc ws.poff")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.cursor, 4 * (size_t)kMaxBuckets + 64), "hipMalloc ws.cursor")))
+        if ((rc = hip_status(hipMalloc((void**)&w.cnt1, 4 * cap), "hipMalloc ws.cnt1")) ||
+            (rc = hip_status(hipMalloc((void**)&w.off1, 4 * cap), "hipMalloc ws.off1")) ||
+            (rc = hip_status(hipMalloc((void**)&w.bsum, 4 * (cap / kScanTile + 2)), "hipMalloc ws.bsum")) ||
+            (rc = hip_status(hipMalloc((void**)&w.poff, 4 * cap), "hipMalloc ws.poff")) ||
+            (rc = hip_status(hipMalloc((void**)&w.cursor, 4 * (size_t)kMaxBuckets + 64), "hipMalloc ws.cursor")))
             return rc;
-        g_ws.cap_m = cap;
+        w.cap_m = cap;
     }
-    if (H + 1 > g_ws.cap_h) {
-        (void)hipFree(g_ws.big);
-        (void)hipFree(g_ws.nbig);
-        g_ws.cap_h = 0;
+    if (H + 1 > w.cap_h) {
+        (void)hipFree(w.big);
+        (void)hipFree(w.nbig);
+        w.cap_h = 0;
         const uint32_t cap = H + 1 + 1024;
-        if ((rc = hip_status(hipMalloc((void**)&g_ws.big, 4ull * cap), "hipMalloc ws.big")) ||
-            (rc = hip_status(hipMalloc((void**)&g_ws.nbig, 16), "hipMalloc ws.nbig")))
+        if ((rc = hip_status(hipMalloc((void**)&w.big, 4ull * cap), "hipMalloc ws.big")) ||
+            (rc = hip_status(hipMalloc((void**)&w.nbig, 16), "hipMalloc ws.nbig")))
             return rc;
-        g_ws.cap_h = cap;
+        w.cap_h = cap;
     }
     return 0;
 }
 
-int slab_reserve(uint32_t H) {
+int slab_reserve(Ws& w, uint32_t H) {
     const size_t need = (size_t)H * kSlab;
-    if (need <= g_ws.cap_slab) return 0;
-    (void)hipFree(g_ws.slab);
-    g_ws.slab = nullptr;
-    g_ws.cap_slab = 0;
-    int rc = hip_status(hipMalloc((void**)&g_ws.slab, sizeof(ShdDeliv) * need), "hipMalloc ws.slab");
-    if (!rc) g_ws.cap_slab = need;
+    if (need <= w.cap_slab) return 0;
+    if (int rc = ws_quiesce(w)) return rc;
+    (void)hipFree(w.slab);
+    w.slab = nullptr;
+    w.cap_slab = 0;
+    int rc = hip_status(hipMalloc((void**)&w.slab, sizeof(ShdDeliv) * need), "hipMalloc ws.slab");
+    if (!rc) w.cap_slab = need;
     return rc;
 }
 
@@ -1249,13 +1262,13 @@ void mark(int stage, hipStream_t s) {
 
 // scan of the count matrix, atomic-free placement into bucket regions,
 // per-bucket LDS sort (shared by both entry points)
-int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n, const Bucketing& bk,
+int group_and_sort(Ws& w, const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n, const Bucketing& bk,
                    ShdDeliv* out, uint32_t* offsets, unsigned long long* counters, hipStream_t s) {
     const size_t m = (size_t)bk.nb * bk.ntiles;
     const uint32_t nb = (uint32_t)((m + kScanTile - 1) / kScanTile);
-    hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, g_ws.cnt1, m, g_ws.off1, g_ws.bsum);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g_ws.bsum, nb);
-    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m + 1, 256, 1u << 30)), dim3(256), 0, s, g_ws.off1, m, g_ws.bsum,
+    hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, w.cnt1, m, w.off1, w.bsum);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, w.bsum, nb);
+    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m + 1, 256, 1u << 30)), dim3(256), 0, s, w.off1, m, w.bsum,
                        nb, counters);
     mark(2, s);
     if (staged_partition()) {
@@ -1265,21 +1278,21 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* ra
         const uint32_t np = (bk.nb + (1u << pshift) - 1) >> pshift;
         const size_t np_cols = (size_t)np * bk.ntiles;
         hipLaunchKernelGGL(k_part_offsets, dim3(grid_for(np_cols > bk.nb ? np_cols : bk.nb, 256, 1u << 30)),
-                           dim3(256), 0, s, g_ws.off1, bk, pshift, np, g_ws.poff, g_ws.cursor);
+                           dim3(256), 0, s, w.off1, bk, pshift, np, w.poff, w.cursor);
         hipLaunchKernelGGL(k_stage_parts, dim3(bk.ntiles), dim3(kStageBlock), 0, s, in, status, n, bk, pshift, np,
-                           g_ws.poff, g_ws.st2);
-        hipLaunchKernelGGL(k_refine, dim3(grid_for(n, kStageTile, 1u << 30)), dim3(kStageBlock), 0, s, g_ws.st2, bk,
-                           pshift, g_ws.off1, g_ws.cursor, g_ws.st1);
+                           w.poff, w.st2);
+        hipLaunchKernelGGL(k_refine, dim3(grid_for(n, kStageTile, 1u << 30)), dim3(kStageBlock), 0, s, w.st2, bk,
+                           pshift, w.off1, w.cursor, w.st1);
     } else {
         hipLaunchKernelGGL(k_place_bucket, dim3(bk.ntiles), dim3(kPlaceBlock), 0, s, in, status, rank, n, bk,
-                           g_ws.off1, g_ws.st1);
+                           w.off1, w.st1);
     }
     mark(3, s);
-    hipLaunchKernelGGL(k_bucket_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, g_ws.st1, bk, g_ws.off1, offsets, out,
-                       g_ws.big, g_ws.nbig);
+    hipLaunchKernelGGL(k_bucket_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, w.st1, bk, w.off1, offsets, out,
+                       w.big, w.nbig);
     if (int rc = mid_attr()) return rc;
-    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, out, offsets, g_ws.big, g_ws.nbig, out);
-    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, out, offsets, g_ws.big, g_ws.nbig, out);
+    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, out, offsets, w.big, w.nbig, out);
+    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, out, offsets, w.big, w.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort launch");
@@ -1289,29 +1302,29 @@ int group_and_sort(const ShdDeliv* in, const uint8_t* status, const uint32_t* ra
 // placement by rank, one wave per destination segment
 // slab: the scatter already wrote each event to its destination's slab (or
 // the overflow list); only overflow events are placed.
-int group_and_sort_rank(const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n,
+int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n,
                         uint32_t host_lo, uint32_t H, ShdDeliv* out, uint32_t* offsets,
                         unsigned long long* counters, hipStream_t s, const ShdDeliv* slab = nullptr,
                         uint32_t slab_rm = 0) {
     const uint32_t nb = (uint32_t)((H + kScanTile - 1) / kScanTile);
-    hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, g_ws.cnt1, (size_t)H, offsets, g_ws.bsum);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, g_ws.bsum, nb);
+    hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, w.cnt1, (size_t)H, offsets, w.bsum);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, w.bsum, nb);
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for((size_t)H + 1, 256, 1u << 30)), dim3(256), 0, s, offsets, (size_t)H,
-                       g_ws.bsum, nb, counters);
+                       w.bsum, nb, counters);
     mark(2, s);
     if (slab)
-        hipLaunchKernelGGL(k_place_ovf, dim3(512), dim3(256), 0, s, g_ws.st2, g_ws.nbig + 1, offsets, host_lo,
-                           g_ws.st1);
+        hipLaunchKernelGGL(k_place_ovf, dim3(512), dim3(256), 0, s, w.st2, w.nbig + 1, offsets, host_lo,
+                           w.st1);
     else if (n)
         hipLaunchKernelGGL(k_place_rank, dim3(grid_for(n, 256 * kBatch, 1u << 20)), dim3(256), 0, s, in, status, rank,
-                           n, host_lo, H, offsets, g_ws.st1, 0u, H);
+                           n, host_lo, H, offsets, w.st1, 0u, H);
     mark(3, s);
-    hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, g_ws.st1, offsets, H, host_lo, out,
-                       g_ws.big, g_ws.nbig, rank_sort(), 0u, H, slab, slab_rm);
+    hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, w.st1, offsets, H, host_lo, out,
+                       w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm);
     if (int rc = mid_attr()) return rc;
-    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig,
+    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, w.st1, offsets, w.big, w.nbig,
                        out);
-    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, g_ws.st1, offsets, g_ws.big, g_ws.nbig, out);
+    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, w.st1, offsets, w.big, w.nbig, out);
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort_rank launch");
@@ -1331,13 +1344,58 @@ int pipeline_for(uint32_t H, bool slab_ok) {
     return kSlabPipe;
 }
 
+// Orders this call's launches on stream s after the workspace's last use on
+// another stream (the buffers are shared); ws_end marks the end of this use.
+int ws_begin(Ws& w, hipStream_t s) {
+    int dev = 0;
+    int rc = hip_status(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    if (w.device >= 0 && w.device != dev) return shd_fail(-EINVAL, "workspace of device %d used on device %d", w.device, dev);
+    w.device = dev;
+    if (!w.done && (rc = hip_status(hipEventCreateWithFlags(&w.done, hipEventDisableTiming), "hipEventCreate ws")))
+        return rc;
+    if (w.used && w.last != s) return hip_status(hipStreamWaitEvent(s, w.done, 0), "hipStreamWaitEvent ws");
+    return 0;
+}
+int ws_end(Ws& w, hipStream_t s) {
+    w.last = s;
+    w.used = true;
+    return hip_status(hipEventRecord(w.done, s), "hipEventRecord ws");
+}
 
 } // namespace
+
+extern "C" int shd_dev_ws_new(void** ws) {
+    *ws = new (std::nothrow) Ws();
+    return *ws ? 0 : shd_fail(-ENOMEM, "workspace");
+}
+
+extern "C" void shd_dev_ws_free(void* p) {
+    if (!p) return;
+    Ws* w = static_cast<Ws*>(p);
+    if (w->used) (void)hipEventSynchronize(w->done);
+    (void)hipFree(w->tmp);
+    (void)hipFree(w->st1);
+    (void)hipFree(w->rnk);
+    (void)hipFree(w->st2);
+    (void)hipFree(w->cnt1);
+    (void)hipFree(w->off1);
+    (void)hipFree(w->poff);
+    (void)hipFree(w->cursor);
+    (void)hipFree(w->bsum);
+    (void)hipFree(w->big);
+    (void)hipFree(w->nbig);
+    (void)hipFree(w->slab);
+    if (w->done) (void)hipEventDestroy(w->done);
+    delete w;
+}
 
 extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                                     uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out,
                                     uint32_t* d_dst_offsets, uint8_t* d_status, uint64_t* d_counters, void* stream) {
     hipStream_t s = (hipStream_t)stream;
+    if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
+    Ws& w = *static_cast<Ws*>(c->ws);
     const uint32_t H = c->nhosts;
     const int pipe = pipeline_for(H, true);
     const bool rk = pipe != kBucketPipe;
@@ -1345,46 +1403,48 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     int rc = make_bucketing(0, H, n, &bk);
     if (rc) return rc;
     const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
-    if ((rc = ws_reserve(n, m, H))) return rc;
-    if (pipe == kSlabPipe && (rc = slab_reserve(H))) return rc;
+    if ((rc = ws_begin(w, s))) return rc;
+    if ((rc = ws_reserve(w, n, m, H))) return rc;
+    if (pipe == kSlabPipe && (rc = slab_reserve(w, H))) return rc;
     unsigned long long* counters = (unsigned long long*)d_counters;
-    if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 8, s), "memset nbig")) ||
+    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 8, s), "memset nbig")) ||
         (rc = hip_status(hipMemsetAsync(counters, 0xff, 16, s), "memset counters")))
         return rc;
     // rank: per-destination counters start at zero; bucket: every tile writes
     // its whole histogram column, only an empty batch needs zeros
-    if ((rk || !n) && (rc = hip_status(hipMemsetAsync(g_ws.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
+    if ((rk || !n) && (rc = hip_status(hipMemsetAsync(w.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
     mark(0, s);
     if (n) {
         const char* sb = getenv("SHD_SCATTER_BATCH");
         if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
             hipLaunchKernelGGL((k_pkt_scatter<2, 8>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
-                               g_ws.nbig + 1);
+                               end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2,
+                               w.nbig + 1);
         else if (pipe == kSlabPipe && sb && strcmp(sb, "2") == 0)
             hipLaunchKernelGGL((k_pkt_scatter<2, 2>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
-                               g_ws.nbig + 1);
+                               end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2,
+                               w.nbig + 1);
         else if (pipe == kSlabPipe)
             hipLaunchKernelGGL(k_pkt_scatter<2>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.slab, d_status, g_ws.cnt1, counters, g_ws.st2,
-                               g_ws.nbig + 1);
+                               end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2,
+                               w.nbig + 1);
         else if (rk)
             hipLaunchKernelGGL(k_pkt_scatter<1>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.tmp, d_status, g_ws.cnt1, counters, nullptr,
+                               end_time, bootstrap_end, bk, w.tmp, d_status, w.cnt1, counters, nullptr,
                                nullptr);
         else
             hipLaunchKernelGGL(k_pkt_scatter<0>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
-                               end_time, bootstrap_end, bk, g_ws.tmp, d_status, g_ws.cnt1, counters, nullptr,
+                               end_time, bootstrap_end, bk, w.tmp, d_status, w.cnt1, counters, nullptr,
                                nullptr);
     }
     mark(1, s);
     if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
     rc = pipe == kSlabPipe
-             ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s, g_ws.slab,
+             ? group_and_sort_rank(w, w.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s, w.slab,
                                    bk.slab_rm)
-         : rk ? group_and_sort_rank(g_ws.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s)
-              : group_and_sort(g_ws.tmp, d_status, nullptr, n, bk, d_out, d_dst_offsets, counters, s);
+         : rk ? group_and_sort_rank(w, w.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s)
+              : group_and_sort(w, w.tmp, d_status, nullptr, n, bk, d_out, d_dst_offsets, counters, s);
+    if (!rc) rc = ws_end(w, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "packet round");
 }
@@ -1417,9 +1477,11 @@ extern "C" int shd_round_timing_read(double* stage_ms, int nstages, int* launche
     return 0;
 }
 
-extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
-                                  uint32_t* d_dst_offsets, void* stream) {
+extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi,
+                                  ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream) {
     hipStream_t s = (hipStream_t)stream;
+    if (!ws) return shd_fail(-ENOMEM, "no round workspace");
+    Ws& w = *static_cast<Ws*>(ws);
     const uint32_t H = host_hi - host_lo;
     const int pipe = pipeline_for(H, true);
     const bool rk = pipe != kBucketPipe;
@@ -1427,27 +1489,29 @@ extern "C" int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_
     int rc = make_bucketing(host_lo, H, n, &bk);
     if (rc) return rc;
     const size_t m = rk ? (size_t)H : (size_t)bk.nb * bk.ntiles;
-    if ((rc = ws_reserve(n, m, H))) return rc;
-    if (pipe == kSlabPipe && (rc = slab_reserve(H))) return rc;
-    if ((rc = hip_status(hipMemsetAsync(g_ws.nbig, 0, 8, s), "memset nbig"))) return rc;
-    if ((rk || !n) && (rc = hip_status(hipMemsetAsync(g_ws.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
+    if ((rc = ws_begin(w, s))) return rc;
+    if ((rc = ws_reserve(w, n, m, H))) return rc;
+    if (pipe == kSlabPipe && (rc = slab_reserve(w, H))) return rc;
+    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 8, s), "memset nbig"))) return rc;
+    if ((rk || !n) && (rc = hip_status(hipMemsetAsync(w.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
     mark(0, s);
     if (n) {
         if (pipe == kSlabPipe)
             hipLaunchKernelGGL(k_hist_slab, dim3(grid_for(n, 256 * kBatch, 1u << 20)), dim3(256), 0, s, d_in, n,
-                               host_lo, H, g_ws.cnt1, g_ws.slab, bk.slab_rm, g_ws.st2, g_ws.nbig + 1);
+                               host_lo, H, w.cnt1, w.slab, bk.slab_rm, w.st2, w.nbig + 1);
         else if (rk)
             hipLaunchKernelGGL(k_hist_rank, dim3(grid_for(n, 256, 1u << 20)), dim3(256), 0, s, d_in, n, host_lo, H,
-                               g_ws.cnt1, g_ws.rnk);
+                               w.cnt1, w.rnk);
         else
-            hipLaunchKernelGGL(k_hist_tiles, dim3(bk.ntiles), dim3(kBlock), 0, s, d_in, n, bk, g_ws.cnt1, g_ws.rnk);
+            hipLaunchKernelGGL(k_hist_tiles, dim3(bk.ntiles), dim3(kBlock), 0, s, d_in, n, bk, w.cnt1, w.rnk);
     }
     mark(1, s);
     rc = pipe == kSlabPipe
-             ? group_and_sort_rank(d_in, nullptr, g_ws.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s, g_ws.slab,
+             ? group_and_sort_rank(w, d_in, nullptr, w.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s, w.slab,
                                    bk.slab_rm)
-         : rk ? group_and_sort_rank(d_in, nullptr, g_ws.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s)
-              : group_and_sort(d_in, nullptr, g_ws.rnk, n, bk, d_out, d_dst_offsets, nullptr, s);
+         : rk ? group_and_sort_rank(w, d_in, nullptr, w.rnk, n, host_lo, H, d_out, d_dst_offsets, nullptr, s)
+              : group_and_sort(w, d_in, nullptr, w.rnk, n, bk, d_out, d_dst_offsets, nullptr, s);
+    if (!rc) rc = ws_end(w, s);
     if (rc) return rc;
     return stream ? 0 : hip_status(hipStreamSynchronize(s), "deliv sort");
 }

@@ -40,7 +40,8 @@ void shd_topology_release_device(ShdTopology* t) {
         if (rc) goto fail;                                        \
     } while (0)
 
-/* Slots, device CSR and host->slot map.  Idempotent until an attach. */
+/* Slots, device CSR and host->slot map.  Idempotent until an attach.
+ * Caller holds setup_mu. */
 static int prepare(ShdTopology* t) {
     if (t->prepared && !t->routes_stale) return 0;
     int rc = shd_dev_init(t->device);
@@ -96,6 +97,7 @@ static int prepare(ShdTopology* t) {
     t->prepared = 1;
     t->built = 0;
     t->routes_stale = 0;
+    __atomic_store_n(&t->ready, 0, __ATOMIC_RELEASE);
     return 0;
 fail:
     free(w);
@@ -131,11 +133,11 @@ static int adopt(ShdTopology* t, ShdEntry* d_tab, int owned) {
     t->d_tab = d_tab;
     t->d_tab_owned = owned;
     t->built = 1;
+    __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE); /* publishes the immutable table to lock-free lookups */
     return 0;
 }
 
-int shd_topology_build_routes(ShdTopology* t) {
-    if (!t) return -EINVAL;
+static int build_routes_locked(ShdTopology* t) {
     if (t->built && !t->routes_stale) return 0;
     int rc = prepare(t);
     if (rc) return rc;
@@ -149,33 +151,53 @@ int shd_topology_build_routes(ShdTopology* t) {
     return rc;
 }
 
+int shd_topology_build_routes(ShdTopology* t) {
+    if (!t) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
+    int rc = build_routes_locked(t);
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
+}
+
+/* The first lookup builds the table (the reference computes rows lazily in
+ * whichever worker misses, topology.c:1940-1961); later ones see `ready`. */
+int shd_ensure_routes(ShdTopology* t) {
+    if (__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return 0;
+    return shd_topology_build_routes(t);
+}
+
 int shd_topology_slot_count(ShdTopology* t, int* A) {
     if (!t || !A) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
     int rc = prepare(t);
-    if (rc) return rc;
-    *A = t->A;
-    return 0;
+    if (!rc) *A = t->A;
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
 }
 
 int shd_topology_build_rows_device(ShdTopology* t, int row_lo, int row_hi, void* d_table) {
     if (!t || !d_table) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
     int rc = prepare(t);
-    if (rc) return rc;
-    if (row_lo < 0 || row_hi > t->A || row_lo > row_hi) return shd_fail(-EINVAL, "row range out of bounds");
+    if (!rc && (row_lo < 0 || row_hi > t->A || row_lo > row_hi)) rc = shd_fail(-EINVAL, "row range out of bounds");
     ShdGraphDev g = graph_dev(t);
-    return shd_dev_build_rows(&g, t->use_sp, row_lo, row_hi, (ShdEntry*)d_table);
+    if (!rc) rc = shd_dev_build_rows(&g, t->use_sp, row_lo, row_hi, (ShdEntry*)d_table);
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
 }
 
 int shd_topology_adopt_table_device(ShdTopology* t, void* d_table) {
     if (!t || !d_table) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
     int rc = prepare(t);
-    if (rc) return rc;
-    return adopt(t, (ShdEntry*)d_table, 0);
+    if (!rc) rc = adopt(t, (ShdEntry*)d_table, 0);
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
 }
 
 int shd_topology_copy_table(ShdTopology* t, double* lat, double* rel, int32_t* slot_vertex, int cap) {
     if (!t) return -EINVAL;
-    int rc = shd_topology_build_routes(t);
+    int rc = shd_ensure_routes(t);
     if (rc) return rc;
     if (cap < t->A) return shd_fail(-ENOSPC, "need %d slots", t->A);
     if (!t->h_tab) return shd_fail(-ENOTSUP, "the table is device-resident (no host mirror)");
@@ -191,7 +213,7 @@ int shd_topology_copy_table(ShdTopology* t, double* lat, double* rel, int32_t* s
 /* Uploads the release state the packet kernel reads (touch order or pair
  * bits) if it changed since the last upload. */
 int shd_sync_touch(ShdTopology* t) {
-    if (!t->touch_dirty) return 0;
+    if (!__atomic_exchange_n(&t->touch_dirty, 0, __ATOMIC_ACQ_REL)) return 0;
     int rc = shd_dev_h2d(t->d_touch, t->touch, sizeof(uint32_t) * (size_t)t->A);
     /* per-host {slot, touch[slot]} records: one 8-byte gather per endpoint */
     uint32_t* hs = t->h_host_info;
@@ -202,7 +224,7 @@ int shd_sync_touch(ShdTopology* t) {
         size_t nbits = (size_t)t->A * (size_t)t->A;
         rc = shd_dev_h2d(t->d_pair_bits, t->pair_bits, ((nbits + 31) / 32) * 4);
     }
-    if (!rc) t->touch_dirty = 0;
+    if (rc) __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
     return rc;
 }
 
@@ -214,4 +236,6 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->pair_bits = t->d_pair_bits;
     c->host_info = t->d_host_info;
     c->nhosts = t->nhosts;
+    if (!t->ws) shd_dev_ws_new(&t->ws); /* (a failure leaves ws NULL: the launch reports -ENOMEM) */
+    c->ws = t->ws;
 }

@@ -94,12 +94,17 @@ typedef struct {
     const uint32_t* pair_bits; /* A*A bits, mode 2 */
     const uint32_t* host_info; /* nhosts x {slot (UINT32_MAX = unattached), touch[slot]}: one 8-B gather */
     uint32_t nhosts;
+    void* ws;                  /* the topology's device workspace (shd_dev_ws_new) */
 } ShdPktCtx;
 
+/* Round-pipeline workspace (grow-only device buffers + the event that marks
+ * the end of its last use), one per topology; callers serialise its use. */
+int shd_dev_ws_new(void** ws);
+void shd_dev_ws_free(void* ws);
 int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                          uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets,
                          uint8_t* d_status, uint64_t* d_counters, void* stream);
-int shd_dev_deliv_sort(const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
+int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                        uint32_t* d_dst_offsets, void* stream);
 
 #ifdef __cplusplus

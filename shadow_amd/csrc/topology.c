@@ -488,6 +488,15 @@ out:
 void shd_topology_free(ShdTopology* t) {
     if (!t) return;
     shd_topology_release_device(t);
+    shd_dev_ws_free(t->ws);
+    for (int w = 0; w < t->nworkers; w++) free(t->wbuf[w].recs);
+    free(t->wbuf);
+    pthread_mutex_destroy(&t->setup_mu);
+    pthread_mutex_destroy(&t->touch_mu);
+    pthread_mutex_destroy(&t->min_mu);
+    pthread_mutex_destroy(&t->pkt_mu);
+    pthread_mutex_destroy(&t->pair_mu);
+    pthread_mutex_destroy(&t->round_mu);
     shd_gml_free(&t->doc);
     free(t->efrom);
     free(t->eto);
@@ -525,6 +534,22 @@ int shd_topology_new_from_text(const char* text, int use_shortest_path, int devi
     if (!t) return -ENOMEM;
     t->use_sp = use_shortest_path ? 1 : 0;
     t->device = device;
+    pthread_mutexattr_t ra;
+    pthread_mutexattr_init(&ra);
+    pthread_mutexattr_settype(&ra, PTHREAD_MUTEX_RECURSIVE);
+    pthread_mutex_init(&t->setup_mu, &ra);
+    pthread_mutexattr_destroy(&ra);
+    pthread_mutex_init(&t->touch_mu, NULL);
+    pthread_mutex_init(&t->min_mu, NULL);
+    pthread_mutex_init(&t->pkt_mu, NULL);
+    pthread_mutex_init(&t->pair_mu, NULL);
+    pthread_mutex_init(&t->round_mu, NULL);
+    t->nworkers = 1;
+    t->wbuf = (ShdWorkerBuf*)calloc(1, sizeof(ShdWorkerBuf));
+    if (!t->wbuf) {
+        free(t);
+        return -ENOMEM;
+    }
     int rc = load(t, text);
     if (rc) {
         shd_topology_free(t);
@@ -582,10 +607,24 @@ static uint32_t ip_of(const char* s) {
  * values exactly as topology.c:2051 / :2146 do */
 static int usable(uint32_t ip) { return ip != 0xffffffffu && ip != 0u && ip != 0x7f000001u; }
 
+static int attach_locked(ShdTopology* t, uint32_t host_id, uint32_t ip_net, uint32_t* rng_state,
+                         const char* ip_hint, const char* city_hint, const char* country_hint, uint64_t* bw_down,
+                         uint64_t* bw_up);
+
 int shd_topology_attach(ShdTopology* t, uint32_t host_id, uint32_t ip_net, uint32_t* rng_state, const char* ip_hint,
                         const char* city_hint, const char* country_hint, uint64_t* bw_down, uint64_t* bw_up) {
     if (!t) return shd_fail(-EINVAL, "null topology");
-    if (t->lookups_started) return shd_fail(-EBUSY, "attach after the first path lookup is not supported");
+    pthread_mutex_lock(&t->setup_mu);
+    int rc = attach_locked(t, host_id, ip_net, rng_state, ip_hint, city_hint, country_hint, bw_down, bw_up);
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
+}
+
+static int attach_locked(ShdTopology* t, uint32_t host_id, uint32_t ip_net, uint32_t* rng_state,
+                         const char* ip_hint, const char* city_hint, const char* country_hint, uint64_t* bw_down,
+                         uint64_t* bw_up) {
+    if (__atomic_load_n(&t->lookups_started, __ATOMIC_ACQUIRE))
+        return shd_fail(-EBUSY, "attach after the first path lookup is not supported");
     int V = t->V;
     int32_t* city = (int32_t*)malloc(sizeof(int32_t) * (size_t)V * 3 + 4);
     if (!city) return -ENOMEM;
@@ -666,8 +705,11 @@ choose:;
     if (host_id >= t->host_cap) {
         uint32_t nc = t->host_cap ? t->host_cap : 64;
         while (nc <= host_id) nc *= 2;
-        t->host_vertex = (int32_t*)realloc(t->host_vertex, sizeof(int32_t) * nc);
-        t->host_ip = (uint32_t*)realloc(t->host_ip, sizeof(uint32_t) * nc);
+        int32_t* hv = (int32_t*)realloc(t->host_vertex, sizeof(int32_t) * nc);
+        if (hv) t->host_vertex = hv;
+        uint32_t* hi = hv ? (uint32_t*)realloc(t->host_ip, sizeof(uint32_t) * nc) : NULL;
+        if (hi) t->host_ip = hi;
+        if (!hv || !hi) return -ENOMEM;
         for (uint32_t h = t->host_cap; h < nc; h++) t->host_vertex[h] = -1;
         t->host_cap = nc;
     }
@@ -677,17 +719,24 @@ choose:;
     if (bw_up) *bw_up = (uint64_t)t->v_bw_up[chosen];
     if (bw_down) *bw_down = (uint64_t)t->v_bw_down[chosen];
     t->routes_stale = 1;
+    __atomic_store_n(&t->ready, 0, __ATOMIC_RELEASE);
     return 0;
 }
 
+/* topology_detach: the reference removes the IP under its writer lock
+ * (topology.c:2274-2281); here the ip map is read lock-free by lookups, so
+ * detaching is a setup-time operation (before or after the simulation, not
+ * concurrently with lookups of the same table). */
 int shd_topology_detach(ShdTopology* t, uint32_t ip) {
     if (!t) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
     IpSlot* s = ipmap_find(&t->ipmap, ip);
     if (s) {
         s->used = 2;
         t->ipmap.n--;
         t->ipmap.tomb++;
     }
+    pthread_mutex_unlock(&t->setup_mu);
     return 0;
 }
 
@@ -705,14 +754,18 @@ int shd_topology_host_count(ShdTopology* t, uint32_t* n) {
 
 int shd_topology_set_min_jump_callback(ShdTopology* t, ShdMinJumpFn fn, void* user) {
     if (!t) return -EINVAL;
+    pthread_mutex_lock(&t->min_mu);
     t->cb = fn;
     t->cb_user = user;
+    pthread_mutex_unlock(&t->min_mu);
     return 0;
 }
 
 int shd_topology_get_min_path_latency(ShdTopology* t, double* m) {
     if (!t || !m) return -EINVAL;
+    pthread_mutex_lock(&t->min_mu);
     *m = t->min_lat;
+    pthread_mutex_unlock(&t->min_mu);
     return 0;
 }
 
@@ -720,12 +773,18 @@ int shd_topology_get_min_path_latency(ShdTopology* t, double* m) {
 /* lookups with the reference's cache side effects                     */
 /* ------------------------------------------------------------------ */
 
-/* _topology_storePathInCache's running min (topology.c:1253-1264) */
+static inline uint32_t touch_of(const ShdTopology* t, int i) { return __atomic_load_n(&t->touch[i], __ATOMIC_ACQUIRE); }
+
+/* _topology_storePathInCache's running min (topology.c:1253-1264); the
+ * callback fires under min_mu, so its calls are ordered and each one reports
+ * a strictly smaller value. */
 static void note_released(ShdTopology* t, double lat) {
+    pthread_mutex_lock(&t->min_mu);
     if (t->min_lat == 0 || lat < t->min_lat) {
         t->min_lat = lat;
         if (t->cb) t->cb(t->min_lat, t->cb_user);
     }
+    pthread_mutex_unlock(&t->min_mu);
 }
 
 /* Entry k of the table: from the host mirror, or one 16-byte read of the
@@ -733,21 +792,32 @@ static void note_released(ShdTopology* t, double lat) {
 static ShdEntry ent(const ShdTopology* t, size_t k) {
     if (t->h_tab) return t->h_tab[k];
     ShdEntry e = {-1.0, 0.0};
-    if (shd_dev_d2h(&e, t->d_tab + k, sizeof e)) e.lat = -1.0;
+    if (shd_dev_init(t->device) || shd_dev_d2h(&e, t->d_tab + k, sizeof e)) e.lat = -1.0;
     return e;
 }
 
-/* Releases row i (a touch): every (i, y) with y untouched.  Device-resident
- * tables release every row at adoption, so they never get here. */
+/* Releases row i (a touch).  The row's sequence number is drawn and
+ * published under touch_mu; the entries it releases are then every (i, y)
+ * whose y is untouched or was touched later (sequence > i's) -- exactly the
+ * pairs the serial execution in sequence order stores from row i, whatever
+ * the interleaving with other touches.  Device-resident tables release every
+ * row at adoption, so they never get here. */
 static void touch_row(ShdTopology* t, int i) {
-    t->touch[i] = t->next_touch++;
-    t->touch_dirty = 1;
-    if (!t->h_tab) return;
+    pthread_mutex_lock(&t->touch_mu);
+    uint32_t seq = t->touch[i];
+    const int mine = seq == SHD_UNTOUCHED;
+    if (mine) {
+        seq = t->next_touch++;
+        __atomic_store_n(&t->touch[i], seq, __ATOMIC_RELEASE);
+        __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
+    }
+    pthread_mutex_unlock(&t->touch_mu);
+    if (!mine || !t->h_tab) return;
     const ShdEntry* row = t->h_tab + (size_t)i * (size_t)t->A;
     double mn = 0;
     int any = 0;
     for (int j = 0; j < t->A; j++)
-        if (j != i && t->touch[j] == SHD_UNTOUCHED && row[j].lat >= 0) {
+        if (j != i && touch_of(t, j) > seq && row[j].lat >= 0) {
             if (!any || row[j].lat < mn) mn = row[j].lat;
             any = 1;
         }
@@ -756,46 +826,59 @@ static void touch_row(ShdTopology* t, int i) {
 
 static int pair_bit(const ShdTopology* t, int i, int j) {
     size_t b = (size_t)i * (size_t)t->A + (size_t)j;
-    return (t->pair_bits[b >> 5] >> (b & 31)) & 1u;
+    return (__atomic_load_n(&t->pair_bits[b >> 5], __ATOMIC_ACQUIRE) >> (b & 31)) & 1u;
 }
 
 static void set_pair_bit(ShdTopology* t, int i, int j) {
     size_t b = (size_t)i * (size_t)t->A + (size_t)j;
-    t->pair_bits[b >> 5] |= 1u << (b & 31);
-    t->touch_dirty = 1;
+    __atomic_fetch_or(&t->pair_bits[b >> 5], 1u << (b & 31), __ATOMIC_ACQ_REL);
+    __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
 }
 
 /* _topology_getPathEntry (topology.c:1900-1981) for slots (si, di): applies
- * the side effects and returns the slot pair whose entry answers. */
+ * the side effects and returns the slot pair whose entry answers.  Lock-free
+ * on a hit; safe to call from any number of threads. */
 int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) {
     size_t A = (size_t)t->A;
     if (t->use_sp) {
         if (si == di) {
-            if (!t->self_released[si]) {
-                t->self_released[si] = 1;
+            if (!__atomic_exchange_n(&t->self_released[si], 1, __ATOMIC_ACQ_REL))
                 note_released(t, ent(t, (size_t)si * A + (size_t)si).lat);
-            }
             *oi = *oj = si;
         } else {
-            uint32_t ts = t->touch[si], td = t->touch[di];
+            uint32_t ts = touch_of(t, si), td = touch_of(t, di);
             int hit = t->directed ? (ts != SHD_UNTOUCHED && ts < td) : (ts != SHD_UNTOUCHED || td != SHD_UNTOUCHED);
             if (!hit && ts == SHD_UNTOUCHED) touch_row(t, si);
-            ts = t->touch[si];
+            /* re-read both: a concurrent touch of di with a smaller sequence
+             * was published before ours (touch_mu), so it is visible here */
+            ts = touch_of(t, si);
+            td = touch_of(t, di);
             if (ts <= td) *oi = si, *oj = di;
             else *oi = di, *oj = si;
         }
     } else {
         int hit = pair_bit(t, si, di) || (!t->directed && pair_bit(t, di, si));
         if (!hit && !pair_bit(t, di, si)) {
-            const double lat = ent(t, (size_t)si * A + (size_t)di).lat;
-            if (lat < 0) return shd_fail(-EHOSTUNREACH, "no direct edge");
-            set_pair_bit(t, si, di);
-            note_released(t, lat);
+            pthread_mutex_lock(&t->pair_mu); /* the reference's writer lock (topology.c:1217-1265) */
+            if (!pair_bit(t, si, di) && !pair_bit(t, di, si)) {
+                const double lat = ent(t, (size_t)si * A + (size_t)di).lat;
+                if (lat < 0) {
+                    pthread_mutex_unlock(&t->pair_mu);
+                    return shd_fail(-EHOSTUNREACH, "no direct edge");
+                }
+                set_pair_bit(t, si, di);
+                note_released(t, lat);
+            }
+            pthread_mutex_unlock(&t->pair_mu);
         }
         if (pair_bit(t, si, di)) *oi = si, *oj = di;
         else *oi = di, *oj = si;
     }
-    if (ent(t, (size_t)*oi * A + (size_t)*oj).lat < 0) return shd_fail(-EHOSTUNREACH, "unroutable pair");
+    /* unroutable check (topology.c:1970-1976): a mirrored table answers it
+     * for free; a device-resident table is use_shortest_path on a validated
+     * (strongly connected) graph, where every pair has a path */
+    if (t->h_tab && t->h_tab[(size_t)*oi * A + (size_t)*oj].lat < 0)
+        return shd_fail(-EHOSTUNREACH, "unroutable pair");
     return 0;
 }
 
@@ -803,8 +886,9 @@ static int slots_of(ShdTopology* t, uint32_t sip, uint32_t dip, int* si, int* di
     IpSlot* a = ipmap_find(&t->ipmap, sip);
     IpSlot* b = ipmap_find(&t->ipmap, dip);
     if (!a || !b) return shd_fail(-ENOENT, "address is not connected to the topology");
-    int rc = shd_topology_build_routes(t);
+    int rc = shd_ensure_routes(t);
     if (rc) return rc;
+    if (!__atomic_load_n(&t->lookups_started, __ATOMIC_RELAXED)) __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
     *si = t->vertex_slot[a->vertex];
     *di = t->vertex_slot[b->vertex];
     return 0;
@@ -853,14 +937,18 @@ int shd_topology_is_routable(ShdTopology* t, uint32_t s, uint32_t d, int* r) {
     return 0;
 }
 
-/* per stored pair packet counters (path.c:58-61) */
-int shd_count_packet(ShdTopology* t, int oi, int oj, uint64_t inc) {
+/* per stored pair packet counters (path.c:58-61); caller holds pkt_mu */
+int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc) {
     uint64_t key = ((uint64_t)(uint32_t)oi << 32) | (uint32_t)oj;
     if ((t->pkt_n + 1) * 2 > t->pkt_cap) {
         uint64_t ncap = t->pkt_cap ? t->pkt_cap * 2 : 4096;
         uint64_t* nk = (uint64_t*)malloc(sizeof(uint64_t) * ncap);
         uint64_t* nv = (uint64_t*)calloc(ncap, sizeof(uint64_t));
-        if (!nk || !nv) return -ENOMEM;
+        if (!nk || !nv) {
+            free(nk);
+            free(nv);
+            return -ENOMEM;
+        }
         memset(nk, 0xff, sizeof(uint64_t) * ncap);
         for (uint64_t i = 0; i < t->pkt_cap; i++)
             if (t->pkt_keys[i] != UINT64_MAX) {
@@ -885,11 +973,19 @@ int shd_count_packet(ShdTopology* t, int oi, int oj, uint64_t inc) {
     return 0;
 }
 
+int shd_count_packet(ShdTopology* t, int oi, int oj, uint64_t inc) {
+    pthread_mutex_lock(&t->pkt_mu);
+    int rc = shd_count_packet_locked(t, oi, oj, inc);
+    pthread_mutex_unlock(&t->pkt_mu);
+    return rc;
+}
+
 int shd_topology_increment_path_packet_counter(ShdTopology* t, uint32_t s, uint32_t d) {
-    ShdEntry e;
-    int oi, oj;
+    int si, di, oi, oj;
     if (!t) return -EINVAL;
-    int rc = entry_of(t, s, d, &e, &oi, &oj);
+    int rc = slots_of(t, s, d, &si, &di);
+    if (rc) return rc;
+    rc = shd_resolve(t, si, di, &oi, &oj);
     if (rc) return rc;
     return shd_count_packet(t, oi, oj, 1);
 }
@@ -899,19 +995,22 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
     *out = 0;
     IpSlot* a = ipmap_find(&t->ipmap, s);
     IpSlot* b = ipmap_find(&t->ipmap, d);
-    if (!a || !b || !t->built) return 0;
+    if (!a || !b || !__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return 0;
     int si = t->vertex_slot[a->vertex], di = t->vertex_slot[b->vertex];
+    pthread_mutex_lock(&t->pkt_mu);
     for (int pass = 0; pass < 2 && t->pkt_cap; pass++) {
         uint64_t key = pass ? (((uint64_t)(uint32_t)di << 32) | (uint32_t)si) : (((uint64_t)(uint32_t)si << 32) | (uint32_t)di);
         uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20 & (t->pkt_cap - 1);
         while (t->pkt_keys[h] != UINT64_MAX) {
             if (t->pkt_keys[h] == key) {
                 *out = t->pkt_vals[h];
-                return 0;
+                pass = 2;
+                break;
             }
             h = (h + 1) & (t->pkt_cap - 1);
         }
     }
+    pthread_mutex_unlock(&t->pkt_mu);
     return 0;
 }
 
@@ -923,37 +1022,55 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
 int shd_topology_adopt_table_device_resident(ShdTopology* t, void* d_table) {
     int A = 0;
     if (!t || !d_table) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
     int rc = shd_topology_slot_count(t, &A); /* prepares the device graph */
-    if (rc) return rc;
-    if (!t->use_sp) return shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
-    if (t->next_touch) return shd_fail(-EBUSY, "rows were already released");
+    if (!rc && !t->use_sp) rc = shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
+    if (!rc && t->next_touch) rc = shd_fail(-EBUSY, "rows were already released");
     double mn = -1.0;
-    if ((rc = shd_dev_min_upper((const ShdEntry*)d_table, A, &mn))) return rc;
-    free(t->h_tab);
-    t->h_tab = NULL;
-    if (t->d_tab && t->d_tab_owned && t->d_tab != (ShdEntry*)d_table) shd_dev_free(t->d_tab);
-    t->d_tab = (ShdEntry*)d_table;
-    t->d_tab_owned = 0;
-    t->built = 1;
-    for (int i = 0; i < A; i++) t->touch[i] = t->next_touch++;
-    t->touch_dirty = 1;
-    if (mn >= 0) note_released(t, mn);
-    return 0;
+    if (!rc) rc = shd_dev_min_upper((const ShdEntry*)d_table, A, &mn);
+    if (!rc) {
+        free(t->h_tab);
+        t->h_tab = NULL;
+        if (t->d_tab && t->d_tab_owned && t->d_tab != (ShdEntry*)d_table) shd_dev_free(t->d_tab);
+        t->d_tab = (ShdEntry*)d_table;
+        t->d_tab_owned = 0;
+        t->built = 1;
+        pthread_mutex_lock(&t->touch_mu);
+        for (int i = 0; i < A; i++) __atomic_store_n(&t->touch[i], t->next_touch++, __ATOMIC_RELEASE);
+        __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
+        pthread_mutex_unlock(&t->touch_mu);
+        __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE);
+        if (mn >= 0) note_released(t, mn);
+    }
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
 }
 
 int shd_topology_touch_all(ShdTopology* t) {
     if (!t) return -EINVAL;
-    int rc = shd_topology_build_routes(t);
+    int rc = shd_ensure_routes(t);
     if (rc) return rc;
+    __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
     if (t->use_sp) {
         for (int i = 0; i < t->A; i++)
-            if (t->touch[i] == SHD_UNTOUCHED) touch_row(t, i);
+            if (touch_of(t, i) == SHD_UNTOUCHED) touch_row(t, i);
     } else {
         for (int i = 0; i < t->A; i++)
             for (int j = 0; j < t->A; j++) {
                 int oi, oj;
                 shd_resolve(t, i, j, &oi, &oj);
             }
+    }
+    return 0;
+}
+
+int shd_topology_touch_order(ShdTopology* t, uint32_t* seq, uint8_t* self, int cap) {
+    if (!t) return -EINVAL;
+    if (!__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return shd_fail(-EAGAIN, "no table yet");
+    if (cap < t->A) return shd_fail(-ENOSPC, "need %d slots", t->A);
+    for (int i = 0; i < t->A; i++) {
+        if (seq) seq[i] = touch_of(t, i);
+        if (self) self[i] = __atomic_load_n(&t->self_released[i], __ATOMIC_ACQUIRE);
     }
     return 0;
 }

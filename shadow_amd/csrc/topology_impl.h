@@ -1,11 +1,37 @@
 /* topology_impl.h -- the ShdTopology object shared by topology.c, routes.c
- * and round.c (host C side of libshdnet). */
+ * and round.c (host C side of libshdnet).
+ *
+ * Threading (the reference is called from every worker thread and guards
+ * its cache with a GMutex + 3 GRWLocks, topology.c:26-85):
+ *   - setup (load, attach, build, adopt) is serialised by setup_mu, and the
+ *     table is immutable once `ready` is published (release store);
+ *   - lookups read the table and the release state lock-free (atomic loads
+ *     of touch[] / pair_bits[]); a row touch takes touch_mu only to draw its
+ *     sequence number, so every released pair is owned by the row with the
+ *     smaller sequence -- the state equals the serial execution in sequence
+ *     order;
+ *   - the running minimum and the min-jump callback are under min_mu, the
+ *     path packet counters under pkt_mu, direct-path (pair bit) misses under
+ *     pair_mu;
+ *   - round staging is per worker (no lock between workers); the round
+ *     pipeline (collect / process / regroup) is serialised by round_mu and
+ *     its device workspace belongs to this topology. */
 #ifndef SHD_TOPOLOGY_IMPL_H
 #define SHD_TOPOLOGY_IMPL_H
+
+#include <pthread.h>
 
 #include "shd_internal.h"
 
 #define SHD_UNTOUCHED 0xffffffffu
+
+/* One worker's staged sends for the current round (cache-line padded: each
+ * worker writes only its own). */
+typedef struct {
+    ShdPkt* recs;
+    size_t n, cap;
+    char pad[40];
+} ShdWorkerBuf;
 
 typedef struct {
     uint32_t ip;
@@ -70,16 +96,27 @@ struct ShdTopology {
     uint64_t *pkt_keys, *pkt_vals;
     uint64_t pkt_cap, pkt_n;
 
-    /* round staging (host API) */
+    /* round staging (host API): one buffer per worker */
     uint64_t barrier, end_time, bootstrap_end;
-    ShdPkt* staged;
-    size_t nstaged, capstaged;
+    ShdWorkerBuf* wbuf;
+    int nworkers;
+    ShdPkt* staged; /* concatenation at collect (worker order) */
+    size_t capstaged;
+
+    /* device workspace of the round pipeline (packet.hip) */
+    void* ws;
+
+    /* synchronisation (see the header comment) */
+    int ready; /* table built and adopted: lookups may proceed (atomic) */
+    pthread_mutex_t setup_mu, touch_mu, min_mu, pkt_mu, pair_mu, round_mu;
 };
 
 void shd_topology_release_device(ShdTopology* t);
 int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj);
 int shd_count_packet(ShdTopology* t, int oi, int oj, uint64_t inc);
+int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc);
 int shd_sync_touch(ShdTopology* t);
 void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c);
+int shd_ensure_routes(ShdTopology* t);
 
 #endif

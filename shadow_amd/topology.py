@@ -127,6 +127,11 @@ class Topology:
         check(lib().shd_topology_get_min_path_latency(self._h, C.byref(out)))
         return out.value
 
+    def next_min_jump_ns(self) -> int:
+        """What controller_updateMinTimeJump (controller.c:141-153) holds after
+        the recorded callback values: (u64)floor(last ms) x 1e6 ns, 0 if none."""
+        return int(self.min_jump_calls[-1]) * 1000000 if self.min_jump_calls else 0
+
     def record_min_jump(self):
         """Records every worker_updateMinTimeJump value into self.min_jump_calls."""
         def cb(ms, _user):

@@ -1,0 +1,83 @@
+/*
+ * stub_dev.c -- TEST ONLY.  A host-memory stand-in for the device layer of
+ * libshdnet (shd_internal.h: shd_dev_*), so that the product's host C
+ * (topology.c, routes.c, round.c, gml.c, units.c) can be exercised for
+ * thread safety under ThreadSanitizer on a machine without a GPU.  It never
+ * ships: the product library links dev.hip / routing.hip / packet.hip.
+ *
+ * The "routing table" it builds is a fixed synthetic table (asymmetric, so
+ * that the owner of a pair matters), not a routing computation: the thread
+ * test checks the cache / release bookkeeping around the table, not the
+ * table's values (those are checked on the GPU against the oracle).
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "shd_internal.h"
+
+int shd_dev_init(int device) { return device == 0 ? 0 : -ENODEV; }
+int shd_dev_malloc(void** p, size_t bytes) {
+    *p = malloc(bytes ? bytes : 4);
+    return *p ? 0 : -ENOMEM;
+}
+int shd_dev_free(void* p) {
+    free(p);
+    return 0;
+}
+int shd_dev_h2d(void* d, const void* h, size_t bytes) {
+    if (bytes) memcpy(d, h, bytes);
+    return 0;
+}
+int shd_dev_d2h(void* h, const void* d, size_t bytes) {
+    if (bytes) memcpy(h, d, bytes);
+    return 0;
+}
+int shd_dev_memset(void* d, int v, size_t bytes) {
+    memset(d, v, bytes);
+    return 0;
+}
+int shd_dev_sync(void) { return 0; }
+
+/* entry (i, j) of the synthetic table */
+void stub_entry(int i, int j, double* lat, double* rel) {
+    uint32_t h = (uint32_t)i * 0x9E3779B1u ^ (uint32_t)j * 0x85EBCA77u;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    h ^= h >> 12;
+    *lat = 1.0 + (double)(h % 1000000u) / 1000.0;
+    *rel = 0.5 + (double)((i * 29 + j * 53) % 41) / 100.0;
+}
+
+int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab) {
+    (void)use_sp;
+    for (int i = row_lo; i < row_hi; i++)
+        for (int j = 0; j < g->A; j++) stub_entry(i, j, &tab[(size_t)i * g->A + j].lat, &tab[(size_t)i * g->A + j].rel);
+    return 0;
+}
+
+int shd_dev_min_upper(const ShdEntry* tab, int A, double* out) {
+    *out = -1.0;
+    for (int i = 0; i < A; i++)
+        for (int j = i + 1; j < A; j++)
+            if (tab[(size_t)i * A + j].lat >= 0 && (*out < 0 || tab[(size_t)i * A + j].lat < *out))
+                *out = tab[(size_t)i * A + j].lat;
+    return 0;
+}
+
+int shd_dev_ws_new(void** ws) {
+    *ws = malloc(1);
+    return *ws ? 0 : -ENOMEM;
+}
+void shd_dev_ws_free(void* ws) { free(ws); }
+
+int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
+                         uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,
+                         uint64_t* d_counters, void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no packet kernels");
+}
+
+int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
+                       uint32_t* d_dst_offsets, void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no packet kernels");
+}

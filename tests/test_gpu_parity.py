@@ -496,3 +496,59 @@ def test_medium_segments_lds_path(pipeline):
     assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
     seg = np.diff(offs)
     assert ((seg > 256) & (seg <= 4096)).sum() >= 4
+
+
+@pytest.mark.parametrize("name", ["sparse200_dir_ns", "complete25_dir"])
+def test_send_time_append_interleaved_with_lookups(name):
+    """Within one round, worker sends (shd_round_append_worker, whose lookup
+    side effect happens at send time like topology_getReliability at
+    worker.c:539) interleave with other callers' lookups (topology_isRoutable
+    at socket.c:808, worker_getLatency at tcp.c:392-393).  On a directed
+    ns-resolution graph the owner of a pair -- and with it the bits of every
+    later answer and the min-jump sequence -- depends on that order.  The
+    oracle replays the same serial sequence; values, the callback sequence
+    and the round's output must match."""
+    gml, H = GRAPHS[name]
+    top, orc, ips, st = make_pair(gml, H)
+    top.record_min_jump()
+    check = __import__("shadow_amd._lib", fromlist=["check"]).check
+    lib = __import__("shadow_amd._lib", fromlist=["lib"]).lib()
+    check(lib.shd_round_set_workers(top.handle, 3))
+    check(lib.shd_round_begin(top.handle, 110_000_000, 10**15, 0))
+    pk = synth.packet_batch(3000, H, 0x5EED0500, 100_000_000, 10_000_000, st)
+    rng = np.random.default_rng(11)
+    order = []  # (worker, record) in append order; pkt_index counts worker 0's first
+    for i in range(len(pk)):
+        for _ in range(int(rng.integers(0, 3))):  # lookups by other callers between two sends
+            a, b = (int(x) for x in rng.integers(0, H, 2))
+            s, d = int(ips[a]), int(ips[b])
+            if rng.integers(0, 2):
+                assert top.is_routable(s, d) == orc.routable(s, d)
+            else:
+                assert bits(top.get_latency(s, d)) == bits(orc.latency(s, d))
+        w = int(rng.integers(0, 3))
+        rec = pk[i:i + 1]
+        check(lib.shd_round_append_worker(top.handle, w, rec.ctypes.data, 1))
+        orc.reliability(int(ips[rec["src_host"][0]]), int(ips[rec["dst_host"][0]]))  # the send's lookup
+        order.append((w, i))
+        assert bits(top.min_path_latency()) == bits(orc.min_path_latency())
+        # the callback fires once per decreasing row release; the reference
+        # fires per stored entry in its target iteration order, ending at the
+        # same value (controller_updateMinTimeJump keeps the last, :141-153)
+        assert (not top.min_jump_calls and orc.min_jump_updates() == 0) or \
+            bits(top.min_jump_calls[-1]) == bits(orc.min_path_latency())
+        assert len(top.min_jump_calls) <= orc.min_jump_updates()
+        assert top.next_min_jump_ns() == orc.next_min_jump_ns()
+    # collect: records in worker order, each worker's in append order
+    perm = [i for w in range(3) for (ww, i) in order if ww == w]
+    staged = pk[perm]
+    out = np.zeros(len(pk), dtype=synth.DELIV_DTYPE)
+    offs = np.zeros(H + 1, dtype=np.uint32)
+    status = np.zeros(len(pk), dtype=np.uint8)
+    nout, mt = C.c_size_t(), C.c_uint64()
+    check(lib.shd_round_collect(top.handle, out.ctypes.data, len(out), C.byref(nout), offs.ctypes.data,
+                                status.ctypes.data, C.byref(mt)))
+    oout, ostatus, omt = orc.round(ips, staged, 110_000_000, 10**15)  # lookups are hits now: no side effects
+    assert np.array_equal(status, ostatus) and mt.value == omt
+    assert np.array_equal(out[:nout.value], oout)
+    assert top.min_jump_calls == sorted(set(top.min_jump_calls), reverse=True)  # strictly decreasing
