@@ -63,27 +63,32 @@ def log(*a):
 
 
 def gpu_state(dev_index):
-    """Clocks and compute/memory partition mode of the box (read-only
-    rocm-smi query) plus the device properties, so that run-to-run spreads
-    can be attributed from the bench record alone."""
-    import subprocess
+    """Clocks and compute/memory partition mode of the box, read from the
+    amdgpu sysfs files (no subprocess: a child that re-execs under the
+    profiler's preload is refused on the box), plus the device properties,
+    so that run-to-run spreads can be attributed from the bench record."""
+    import glob
 
     import torch
     p = torch.cuda.get_device_properties(dev_index)
     st = {"name": p.name, "gcn_arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
           "total_mem_gb": round(p.total_memory / 2**30, 1)}
-    try:
-        r = subprocess.run(["rocm-smi", "--showclocks", "--showcomputepartition", "--showmemorypartition",
-                            "--json"], capture_output=True, text=True, timeout=30)
-        js = json.loads(r.stdout) if r.returncode == 0 and r.stdout.strip().startswith("{") else {}
-        keep = {}
-        for card, kv in js.items():
-            if isinstance(kv, dict):
-                keep[card] = {k: v for k, v in kv.items()
-                              if any(w in k.lower() for w in ("sclk", "mclk", "fclk", "socclk", "partition"))}
-        st["rocm_smi"] = keep
-    except Exception as e:  # the record is informational; never fail the bench on it
-        st["rocm_smi_error"] = repr(e)[:200]
+    cards = {}
+    for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+        info = {}
+        for f in ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk", "current_compute_partition",
+                  "current_memory_partition", "power_dpm_force_performance_level"):
+            try:
+                with open(os.path.join(dev, f)) as fh:
+                    txt = fh.read().strip()
+            except OSError:
+                continue
+            if f.startswith("pp_dpm"):  # keep the active level (marked '*')
+                txt = " ".join(ln.strip() for ln in txt.splitlines() if ln.strip().endswith("*")) or txt[:80]
+            info[f] = txt
+        if info:
+            cards[dev.split("/")[-2]] = info
+    st["sysfs"] = cards
     return st
 
 

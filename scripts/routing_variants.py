@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Times the slab routing kernel's measurement variants (same exact
+algorithm: SHD_SSSP_LAZYPOS, SHD_SSSP_SINK, SHD_SSSP_WAVES) on the C2 (and
+optionally C4) build and checks every variant's table is bitwise equal to
+the first one's.  Usage: routing_variants.py [--c4] VARIANT...
+VARIANT = "lazy=1,sink=5[,waves=N]"."""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--c4", action="store_true")
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import torch
+
+    from shadow_amd import Topology, scenario, synth
+    cfgs = [("C2", 20_000, 100_000, 0x5EED0002)] + ([("C4", 100_000, 200_000, 0x5EED0004)] if a.c4 else [])
+    for name, V, H, seed in cfgs:
+        top = Topology(synth.sparse_graph_gml(V, seed))
+        scenario.register_hosts(top, H, seed=1)
+        A = top.slot_count()
+        ref = None
+        tab = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
+        for v in a.variants:
+            kv = dict(x.split("=") for x in v.split(","))
+            os.environ["SHD_SSSP_LAZYPOS"] = kv.get("lazy", "1")
+            os.environ["SHD_SSSP_SINK"] = kv.get("sink", "5")
+            if "waves" in kv:
+                os.environ["SHD_SSSP_WAVES"] = kv["waves"]
+            else:
+                os.environ.pop("SHD_SSSP_WAVES", None)
+            ts = []
+            for _ in range(a.reps if name == "C2" else 1):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                top.build_rows_device(0, A, tab.data_ptr())
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t0)
+            # checksum of the table bits (a full copy of C4 is 120 GB)
+            h = tab.view(torch.int64)
+            sig = (int(h[::997].sum().item()), int(h[1::1009].sum().item()), int((h[: A * 2 * 64]).sum().item()))
+            if ref is None:
+                ref = sig
+            print(f"{name} {v}: {min(ts):.3f}s (all {', '.join(f'{t:.3f}' for t in ts)}) "
+                  f"{'same' if sig == ref else 'DIFFERENT'}", flush=True)
+            if sig != ref:
+                sys.exit(1)
+        del tab
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -69,13 +69,24 @@ __device__ __forceinline__ double uni_d(double v) {
 // igraph_2wheap over split storage.  kAll: every position in LDS (top).
 // Else positions < kTop in LDS and position p >= kTop at rest[p + 1], which
 // puts each child pair (2e+1, 2e+2) in one 32-B sector.
+//
+// pos (igraph's index2, vertex -> position + 2) is what a decrease-key needs
+// to find a vertex.  In the slab kernel every pos store is one random HBM
+// request and a sink moves a node at every level it passes, most of them in
+// the LDS top; so with `lazy` set, pos of a node in the LDS top is the
+// marker 1 ("somewhere in the top"), written only when the node enters the
+// top, and a decrease-key of such a node finds it by a wave-wide search of
+// the (at most kTop) top positions.  A pop does not clear pos: a popped
+// vertex is never decreased again (alt = dist[u] + w >= dist[v] for every
+// popped v, weights > 0).  Neither changes a heap operation.
 template <bool kAll>
 struct Heap {
     HNode* top;
     HNode* rest;
-    int* pos; // vertex -> position + 2 (igraph index2; 0 once popped)
+    int* pos; // vertex -> position + 2 (1: in the LDS top, lazy mode)
     int n;
     int lane;
+    bool lazy;
 
     // every heap operand is wave-uniform: readfirstlane tells the compiler
     // so, and the heap then runs on scalar branches with LDS- or
@@ -94,7 +105,8 @@ struct Heap {
         if (kAll) return x; // (the LDS kernel is faster without the readfirstlanes)
         return HNode{uni_d(x.key), uni(x.v), 0};
     }
-    __device__ __forceinline__ void st(int p, const HNode& x) {
+    // stores node x at position p; `from` = its previous position (-1: new)
+    __device__ __forceinline__ void st(int p, const HNode& x, int from) {
         if (kAll || p < kTop) {
             top[p] = x;
             if (!kAll) __asm__ volatile("; heap lds st" ::: "memory");
@@ -102,22 +114,28 @@ struct Heap {
             rest[p + 1] = x;
             __asm__ volatile("; heap hbm st" ::: "memory");
         }
-        pos[x.v] = p + 2;
+        if (kAll || !lazy) {
+            if (p != from) pos[x.v] = p + 2;
+        } else if (p >= kTop) {
+            if (p != from) pos[x.v] = p + 2;
+        } else if (from < 0 || from >= kTop) {
+            pos[x.v] = 1; // entered the LDS top
+        }
     }
-    // climb while !(x < parent)
-    __device__ __forceinline__ void shift_up(int e, const HNode& x) {
+    // climb while !(x < parent); x was at position `from` (-1: new)
+    __device__ __forceinline__ void shift_up(int e, const HNode& x, int from) {
         while (e > 0) {
             const int p = ((e + 1) >> 1) - 1;
             const HNode pn = ld(p);
             if (x.key < pn.key) break;
-            st(e, pn);
+            st(e, pn, p);
             e = p;
         }
-        st(e, x);
+        st(e, x, from);
     }
     // descend towards the larger child (the left one when left >= right)
     // while x < child, one level at a time
-    __device__ __forceinline__ void sink_seq(int e, const HNode& x) {
+    __device__ __forceinline__ void sink_seq(int e, const HNode& x, int from) {
         for (;;) {
             const int l = 2 * e + 1;
             if (l >= n) break;
@@ -128,25 +146,19 @@ struct Heap {
                 if (!(c.key >= r.key)) c = r, ci = l + 1;
             }
             if (!(x.key < c.key)) break;
-            st(e, c);
+            st(e, c, ci);
             e = ci;
         }
-        st(e, x);
-    }
-    // the slab kernel sinks by blocks; for the all-LDS kernel a level is a
-    // short LDS round trip and the sequential form is faster (C1 4.99 vs
-    // 5.17 ms measured)
-    __device__ __forceinline__ void sink(int e, const HNode& x) {
-        if (kAll) sink_seq(e, x);
-        else sink_blocks(e, x);
+        st(e, x, from);
     }
     // Sink by blocks: a level of the HBM slab costs a ~µs round trip, so
-    // the wave loads the 62 nodes of the next 5 levels at
-    // once (lane t: level j = log2(t + 2), index t + 2 - 2^j under e, only
+    // the wave loads the 2^(L+1) - 2 nodes of the next L levels at once
+    // (lane t: level j = log2(t + 2), index t + 2 - 2^j under e, only
     // positions < n) and makes the same comparisons and moves on readlane'd
-    // copies, reloading every 5 levels.  Moved nodes are stored above the
+    // copies, reloading every L levels.  Moved nodes are stored above the
     // next block, so a block never reads a position this sink has written.
-    __device__ __forceinline__ void sink_blocks(int e, const HNode& x) {
+    template <int L>
+    __device__ __forceinline__ void sink_blocks(int e, const HNode& x, int from) {
         const int j = 31 - __builtin_clz((unsigned)lane + 2);
         const int bi = lane + 2 - (1 << j);
         for (;;) {
@@ -154,13 +166,13 @@ struct Heap {
             const int p = (e + 1) * (1 << j) - 1 + bi;
             double ck_l = 0.0;
             int cv_l = 0;
-            if (lane < 62 && p < n) {
+            if (lane < (2 << L) - 2 && p < n) {
                 const HNode c = (kAll || p < kTop) ? top[p] : rest[p + 1];
                 ck_l = c.key;
                 cv_l = c.v;
             }
             int lv = 0, li = 0; // block level and index of e
-            for (; lv < 5; lv++) {
+            for (; lv < L; lv++) {
                 const int l = 2 * e + 1;
                 if (l >= n) break;
                 const int cl = (2 << lv) - 2 + 2 * li; // lane of the left child
@@ -176,31 +188,59 @@ struct Heap {
                     }
                 }
                 if (!(x.key < ck)) break;
-                st(e, HNode{ck, cv, 0});
+                st(e, HNode{ck, cv, 0}, ci);
                 li = 2 * li + (ci - l);
                 e = ci;
             }
-            if (lv < 5) break;
+            if (lv < L) break;
         }
-        st(e, x);
+        st(e, x, from);
+    }
+    // sink_mode: 5 / 3 / 2 levels per block, 1 sequential (slab kernel); the
+    // all-LDS kernel always sinks level by level (C1 4.99 vs 5.17 ms)
+    int sink_mode;
+    __device__ __forceinline__ void sink(int e, const HNode& x, int from) {
+        if (kAll || sink_mode == 1) sink_seq(e, x, from);
+        else if (sink_mode == 2) sink_blocks<2>(e, x, from);
+        else if (sink_mode == 3) sink_blocks<3>(e, x, from);
+        else sink_blocks<5>(e, x, from);
     }
     __device__ __forceinline__ void push(int v, double key) {
         const int e = n++;
-        shift_up(e, HNode{key, v, 0});
+        shift_up(e, HNode{key, v, 0}, -1);
     }
     // delete_max in two halves: the root is read first (top), then removed
     // (the last node takes the root and sinks)
     __device__ __forceinline__ HNode top_node() const { return ld(0); }
     __device__ __forceinline__ void pop_top(int v) {
         const int last = --n;
-        pos[v] = 0;
-        if (last > 0) sink(0, ld(last));
+        if (kAll) pos[v] = 0;
+        if (last > 0) sink(0, ld(last), last);
+    }
+    // position of v in the LDS top (lazy mode): every lane compares its
+    // share of the occupied top positions, a ballot names the one holding v
+    __device__ __forceinline__ int find_top(int v) const {
+        const int m = n < kTop ? n : kTop;
+        int found = -1;
+        for (int q = lane; q < m; q += 64)
+            if (top[q].v == v) found = q;
+        const unsigned long long b = __ballot(found >= 0);
+        return __builtin_amdgcn_readlane(found, b ? __builtin_ctzll(b) : 0);
     }
     // igraph_2wheap_modify with a larger key (Dijkstra only lowers a
     // distance, strictly): its sink step cannot move the node -- the heap
     // keeps parent >= child, so every child is <= the old key < the new key --
     // which leaves the shift-up at the node's position.
-    __device__ __forceinline__ void raise(int v, double key) { shift_up((kAll ? pos[v] : uni(pos[v])) - 2, HNode{key, v, 0}); }
+    __device__ __forceinline__ void raise(int v, double key) {
+        int e;
+        if (kAll) {
+            e = pos[v] - 2;
+        } else {
+            const int pv = uni(pos[v]);
+            e = (lazy && pv == 1) ? uni(find_top(v)) : pv - 2;
+        }
+        shift_up(e, HNode{key, v, 0}, e);
+    }
 };
 
 
@@ -246,7 +286,7 @@ __device__ void self_entry(const ShdGraphDev& g, int u, ShdEntry* out, int lane)
 template <bool kAll>
 __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, int row_lo, int row_hi,
                                                               ShdEntry* __restrict__ tab, char* __restrict__ slab,
-                                                              size_t slab_stride) {
+                                                              size_t slab_stride, int lazy_pos, int sink_mode) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int gw = (int)blockIdx.x * wpb + w, nw = (int)gridDim.x * wpb;
@@ -271,7 +311,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
         const int src = g.slot_vertex[row];
         for (int v = lane; v < V; v += 64) DI(v) = -1.0;
         wave_fence();
-        Heap<kAll> h{top, rest, pos, 0, lane};
+        Heap<kAll> h{top, rest, pos, 0, lane, lazy_pos != 0, sink_mode};
         DI(src) = 0.0;
         RI(src) = 1.0;
         h.push(src, 0.0);
@@ -418,7 +458,7 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
                              "hipFuncSetAttribute")))
             return rc;
         hipLaunchKernelGGL(k_sssp_rows<true>, dim3(rows), dim3(64), lds, nullptr, g, row_lo, row_hi, tab,
-                           (char*)nullptr, (size_t)0);
+                           (char*)nullptr, (size_t)0, 0, 1);
         if ((rc = hip_status(hipGetLastError(), "k_sssp_rows<lds> launch"))) return rc;
         return hip_status(hipDeviceSynchronize(), "k_sssp_rows<lds>");
     }
@@ -443,8 +483,15 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         if (grid <= 16) return shd_fail(-ENOMEM, "cannot allocate SSSP workspace");
         grid /= 2;
     }
+    // SHD_SSSP_LAZYPOS=0 / SHD_SSSP_SINK=1|2|3|5: measurement variants of the
+    // same exact algorithm (pos bookkeeping, sink block depth)
+    const char* lp = getenv("SHD_SSSP_LAZYPOS");
+    const char* sm = getenv("SHD_SSSP_SINK");
+    const int lazy = lp ? atoi(lp) != 0 : 1;
+    int sink_mode = sm ? atoi(sm) : 5;
+    if (sink_mode != 1 && sink_mode != 2 && sink_mode != 3) sink_mode = 5;
     hipLaunchKernelGGL(k_sssp_rows<false>, dim3(grid), dim3(64 * kSlabWaves), sizeof(HNode) * kTop * kSlabWaves,
-                       nullptr, g, row_lo, row_hi, tab, slab, stride);
+                       nullptr, g, row_lo, row_hi, tab, slab, stride, lazy, sink_mode);
     rc = hip_status(hipGetLastError(), "k_sssp_rows<hbm> launch");
     if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_rows<hbm>");
     (void)hipFree(slab);
