@@ -26,6 +26,11 @@ void shd_topology_release_device(ShdTopology* t) {
     shd_dev_free(t->d_host_info);
     shd_dev_free(t->d_touch);
     shd_dev_free(t->d_pair_bits);
+    shd_dev_free(t->d_snb);
+    shd_dev_free(t->d_swr);
+    shd_dev_free(t->d_soff);
+    t->d_snb = t->d_swr = NULL;
+    t->d_soff = NULL;
     t->d_tab = NULL;
     t->d_host_info = NULL;
     t->d_inc_off = t->d_inc_nbr = t->d_slot_vertex = t->d_vertex_slot = NULL;
@@ -77,6 +82,42 @@ static int prepare(ShdTopology* t) {
     UPLOAD(t->d_slot_vertex, t->slot_vertex, sizeof(int32_t) * (size_t)t->A);
     UPLOAD(t->d_vertex_slot, t->vertex_slot, sizeof(int32_t) * (size_t)t->V);
     UPLOAD(t->d_host_info, hs, sizeof(uint32_t) * 2 * (size_t)t->nhosts);
+    {
+        /* sentinel-terminated lists for the slab kernel (shd_internal.h) */
+        const size_t SM = M + (size_t)t->V + 64;
+        int32_t* snb = (int32_t*)calloc(2 * SM, sizeof(int32_t));
+        double* swr = (double*)calloc(2 * SM, sizeof(double));
+        int32_t* soff = (int32_t*)malloc(sizeof(int32_t) * ((size_t)t->V + 1));
+        if (!snb || !swr || !soff) {
+            free(snb);
+            free(swr);
+            free(soff);
+            rc = -ENOMEM;
+            goto fail;
+        }
+        for (int v = 0; v < t->V; v++) soff[v] = t->inc_off[v] + v;
+        for (int v = 0; v < t->V; v++) {
+            size_t o = (size_t)soff[v];
+            for (int32_t k = t->inc_off[v]; k < t->inc_off[v + 1]; k++, o++) {
+                snb[2 * o] = t->inc_nbr[k];
+                snb[2 * o + 1] = soff[t->inc_nbr[k]];
+                swr[2 * o] = w[k];
+                swr[2 * o + 1] = r[k];
+            }
+            snb[2 * o] = t->v_attached[v] ? -2 : -1;
+        }
+        for (size_t o = M + (size_t)t->V; o < SM; o++) snb[2 * o] = -1;
+        rc = shd_dev_malloc(&t->d_snb, sizeof(int32_t) * 2 * SM);
+        if (!rc) rc = shd_dev_h2d(t->d_snb, snb, sizeof(int32_t) * 2 * SM);
+        if (!rc) rc = shd_dev_malloc(&t->d_swr, sizeof(double) * 2 * SM);
+        if (!rc) rc = shd_dev_h2d(t->d_swr, swr, sizeof(double) * 2 * SM);
+        if (!rc) rc = shd_dev_malloc((void**)&t->d_soff, sizeof(int32_t) * (size_t)t->V);
+        if (!rc) rc = shd_dev_h2d(t->d_soff, soff, sizeof(int32_t) * (size_t)t->V);
+        free(snb);
+        free(swr);
+        free(soff);
+        if (rc) goto fail;
+    }
     free(w);
     free(r);
     hs = NULL;
@@ -119,6 +160,9 @@ static ShdGraphDev graph_dev(const ShdTopology* t) {
     g.inc_r = t->d_inc_r;
     g.slot_vertex = t->d_slot_vertex;
     g.vertex_slot = t->d_vertex_slot;
+    g.snb = t->d_snb;
+    g.swr = t->d_swr;
+    g.soff = t->d_soff;
     return g;
 }
 

@@ -1,11 +1,11 @@
 // routing.hip -- routing-table rows on gfx950.
 //
-// k_sssp_rows: one 64-lane wave per source slot runs igraph 0.8's
-// get_shortest_paths_dijkstra exactly (routing/topology.c:1682 ->
-// igraph structural_properties.c): indexed binary max-heap on -dist
-// (igraph_2wheap: shift-up swaps while !(x < parent), sink prefers the left
-// child when left >= right, modify = sink then shift-up at the original
-// position, delete_max = swap root/last, pop, sink), incidence lists in
+// Both SSSP kernels run igraph 0.8's get_shortest_paths_dijkstra exactly,
+// one 64-lane wave per source (routing/topology.c:1682 -> igraph
+// structural_properties.c): indexed binary max-heap on -dist (igraph_2wheap:
+// shift-up swaps while !(x < parent), sink prefers the left child when
+// left >= right, modify = sink then shift-up at the original position,
+// delete_max = swap root/last, pop, sink), incidence lists in
 // igraph_incident(mode OUT) order, "first finite distance" -> push,
 // "alt < cur" -> modify, early exit once every attached vertex is popped.
 // Reliability is folded along the final parent chain exactly as
@@ -23,14 +23,19 @@
 // with the same address and value, so each lane reads back its own writes in
 // program order and the loop needs no barrier.
 //
-// Storage: 16-B heap nodes {key = -dist, vertex} plus igraph's index2 (pos).
-//  * V <= kLdsMaxV: everything in LDS (36 B per vertex), one wave per block.
-//  * larger graphs: a private HBM slab per wave (heap, dist, rel, pos), with
-//    heap positions [0, kTop) -- the levels every pop walks through -- kept in
-//    LDS; kSlabWaves independent waves per block, up to kWavesPerCU per CU,
-//    persistent over rows.  A row is bound by its chain of dependent heap
-//    loads, not by bandwidth, so the kernel keeps as many rows in flight as
-//    the CUs hold.
+//  * k_sssp_lds (V <= kLdsMaxV, the dense C1 graphs): everything in LDS
+//    (36 B per vertex), one wave per block, 16 batches of 64 incident edges
+//    in flight per pop.
+//  * k_sssp_slab (larger graphs): a private HBM slab per wave (heap, {dist,
+//    rel} records, pos), heap positions [0, kTop) in LDS, persistent waves.
+//    A row is a chain of dependent memory round trips (~1-2 us each under
+//    load), so the pop is arranged to overlap them: the root node carries
+//    the start of its vertex's sentinel-terminated incidence list, so the
+//    edge loads of u, the removal's last-node load and rel[u] are issued
+//    together the moment u is known, the neighbours' distance gathers are
+//    issued as soon as the edges arrive, and the sink's HBM block loads
+//    then wait behind them -- the relaxation data is in registers when the
+//    sink ends.
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
@@ -45,11 +50,14 @@ constexpr int kTop = 256;       // heap positions in LDS for the slab kernel (le
 constexpr int kSlabWaves = 4;   // independent waves per slab-kernel block
 constexpr int kWavesPerCU = 32; // gfx950: resident waves per CU
 constexpr int kLdsMaxV = 4096;  // 36 B per vertex -> 144 KiB of the 160 KiB LDS
+constexpr int kSinkLevels = 5;  // heap levels loaded per sink block (62 nodes, one per lane)
 
+// so: in the slab kernel, the start of v's list in the sentinel-terminated
+// incidence arrays (g.snb / g.swr); unused by the LDS kernel
 struct __attribute__((aligned(16))) HNode {
     double key; // -dist
     int v;
-    int pad;
+    int so;
 };
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -65,6 +73,7 @@ __device__ __forceinline__ double uni_d(double v) {
     const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(b >> 32));
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+__device__ __forceinline__ HNode uni_n(const HNode& x) { return HNode{uni_d(x.key), uni(x.v), uni(x.so)}; }
 
 // igraph_2wheap over split storage.  kAll: every position in LDS (top).
 // Else positions < kTop in LDS and position p >= kTop at rest[p + 1], which
@@ -73,25 +82,23 @@ __device__ __forceinline__ double uni_d(double v) {
 // pos (igraph's index2, vertex -> position + 2) is what a decrease-key needs
 // to find a vertex.  In the slab kernel every pos store is one random HBM
 // request and a sink moves a node at every level it passes, most of them in
-// the LDS top; so with `lazy` set, pos of a node in the LDS top is the
-// marker 1 ("somewhere in the top"), written only when the node enters the
-// top, and a decrease-key of such a node finds it by a wave-wide search of
-// the (at most kTop) top positions.  A pop does not clear pos: a popped
-// vertex is never decreased again (alt = dist[u] + w >= dist[v] for every
-// popped v, weights > 0).  Neither changes a heap operation.
+// the LDS top; so there pos of a node in the LDS top is the marker 1
+// ("somewhere in the top"), written only when the node enters the top, and
+// a decrease-key of such a node finds it by a wave-wide search of the (at
+// most kTop) top positions.  The slab kernel's pop does not clear pos: a
+// popped vertex is never decreased again (alt = dist[u] + w >= dist[v] for
+// every popped v, weights > 0).  Neither changes a heap operation.
 template <bool kAll>
 struct Heap {
     HNode* top;
     HNode* rest;
-    int* pos; // vertex -> position + 2 (1: in the LDS top, lazy mode)
+    int* pos; // vertex -> position + 2 (slab: 1 = in the LDS top)
     int n;
     int lane;
-    bool lazy;
 
-    // every heap operand is wave-uniform: readfirstlane tells the compiler
-    // so, and the heap then runs on scalar branches with LDS- or
-    // global-specific accesses (not exec-masked flat ones)
-    __device__ __forceinline__ HNode ld(int p) const {
+    // the node at p as loaded (per lane); the slab kernel makes it uniform
+    // with uni_n only where it is used, so that the load can be issued early
+    __device__ __forceinline__ HNode ld_raw(int p) const {
         HNode x;
         // (distinct asm markers after each access keep the compiler from
         // sinking the LDS and the global access into one flat access)
@@ -102,8 +109,14 @@ struct Heap {
             x = rest[p + 1];
             __asm__ volatile("; heap hbm" ::: "memory");
         }
-        if (kAll) return x; // (the LDS kernel is faster without the readfirstlanes)
-        return HNode{uni_d(x.key), uni(x.v), 0};
+        return x;
+    }
+    // every heap operand is wave-uniform: readfirstlane tells the compiler
+    // so, and the heap then runs on scalar branches with LDS- or
+    // global-specific accesses (not exec-masked flat ones)
+    __device__ __forceinline__ HNode ld(int p) const {
+        if (kAll) return ld_raw(p); // (the LDS kernel is faster without the readfirstlanes)
+        return uni_n(ld_raw(p));
     }
     // stores node x at position p; `from` = its previous position (-1: new)
     __device__ __forceinline__ void st(int p, const HNode& x, int from) {
@@ -114,9 +127,7 @@ struct Heap {
             rest[p + 1] = x;
             __asm__ volatile("; heap hbm st" ::: "memory");
         }
-        if (kAll || !lazy) {
-            if (p != from) pos[x.v] = p + 2;
-        } else if (p >= kTop) {
+        if (kAll || p >= kTop) {
             if (p != from) pos[x.v] = p + 2;
         } else if (from < 0 || from >= kTop) {
             pos[x.v] = 1; // entered the LDS top
@@ -151,13 +162,14 @@ struct Heap {
         }
         st(e, x, from);
     }
-    // Sink by blocks: a level of the HBM slab costs a ~µs round trip, so
-    // the wave loads the 2^(L+1) - 2 nodes of the next L levels at once
-    // (lane t: level j = log2(t + 2), index t + 2 - 2^j under e, only
+    // Sink by blocks (slab kernel): a level of the HBM slab costs a ~us
+    // round trip, so the wave loads the 62 nodes of the next 5 levels at
+    // once (lane t: level j = log2(t + 2), index t + 2 - 2^j under e, only
     // positions < n) and makes the same comparisons and moves on readlane'd
-    // copies, reloading every L levels.  Moved nodes are stored above the
-    // next block, so a block never reads a position this sink has written.
-    template <int L>
+    // copies, reloading every 5 levels (5 levels per block measured fastest
+    // against 3, 2 and level by level on C2 and C4).  Moved nodes are stored
+    // above the next block, so a block never reads a position this sink has
+    // written.
     __device__ __forceinline__ void sink_blocks(int e, const HNode& x, int from) {
         const int j = 31 - __builtin_clz((unsigned)lane + 2);
         const int bi = lane + 2 - (1 << j);
@@ -165,59 +177,54 @@ struct Heap {
             if (2 * e + 1 >= n) break;
             const int p = (e + 1) * (1 << j) - 1 + bi;
             double ck_l = 0.0;
-            int cv_l = 0;
-            if (lane < (2 << L) - 2 && p < n) {
+            int cv_l = 0, cs_l = 0;
+            if (lane < (2 << kSinkLevels) - 2 && p < n) {
                 const HNode c = (kAll || p < kTop) ? top[p] : rest[p + 1];
                 ck_l = c.key;
                 cv_l = c.v;
+                cs_l = c.so;
             }
             int lv = 0, li = 0; // block level and index of e
-            for (; lv < L; lv++) {
+            for (; lv < kSinkLevels; lv++) {
                 const int l = 2 * e + 1;
                 if (l >= n) break;
-                const int cl = (2 << lv) - 2 + 2 * li; // lane of the left child
+                int cl = (2 << lv) - 2 + 2 * li; // lane of the left child
                 double ck = readlane_d(ck_l, cl);
-                int cv = __builtin_amdgcn_readlane(cv_l, cl);
                 int ci = l;
                 if (l + 1 < n) {
                     const double rk = readlane_d(ck_l, cl + 1);
                     if (!(ck >= rk)) {
                         ck = rk;
-                        cv = __builtin_amdgcn_readlane(cv_l, cl + 1);
+                        cl += 1;
                         ci = l + 1;
                     }
                 }
                 if (!(x.key < ck)) break;
-                st(e, HNode{ck, cv, 0}, ci);
+                st(e, HNode{ck, __builtin_amdgcn_readlane(cv_l, cl), __builtin_amdgcn_readlane(cs_l, cl)}, ci);
                 li = 2 * li + (ci - l);
                 e = ci;
             }
-            if (lv < L) break;
+            if (lv < kSinkLevels) break;
         }
         st(e, x, from);
     }
-    // sink_mode: 5 / 3 / 2 levels per block, 1 sequential (slab kernel); the
-    // all-LDS kernel always sinks level by level (C1 4.99 vs 5.17 ms)
-    int sink_mode;
     __device__ __forceinline__ void sink(int e, const HNode& x, int from) {
-        if (kAll || sink_mode == 1) sink_seq(e, x, from);
-        else if (sink_mode == 2) sink_blocks<2>(e, x, from);
-        else if (sink_mode == 3) sink_blocks<3>(e, x, from);
-        else sink_blocks<5>(e, x, from);
+        if (kAll) sink_seq(e, x, from); // a level of LDS is a short round trip (C1 4.99 vs 5.17 ms)
+        else sink_blocks(e, x, from);
     }
-    __device__ __forceinline__ void push(int v, double key) {
+    __device__ __forceinline__ void push(int v, double key, int so) {
         const int e = n++;
-        shift_up(e, HNode{key, v, 0}, -1);
+        shift_up(e, HNode{key, v, so}, -1);
     }
-    // delete_max in two halves: the root is read first (top), then removed
-    // (the last node takes the root and sinks)
+    // delete_max in two halves: the root is read first (top_node), then
+    // removed (the last node takes the root and sinks)
     __device__ __forceinline__ HNode top_node() const { return ld(0); }
     __device__ __forceinline__ void pop_top(int v) {
         const int last = --n;
-        if (kAll) pos[v] = 0;
+        pos[v] = 0;
         if (last > 0) sink(0, ld(last), last);
     }
-    // position of v in the LDS top (lazy mode): every lane compares its
+    // position of v in the LDS top (slab kernel): every lane compares its
     // share of the occupied top positions, a ballot names the one holding v
     __device__ __forceinline__ int find_top(int v) const {
         const int m = n < kTop ? n : kTop;
@@ -231,18 +238,17 @@ struct Heap {
     // distance, strictly): its sink step cannot move the node -- the heap
     // keeps parent >= child, so every child is <= the old key < the new key --
     // which leaves the shift-up at the node's position.
-    __device__ __forceinline__ void raise(int v, double key) {
+    __device__ __forceinline__ void raise(int v, double key, int so) {
         int e;
         if (kAll) {
             e = pos[v] - 2;
         } else {
             const int pv = uni(pos[v]);
-            e = (lazy && pv == 1) ? uni(find_top(v)) : pv - 2;
+            e = pv == 1 ? uni(find_top(v)) : pv - 2;
         }
-        shift_up(e, HNode{key, v, 0}, e);
+        shift_up(e, HNode{key, v, so}, e);
     }
 };
-
 
 // orders one wave's per-lane accesses before its uniform ones (and back)
 __device__ __forceinline__ void wave_fence() {
@@ -283,58 +289,68 @@ __device__ void self_entry(const ShdGraphDev& g, int u, ShdEntry* out, int lane)
     }
 }
 
-template <bool kAll>
-__global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, int row_lo, int row_hi,
-                                                              ShdEntry* __restrict__ tab, char* __restrict__ slab,
-                                                              size_t slab_stride, int lazy_pos, int sink_mode) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
-    const int gw = (int)blockIdx.x * wpb + w, nw = (int)gridDim.x * wpb;
-    const int V = g.V, A = g.A;
-    // dense graphs (LDS kernel): 4 batches in flight; sparse ones rarely
-    // have a second batch, and the slab kernel keeps its registers for
-    // occupancy
-    constexpr int kRelax = kAll ? 16 : 1;
-    HNode* top = reinterpret_cast<HNode*>(smem) + (kAll ? 0 : w * kTop);
-    HNode* rest = kAll ? nullptr : reinterpret_cast<HNode*>(slab + (size_t)gw * slab_stride);
-    // per-vertex distance and reliability: separate LDS arrays in the LDS
-    // kernel; in the slab one 16-B record {dist, rel} per vertex, so the
-    // stores after an improvement and the rel[u] read at its pop fall on the
-    // line the distance gather already fetched (the slab kernel is bound by
-    // random HBM line requests)
-    double* dr = reinterpret_cast<double*>(kAll ? top + V + 1 : rest + V + 2);
-    int* pos = reinterpret_cast<int*>(dr + 2 * (size_t)V);
-    auto DI = [&](int x) -> double& { return kAll ? dr[x] : dr[2 * (size_t)x]; };
-    auto RI = [&](int x) -> double& { return kAll ? dr[V + x] : dr[2 * (size_t)x + 1]; };
+// Row output (topology.c:1744-1791): every attached target but the source
+// itself -- latency 0 becomes 1 ms -- then the self path.
+template <typename DistRel>
+__device__ __forceinline__ void write_row(const ShdGraphDev& g, int row, int src, ShdEntry* __restrict__ tab, int lane,
+                                          DistRel dist_rel) {
+    const int A = g.A;
+    ShdEntry* out = tab + (size_t)row * (size_t)A;
+    for (int j = lane; j < A; j += 64) {
+        if (j == row) continue;
+        double l, r;
+        dist_rel(g.slot_vertex[j], l, r);
+        ShdEntry e;
+        if (l < 0) {
+            e.lat = -1.0; // unreachable: impossible on a validated (strongly connected) graph
+            e.rel = 0.0;
+        } else {
+            e.lat = (l == 0) ? 1.0 : l; // topology.c:1787-1791
+            e.rel = r;
+        }
+        out[j] = e;
+    }
+    self_entry(g, src, out + row, lane);
+}
 
-    for (int row = row_lo + gw; row < row_hi; row += nw) {
+// ---- LDS kernel: the whole per-row state in LDS (dense graphs, C1) ----
+__global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int V = g.V, A = g.A;
+    // a complete graph's CSR is 24 MB (Infinity-Cache round trips): 16
+    // batches of 64 incident edges are loaded together per pop
+    constexpr int kRelax = 16;
+    HNode* top = reinterpret_cast<HNode*>(smem);
+    double* dist = reinterpret_cast<double*>(top + V + 1);
+    double* rel = dist + V;
+    int* pos = reinterpret_cast<int*>(rel + V);
+    for (int row = row_lo + (int)blockIdx.x; row < row_hi; row += (int)gridDim.x) {
         const int src = g.slot_vertex[row];
-        for (int v = lane; v < V; v += 64) DI(v) = -1.0;
+        for (int v = lane; v < V; v += 64) dist[v] = -1.0;
         wave_fence();
-        Heap<kAll> h{top, rest, pos, 0, lane, lazy_pos != 0, sink_mode};
-        DI(src) = 0.0;
-        RI(src) = 1.0;
-        h.push(src, 0.0);
+        Heap<true> h{top, nullptr, pos, 0, lane};
+        dist[src] = 0.0;
+        rel[src] = 1.0;
+        h.push(src, 0.0, 0);
         int to_reach = A;
         while (h.n > 0 && to_reach > 0) {
-            // the loads that relaxing u needs (CSR range, rel[u], its slot)
-            // are issued before the root is removed: the sink touches heap
-            // nodes and positions only, so their latency overlaps it
+            // the loads that relaxing u needs (CSR range, its slot) are
+            // issued before the root is removed: their latency overlaps it
             const HNode t = h.top_node();
             const int u = t.v;
             const double mindist = -t.key;
-            int k0 = g.inc_off[u], k1 = g.inc_off[u + 1];
-            double ru = RI(u);
-            int uslot = g.vertex_slot[u];
-            if (!kAll) k0 = uni(k0), k1 = uni(k1), ru = uni_d(ru), uslot = uni(uslot);
+            const int k0 = g.inc_off[u], k1 = g.inc_off[u + 1];
+            const double ru = rel[u];
+            const int uslot = g.vertex_slot[u];
             h.pop_top(u);
             if (uslot >= 0) --to_reach;
             // kRelax batches of 64 incident edges are loaded together (CSR
-            // loads, then the dist gathers) before their updates are applied:
+            // loads, then the dist reads) before their updates are applied:
             // an update only writes the dist of its own neighbour, and a
             // neighbour occurs once per incidence list (parallel edges are
-            // rejected at load; a loop never improves), so the early gathers
-            // read exactly what one-at-a-time relaxation would.
+            // rejected at load; a loop never improves), so the early reads
+            // see exactly what one-at-a-time relaxation would.
             for (int b0 = k0; b0 < k1; b0 += 64 * kRelax) {
                 int v[kRelax];
                 double alt[kRelax], rv[kRelax];
@@ -349,7 +365,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
                 }
 #pragma unroll
                 for (int q = 0; q < kRelax; q++) {
-                    const double cur = DI(v[q]);
+                    const double cur = dist[v[q]];
                     const bool ok = b0 + q * 64 + lane < k1;
                     fresh[q] = ok && cur < 0;
                     imp[q] = ok && (cur < 0 || alt[q] < cur);
@@ -363,31 +379,112 @@ __global__ __launch_bounds__(64 * kSlabWaves) void k_sssp_rows(ShdGraphDev g, in
                         m &= m - 1;
                         const int vv = __builtin_amdgcn_readlane(v[q], l);
                         const double aa = readlane_d(alt[q], l);
-                        DI(vv) = aa;
-                        RI(vv) = readlane_d(rv[q], l);
-                        if ((fm >> l) & 1ull) h.push(vv, -aa);
-                        else h.raise(vv, -aa);
+                        dist[vv] = aa;
+                        rel[vv] = readlane_d(rv[q], l);
+                        if ((fm >> l) & 1ull) h.push(vv, -aa, 0);
+                        else h.raise(vv, -aa, 0);
                     }
                 }
             }
         }
         wave_fence();
-        ShdEntry* out = tab + (size_t)row * (size_t)A;
-        for (int j = lane; j < A; j += 64) {
-            if (j == row) continue;
-            const int v = g.slot_vertex[j];
-            const double l = DI(v);
-            ShdEntry e;
-            if (l < 0) {
-                e.lat = -1.0; // unreachable: impossible on a validated (strongly connected) graph
-                e.rel = 0.0;
-            } else {
-                e.lat = (l == 0) ? 1.0 : l; // topology.c:1787-1791
-                e.rel = RI(v);
+        write_row(g, row, src, tab, lane, [&](int v, double& l, double& r) {
+            l = dist[v];
+            r = rel[v];
+        });
+        wave_fence();
+    }
+}
+
+// ---- slab kernel: per-wave HBM slab, LDS heap top (sparse graphs, C2/C4) ----
+// Incidence lists are read from the sentinel-terminated copy: list of v at
+// g.soff[v], entries {nbr, soff[nbr]} in g.snb and {w, 1 - loss} in g.swr,
+// closed by {-1 or -2 (v attached), 0}; the arrays are padded by 64 entries,
+// so a 64-lane batch never reads past them.
+__global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80))) void k_sssp_slab(ShdGraphDev g, int row_lo, int row_hi,
+                                                              ShdEntry* __restrict__ tab, char* __restrict__ slab,
+                                                              size_t slab_stride) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int gw = (int)blockIdx.x * wpb + w, nw = (int)gridDim.x * wpb;
+    const int V = g.V, A = g.A;
+    HNode* top = reinterpret_cast<HNode*>(smem) + w * kTop;
+    HNode* rest = reinterpret_cast<HNode*>(slab + (size_t)gw * slab_stride);
+    // one 16-B {dist, rel} record per vertex: the stores after an
+    // improvement and the rel[u] read at its pop fall on the line the
+    // distance gather fetched
+    double2* dr = reinterpret_cast<double2*>(rest + V + 2);
+    int* pos = reinterpret_cast<int*>(dr + V);
+    const int2* __restrict__ snb = static_cast<const int2*>(g.snb);
+    const double2* __restrict__ swr = static_cast<const double2*>(g.swr);
+
+    for (int row = row_lo + gw; row < row_hi; row += nw) {
+        const int src = g.slot_vertex[row];
+        for (int v = lane; v < V; v += 64) dr[v].x = -1.0;
+        wave_fence();
+        Heap<false> h{top, rest, pos, 0, lane};
+        dr[src] = make_double2(0.0, 1.0);
+        h.push(src, 0.0, uni(g.soff[src]));
+        int to_reach = A;
+        while (h.n > 0 && to_reach > 0) {
+            const HNode t = h.top_node(); // LDS
+            const int u = t.v;
+            const double mindist = -t.key;
+            int b = t.so;
+            // issued together: u's first 64 incidence entries, the last heap
+            // node (the removal sinks it) and rel[u]
+            int2 nb = snb[b + lane];
+            double2 wr = swr[b + lane];
+            const int last = --h.n;
+            const HNode xl = h.ld_raw(last);
+            const double ru_l = dr[u].y;
+            bool first = true;
+            double ru = 0.0;
+            for (;;) {
+                // the list ends at the first sentinel; its value says whether
+                // u is an attached vertex (a target of the row)
+                const unsigned long long sm = __ballot(nb.x < 0);
+                const int fs = sm ? __builtin_ctzll(sm) : 64;
+                const bool ok = lane < fs;
+                const double cur = ok ? dr[nb.x].x : 0.0; // neighbour distance gathers
+                if (first) {
+                    // the removal of the root: the sink's HBM block loads
+                    // queue behind the gathers just issued
+                    if (last > 0) h.sink(0, uni_n(xl), last);
+                    ru = uni_d(ru_l);
+                    first = false;
+                }
+                if (fs < 64 && __builtin_amdgcn_readlane(nb.x, fs) == -2) --to_reach;
+                const double alt = mindist + wr.x;
+                const double rv = ru * wr.y;
+                const bool fresh = ok && cur < 0;
+                unsigned long long m = __ballot(ok && (cur < 0 || alt < cur));
+                const unsigned long long fm = __ballot(fresh);
+                // the batch's gathers precede its updates: an update writes
+                // only its own neighbour's record and a neighbour occurs once
+                // per list (parallel edges rejected; a loop never improves)
+                while (m) { // igraph's order: incidence order, one edge at a time
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const int vv = __builtin_amdgcn_readlane(nb.x, l);
+                    const int vs = __builtin_amdgcn_readlane(nb.y, l);
+                    const double aa = readlane_d(alt, l);
+                    dr[vv] = make_double2(aa, readlane_d(rv, l));
+                    if ((fm >> l) & 1ull) h.push(vv, -aa, vs);
+                    else h.raise(vv, -aa, vs);
+                }
+                if (fs < 64) break;
+                b += 64; // lists longer than 64 entries: next batch
+                nb = snb[b + lane];
+                wr = swr[b + lane];
             }
-            out[j] = e;
         }
-        self_entry(g, src, out + row, lane);
+        wave_fence();
+        write_row(g, row, src, tab, lane, [&](int v, double& l, double& r) {
+            const double2 x = dr[v];
+            l = x.x;
+            r = x.y;
+        });
         wave_fence();
     }
 }
@@ -453,17 +550,17 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
     if (g.V <= kLdsMaxV) {
         const size_t lds = sizeof(HNode) * ((size_t)g.V + 1) + 20 * (size_t)g.V;
         if (lds > 65536 &&
-            (rc = hip_status(hipFuncSetAttribute((const void*)k_sssp_rows<true>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+            (rc = hip_status(hipFuncSetAttribute((const void*)k_sssp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lds),
                              "hipFuncSetAttribute")))
             return rc;
-        hipLaunchKernelGGL(k_sssp_rows<true>, dim3(rows), dim3(64), lds, nullptr, g, row_lo, row_hi, tab,
-                           (char*)nullptr, (size_t)0, 0, 1);
-        if ((rc = hip_status(hipGetLastError(), "k_sssp_rows<lds> launch"))) return rc;
-        return hip_status(hipDeviceSynchronize(), "k_sssp_rows<lds>");
+        hipLaunchKernelGGL(k_sssp_lds, dim3(rows), dim3(64), lds, nullptr, g, row_lo, row_hi, tab);
+        if ((rc = hip_status(hipGetLastError(), "k_sssp_lds launch"))) return rc;
+        return hip_status(hipDeviceSynchronize(), "k_sssp_lds");
     }
+    if (!g.snb || !g.swr || !g.soff) return shd_fail(-EINVAL, "slab kernel needs the sentinel incidence arrays");
     // large graphs: persistent waves, one HBM slab each (heap V+2 nodes,
-    // dist, rel, pos); SHD_SSSP_WAVES overrides the wave count
+    // {dist, rel}, pos); SHD_SSSP_WAVES overrides the wave count
     const size_t stride = (sizeof(HNode) * ((size_t)g.V + 2) + 20 * (size_t)g.V + 255) & ~(size_t)255;
     int dev = 0, cus = 0;
     if ((rc = hip_status(hipGetDevice(&dev), "hipGetDevice")) ||
@@ -483,17 +580,10 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         if (grid <= 16) return shd_fail(-ENOMEM, "cannot allocate SSSP workspace");
         grid /= 2;
     }
-    // SHD_SSSP_LAZYPOS=0 / SHD_SSSP_SINK=1|2|3|5: measurement variants of the
-    // same exact algorithm (pos bookkeeping, sink block depth)
-    const char* lp = getenv("SHD_SSSP_LAZYPOS");
-    const char* sm = getenv("SHD_SSSP_SINK");
-    const int lazy = lp ? atoi(lp) != 0 : 1;
-    int sink_mode = sm ? atoi(sm) : 5;
-    if (sink_mode != 1 && sink_mode != 2 && sink_mode != 3) sink_mode = 5;
-    hipLaunchKernelGGL(k_sssp_rows<false>, dim3(grid), dim3(64 * kSlabWaves), sizeof(HNode) * kTop * kSlabWaves,
-                       nullptr, g, row_lo, row_hi, tab, slab, stride, lazy, sink_mode);
-    rc = hip_status(hipGetLastError(), "k_sssp_rows<hbm> launch");
-    if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_rows<hbm>");
+    hipLaunchKernelGGL(k_sssp_slab, dim3(grid), dim3(64 * kSlabWaves), sizeof(HNode) * kTop * kSlabWaves, nullptr,
+                       g, row_lo, row_hi, tab, slab, stride);
+    rc = hip_status(hipGetLastError(), "k_sssp_slab launch");
+    if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_slab");
     (void)hipFree(slab);
     return rc;
 }

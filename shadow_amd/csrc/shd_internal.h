@@ -62,6 +62,13 @@ typedef struct {
     const double* inc_r;    /* M, 1 - packet_loss */
     const int32_t* slot_vertex; /* A */
     const int32_t* vertex_slot; /* V, -1 = not attached */
+    /* sentinel-terminated copy of the incidence lists for the slab kernel:
+     * v's list starts at soff[v] = inc_off[v] + v; entries {nbr, soff[nbr]}
+     * (snb, int2) and {w_ms, 1 - loss} (swr, double2), closed by {-1, 0}
+     * (-2 when v is attached); both padded by 64 entries */
+    const void* snb;
+    const void* swr;
+    const int32_t* soff; /* V */
 } ShdGraphDev;
 
 typedef struct {

@@ -80,6 +80,8 @@ struct ShdTopology {
     uint32_t* d_host_info; /* nhosts x {slot, touch[slot]} for the packet kernel */
     uint32_t* h_host_info;
     double *d_inc_w, *d_inc_r;
+    void *d_snb, *d_swr; /* sentinel-terminated incidence lists (slab kernel) */
+    int32_t* d_soff;
     uint32_t *d_touch, *d_pair_bits;
 
     /* release (cache) state */
