@@ -429,6 +429,16 @@ def cpu_baseline(gml, H, states, top, result, c4_ctx=None):
     base = {"value": n / dt, "unit": "packets/s", "cores": 1, "kind": "port",
             "sample": f"{n} packets among the {len(hosts)} hosts attached to {nslot} of the C2 graph's attached "
                       f"vertices; rows preloaded (routing excluded, as in the GPU timed region); {dt:.1f}s"}
+    # the same sample on the box's CPU share: worker threads sharded by source
+    # host, per-destination queue mutexes (the host-single policy analogue)
+    threads = int(os.environ.get("SHD_CPU_THREADS", "16"))
+    t0 = time.perf_counter()
+    out_mt, status_mt, mt_mt = O.round_mt(orc, ips, pk, 110_000_000, 10**15, threads)
+    dt_mt = time.perf_counter() - t0
+    assert mt_mt == mt and len(out_mt) == len(out)
+    base["handoff_mt"] = {"value": n / dt_mt, "unit": "packets/s", "cores": threads, "kind": "port",
+                          "sample": f"the same {n} packets, {threads} threads sharded by source host with "
+                                    f"per-destination queue mutexes; {dt_mt:.2f}s"}
     # routing baseline: oracle Dijkstra rows of C1 (1 core, the reference holds a global graphLock)
     g1 = synth.complete_graph_gml(1000, 0x5EED0001)
     o1 = O.OracleTopology(g1)

@@ -201,6 +201,75 @@ int shd_topology_host_count(ShdTopology* top, uint32_t* nhosts);
 int shd_deliv_sort_device(ShdTopology* top, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi,
                           ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream);
 
+/* ---------------------------------------------------------------------- */
+/* Multi-GPU rounds: one topology per GPU / rank           */
+/* ---------------------------------------------------------------------- */
+
+/* The collectives a multi-GPU round needs, supplied by the caller: Shadow's
+ * C host plugs in RCCL (shd_transport_rccl_new below: ncclSend/ncclRecv over
+ * xGMI); tests plug in gloo.  Both calls are collective over `world` ranks.
+ *   alltoall_u64: host arrays of `world` values; recv[r] = what rank r sent
+ *                 to this rank.
+ *   alltoallv:    device buffers; this rank's block for peer r is
+ *                 send_bytes[r] bytes, blocks contiguous in rank order in
+ *                 d_send; the blocks received land contiguous in rank order
+ *                 in d_recv.  Enqueued on `stream` (hipStream_t) or completed
+ *                 before returning.  Return 0 or a negative errno. */
+typedef struct ShdTransport {
+    int rank, world;
+    void* user;
+    int (*alltoall_u64)(void* user, const uint64_t* send, uint64_t* recv);
+    int (*alltoallv)(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
+                     const uint64_t* recv_bytes, void* stream);
+} ShdTransport;
+
+/* Destination-owner exchange of one round's delivered events: rank r owns
+ * the destination hosts [host_bounds[r], host_bounds[r+1]) (host memory,
+ * world+1 ids).  d_events / d_dst_offsets are this rank's
+ * shd_round_process_device output (events grouped by destination over all
+ * nhosts).  The events of every rank's destinations are sent there
+ * (alltoallv), received into d_recv (capacity recv_cap events) and regrouped
+ * into event_compare order per owned destination: d_out (recv_cap events),
+ * d_out_offsets (owned hosts + 1).  *n_out = events received.  The union
+ * over ranks equals a single-GPU round over all ranks' records (the order
+ * is a total order).  Synchronous. */
+int shd_round_exchange(ShdTopology* top, const ShdTransport* xport, const ShdDeliv* d_events,
+                       const uint32_t* d_dst_offsets, const uint32_t* host_bounds, ShdDeliv* d_recv, size_t recv_cap,
+                       ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, void* stream);
+/* Row-sharded tables (C4 at N > 1, no full matrix anywhere): rank r holds
+ * rows [row_bounds[r], row_bounds[r+1]) (slot ids, host memory).  Each
+ * record is sent to the rank holding the row that answers it -- the row of
+ * the endpoint touched first (use_shortest_path; records naming unattached
+ * hosts go to rank 0, which reports them undelivered) -- preserving record
+ * order per source rank (partitioned into d_scratch, n records, which is
+ * what the transport sends); received records land in d_recv (recv_cap) in
+ * source-rank order, *n_recv set.  The receiver then decides them with
+ * shd_round_process_device on its shard and exchanges the events with
+ * shd_round_exchange.  Synchronous. */
+int shd_round_route_records(ShdTopology* top, const ShdTransport* xport, const ShdPkt* d_recs, size_t n,
+                            const uint32_t* row_bounds, ShdPkt* d_scratch, ShdPkt* d_recv, size_t recv_cap,
+                            size_t* n_recv, void* stream);
+/* Adopts rows [row_lo, row_hi) of the table (d_rows: (row_hi - row_lo) * A
+ * entries) as this rank's device-resident shard and releases every row in
+ * slot order (the touch_all steady state); lookups and rounds on this
+ * topology may then only use pairs whose answering row is in the shard.
+ * global_min_ms: the released minimum over the whole table (min over ranks
+ * of shd_topology_shard_min_latency), or < 0 to use this shard's. */
+int shd_topology_adopt_table_shard_device_resident(ShdTopology* top, void* d_rows, int row_lo, int row_hi,
+                                                   double global_min_ms);
+/* Released minimum over this shard's rows (pairs i < j), -1 if none. */
+int shd_topology_shard_min_latency(ShdTopology* top, const void* d_rows, int row_lo, int row_hi, double* min_ms);
+
+/* RCCL transport (xGMI): rank 0 creates the id (128 bytes), every rank gets
+ * it out of band and creates its transport on its device; free after use. */
+int shd_transport_rccl_unique_id(void* id128);
+int shd_transport_rccl_new(int rank, int world, const void* id128, int device, ShdTransport** out);
+void shd_transport_rccl_free(ShdTransport* xport);
+
+/* Copies between device and/or host memory (unified addressing), e.g. for a
+ * transport that bounces device blocks through host memory. */
+int shd_memcpy(void* dst, const void* src, size_t bytes);
+
 /* Device timing of the round pipeline with HIP events recorded on the launch
  * stream (for benchmarks): stages 0 packet-scatter (decision + gathers +
  * per-destination count), 1 scan, 2 place, 3 segment sort.  enable resets

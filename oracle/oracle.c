@@ -1459,3 +1459,144 @@ size_t orc_round(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint64_t
     if (min_time) *min_time = mn;
     return k;
 }
+
+/* ======================================================================= */
+/* the hand-off on N threads (CPU baseline of SURVEY.md §8d C3): Shadow's   */
+/* worker pool with the host-single policy -- each worker sends its own     */
+/* hosts' packets (sharded by source) and pushes into the destination's     */
+/* queue under that queue's mutex (scheduler_policy_host_single.c:207-219). */
+/* Needs every row the packets touch already cached (preload): lookups are */
+/* then read-only; the path counter increment is atomic.  Output identical  */
+/* to orc_round (event_compare is a total order).                           */
+/* ======================================================================= */
+#include <pthread.h>
+
+typedef struct {
+    OrcTopo* t;
+    const uint32_t* host_ips;
+    uint32_t nhosts;
+    uint64_t barrier, end_time, bootstrap_end;
+    const OrcPkt* pkts;
+    size_t n;
+    uint8_t* status;
+    OrcEvKey* keys;
+    Pq* qs;
+    pthread_mutex_t* qlock;
+    int nthreads;
+    size_t* qoff;
+    OrcDeliv* out;
+} RoundMt;
+
+typedef struct {
+    RoundMt* r;
+    int tid;
+    uint64_t mn;
+    int missing;
+} RoundMtArg;
+
+static PathE* cached_entry(OrcTopo* t, uint32_t sip, uint32_t dip) {
+    int s = orc_vertex_of_ip(t, sip), d = orc_vertex_of_ip(t, dip);
+    if (s < 0 || d < 0) return NULL;
+    PathE* p = cache_get(t, s, d);
+    if (!p && !t->directed) p = cache_get(t, d, s);
+    if (!p) p = cache_get(t, d, s); /* the re-read after a (here: no-op) row computation, topology.c:1963-1968 */
+    return p;
+}
+
+static void* round_mt_send(void* arg) {
+    RoundMtArg* a = (RoundMtArg*)arg;
+    RoundMt* r = a->r;
+    uint64_t mn = UINT64_MAX;
+    for (size_t i = 0; i < r->n; i++) {
+        const OrcPkt* p = &r->pkts[i];
+        if ((int)(p->src_host % (uint32_t)r->nthreads) != a->tid) continue; /* this worker's hosts */
+        PathE* e = cached_entry(r->t, r->host_ips[p->src_host], r->host_ips[p->dst_host]);
+        if (!e) {
+            a->missing++;
+            continue;
+        }
+        uint32_t st = p->rng_state;
+        double chance = orc_next_double(&st);
+        if (p->now < r->bootstrap_end || chance <= e->rel || p->payload_len == 0) {
+            uint64_t tm = p->now + (uint64_t)ceil(e->lat * 1000000.0);
+            __atomic_fetch_add(&e->pkts, 1, __ATOMIC_RELAXED);
+            if (tm >= r->end_time) {
+                r->status[i] = ORC_DROP_END;
+                continue;
+            }
+            if (p->src_host != p->dst_host && tm < r->barrier) tm = r->barrier;
+            r->keys[i] = (OrcEvKey){tm, p->dst_host, p->src_host, p->seq};
+            pthread_mutex_lock(&r->qlock[p->dst_host]);
+            pq_push(&r->qs[p->dst_host], (uint32_t)i);
+            pthread_mutex_unlock(&r->qlock[p->dst_host]);
+            if (tm >= r->barrier && tm < mn) mn = tm;
+            r->status[i] = ORC_DELIVERED;
+        } else {
+            r->status[i] = ORC_DROP_LOSS;
+        }
+    }
+    a->mn = mn;
+    return NULL;
+}
+
+static void* round_mt_pop(void* arg) {
+    RoundMtArg* a = (RoundMtArg*)arg;
+    RoundMt* r = a->r;
+    for (uint32_t h = (uint32_t)a->tid; h < r->nhosts; h += (uint32_t)r->nthreads) {
+        size_t k = r->qoff[h];
+        while (r->qs[h].size) {
+            uint32_t i = pq_pop(&r->qs[h]);
+            r->out[k++] = (OrcDeliv){r->keys[i].time, r->keys[i].seq, r->keys[i].src, r->keys[i].dst, i, 0};
+        }
+        free(r->qs[h].heap);
+    }
+    return NULL;
+}
+
+/* Returns the number of delivered events, or (size_t)-1 if a packet's path
+ * is not cached (preload first). */
+size_t orc_round_mt(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint64_t barrier, uint64_t end_time,
+                    uint64_t bootstrap_end, const OrcPkt* pkts, size_t n, int nthreads, OrcDeliv* out,
+                    uint8_t* status, uint64_t* min_time) {
+    if (nthreads < 1) nthreads = 1;
+    RoundMt r = {t, host_ips, nhosts, barrier, end_time, bootstrap_end, pkts, n, status, NULL, NULL, NULL, nthreads,
+                 NULL, out};
+    r.keys = (OrcEvKey*)malloc(sizeof(OrcEvKey) * (n ? n : 1));
+    r.qs = (Pq*)calloc(nhosts ? nhosts : 1, sizeof(Pq));
+    r.qlock = (pthread_mutex_t*)malloc(sizeof(pthread_mutex_t) * (nhosts ? nhosts : 1));
+    r.qoff = (size_t*)malloc(sizeof(size_t) * ((size_t)nhosts + 1));
+    for (uint32_t h = 0; h < nhosts; h++) {
+        r.qs[h].keys = r.keys;
+        pthread_mutex_init(&r.qlock[h], NULL);
+    }
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    RoundMtArg* args = (RoundMtArg*)calloc((size_t)nthreads, sizeof(RoundMtArg));
+    for (int i = 0; i < nthreads; i++) {
+        args[i].r = &r;
+        args[i].tid = i;
+        pthread_create(&th[i], NULL, round_mt_send, &args[i]);
+    }
+    uint64_t mn = UINT64_MAX;
+    int missing = 0;
+    for (int i = 0; i < nthreads; i++) {
+        pthread_join(th[i], NULL);
+        if (args[i].mn < mn) mn = args[i].mn;
+        missing += args[i].missing;
+    }
+    size_t k = 0;
+    for (uint32_t h = 0; h < nhosts; h++) {
+        r.qoff[h] = k;
+        k += r.qs[h].size;
+    }
+    for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, round_mt_pop, &args[i]);
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    for (uint32_t h = 0; h < nhosts; h++) pthread_mutex_destroy(&r.qlock[h]);
+    free(th);
+    free(args);
+    free(r.qlock);
+    free(r.qoff);
+    free(r.qs);
+    free(r.keys);
+    if (min_time) *min_time = mn;
+    return missing ? (size_t)-1 : k;
+}

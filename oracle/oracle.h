@@ -121,6 +121,12 @@ enum { ORC_DROP_LOSS = 0, ORC_DELIVERED = 1, ORC_DROP_END = 2 };
 size_t orc_round(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint64_t barrier,
                  uint64_t end_time, uint64_t bootstrap_end, const OrcPkt* pkts, size_t n,
                  OrcDeliv* out, uint8_t* status, uint64_t* min_time);
+/* The same hand-off on nthreads worker threads sharded by source host, with
+ * per-destination queue mutexes (host-single policy analogue); every path
+ * the packets use must already be cached (else returns (size_t)-1). */
+size_t orc_round_mt(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint64_t barrier, uint64_t end_time,
+                    uint64_t bootstrap_end, const OrcPkt* pkts, size_t n, int nthreads, OrcDeliv* out,
+                    uint8_t* status, uint64_t* min_time);
 
 /* Binary heap restating utility/priority_queue.c with event_compare
  * (core/work/event.c:109-152); exposed for the PQ golden test. */

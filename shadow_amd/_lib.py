@@ -66,6 +66,15 @@ PROTOS = {
     "shd_deliv_sort_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "shd_round_timing_enable": (C.c_int, [C.c_int]),
     "shd_round_timing_read": (C.c_int, [_dp, C.c_int, _ip]),
+    "shd_round_exchange": (C.c_int, [_P, _P, _P, _P, _u32p, _P, C.c_size_t, _P, _P, C.POINTER(C.c_size_t), _P]),
+    "shd_round_route_records": (C.c_int, [_P, _P, _P, C.c_size_t, _u32p, _P, _P, C.c_size_t,
+                                          C.POINTER(C.c_size_t), _P]),
+    "shd_topology_adopt_table_shard_device_resident": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_double]),
+    "shd_topology_shard_min_latency": (C.c_int, [_P, _P, C.c_int, C.c_int, _dp]),
+    "shd_transport_rccl_unique_id": (C.c_int, [_P]),
+    "shd_transport_rccl_new": (C.c_int, [C.c_int, C.c_int, _P, C.c_int, C.POINTER(_P)]),
+    "shd_transport_rccl_free": (None, [_P]),
+    "shd_memcpy": (C.c_int, [_P, _P, C.c_size_t]),
     "shd_parse_time_ns": (C.c_int, [C.c_char_p, _u64p]),
     "shd_parse_bandwidth_bits": (C.c_int, [C.c_char_p, _u64p]),
     "shd_last_error": (C.c_char_p, []),

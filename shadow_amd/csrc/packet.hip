@@ -210,6 +210,9 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
                     if (!((c.pair_bits[b >> 5] >> (b & 31)) & 1u)) oi = di[k], oj = si[k];
                 }
             }
+            // a row-sharded table holds rows [row_lo, row_hi) only: a record
+            // answered by another rank's row is not decided here (status 0xff)
+            if (oi < c.row_lo || oi >= c.row_hi) si[k] = -1;
             ei[k] = (size_t)(oi < 0 ? 0 : oi) * A + (size_t)(oj < 0 ? 0 : oj);
         }
         ShdEntry e[kB];

@@ -219,3 +219,45 @@ int shd_deliv_sort_device(ShdTopology* t, const ShdDeliv* d_in, size_t n, uint32
     pthread_mutex_unlock(&t->round_mu);
     return rc;
 }
+
+/* ---- multi-GPU rounds (kernels and RCCL in xchg.hip) ---- */
+
+int shd_round_exchange(ShdTopology* t, const ShdTransport* x, const ShdDeliv* d_events, const uint32_t* d_dst_offsets,
+                       const uint32_t* host_bounds, ShdDeliv* d_recv, size_t recv_cap, ShdDeliv* d_out,
+                       uint32_t* d_out_offsets, size_t* n_out, void* stream) {
+    if (!t || !x || !host_bounds || !n_out || x->world < 1 || x->rank < 0 || x->rank >= x->world)
+        return shd_fail(-EINVAL, "bad exchange arguments");
+    if (host_bounds[0] != 0 || host_bounds[x->world] != t->nhosts)
+        return shd_fail(-EINVAL, "host bounds must cover [0, %u)", t->nhosts);
+    int rc = shd_dev_init(t->device);
+    if (rc) return rc;
+    uint64_t* send = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)x->world);
+    if (!send) return -ENOMEM;
+    size_t nrecv = 0;
+    if (!(rc = shd_dev_event_cuts(d_dst_offsets, host_bounds, x->world, send, stream)) &&
+        !(rc = shd_dev_exchange_blocks(x, d_events, send, sizeof(ShdDeliv), d_recv, recv_cap, &nrecv, stream)))
+        rc = shd_deliv_sort_device(t, d_recv, nrecv, host_bounds[x->rank], host_bounds[x->rank + 1], d_out,
+                                   d_out_offsets, stream);
+    free(send);
+    if (!rc) *n_out = nrecv;
+    return rc;
+}
+
+int shd_round_route_records(ShdTopology* t, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
+                            const uint32_t* row_bounds, ShdPkt* d_scratch, ShdPkt* d_recv, size_t recv_cap,
+                            size_t* n_recv, void* stream) {
+    if (!t || !x || !row_bounds || !n_recv || x->world < 1) return shd_fail(-EINVAL, "bad route arguments");
+    int rc = shd_ensure_routes(t);
+    if (rc) return rc;
+    if (!t->use_sp) return shd_fail(-ENOTSUP, "row routing needs use_shortest_path (touch order)");
+    if (row_bounds[0] != 0 || (int)row_bounds[x->world] != t->A)
+        return shd_fail(-EINVAL, "row bounds must cover [0, %d)", t->A);
+    pthread_mutex_lock(&t->round_mu);
+    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t))) {
+        ShdPktCtx c;
+        shd_pkt_ctx(t, &c);
+        rc = shd_dev_route_records(&c, x, d_recs, n, row_bounds, d_scratch, d_recv, recv_cap, n_recv, stream);
+    }
+    pthread_mutex_unlock(&t->round_mu);
+    return rc;
+}

@@ -176,6 +176,8 @@ static int adopt(ShdTopology* t, ShdEntry* d_tab, int owned) {
     if (t->d_tab && t->d_tab_owned && t->d_tab != d_tab) shd_dev_free(t->d_tab);
     t->d_tab = d_tab;
     t->d_tab_owned = owned;
+    t->tab_row_lo = 0;
+    t->tab_row_hi = t->A;
     t->built = 1;
     __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE); /* publishes the immutable table to lock-free lookups */
     return 0;
@@ -280,6 +282,8 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->pair_bits = t->d_pair_bits;
     c->host_info = t->d_host_info;
     c->nhosts = t->nhosts;
+    c->row_lo = t->tab_row_lo;
+    c->row_hi = t->tab_row_hi;
     if (!t->ws) shd_dev_ws_new(&t->ws); /* (a failure leaves ws NULL: the launch reports -ENOMEM) */
     c->ws = t->ws;
 }

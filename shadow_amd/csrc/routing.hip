@@ -446,7 +446,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
                 const unsigned long long sm = __ballot(nb.x < 0);
                 const int fs = sm ? __builtin_ctzll(sm) : 64;
                 const bool ok = lane < fs;
-                const double cur = ok ? dr[nb.x].x : 0.0; // neighbour distance gathers
+                double cur = ok ? dr[nb.x].x : 0.0; // neighbour distance gathers
                 if (first) {
                     // the removal of the root: the sink's HBM block loads
                     // queue behind the gathers just issued
@@ -454,6 +454,10 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
                     ru = uni_d(ru_l);
                     first = false;
                 }
+                // keeps the gathered values' first use after the sink (else the
+                // compiler hoists the compares above it and waits for the
+                // gathers before sinking, serialising the two round trips)
+                __asm__ volatile("" : "+v"(cur));
                 if (fs < 64 && __builtin_amdgcn_readlane(nb.x, fs) == -2) --to_reach;
                 const double alt = mindist + wr.x;
                 const double rv = ru * wr.y;
@@ -509,11 +513,11 @@ __global__ __launch_bounds__(256) void k_direct_rows(ShdGraphDev g, int row_lo, 
 // lat >= 0 (the pairs touch_all's row-by-row release stores).  Latencies
 // are >= 0 doubles, whose bit patterns order like u64; ~0 = none.  One
 // block per row range; lanes read consecutive entries of a row (coalesced).
-__global__ __launch_bounds__(256) void k_min_upper(const ShdEntry* __restrict__ tab, int A,
+__global__ __launch_bounds__(256) void k_min_upper(const ShdEntry* __restrict__ rows, int A, int row_lo, int row_hi,
                                                    unsigned long long* __restrict__ out) {
     unsigned long long m = ~0ull;
-    for (int i = blockIdx.x; i < A; i += gridDim.x) {
-        const ShdEntry* row = tab + (size_t)i * (size_t)A;
+    for (int i = row_lo + (int)blockIdx.x; i < row_hi; i += gridDim.x) {
+        const ShdEntry* row = rows + (size_t)(i - row_lo) * (size_t)A;
         for (int j = i + 1 + threadIdx.x; j < A; j += blockDim.x) {
             const double l = row[j].lat;
             if (l >= 0.0) {
@@ -588,15 +592,16 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
     return rc;
 }
 
-extern "C" int shd_dev_min_upper(const ShdEntry* tab, int A, double* out) {
+extern "C" int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out) {
     *out = -1.0;
-    if (A < 2) return 0;
+    if (A < 2 || row_hi <= row_lo) return 0;
     unsigned long long* d = nullptr;
     int rc = hip_status(hipMalloc((void**)&d, sizeof *d), "hipMalloc min");
     if (rc) return rc;
     unsigned long long h = ~0ull;
     if (!(rc = hip_status(hipMemcpy(d, &h, sizeof h, hipMemcpyHostToDevice), "hipMemcpy min"))) {
-        hipLaunchKernelGGL(k_min_upper, dim3(A < 8192 ? A : 8192), dim3(256), 0, nullptr, tab, A, d);
+        const int nr = row_hi - row_lo;
+        hipLaunchKernelGGL(k_min_upper, dim3(nr < 8192 ? nr : 8192), dim3(256), 0, nullptr, rows, A, row_lo, row_hi, d);
         rc = hip_status(hipGetLastError(), "k_min_upper launch");
         if (!rc) rc = hip_status(hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost), "hipMemcpy min");
     }

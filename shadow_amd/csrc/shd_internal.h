@@ -89,8 +89,9 @@ int shd_dev_sync(void);
  * use_sp = 1: igraph-exact Dijkstra per source slot + self path (R-7, R-9);
  * use_sp = 0: direct edge per pair (R-10).  Synchronous. */
 int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab);
-/* min latency over the entries (i, j), i < j, lat >= 0 of an A x A table; -1 if none */
-int shd_dev_min_upper(const ShdEntry* tab, int A, double* out);
+/* min latency over the entries (i, j), i < j, lat >= 0, of rows [row_lo,
+ * row_hi) of an A-column table (rows: row i at rows + (i - row_lo) * A); -1 if none */
+int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out);
 
 /* Packet round on device arrays (see shd_round_process_device). */
 typedef struct {
@@ -102,6 +103,7 @@ typedef struct {
     const uint32_t* host_info; /* nhosts x {slot (UINT32_MAX = unattached), touch[slot]}: one 8-B gather */
     uint32_t nhosts;
     void* ws;                  /* the topology's device workspace (shd_dev_ws_new) */
+    int row_lo, row_hi;        /* rows of tab present (a shard: others are never read) */
 } ShdPktCtx;
 
 /* Round-pipeline workspace (grow-only device buffers + the event that marks
@@ -113,6 +115,15 @@ int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uin
                          uint8_t* d_status, uint64_t* d_counters, void* stream);
 int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                        uint32_t* d_dst_offsets, void* stream);
+
+/* multi-GPU rounds (xchg.hip) */
+int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
+                          const uint32_t* row_bounds, ShdPkt* d_scratch, ShdPkt* d_recv, size_t recv_cap,
+                          size_t* n_recv, void* stream);
+int shd_dev_event_cuts(const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world, uint64_t* send_elems,
+                       void* stream);
+int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
+                            void* d_recv, size_t recv_cap, size_t* n_recv, void* stream);
 
 #ifdef __cplusplus
 }

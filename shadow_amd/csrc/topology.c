@@ -792,6 +792,8 @@ static void note_released(ShdTopology* t, double lat) {
 static ShdEntry ent(const ShdTopology* t, size_t k) {
     if (t->h_tab) return t->h_tab[k];
     ShdEntry e = {-1.0, 0.0};
+    const size_t row = k / (size_t)t->A;
+    if (row < (size_t)t->tab_row_lo || row >= (size_t)t->tab_row_hi) return e; /* another rank's row */
     if (shd_dev_init(t->device) || shd_dev_d2h(&e, t->d_tab + k, sizeof e)) e.lat = -1.0;
     return e;
 }
@@ -1027,13 +1029,15 @@ int shd_topology_adopt_table_device_resident(ShdTopology* t, void* d_table) {
     if (!rc && !t->use_sp) rc = shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
     if (!rc && t->next_touch) rc = shd_fail(-EBUSY, "rows were already released");
     double mn = -1.0;
-    if (!rc) rc = shd_dev_min_upper((const ShdEntry*)d_table, A, &mn);
+    if (!rc) rc = shd_dev_min_upper((const ShdEntry*)d_table, A, 0, A, &mn);
     if (!rc) {
         free(t->h_tab);
         t->h_tab = NULL;
         if (t->d_tab && t->d_tab_owned && t->d_tab != (ShdEntry*)d_table) shd_dev_free(t->d_tab);
         t->d_tab = (ShdEntry*)d_table;
         t->d_tab_owned = 0;
+        t->tab_row_lo = 0;
+        t->tab_row_hi = A;
         t->built = 1;
         pthread_mutex_lock(&t->touch_mu);
         for (int i = 0; i < A; i++) __atomic_store_n(&t->touch[i], t->next_touch++, __ATOMIC_RELEASE);
@@ -1073,4 +1077,50 @@ int shd_topology_touch_order(ShdTopology* t, uint32_t* seq, uint8_t* self, int c
         if (self) self[i] = __atomic_load_n(&t->self_released[i], __ATOMIC_ACQUIRE);
     }
     return 0;
+}
+
+/* Row shard of a device-resident table (C4 at N > 1): d_rows holds rows
+ * [row_lo, row_hi); every row counts as released in slot order (as
+ * adopt_table_device_resident), the min-jump feed gets the whole table's
+ * minimum from the caller (a min over ranks of shd_topology_shard_min_latency). */
+int shd_topology_shard_min_latency(ShdTopology* t, const void* d_rows, int row_lo, int row_hi, double* min_ms) {
+    int A = 0;
+    if (!t || !d_rows || !min_ms) return -EINVAL;
+    int rc = shd_topology_slot_count(t, &A);
+    if (rc) return rc;
+    if (row_lo < 0 || row_hi > A || row_lo > row_hi) return shd_fail(-EINVAL, "row range out of bounds");
+    if ((rc = shd_dev_init(t->device))) return rc;
+    return shd_dev_min_upper((const ShdEntry*)d_rows, A, row_lo, row_hi, min_ms);
+}
+
+int shd_topology_adopt_table_shard_device_resident(ShdTopology* t, void* d_rows, int row_lo, int row_hi,
+                                                   double global_min_ms) {
+    int A = 0;
+    if (!t || !d_rows) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
+    int rc = shd_topology_slot_count(t, &A);
+    if (!rc && (row_lo < 0 || row_hi > A || row_lo > row_hi)) rc = shd_fail(-EINVAL, "row range out of bounds");
+    if (!rc && !t->use_sp) rc = shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
+    if (!rc && t->next_touch) rc = shd_fail(-EBUSY, "rows were already released");
+    double mn = global_min_ms;
+    if (!rc && mn < 0) rc = shd_dev_min_upper((const ShdEntry*)d_rows, A, row_lo, row_hi, &mn);
+    if (!rc) {
+        free(t->h_tab);
+        t->h_tab = NULL;
+        if (t->d_tab && t->d_tab_owned) shd_dev_free(t->d_tab);
+        /* row i lives at d_rows + (i - row_lo) * A: keep the base of row 0 */
+        t->d_tab = (ShdEntry*)d_rows - (ptrdiff_t)row_lo * (ptrdiff_t)A;
+        t->d_tab_owned = 0;
+        t->tab_row_lo = row_lo;
+        t->tab_row_hi = row_hi;
+        t->built = 1;
+        pthread_mutex_lock(&t->touch_mu);
+        for (int i = 0; i < A; i++) __atomic_store_n(&t->touch[i], t->next_touch++, __ATOMIC_RELEASE);
+        __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
+        pthread_mutex_unlock(&t->touch_mu);
+        __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE);
+        if (mn >= 0) note_released(t, mn);
+    }
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
 }

@@ -71,6 +71,7 @@ struct ShdTopology {
     int32_t* slot_vertex;
     int32_t* vertex_slot;
     ShdEntry* h_tab; /* host mirror of the device table */
+    int tab_row_lo, tab_row_hi; /* rows present in d_tab (a rank's shard, else 0..A) */
     int built, prepared;
     int d_tab_owned;
 

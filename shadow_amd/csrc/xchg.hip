@@ -1,0 +1,320 @@
+// xchg.hip -- multi-GPU rounds: the destination-owner event
+// exchange, the owner-row routing of records for row-sharded tables, and an
+// RCCL transport (ncclSend / ncclRecv over xGMI).  The reference has no
+// multi-process or multi-GPU path (one process, pthread workers,
+// core/worker.c:132-185); the exchange is what replaces the direct push into
+// another host's locked queue (scheduler_policy_host_single.c:198-219) when
+// the destination host lives on another GPU.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cerrno>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "shd_internal.h"
+
+namespace {
+
+constexpr int kMaxWorld = 64;
+constexpr int kRouteBlock = 256;
+
+int hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+struct RouteArgs {
+    uint32_t bounds[kMaxWorld + 1]; // row (slot) bounds per rank
+    int world;
+};
+
+// Rank holding the row that answers record p: the slot of the endpoint
+// touched first (topology.c:1189-1215; touch order = host_info[.].y).
+__device__ __forceinline__ int route_rank(const ShdPkt& p, const uint2* __restrict__ host_info, uint32_t nhosts,
+                                          const RouteArgs& ra) {
+    if (p.src_host >= nhosts || p.dst_host >= nhosts) return 0;
+    const uint2 hs = host_info[p.src_host], hd = host_info[p.dst_host];
+    if (hs.x == ~0u || hd.x == ~0u) return 0; // unattached: rank 0 reports it undelivered
+    const uint32_t owner = (hs.x != hd.x && hd.y < hs.y) ? hd.x : hs.x;
+    int r = 0;
+    while (r + 1 < ra.world && owner >= ra.bounds[r + 1]) r++;
+    return r;
+}
+
+// Two passes over the same chunks: pass 0 counts records per (rank, block),
+// pass 1 writes each record to its rank's region at off[rank * nblocks +
+// block] + its stable position (ballot prefix per tile), so records keep
+// their order within each destination rank.
+template <int kPass>
+__global__ __launch_bounds__(kRouteBlock) void k_route(const ShdPkt* __restrict__ recs, size_t n,
+                                                       const uint2* __restrict__ host_info, uint32_t nhosts,
+                                                       RouteArgs ra, size_t chunk, uint32_t* __restrict__ cnt,
+                                                       const uint32_t* __restrict__ off, ShdPkt* __restrict__ out) {
+    __shared__ uint32_t wsum[kRouteBlock / 64][kMaxWorld];
+    __shared__ uint32_t base[kMaxWorld];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t nb = gridDim.x;
+    for (int r = threadIdx.x; r < ra.world; r += kRouteBlock) base[r] = kPass ? off[(size_t)r * nb + blockIdx.x] : 0u;
+    __syncthreads();
+    const size_t beg = (size_t)blockIdx.x * chunk;
+    const size_t end = beg + chunk < n ? beg + chunk : n;
+    for (size_t t0 = beg; t0 < end; t0 += kRouteBlock) {
+        const size_t i = t0 + threadIdx.x;
+        ShdPkt p;
+        int r = -1;
+        if (i < end) {
+            p = recs[i];
+            r = route_rank(p, host_info, nhosts, ra);
+        }
+        uint32_t prefix = 0;
+        for (int rr = 0; rr < ra.world; rr++) {
+            const unsigned long long m = __ballot(r == rr);
+            if (r == rr) prefix = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (lane == 0) wsum[w][rr] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        if (r >= 0 && kPass) {
+            uint32_t pos = base[r] + prefix;
+            for (int k = 0; k < w; k++) pos += wsum[k][r];
+            out[pos] = p;
+        }
+        __syncthreads();
+        for (int rr = threadIdx.x; rr < ra.world; rr += kRouteBlock) {
+            uint32_t s = 0;
+            for (int k = 0; k < kRouteBlock / 64; k++) s += wsum[k][rr];
+            base[rr] += s;
+        }
+        __syncthreads();
+    }
+    if (!kPass)
+        for (int r = threadIdx.x; r < ra.world; r += kRouteBlock) cnt[(size_t)r * nb + blockIdx.x] = base[r];
+}
+
+// exclusive scan of m counts (one block; m <= world * nblocks, small)
+__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t* __restrict__ in, uint32_t m,
+                                                     uint32_t* __restrict__ out) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (m + 1023) / 1024;
+    const uint32_t b = threadIdx.x * per;
+    uint32_t s = 0;
+    for (uint32_t k = 0; k < per && b + k < m; k++) s += in[b + k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < 1024; k++) {
+            const uint32_t v = part[k];
+            part[k] = acc;
+            acc += v;
+        }
+        out[m] = acc;
+    }
+    __syncthreads();
+    uint32_t acc = part[threadIdx.x];
+    for (uint32_t k = 0; k < per && b + k < m; k++) {
+        out[b + k] = acc;
+        acc += in[b + k];
+    }
+}
+
+// offsets[bounds[r]] for r = 0..world (the per-rank cuts of a CSR array)
+__global__ void k_cuts(const uint32_t* __restrict__ offsets, RouteArgs ra, uint32_t* __restrict__ cuts) {
+    const int r = threadIdx.x;
+    if (r <= ra.world) cuts[r] = offsets[ra.bounds[r]];
+}
+
+int make_args(const uint32_t* bounds, int world, RouteArgs* ra) {
+    if (world < 1 || world > kMaxWorld) return shd_fail(-EINVAL, "world %d outside 1..%d", world, kMaxWorld);
+    ra->world = world;
+    for (int r = 0; r <= world; r++) {
+        ra->bounds[r] = bounds[r];
+        if (r && bounds[r] < bounds[r - 1]) return shd_fail(-EINVAL, "bounds not ascending");
+    }
+    return 0;
+}
+
+// all-to-all of per-peer element counts, then of the blocks themselves
+int exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
+                    void* d_recv, size_t recv_cap, size_t* n_recv, hipStream_t s) {
+    const int W = x->world;
+    std::vector<uint64_t> recv_elems(W), sb(W), rb(W);
+    int rc = x->alltoall_u64(x->user, send_elems, recv_elems.data());
+    if (rc) return rc < 0 ? rc : -EIO;
+    uint64_t total = 0;
+    for (int r = 0; r < W; r++) {
+        total += recv_elems[r];
+        sb[r] = send_elems[r] * elem_bytes;
+        rb[r] = recv_elems[r] * elem_bytes;
+    }
+    if (total > recv_cap) return shd_fail(-ENOSPC, "receive %llu elements > capacity %zu", (unsigned long long)total, recv_cap);
+    rc = x->alltoallv(x->user, d_send, sb.data(), d_recv, rb.data(), (void*)s);
+    if (rc) return rc < 0 ? rc : -EIO;
+    *n_recv = (size_t)total;
+    return 0;
+}
+
+// ---- RCCL transport ----
+struct Rccl {
+    ShdTransport x;
+    ncclComm_t comm;
+    int device;
+    uint64_t* d_u64; // 2 x world staging for the count exchange
+};
+
+int nccl_status(ncclResult_t r, const char* what) {
+    return r == ncclSuccess ? 0 : shd_fail(-EIO, "%s: %s", what, ncclGetErrorString(r));
+}
+
+int rccl_alltoall_u64(void* user, const uint64_t* send, uint64_t* recv) {
+    Rccl* t = static_cast<Rccl*>(user);
+    const int W = t->x.world;
+    int rc = hip_status(hipMemcpy(t->d_u64, send, 8 * (size_t)W, hipMemcpyHostToDevice), "hipMemcpy counts");
+    if (rc) return rc;
+    if ((rc = nccl_status(ncclGroupStart(), "ncclGroupStart"))) return rc;
+    for (int r = 0; r < W; r++) {
+        if ((rc = nccl_status(ncclSend(t->d_u64 + r, 1, ncclUint64, r, t->comm, nullptr), "ncclSend")) ||
+            (rc = nccl_status(ncclRecv(t->d_u64 + W + r, 1, ncclUint64, r, t->comm, nullptr), "ncclRecv"))) {
+            (void)ncclGroupEnd();
+            return rc;
+        }
+    }
+    if ((rc = nccl_status(ncclGroupEnd(), "ncclGroupEnd"))) return rc;
+    return hip_status(hipMemcpy(recv, t->d_u64 + W, 8 * (size_t)W, hipMemcpyDeviceToHost), "hipMemcpy counts");
+}
+
+int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
+                   const uint64_t* recv_bytes, void* stream) {
+    Rccl* t = static_cast<Rccl*>(user);
+    const int W = t->x.world;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = nccl_status(ncclGroupStart(), "ncclGroupStart");
+    if (rc) return rc;
+    uint64_t so = 0, ro = 0;
+    for (int r = 0; r < W; r++) {
+        if (send_bytes[r] &&
+            (rc = nccl_status(ncclSend((const char*)d_send + so, send_bytes[r], ncclChar, r, t->comm, s), "ncclSend")))
+            break;
+        if (recv_bytes[r] &&
+            (rc = nccl_status(ncclRecv((char*)d_recv + ro, recv_bytes[r], ncclChar, r, t->comm, s), "ncclRecv")))
+            break;
+        so += send_bytes[r];
+        ro += recv_bytes[r];
+    }
+    const int rc2 = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+    return rc ? rc : rc2;
+}
+
+} // namespace
+
+extern "C" int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
+                                     const uint32_t* row_bounds, ShdPkt* d_part, ShdPkt* d_recv, size_t recv_cap,
+                                     size_t* n_recv, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    RouteArgs ra;
+    int rc = make_args(row_bounds, x->world, &ra);
+    if (rc) return rc;
+    const int W = x->world;
+    size_t nblocks = n ? (n + 65535) / 65536 : 1;
+    if (nblocks > 1024) nblocks = 1024;
+    const size_t chunk = n ? (n + nblocks - 1) / nblocks : 1;
+    const size_t m = (size_t)W * nblocks;
+    uint32_t *d_cnt = nullptr, *d_off = nullptr;
+    std::vector<uint32_t> off(m + 1);
+    std::vector<uint64_t> send(W);
+    if ((rc = hip_status(hipMalloc((void**)&d_cnt, 4 * m), "hipMalloc route")) ||
+        (rc = hip_status(hipMalloc((void**)&d_off, 4 * (m + 1)), "hipMalloc route")))
+        goto done;
+    {
+        const uint2* hi = reinterpret_cast<const uint2*>(c->host_info);
+        hipLaunchKernelGGL(k_route<0>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
+                           d_cnt, nullptr, nullptr);
+        hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, d_cnt, (uint32_t)m, d_off);
+        hipLaunchKernelGGL(k_route<1>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
+                           nullptr, d_off, d_part);
+        if ((rc = hip_status(hipGetLastError(), "k_route launch"))) goto done;
+        if ((rc = hip_status(hipMemcpyAsync(off.data(), d_off, 4 * (m + 1), hipMemcpyDeviceToHost, s), "route D2H")) ||
+            (rc = hip_status(hipStreamSynchronize(s), "route sync")))
+            goto done;
+        for (int r = 0; r < W; r++) send[r] = off[(size_t)(r + 1) * nblocks] - off[(size_t)r * nblocks];
+        rc = exchange_blocks(x, d_part, send.data(), sizeof(ShdPkt), d_recv, recv_cap, n_recv, s);
+        if (!rc) rc = hip_status(hipStreamSynchronize(s), "route exchange");
+    }
+done:
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_off);
+    return rc;
+}
+
+extern "C" int shd_dev_event_cuts(const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world,
+                                  uint64_t* send_elems, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    RouteArgs ra;
+    int rc = make_args(host_bounds, world, &ra);
+    if (rc) return rc;
+    uint32_t* d_cuts = nullptr;
+    uint32_t cuts[kMaxWorld + 1];
+    if ((rc = hip_status(hipMalloc((void**)&d_cuts, 4 * (kMaxWorld + 1)), "hipMalloc cuts"))) return rc;
+    hipLaunchKernelGGL(k_cuts, dim3(1), dim3(kMaxWorld + 1), 0, s, d_dst_offsets, ra, d_cuts);
+    rc = hip_status(hipMemcpyAsync(cuts, d_cuts, 4 * (size_t)(world + 1), hipMemcpyDeviceToHost, s), "cuts D2H");
+    if (!rc) rc = hip_status(hipStreamSynchronize(s), "cuts sync");
+    (void)hipFree(d_cuts);
+    if (!rc)
+        for (int r = 0; r < world; r++) send_elems[r] = cuts[r + 1] - cuts[r];
+    return rc;
+}
+
+extern "C" int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems,
+                                       size_t elem_bytes, void* d_recv, size_t recv_cap, size_t* n_recv,
+                                       void* stream) {
+    int rc = exchange_blocks(x, d_send, send_elems, elem_bytes, d_recv, recv_cap, n_recv, (hipStream_t)stream);
+    if (!rc) rc = hip_status(hipStreamSynchronize((hipStream_t)stream), "exchange");
+    return rc;
+}
+
+extern "C" int shd_transport_rccl_unique_id(void* id128) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    ncclUniqueId id;
+    int rc = nccl_status(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    if (!rc) std::memcpy(id128, &id, sizeof id);
+    return rc;
+}
+
+extern "C" int shd_transport_rccl_new(int rank, int world, const void* id128, int device, ShdTransport** out) {
+    if (!out || !id128 || world < 1 || rank < 0 || rank >= world) return shd_fail(-EINVAL, "bad RCCL transport args");
+    *out = nullptr;
+    int rc = shd_dev_init(device);
+    if (rc) return rc;
+    Rccl* t = new (std::nothrow) Rccl();
+    if (!t) return -ENOMEM;
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof id);
+    t->device = device;
+    if ((rc = hip_status(hipMalloc((void**)&t->d_u64, 16 * (size_t)world), "hipMalloc transport")) ||
+        (rc = nccl_status(ncclCommInitRank(&t->comm, world, id, rank), "ncclCommInitRank"))) {
+        (void)hipFree(t->d_u64);
+        delete t;
+        return rc;
+    }
+    t->x.rank = rank;
+    t->x.world = world;
+    t->x.user = t;
+    t->x.alltoall_u64 = rccl_alltoall_u64;
+    t->x.alltoallv = rccl_alltoallv;
+    *out = &t->x;
+    return 0;
+}
+
+extern "C" void shd_transport_rccl_free(ShdTransport* x) {
+    if (!x) return;
+    Rccl* t = static_cast<Rccl*>(x->user);
+    (void)ncclCommDestroy(t->comm);
+    (void)hipFree(t->d_u64);
+    delete t;
+}
+
+extern "C" int shd_memcpy(void* dst, const void* src, size_t bytes) {
+    return bytes ? hip_status(hipMemcpy(dst, src, bytes, hipMemcpyDefault), "hipMemcpy") : 0;
+}

@@ -168,6 +168,42 @@ class Topology:
                                              C.c_void_p(d_out), C.c_void_p(d_offsets), C.c_void_p(d_status),
                                              C.c_void_p(d_counters), C.c_void_p(stream)))
 
+    # -- multi-GPU rounds (shadow_amd.transport) -----------------------------------
+    def exchange(self, xport, d_events: int, d_offsets: int, host_bounds, d_recv: int, recv_cap: int, d_out: int,
+                 d_out_offsets: int, stream: int = 0) -> int:
+        """shd_round_exchange: destination-owner all-to-all + regroup; returns
+        the number of events received (grouped in d_out by owned host)."""
+        hb = (C.c_uint32 * len(host_bounds))(*[int(x) for x in host_bounds])
+        n = C.c_size_t()
+        rc = lib().shd_round_exchange(self._h, xport.handle, C.c_void_p(d_events), C.c_void_p(d_offsets), hb,
+                                      C.c_void_p(d_recv), recv_cap, C.c_void_p(d_out), C.c_void_p(d_out_offsets),
+                                      C.byref(n), C.c_void_p(stream))
+        if getattr(xport, "error", None) is not None:
+            raise xport.error
+        check(rc)
+        return n.value
+
+    def route_records(self, xport, d_recs: int, n: int, row_bounds, d_scratch: int, d_recv: int, recv_cap: int,
+                      stream: int = 0) -> int:
+        """shd_round_route_records: each record to the rank holding its answering row."""
+        rb = (C.c_uint32 * len(row_bounds))(*[int(x) for x in row_bounds])
+        nr = C.c_size_t()
+        rc = lib().shd_round_route_records(self._h, xport.handle, C.c_void_p(d_recs), n, rb, C.c_void_p(d_scratch),
+                                           C.c_void_p(d_recv), recv_cap, C.byref(nr), C.c_void_p(stream))
+        if getattr(xport, "error", None) is not None:
+            raise xport.error
+        check(rc)
+        return nr.value
+
+    def shard_min_latency(self, d_rows: int, row_lo: int, row_hi: int) -> float:
+        out = C.c_double()
+        check(lib().shd_topology_shard_min_latency(self._h, C.c_void_p(d_rows), row_lo, row_hi, C.byref(out)))
+        return out.value
+
+    def adopt_table_shard_device_resident(self, d_rows: int, row_lo: int, row_hi: int, global_min_ms: float = -1.0):
+        check(lib().shd_topology_adopt_table_shard_device_resident(self._h, C.c_void_p(d_rows), row_lo, row_hi,
+                                                                   global_min_ms))
+
     def deliv_sort_device(self, d_in: int, n: int, host_lo: int, host_hi: int, d_out: int, d_offsets: int,
                           stream: int = 0):
         check(lib().shd_deliv_sort_device(self._h, C.c_void_p(d_in), n, host_lo, host_hi, C.c_void_p(d_out),

@@ -1,0 +1,117 @@
+"""Transports for multi-GPU rounds (include/shdnet.h ``ShdTransport``).
+
+``shd_round_exchange`` / ``shd_round_route_records`` take the two collectives
+they need from the caller.  Shadow's C host plugs in RCCL
+(``RcclTransport``: ncclSend/ncclRecv over xGMI, inside libshdnet); these
+Python transports wrap ``torch.distributed`` for tests and the benchmark:
+``TorchTransport`` runs the all-to-all(v) on device tensors with the
+"nccl" backend (RCCL) or bounces the blocks through host memory with "gloo".
+Device buffers handed to the C calls must be registered (``register``) so
+that the callbacks can find the tensors behind the raw pointers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+import torch.distributed as dist
+
+from ._lib import check, lib
+
+A2A_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
+A2AV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p, C.POINTER(C.c_uint64),
+                      C.c_void_p)
+
+
+class ShdTransport(C.Structure):
+    _fields_ = [("rank", C.c_int), ("world", C.c_int), ("user", C.c_void_p), ("alltoall_u64", A2A_FN),
+                ("alltoallv", A2AV_FN)]
+
+
+class TorchTransport:
+    def __init__(self, group=None, device=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.cdev = self.device if self.backend == "nccl" else torch.device("cpu")
+        self._bufs: dict[int, torch.Tensor] = {}
+        self.error: BaseException | None = None
+        self._a2a = A2A_FN(self._alltoall_u64)
+        self._a2av = A2AV_FN(self._alltoallv)
+        self.struct = ShdTransport(self.rank, self.world, None, self._a2a, self._a2av)
+
+    def register(self, *tensors: torch.Tensor):
+        """Device buffers the C calls will pass to alltoallv (by base pointer)."""
+        for t in tensors:
+            self._bufs[t.data_ptr()] = t.view(torch.uint8).view(-1)
+
+    def _buf(self, ptr: int) -> torch.Tensor:
+        if ptr not in self._bufs:
+            raise KeyError(f"device buffer {ptr:#x} was not registered with the transport")
+        return self._bufs[ptr]
+
+    def _alltoall_u64(self, _user, send, recv):
+        try:
+            s = torch.tensor([send[r] for r in range(self.world)], dtype=torch.int64, device=self.cdev)
+            out = torch.empty_like(s)
+            dist.all_to_all_single(out, s, group=self.group)
+            for r, v in enumerate(out.cpu().tolist()):
+                recv[r] = v
+            return 0
+        except BaseException as e:  # never unwind through the C caller
+            self.error = e
+            return -5
+
+    def _alltoallv(self, _user, d_send, send_bytes, d_recv, recv_bytes, _stream):
+        try:
+            sb = [int(send_bytes[r]) for r in range(self.world)]
+            rb = [int(recv_bytes[r]) for r in range(self.world)]
+            src = self._buf(d_send)[:sum(sb)]
+            dst = self._buf(d_recv)[:sum(rb)]
+            if self.backend == "nccl":
+                dist.all_to_all_single(dst, src, rb, sb, group=self.group)
+            else:
+                out = torch.empty(sum(rb), dtype=torch.uint8)
+                dist.all_to_all_single(out, src.cpu(), rb, sb, group=self.group)
+                dst.copy_(out.to(dst.device))
+            torch.cuda.synchronize(self.device)
+            return 0
+        except BaseException as e:
+            self.error = e
+            return -5
+
+    @property
+    def handle(self):
+        return C.byref(self.struct)
+
+
+class RcclTransport:
+    """libshdnet's native RCCL transport (one communicator over the ranks of
+    ``torch.distributed``'s default group, whose only role is to hand rank
+    0's unique id to the others)."""
+
+    def __init__(self, device: int):
+        rank, world = dist.get_rank(), dist.get_world_size()
+        uid = (C.c_char * 128)()
+        if rank == 0:
+            check(lib().shd_transport_rccl_unique_id(uid))
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)
+        C.memmove(uid, box[0], 128)
+        self._p = C.c_void_p()
+        check(lib().shd_transport_rccl_new(rank, world, uid, device, C.byref(self._p)))
+        self.rank, self.world = rank, world
+
+    def register(self, *tensors):  # the native transport takes raw device pointers
+        pass
+
+    @property
+    def handle(self):
+        return self._p
+
+    def close(self):
+        if self._p:
+            lib().shd_transport_rccl_free(self._p)
+            self._p = C.c_void_p()

@@ -56,12 +56,13 @@ int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi,
     return 0;
 }
 
-int shd_dev_min_upper(const ShdEntry* tab, int A, double* out) {
+int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out) {
     *out = -1.0;
-    for (int i = 0; i < A; i++)
-        for (int j = i + 1; j < A; j++)
-            if (tab[(size_t)i * A + j].lat >= 0 && (*out < 0 || tab[(size_t)i * A + j].lat < *out))
-                *out = tab[(size_t)i * A + j].lat;
+    for (int i = row_lo; i < row_hi; i++)
+        for (int j = i + 1; j < A; j++) {
+            const double l = rows[(size_t)(i - row_lo) * A + j].lat;
+            if (l >= 0 && (*out < 0 || l < *out)) *out = l;
+        }
     return 0;
 }
 
@@ -80,4 +81,18 @@ int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uin
 int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                        uint32_t* d_dst_offsets, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no packet kernels");
+}
+
+int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
+                          const uint32_t* row_bounds, ShdPkt* d_scratch, ShdPkt* d_recv, size_t recv_cap,
+                          size_t* n_recv, void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no exchange");
+}
+int shd_dev_event_cuts(const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world, uint64_t* send_elems,
+                       void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no exchange");
+}
+int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
+                            void* d_recv, size_t recv_cap, size_t* n_recv, void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no exchange");
 }

@@ -71,6 +71,9 @@ lib.orc_topology_preload_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_v
 lib.orc_round.restype = C.c_size_t
 lib.orc_round.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
                           C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, u64p]
+lib.orc_round_mt.restype = C.c_size_t
+lib.orc_round_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
+                             C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p, u64p]
 lib.orc_pq_order.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
 
 
@@ -192,6 +195,22 @@ class OracleTopology:
         k = lib.orc_round(self.h, host_ips.ctypes.data, len(host_ips), barrier, end_time, bootstrap_end,
                           pkts.ctypes.data, n, out.ctypes.data, status.ctypes.data, C.byref(mt))
         return out[:k], status, mt.value
+
+
+def round_mt(orc, host_ips, pkts, barrier, end_time, threads, bootstrap_end=0):
+    """orc_round_mt: the hand-off on `threads` worker threads (rows must be preloaded)."""
+    from shadow_amd.synth import DELIV_DTYPE
+    host_ips = np.ascontiguousarray(host_ips, dtype=np.uint32)
+    pkts = np.ascontiguousarray(pkts)
+    n = len(pkts)
+    out = np.zeros(n, dtype=DELIV_DTYPE)
+    status = np.zeros(n, dtype=np.uint8)
+    mt = C.c_uint64(0)
+    k = lib.orc_round_mt(orc.h, host_ips.ctypes.data, len(host_ips), barrier, end_time, bootstrap_end,
+                         pkts.ctypes.data, n, threads, out.ctypes.data, status.ctypes.data, C.byref(mt))
+    if k == C.c_size_t(-1).value:
+        raise ValueError("a packet's path is not cached: preload the rows first")
+    return out[:k], status, mt.value
 
 
 def parse_time_ns(s):

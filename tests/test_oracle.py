@@ -200,3 +200,22 @@ def test_preload_fast_path_equals_store_rule():
         for d in ips[::5]:
             assert a.latency(int(s), int(d)) == b.latency(int(s), int(d))
             assert a.reliability(int(s), int(d)) == b.reliability(int(s), int(d))
+
+
+def test_round_mt_equals_serial_round():
+    """The 16-thread CPU baseline (sharded by source, per-destination queue
+    mutexes) produces exactly the serial oracle's round."""
+    gml = synth.sparse_graph_gml(120, 0x5EED0098, ns_variant=True)
+    a, b = O.OracleTopology(gml), O.OracleTopology(gml)
+    ips, st, verts = scenario.register_hosts(a, 400, 1)
+    scenario.register_hosts(b, 400, 1)
+    sv = np.unique(verts).astype(np.int32)
+    lat, rel = a.rows_parallel(sv, sv, 4)
+    a.preload(sv, lat, rel)
+    b.preload(sv, lat, rel)
+    pk = synth.packet_batch(50000, 400, 0x5EED0097, 100_000_000, 10_000_000, st)
+    out, status, mt = a.round(ips, pk, 110_000_000, 10**15)
+    out2, status2, mt2 = O.round_mt(b, ips, pk, 110_000_000, 10**15, threads=7)
+    assert np.array_equal(status, status2) and mt == mt2 and np.array_equal(out, out2)
+    for s, d in zip(ips[::37], ips[::53]):
+        assert a.packet_count(int(s), int(d)) == b.packet_count(int(s), int(d))
