@@ -116,8 +116,6 @@ def main():
 
     from shadow_amd import Topology, _lib, scenario, synth
 
-    from shadow_amd import exchange
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -190,26 +188,31 @@ def main():
     d_off = torch.empty(H + 1, dtype=torch.int32, device=dev)
     d_status = torch.empty(P, dtype=torch.uint8, device=dev)
     d_cnt = torch.empty(2, dtype=torch.int64, device=dev)
-    own_lo = exchange.owner_bounds(H, world)
+    # destination hosts owned by rank r: [own_lo[r], own_lo[r+1])
+    own_lo = [r * H // world for r in range(world + 1)]
     my_lo, my_hi = own_lo[rank], own_lo[rank + 1]
-    d_final = torch.empty(P * 32 * (2 if world > 1 else 1), dtype=torch.uint8, device=dev)
-    d_final_off = torch.empty(my_hi - my_lo + 1, dtype=torch.int32, device=dev)
     sptr = stream.cuda_stream
     last = {}
+    xport = None
+    if world > 1:
+        # the exchange runs inside libshdnet (shd_round_exchange); the
+        # collectives come from RCCL: torch's communicator by default, the
+        # library's own with SHD_XPORT=rccl (gloo only in CPU rehearsals)
+        d_recv = torch.empty(2 * P * 32, dtype=torch.uint8, device=dev)
+        d_final = torch.empty(2 * P * 32, dtype=torch.uint8, device=dev)
+        d_final_off = torch.empty(my_hi - my_lo + 1, dtype=torch.int32, device=dev)
+        from shadow_amd.transport import RcclTransport, TorchTransport
+        xport = RcclTransport(local) if os.environ.get("SHD_XPORT") == "rccl" else TorchTransport(device=dev)
+        xport.register(d_out, d_recv)
 
     def step():
         top.process_device(d_recs.data_ptr(), P, barrier_t, end_t, 0, d_out.data_ptr(), d_off.data_ptr(),
                            d_status.data_ptr(), d_cnt.data_ptr(), sptr)
         if world == 1:
             return
-        # destination-owner exchange (RCCL all-to-all over xGMI), then regroup
-        if cdev == dev:
-            rbuf, nrecv, _ = exchange.exchange_events(d_out, d_off, own_lo)
-        else:
-            h, n, _ = exchange.exchange_events(d_out.cpu(), d_off.cpu(), own_lo)
-            rbuf, nrecv = h.to(dev), n
-        top.deliv_sort_device(rbuf.data_ptr(), nrecv, my_lo, my_hi, d_final.data_ptr(), d_final_off.data_ptr(), sptr)
-        last["nrecv"] = nrecv
+        # destination-owner exchange (all-to-all over xGMI), then regroup
+        last["nrecv"] = top.exchange(xport, d_out.data_ptr(), d_off.data_ptr(), own_lo, d_recv.data_ptr(), 2 * P,
+                                     d_final.data_ptr(), d_final_off.data_ptr(), sptr)
 
     for _ in range(args.warmup):
         step()
@@ -346,41 +349,76 @@ def main():
             "roofline": routing_roofline(A4, tr4, 20.0 * 2 * t4.info()["edges"] + 4 * (args.c4_vertices + 1),
                                          max(h4 - l4, 0), args.c4_vertices, tj.get("routing_slab_c4")),
         }
-        # C4 packet delivery: 1,000 rounds of packets on the full 100k-vertex
-        # table.  At N=1 the table is resident (A4^2 x 16 B = 120 GB of the
-        # 288 GB); at N>1 the rows stay sharded (no full matrix requested), so
-        # the rounds leg runs on one GPU only.
-        if world == 1 and args.c4_rounds > 0:
-            t4.adopt_table_device_resident(shard4.data_ptr())  # no 120 GB host mirror
+        # C4 packet delivery: 1,000 rounds on the 100k-vertex table.  N=1: the
+        # whole table is resident (A4^2 x 16 B = 120 GB of the 288 GB).  N>1:
+        # the rows stay sharded (no full matrix anywhere): each record first
+        # goes to the rank holding its answering row (shd_round_route_records),
+        # is decided there, and its event goes to its destination's owner
+        # (shd_round_exchange).  Weak scaling: c4_packets per rank per round.
+        if args.c4_rounds > 0:
+            if world == 1:
+                t4.adopt_table_device_resident(shard4.data_ptr())  # no 120 GB host mirror
+            else:
+                mn = torch.tensor([t4.shard_min_latency(shard4.data_ptr(), l4, h4) if h4 > l4 else -1.0],
+                                  dtype=torch.float64, device=cdev)
+                mn[mn < 0] = float("inf")
+                dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+                t4.adopt_table_shard_device_resident(shard4.data_ptr(), l4, h4, float(mn.item()))
             P4 = args.c4_packets
-            pk4 = synth.packet_batch(P4, args.c4_hosts, 0x5EED0008, 100_000_000, 10_000_000, states4)
+            H4 = args.c4_hosts
+            s_lo, s_hi = rank * H4 // world, (rank + 1) * H4 // world
+            pk4 = synth.packet_batch(P4, H4, 0x5EED0008 + rank, 100_000_000, 10_000_000, states4,
+                                     hosts_lo=s_lo, hosts_hi=s_hi)
+            cap4 = 2 * P4
             r_recs = torch.from_numpy(pk4.view(np.uint8)).to(dev)
-            r_out = torch.empty(P4 * 32, dtype=torch.uint8, device=dev)
-            r_off = torch.empty(args.c4_hosts + 1, dtype=torch.int32, device=dev)
-            r_status = torch.empty(P4, dtype=torch.uint8, device=dev)
+            r_in = torch.empty(cap4 * 32, dtype=torch.uint8, device=dev) if world > 1 else r_recs
+            r_scr = torch.empty(P4 * 32, dtype=torch.uint8, device=dev) if world > 1 else None
+            r_out = torch.empty(cap4 * 32, dtype=torch.uint8, device=dev)
+            r_off = torch.empty(H4 + 1, dtype=torch.int32, device=dev)
+            r_status = torch.empty(cap4, dtype=torch.uint8, device=dev)
             r_cnt = torch.empty(2, dtype=torch.int64, device=dev)
+            row_bounds = [min(A4, r * per4) for r in range(world + 1)]
+            host_bounds4 = [r * H4 // world for r in range(world + 1)]
+            if world > 1:
+                r_recv = torch.empty(cap4 * 32, dtype=torch.uint8, device=dev)
+                r_fin = torch.empty(cap4 * 32, dtype=torch.uint8, device=dev)
+                r_fin_off = torch.empty(host_bounds4[rank + 1] - host_bounds4[rank] + 1, dtype=torch.int32,
+                                        device=dev)
+                xport.register(r_scr, r_in, r_out, r_recv)
 
             def round4():
-                t4.process_device(r_recs.data_ptr(), P4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
+                n4 = P4
+                if world > 1:
+                    n4 = t4.route_records(xport, r_recs.data_ptr(), P4, row_bounds, r_scr.data_ptr(),
+                                          r_in.data_ptr(), cap4, sptr)
+                t4.process_device(r_in.data_ptr(), n4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
                                   r_status.data_ptr(), r_cnt.data_ptr(), sptr)
+                if world > 1:
+                    t4.exchange(xport, r_out.data_ptr(), r_off.data_ptr(), host_bounds4, r_recv.data_ptr(), cap4,
+                                r_fin.data_ptr(), r_fin_off.data_ptr(), sptr)
 
             for _ in range(3):
                 round4()
             torch.cuda.synchronize(dev)
+            barrier()
             s0 = time.perf_counter()
             for _ in range(args.c4_rounds):
                 round4()
             torch.cuda.synchronize(dev)
-            tp4 = time.perf_counter() - s0
+            barrier()
+            tp4 = max_over_ranks(time.perf_counter() - s0)
             c4 = result["routing"]["c4"]
             c4["rounds"] = {
-                "rounds": args.c4_rounds, "packets_per_round": P4, "seconds": tp4,
-                "packets_per_s": P4 * args.c4_rounds / tp4, "ms_per_round": tp4 / args.c4_rounds * 1e3,
-                "delivered_per_round": int(r_cnt.cpu().numpy().view(np.uint64)[0]),
-                "input": "one synthetic batch (uniform src/dst over the 200k hosts, reserved rand_r pre-states) "
-                         "replayed every round, resident in HBM; full 120 GB table resident",
+                "rounds": args.c4_rounds, "packets_per_round": P4 * world, "seconds": tp4,
+                "packets_per_s": P4 * world * args.c4_rounds / tp4, "ms_per_round": tp4 / args.c4_rounds * 1e3,
+                "delivered_per_round_rank0": int(r_cnt.cpu().numpy().view(np.uint64)[0]),
+                "input": "one synthetic batch per rank (senders = the rank's host shard, uniform destinations over "
+                         "the 200k hosts, reserved rand_r pre-states) replayed every round, resident in HBM; "
+                         + ("full 120 GB table resident" if world == 1 else
+                            "rows sharded by source slot; records routed to their answering row's rank, events "
+                            "exchanged to their destination's owner"),
             }
-            log(f"C4 {args.c4_rounds} rounds x {P4} packets in {tp4:.2f}s")
+            log(f"C4 {args.c4_rounds} rounds x {P4} packets/rank in {tp4:.2f}s")
             del r_recs, r_out, r_status
         del shard4, t4
         torch.cuda.empty_cache()

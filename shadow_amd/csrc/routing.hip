@@ -445,7 +445,8 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
                 // u is an attached vertex (a target of the row)
                 const unsigned long long sm = __ballot(nb.x < 0);
                 const int fs = sm ? __builtin_ctzll(sm) : 64;
-                const bool ok = lane < fs;
+                // (a loop entry -- listed twice per loop -- never improves: no gather)
+                const bool ok = lane < fs && nb.x != u;
                 double cur = ok ? dr[nb.x].x : 0.0; // neighbour distance gathers
                 if (first) {
                     // the removal of the root: the sink's HBM block loads

@@ -76,7 +76,8 @@ class TorchTransport:
                 out = torch.empty(sum(rb), dtype=torch.uint8)
                 dist.all_to_all_single(out, src.cpu(), rb, sb, group=self.group)
                 dst.copy_(out.to(dst.device))
-            torch.cuda.synchronize(self.device)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
             return 0
         except BaseException as e:
             self.error = e
