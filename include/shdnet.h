@@ -87,6 +87,14 @@ int shd_topology_is_routable(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip,
 int shd_topology_increment_path_packet_counter(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip);
 int shd_topology_get_path_packet_count(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip, uint64_t* count);
 
+/* n lookups in one call, in order, with the same side effects as n calls of
+ * topology_getLatency (the pair's row touch, min-jump): lat_ms / rel (either
+ * may be NULL) receive the answers.  For a device-resident table the answers
+ * come from one device gather instead of n 16-byte PCIe reads.  Stops at
+ * the first unattached address (-ENOENT; earlier lookups took effect). */
+int shd_topology_lookup_batch(ShdTopology* top, const uint32_t* src_ips, const uint32_t* dst_ips, size_t n,
+                              double* lat_ms, double* rel);
+
 int shd_topology_set_min_jump_callback(ShdTopology* top, ShdMinJumpFn fn, void* user);
 /* Running min of released latencies (topology.c:48, 1253-1264); 0 if none. */
 int shd_topology_get_min_path_latency(ShdTopology* top, double* min_ms);

@@ -208,6 +208,30 @@ int main() {
                run<Ent8, 4>(r, n, hs, H, (const Ent8*)tab, A, st, 8192),
                run<Ent8, 8>(r, n, hs, H, (const Ent8*)tab, A, st, 8192));
     }
+    // the same A=19870 gathers from tables allocated uncached / fine-grained
+    // (MTYPE UC / CC: no L2 line fill on a miss) -- does a random 16-B read
+    // then fetch less than a 128-B line?
+    {
+        std::vector<int> hhs(H);
+        for (unsigned h = 0; h < H; h++) hhs[h] = (int)(rnd() % maxA);
+        CHECK(hipMemcpy(hs, hhs.data(), H * 4, hipMemcpyHostToDevice));
+        const unsigned flags[] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
+        const char* names[] = {"uncached", "finegrained"};
+        for (int f = 0; f < 2; f++) {
+            void* t2 = nullptr;
+            if (hipExtMallocWithFlags(&t2, maxA * maxA * 16, flags[f]) != hipSuccess) {
+                (void)hipGetLastError();
+                printf("%s: allocation refused\n", names[f]);
+                continue;
+            }
+            CHECK(hipMemset(t2, 0x3f, maxA * maxA * 16));
+            printf("A=%5u %s | 16B entries: b4 %.3f ms  b8 %.3f ms | +32B write b4 %.3f ms\n", (unsigned)maxA, names[f],
+                   run<Ent16, 4>(r, n, hs, H, (const Ent16*)t2, maxA, st, 8192),
+                   run<Ent16, 8>(r, n, hs, H, (const Ent16*)t2, maxA, st, 8192),
+                   runw<Ent16, 4>(r, n, hs, H, (const Ent16*)t2, maxA, o, st, 8192));
+            CHECK(hipFree(t2));
+        }
+    }
     CHECK(hipDeviceSynchronize());
     return 0;
 }

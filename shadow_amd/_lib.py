@@ -43,6 +43,7 @@ PROTOS = {
     "shd_topology_is_routable": (C.c_int, [_P, C.c_uint32, C.c_uint32, _ip]),
     "shd_topology_increment_path_packet_counter": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "shd_topology_get_path_packet_count": (C.c_int, [_P, C.c_uint32, C.c_uint32, _u64p]),
+    "shd_topology_lookup_batch": (C.c_int, [_P, _P, _P, C.c_size_t, _P, _P]),
     "shd_topology_set_min_jump_callback": (C.c_int, [_P, MINJUMP_FN, _P]),
     "shd_topology_get_min_path_latency": (C.c_int, [_P, _dp]),
     "shd_topology_info": (C.c_int, [_P, _ip, _ip, _ip, _ip, _ip]),

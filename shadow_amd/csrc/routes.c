@@ -84,7 +84,7 @@ static int prepare(ShdTopology* t) {
     UPLOAD(t->d_host_info, hs, sizeof(uint32_t) * 2 * (size_t)t->nhosts);
     {
         /* sentinel-terminated lists for the slab kernel (shd_internal.h) */
-        const size_t SM = M + (size_t)t->V + 64;
+        const size_t SM = M + (size_t)t->V + 64 * 16; /* a wave reads up to 16 batches of 64 past a list start */
         int32_t* snb = (int32_t*)calloc(2 * SM, sizeof(int32_t));
         double* swr = (double*)calloc(2 * SM, sizeof(double));
         int32_t* soff = (int32_t*)malloc(sizeof(int32_t) * ((size_t)t->V + 1));

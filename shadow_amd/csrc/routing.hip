@@ -314,17 +314,22 @@ __device__ __forceinline__ void write_row(const ShdGraphDev& g, int row, int src
 }
 
 // ---- LDS kernel: the whole per-row state in LDS (dense graphs, C1) ----
+// The root node carries the start of its vertex's sentinel-terminated list
+// (as in the slab kernel), so a pop's only memory round trip is the edge
+// loads: kRelax batches of 64 entries are issued together (a complete
+// graph's lists are 24 MB: Infinity-Cache round trips); the list's sentinel
+// also says whether u is attached.
 __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int V = g.V, A = g.A;
-    // a complete graph's CSR is 24 MB (Infinity-Cache round trips): 16
-    // batches of 64 incident edges are loaded together per pop
     constexpr int kRelax = 16;
     HNode* top = reinterpret_cast<HNode*>(smem);
     double* dist = reinterpret_cast<double*>(top + V + 1);
     double* rel = dist + V;
     int* pos = reinterpret_cast<int*>(rel + V);
+    const int2* __restrict__ snb = static_cast<const int2*>(g.snb);
+    const double2* __restrict__ swr = static_cast<const double2*>(g.swr);
     for (int row = row_lo + (int)blockIdx.x; row < row_hi; row += (int)gridDim.x) {
         const int src = g.slot_vertex[row];
         for (int v = lane; v < V; v += 64) dist[v] = -1.0;
@@ -332,41 +337,44 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
         Heap<true> h{top, nullptr, pos, 0, lane};
         dist[src] = 0.0;
         rel[src] = 1.0;
-        h.push(src, 0.0, 0);
+        h.push(src, 0.0, g.soff[src]);
         int to_reach = A;
         while (h.n > 0 && to_reach > 0) {
-            // the loads that relaxing u needs (CSR range, its slot) are
-            // issued before the root is removed: their latency overlaps it
             const HNode t = h.top_node();
             const int u = t.v;
             const double mindist = -t.key;
-            const int k0 = g.inc_off[u], k1 = g.inc_off[u + 1];
             const double ru = rel[u];
-            const int uslot = g.vertex_slot[u];
+            // the list's first kRelax batches are loaded before the root is
+            // removed: their latency overlaps the (LDS) sink
+            int b = t.so;
+            int2 nb[kRelax];
+            double2 wr[kRelax];
+#pragma unroll
+            for (int q = 0; q < kRelax; q++) {
+                nb[q] = snb[b + q * 64 + lane];
+                wr[q] = swr[b + q * 64 + lane];
+            }
             h.pop_top(u);
-            if (uslot >= 0) --to_reach;
-            // kRelax batches of 64 incident edges are loaded together (CSR
-            // loads, then the dist reads) before their updates are applied:
-            // an update only writes the dist of its own neighbour, and a
-            // neighbour occurs once per incidence list (parallel edges are
+            // kRelax batches are relaxed together (dist reads, then the
+            // updates): an update only writes the dist of its own neighbour,
+            // and a neighbour occurs once per list (parallel edges are
             // rejected at load; a loop never improves), so the early reads
             // see exactly what one-at-a-time relaxation would.
-            for (int b0 = k0; b0 < k1; b0 += 64 * kRelax) {
-                int v[kRelax];
-                double alt[kRelax], rv[kRelax];
-                bool imp[kRelax], fresh[kRelax];
+            for (;;) {
+                int end = 64 * kRelax; // entries of this group before the sentinel
 #pragma unroll
-                for (int q = 0; q < kRelax; q++) {
-                    const int k = b0 + q * 64 + lane;
-                    const int kk = k < k1 ? k : k1 - 1; // branch-free: clamp, then mask
-                    v[q] = g.inc_nbr[kk];
-                    alt[q] = mindist + g.inc_w[kk];
-                    rv[q] = ru * g.inc_r[kk];
+                for (int q = kRelax - 1; q >= 0; q--) {
+                    const unsigned long long m = __ballot(nb[q].x < 0);
+                    if (m) end = q * 64 + __builtin_ctzll(m);
                 }
+                bool imp[kRelax], fresh[kRelax];
+                double alt[kRelax], rv[kRelax];
 #pragma unroll
                 for (int q = 0; q < kRelax; q++) {
-                    const double cur = dist[v[q]];
-                    const bool ok = b0 + q * 64 + lane < k1;
+                    const bool ok = q * 64 + lane < end && nb[q].x != u;
+                    const double cur = ok ? dist[nb[q].x] : 0.0;
+                    alt[q] = mindist + wr[q].x;
+                    rv[q] = ru * wr[q].y;
                     fresh[q] = ok && cur < 0;
                     imp[q] = ok && (cur < 0 || alt[q] < cur);
                 }
@@ -377,13 +385,28 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
                     while (m) { // igraph's order: incidence order, one edge at a time
                         const int l = __builtin_ctzll(m);
                         m &= m - 1;
-                        const int vv = __builtin_amdgcn_readlane(v[q], l);
+                        const int vv = __builtin_amdgcn_readlane(nb[q].x, l);
                         const double aa = readlane_d(alt[q], l);
                         dist[vv] = aa;
                         rel[vv] = readlane_d(rv[q], l);
-                        if ((fm >> l) & 1ull) h.push(vv, -aa, 0);
-                        else h.raise(vv, -aa, 0);
+                        if ((fm >> l) & 1ull) h.push(vv, -aa, __builtin_amdgcn_readlane(nb[q].y, l));
+                        else h.raise(vv, -aa, __builtin_amdgcn_readlane(nb[q].y, l));
                     }
+                }
+                if (end < 64 * kRelax) {
+                    // the sentinel: -2 when u is an attached vertex
+                    int sv = 0;
+#pragma unroll
+                    for (int q = 0; q < kRelax; q++)
+                        if (end >= q * 64 && end < q * 64 + 64) sv = __builtin_amdgcn_readlane(nb[q].x, end - q * 64);
+                    if (sv == -2) --to_reach;
+                    break;
+                }
+                b += 64 * kRelax; // lists longer than kRelax * 64 entries
+#pragma unroll
+                for (int q = 0; q < kRelax; q++) {
+                    nb[q] = snb[b + q * 64 + lane];
+                    wr[q] = swr[b + q * 64 + lane];
                 }
             }
         }
@@ -399,7 +422,7 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
 // ---- slab kernel: per-wave HBM slab, LDS heap top (sparse graphs, C2/C4) ----
 // Incidence lists are read from the sentinel-terminated copy: list of v at
 // g.soff[v], entries {nbr, soff[nbr]} in g.snb and {w, 1 - loss} in g.swr,
-// closed by {-1 or -2 (v attached), 0}; the arrays are padded by 64 entries,
+// closed by {-1 or -2 (v attached), 0}; the arrays are padded by 64 x 16 entries,
 // so a 64-lane batch never reads past them.
 __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80))) void k_sssp_slab(ShdGraphDev g, int row_lo, int row_hi,
                                                               ShdEntry* __restrict__ tab, char* __restrict__ slab,

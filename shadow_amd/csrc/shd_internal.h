@@ -65,7 +65,7 @@ typedef struct {
     /* sentinel-terminated copy of the incidence lists for the slab kernel:
      * v's list starts at soff[v] = inc_off[v] + v; entries {nbr, soff[nbr]}
      * (snb, int2) and {w_ms, 1 - loss} (swr, double2), closed by {-1, 0}
-     * (-2 when v is attached); both padded by 64 entries */
+     * (-2 when v is attached); both padded by 64 x 16 entries */
     const void* snb;
     const void* swr;
     const int32_t* soff; /* V */
@@ -115,6 +115,9 @@ int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uin
                          uint8_t* d_status, uint64_t* d_counters, void* stream);
 int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                        uint32_t* d_dst_offsets, void* stream);
+
+/* out[i] = tab[idx[i]] for n entries (device pointers; synchronous) */
+int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n, ShdEntry* d_out);
 
 /* multi-GPU rounds (xchg.hip) */
 int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,

@@ -939,6 +939,46 @@ int shd_topology_is_routable(ShdTopology* t, uint32_t s, uint32_t d, int* r) {
     return 0;
 }
 
+int shd_topology_lookup_batch(ShdTopology* t, const uint32_t* sips, const uint32_t* dips, size_t n, double* lat,
+                              double* rel) {
+    if (!t || (n && (!sips || !dips))) return -EINVAL;
+    uint64_t* idx = (uint64_t*)malloc(sizeof(uint64_t) * (n ? n : 1));
+    if (!idx) return -ENOMEM;
+    int rc = 0;
+    size_t done = 0;
+    for (; done < n; done++) { /* the side effects, in call order */
+        int si, di, oi, oj;
+        if ((rc = slots_of(t, sips[done], dips[done], &si, &di)) || (rc = shd_resolve(t, si, di, &oi, &oj))) break;
+        idx[done] = (uint64_t)oi * (uint64_t)t->A + (uint64_t)oj;
+    }
+    if (done && (lat || rel)) {
+        ShdEntry* e = (ShdEntry*)malloc(sizeof(ShdEntry) * done);
+        int rc2 = e ? 0 : -ENOMEM;
+        if (!rc2 && t->h_tab) {
+            for (size_t i = 0; i < done; i++) e[i] = t->h_tab[idx[i]];
+        } else if (!rc2) { /* device-resident: one gather instead of `done` PCIe reads */
+            uint64_t* d_idx = NULL;
+            ShdEntry* d_e = NULL;
+            if (!(rc2 = shd_dev_init(t->device)) && !(rc2 = shd_dev_malloc((void**)&d_idx, 8 * done)) &&
+                !(rc2 = shd_dev_malloc((void**)&d_e, sizeof(ShdEntry) * done)) &&
+                !(rc2 = shd_dev_h2d(d_idx, idx, 8 * done)) &&
+                !(rc2 = shd_dev_gather_entries(t->d_tab, d_idx, done, d_e)))
+                rc2 = shd_dev_d2h(e, d_e, sizeof(ShdEntry) * done);
+            shd_dev_free(d_idx);
+            shd_dev_free(d_e);
+        }
+        if (!rc2)
+            for (size_t i = 0; i < done; i++) {
+                if (lat) lat[i] = e[i].lat;
+                if (rel) rel[i] = e[i].rel;
+            }
+        free(e);
+        if (!rc) rc = rc2;
+    }
+    free(idx);
+    return rc;
+}
+
 /* per stored pair packet counters (path.c:58-61); caller holds pkt_mu */
 int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc) {
     uint64_t key = ((uint64_t)(uint32_t)oi << 32) | (uint32_t)oj;

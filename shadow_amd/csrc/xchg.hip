@@ -315,6 +315,23 @@ extern "C" void shd_transport_rccl_free(ShdTransport* x) {
     delete t;
 }
 
+namespace {
+__global__ __launch_bounds__(256) void k_gather_entries(const ShdEntry* __restrict__ tab,
+                                                        const uint64_t* __restrict__ idx, size_t n,
+                                                        ShdEntry* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = tab[idx[i]];
+}
+} // namespace
+
+extern "C" int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n, ShdEntry* d_out) {
+    if (!n) return 0;
+    const size_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(k_gather_entries, dim3(g < 4096 ? g : 4096), dim3(256), 0, nullptr, tab, d_idx, n, d_out);
+    int rc = hip_status(hipGetLastError(), "k_gather_entries launch");
+    return rc ? rc : hip_status(hipDeviceSynchronize(), "k_gather_entries");
+}
+
 extern "C" int shd_memcpy(void* dst, const void* src, size_t bytes) {
     return bytes ? hip_status(hipMemcpy(dst, src, bytes, hipMemcpyDefault), "hipMemcpy") : 0;
 }

@@ -114,6 +114,16 @@ class Topology:
         check(lib().shd_topology_is_routable(self._h, src_ip, dst_ip, C.byref(out)))
         return bool(out.value)
 
+    def lookup_batch(self, src_ips, dst_ips):
+        """n getLatency lookups in order (side effects included): (lat_ms[n], rel[n])."""
+        s = np.ascontiguousarray(src_ips, dtype=np.uint32)
+        d = np.ascontiguousarray(dst_ips, dtype=np.uint32)
+        lat = np.empty(len(s), dtype=np.float64)
+        rel = np.empty(len(s), dtype=np.float64)
+        check(lib().shd_topology_lookup_batch(self._h, s.ctypes.data, d.ctypes.data, len(s), lat.ctypes.data,
+                                              rel.ctypes.data))
+        return lat, rel
+
     def increment_path_packet_counter(self, src_ip: int, dst_ip: int):
         check(lib().shd_topology_increment_path_packet_counter(self._h, src_ip, dst_ip))
 

@@ -96,3 +96,8 @@ int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uin
                             void* d_recv, size_t recv_cap, size_t* n_recv, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no exchange");
 }
+
+int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n, ShdEntry* d_out) {
+    for (size_t i = 0; i < n; i++) d_out[i] = tab[d_idx[i]];
+    return 0;
+}

@@ -552,3 +552,32 @@ def test_send_time_append_interleaved_with_lookups(name):
     assert np.array_equal(status, ostatus) and mt.value == omt
     assert np.array_equal(out[:nout.value], oout)
     assert top.min_jump_calls == sorted(set(top.min_jump_calls), reverse=True)  # strictly decreasing
+
+
+@pytest.mark.parametrize("resident", [False, True])
+def test_lookup_batch_matches_single_lookups(resident):
+    """shd_topology_lookup_batch: the same answers and side effects as one
+    topology_getLatency call per pair, in order; on a device-resident table
+    they come from one device gather (no per-lookup PCIe read)."""
+    import torch
+    gml, H = GRAPHS["sparse200_dir_ns"]
+    top, orc, ips, _ = make_pair(gml, H)
+    rng = np.random.default_rng(21)
+    a, b = rng.integers(0, H, 3000), rng.integers(0, H, 3000)
+    s, d = ips[a], ips[b]
+    if resident:
+        A = top.slot_count()
+        tab = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
+        top.build_rows_device(0, A, tab.data_ptr())
+        torch.cuda.synchronize()
+        top.adopt_table_device_resident(tab.data_ptr())
+        lat_t, rel_t, sv = top.table() if False else (None, None, None)
+        top2, orc2, _, _ = make_pair(gml, H)
+        top2.touch_all()
+        lat2, rel2, sv2 = top2.table()
+        orc.preload(sv2, lat2, rel2)  # every row released in slot order, as the resident adoption
+    lat, rel = top.lookup_batch(s, d)
+    for i in range(len(s)):
+        assert bits(lat[i]) == bits(orc.latency(int(s[i]), int(d[i])))
+        assert bits(rel[i]) == bits(orc.reliability(int(s[i]), int(d[i])))
+    assert bits(top.min_path_latency()) == bits(orc.min_path_latency())
