@@ -274,6 +274,47 @@ int shd_transport_rccl_unique_id(void* id128);
 int shd_transport_rccl_new(int rank, int world, const void* id128, int device, ShdTransport** out);
 void shd_transport_rccl_free(ShdTransport* xport);
 
+/* ---------------------------------------------------------------------- */
+/* Destination routers: router_enqueue + CoDel           */
+/* ---------------------------------------------------------------------- */
+
+/* One upstream-router queue (routing/router_queue_codel.c:56-78), with its
+ * packets in a caller-provided ring of ShdCodelEntry (ring_cap per router). */
+typedef struct ShdCodelState {
+    uint64_t interval_expire; /* intervalExpireTS */
+    uint64_t next_drop;       /* nextDropTS */
+    uint64_t total_size;      /* bytes queued (payload + header) */
+    uint32_t mode;            /* 0 store, 1 drop (CoDelMode) */
+    uint32_t drop_count, drop_count_last;
+    uint32_t head, len;       /* ring position of the oldest entry, entries queued */
+    uint32_t pad;
+} ShdCodelState;
+typedef struct ShdCodelEntry {
+    uint64_t enqueue_ts;
+    uint32_t pkt, length;
+} ShdCodelEntry;
+/* One queue operation at simulated time `time`: kind 0 = router_enqueue of
+ * packet `pkt` (router.c:103-121; `length` = payload + header bytes), kind 1
+ * = router_dequeue (router.c:123-131, what networkinterface_receivePackets
+ * calls, network_interface.c:448-478). */
+typedef struct ShdCodelOp {
+    uint64_t time;
+    uint32_t kind, pkt, length, pad;
+} ShdCodelOp;
+enum { SHD_CODEL_QUEUED = 0, SHD_CODEL_DEQUEUED = 1, SHD_CODEL_DROPPED = 2 };
+/* Runs every router's operations in order (device pointers): router r's ops
+ * are ops[op_offsets[r] .. op_offsets[r+1]) in time order, its state
+ * states[r], its ring rings[r * ring_cap ...].  deq_out[i] = the packet a
+ * dequeue op returned (UINT32_MAX: none; enqueue ops get their packet id);
+ * fate[pkt] = (op index << 2) | SHD_CODEL_DEQUEUED or SHD_CODEL_DROPPED for
+ * every packet that left its queue (PDS_ROUTER_DEQUEUED / _DROPPED), entries
+ * of packets still queued untouched.  Exactly the reference's CoDel,
+ * control law included (router_queue_codel.c:113-265: target 10 ms, interval
+ * 100 ms, MTU 1500, unbounded queue).  Synchronous; -ENOSPC if a ring would
+ * overflow (that router's remaining ops are not run). */
+int shd_codel_run(uint32_t nrouters, const uint32_t* d_op_offsets, const ShdCodelOp* d_ops, ShdCodelState* d_states,
+                  ShdCodelEntry* d_rings, uint32_t ring_cap, uint32_t* d_deq_out, uint64_t* d_fate, void* stream);
+
 /* Copies between device and/or host memory (unified addressing), e.g. for a
  * transport that bounces device blocks through host memory. */
 int shd_memcpy(void* dst, const void* src, size_t bytes);

@@ -1600,3 +1600,143 @@ size_t orc_round_mt(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint6
     if (min_time) *min_time = mn;
     return missing ? (size_t)-1 : k;
 }
+
+/* ---------------------------------------------------------------------------
+ * Destination routers with CoDel (routing/router.c:103-131,
+ * routing/router_queue_codel.c:113-265).  The router state and the entries
+ * still queued travel in the same records as libshdnet's (a ring per router:
+ * `head`, `len` index `rings + r * ring_cap`) so that a round can resume from
+ * either implementation; inside, each router's queue is a plain FIFO array
+ * with a read cursor (g_queue_push_tail / g_queue_pop_head). */
+
+#define ORC_CODEL_TARGET (10ull * 1000000ull)    /* CODEL_PARAM_TARGET_DELAY_SIMTIME, :42 */
+#define ORC_CODEL_INTERVAL (100ull * 1000000ull) /* CODEL_PARAM_INTERVAL_SIMTIME, :48 */
+#define ORC_CODEL_MTU 1500ull                    /* CONFIG_MTU, core/support/definitions.h:185 */
+enum { ORC_STORE = 0, ORC_DROP = 1 };
+
+typedef struct {
+    OrcCodelState* st;
+    OrcCodelEntry* q; /* FIFO storage */
+    size_t rd, wr, cap;
+    uint64_t* fate;
+    uint32_t op;
+    int bad;
+} OrcRouter;
+
+static void orc_codel_drop(OrcRouter* R, uint32_t pkt) { /* :138-146 */
+    R->fate[pkt] = ((uint64_t)R->op << 2) | 2u;
+}
+
+/* :148-196 */
+static int64_t orc_codel_helper(OrcRouter* R, uint64_t now, int* ok) {
+    *ok = 0;
+    if (R->rd == R->wr) {
+        R->st->interval_expire = 0;
+        return -1;
+    }
+    OrcCodelEntry e = R->q[R->rd++];
+    if (e.length > R->st->total_size) R->bad = 1; /* utility_assert(length <= totalSize) */
+    R->st->total_size -= e.length;
+    if (now < e.enqueue_ts) R->bad = 1; /* utility_assert(now >= ts) */
+    uint64_t sojourn = now - e.enqueue_ts;
+    if (sojourn < ORC_CODEL_TARGET || R->st->total_size < ORC_CODEL_MTU) {
+        R->st->interval_expire = 0;
+    } else if (R->st->interval_expire == 0) {
+        R->st->interval_expire = now + ORC_CODEL_INTERVAL;
+    } else if (now >= R->st->interval_expire) {
+        *ok = 1;
+    }
+    return e.pkt;
+}
+
+/* :198-205 */
+static uint64_t orc_codel_law(uint32_t count, uint64_t ts) {
+    uint64_t nts = ts + ORC_CODEL_INTERVAL;
+    double result = ((double)nts) / sqrt((double)count);
+    return (uint64_t)round(result);
+}
+
+/* :207-267 */
+static int64_t orc_codel_dequeue(OrcRouter* R, uint64_t now) {
+    OrcCodelState* s = R->st;
+    int ok = 0;
+    int64_t p = orc_codel_helper(R, now, &ok);
+    if (p < 0) {
+        s->mode = ORC_STORE;
+        return p;
+    }
+    if (s->mode == ORC_DROP) {
+        if (!ok) s->mode = ORC_STORE;
+        while (now >= s->next_drop && s->mode == ORC_DROP) {
+            orc_codel_drop(R, (uint32_t)p);
+            s->drop_count++;
+            p = orc_codel_helper(R, now, &ok);
+            if (ok)
+                s->next_drop = orc_codel_law(s->drop_count, s->next_drop);
+            else
+                s->mode = ORC_STORE;
+        }
+    } else if (ok) {
+        orc_codel_drop(R, (uint32_t)p);
+        p = orc_codel_helper(R, now, &ok);
+        s->mode = ORC_DROP;
+        uint32_t delta = s->drop_count - s->drop_count_last;
+        s->drop_count = 1;
+        int recently = now < s->next_drop + (16 * ORC_CODEL_INTERVAL);
+        if (recently && delta > 1) s->drop_count = delta;
+        s->next_drop = orc_codel_law(s->drop_count, now);
+        s->drop_count_last = s->drop_count;
+    }
+    return p;
+}
+
+int orc_codel_run(uint32_t nrouters, const uint32_t* op_offsets, const OrcCodelOp* ops, OrcCodelState* states,
+                  OrcCodelEntry* rings, uint32_t ring_cap, uint32_t* deq_out, uint64_t* fate) {
+    int rc = 0;
+    size_t fcap = 16;
+    OrcCodelEntry* fifo = malloc(fcap * sizeof *fifo);
+    if (!fifo) return -3;
+    for (uint32_t r = 0; r < nrouters; r++) {
+        OrcCodelState* st = &states[r];
+        OrcCodelEntry* ring = rings + (size_t)r * ring_cap;
+        size_t need = (size_t)st->len + (op_offsets[r + 1] - op_offsets[r]);
+        if (need > fcap) {
+            while (fcap < need) fcap *= 2;
+            free(fifo);
+            fifo = malloc(fcap * sizeof *fifo);
+            if (!fifo) return -3;
+        }
+        OrcRouter R = {st, fifo, 0, 0, fcap, fate, 0, 0};
+        for (uint32_t k = 0; k < st->len; k++) fifo[R.wr++] = ring[(st->head + k) % ring_cap];
+        int failed = 0;
+        for (uint32_t i = op_offsets[r]; i < op_offsets[r + 1]; i++) {
+            const OrcCodelOp* o = &ops[i];
+            R.op = i;
+            if (o->kind == 0) { /* router_enqueue (router.c:103-121) -> :113-136 */
+                if (R.wr - R.rd == ring_cap) {
+                    rc = -2, failed = 1;
+                    break;
+                }
+                fifo[R.wr++] = (OrcCodelEntry){o->time, o->pkt, o->length};
+                st->total_size += o->length;
+                deq_out[i] = o->pkt;
+            } else { /* router_dequeue (router.c:123-131) */
+                int64_t p = orc_codel_dequeue(&R, o->time);
+                deq_out[i] = p < 0 ? UINT32_MAX : (uint32_t)p;
+                if (p >= 0) fate[p] = ((uint64_t)i << 2) | 1u;
+                if (R.bad) {
+                    rc = rc ? rc : -1, failed = 1;
+                    break;
+                }
+            }
+        }
+        (void)failed;
+        /* hand the remaining entries back in ring form: every pop advanced the head */
+        uint32_t n = (uint32_t)(R.wr - R.rd);
+        st->head = (uint32_t)((st->head + R.rd) % ring_cap);
+        for (uint32_t k = 0; k < n; k++) ring[(st->head + k) % ring_cap] = fifo[R.rd + k];
+        st->len = n;
+    }
+    free(fifo);
+    return rc;
+}

@@ -139,6 +139,28 @@ typedef struct OrcEvKey {
 /* Pushes keys[0..n) in order, pops all; writes pop order (indices) to order. */
 void orc_pq_order(const OrcEvKey* keys, size_t n, uint32_t* order);
 
+/* Destination routers (routing/router.c:103-131) with the CoDel queue
+ * manager (routing/router_queue_codel.c:113-265), one router after another.
+ * Same record layouts as include/shdnet.h's ShdCodel*; the oracle keeps its
+ * queues as growable FIFOs (the reference's GQueue), not rings: entries in
+ * flight are carried in and out through `queues`/`qlen` (per router, FIFO
+ * order, capacity `qcap` each).  Returns 0, -2 if a queue would exceed qcap,
+ * -1 on a dequeue before an entry's enqueue time (utility_assert :172). */
+typedef struct OrcCodelState {
+    uint64_t interval_expire, next_drop, total_size;
+    uint32_t mode, drop_count, drop_count_last, head, len, pad;
+} OrcCodelState;
+typedef struct OrcCodelEntry {
+    uint64_t enqueue_ts;
+    uint32_t pkt, length;
+} OrcCodelEntry;
+typedef struct OrcCodelOp {
+    uint64_t time;
+    uint32_t kind, pkt, length, pad;
+} OrcCodelOp;
+int orc_codel_run(uint32_t nrouters, const uint32_t* op_offsets, const OrcCodelOp* ops, OrcCodelState* states,
+                  OrcCodelEntry* rings, uint32_t ring_cap, uint32_t* deq_out, uint64_t* fate);
+
 #ifdef __cplusplus
 }
 #endif

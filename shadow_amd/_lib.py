@@ -76,6 +76,7 @@ PROTOS = {
     "shd_transport_rccl_new": (C.c_int, [C.c_int, C.c_int, _P, C.c_int, C.POINTER(_P)]),
     "shd_transport_rccl_free": (None, [_P]),
     "shd_memcpy": (C.c_int, [_P, _P, C.c_size_t]),
+    "shd_codel_run": (C.c_int, [C.c_uint32, _P, _P, _P, _P, C.c_uint32, _P, _P, _P]),
     "shd_parse_time_ns": (C.c_int, [C.c_char_p, _u64p]),
     "shd_parse_bandwidth_bits": (C.c_int, [C.c_char_p, _u64p]),
     "shd_last_error": (C.c_char_p, []),

@@ -75,6 +75,8 @@ lib.orc_round_mt.restype = C.c_size_t
 lib.orc_round_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
                              C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p, u64p]
 lib.orc_pq_order.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+lib.orc_codel_run.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                              C.c_void_p]
 
 
 def _s(x):
@@ -211,6 +213,30 @@ def round_mt(orc, host_ips, pkts, barrier, end_time, threads, bootstrap_end=0):
     if k == C.c_size_t(-1).value:
         raise ValueError("a packet's path is not cached: preload the rows first")
     return out[:k], status, mt.value
+
+
+class OracleRouters:
+    """orc_codel_run with the same state/ring records as shadow_amd.router."""
+
+    def __init__(self, nrouters, ring_cap):
+        from shadow_amd.router import ENTRY_DTYPE, STATE_DTYPE
+        self.n, self.cap = nrouters, ring_cap
+        self.states = np.zeros(nrouters, dtype=STATE_DTYPE)
+        self.rings = np.zeros(nrouters * ring_cap, dtype=ENTRY_DTYPE)
+
+    def run(self, op_offsets, ops, npkts):
+        op_offsets = np.ascontiguousarray(op_offsets, dtype=np.uint32)
+        ops = np.ascontiguousarray(ops)
+        deq = np.zeros(max(len(ops), 1), dtype=np.uint32)
+        fate = np.full(max(npkts, 1), np.uint64(0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+        rc = lib.orc_codel_run(self.n, op_offsets.ctypes.data, ops.ctypes.data, self.states.ctypes.data,
+                               self.rings.ctypes.data, self.cap, deq.ctypes.data, fate.ctypes.data)
+        return rc, deq[:len(ops)], fate[:npkts]
+
+    def queued(self, r):
+        st = self.states[r]
+        ring = self.rings[r * self.cap:(r + 1) * self.cap]
+        return ring[(int(st["head"]) + np.arange(int(st["len"]))) % self.cap].copy()
 
 
 def parse_time_ns(s):
