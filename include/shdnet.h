@@ -87,6 +87,46 @@ int shd_topology_is_routable(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip,
 int shd_topology_increment_path_packet_counter(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip);
 int shd_topology_get_path_packet_count(ShdTopology* top, uint32_t src_ip, uint32_t dst_ip, uint64_t* count);
 
+/* ---- DNS: host address assignment (routing/dns.c) ---------------------- */
+/* dns_new (dns.c:294-305): the generator starts after 11.0.0.0. */
+typedef struct ShdDns ShdDns;
+int shd_dns_new(ShdDns** out);
+void shd_dns_free(ShdDns* dns);
+/* dns_register (dns.c:125-163): requested_ip may be NULL (generate); an
+ * unparsable, reserved (_dns_isRestricted, :89-106) or taken address is
+ * replaced by the next free generated one; "127.0.0.1" is a local address
+ * and is not stored.  Every call takes the next MAC number.  ip_net is in
+ * network byte order. */
+int shd_dns_register(ShdDns* dns, const char* name, const char* requested_ip, uint32_t* ip_net, uint32_t* mac,
+                     int* is_local);
+/* n registrations in order under one lock (startup: 200k hosts); the
+ * request array may be NULL (all generated). */
+int shd_dns_register_batch(ShdDns* dns, uint32_t n, const char* const* names, const char* const* requested_ips,
+                           uint32_t* ip_net, uint32_t* mac, uint8_t* is_local);
+/* dns_deregister (dns.c:165-181) of the address (ip_net, name, is_local) */
+int shd_dns_deregister(ShdDns* dns, uint32_t ip_net, const char* name, int is_local);
+/* dns_resolveIPToAddress / dns_resolveNameToAddress (dns.c:183-203):
+ * -ENOENT when absent.  name gets at most cap bytes (NUL included). */
+int shd_dns_resolve_ip(ShdDns* dns, uint32_t ip_net, char* name, size_t cap, uint32_t* mac);
+int shd_dns_resolve_name(ShdDns* dns, const char* name, uint32_t* ip_net, uint32_t* mac);
+/* The hosts file dns_getHostsFilePath writes (dns.c:231-290): "127.0.0.1
+ * localhost" then "<ip> <name>" per name mapping, in registration order
+ * (the reference's order is glib's hash order).  At most cap bytes (NUL
+ * included) into buf; *len = the full length. */
+int shd_dns_hosts_file(ShdDns* dns, char* buf, size_t cap, size_t* len);
+
+/* topology_free's teardown log (_topology_logAllCachedPaths,
+ * topology.c:1860-1897 called at :2287; path_toString, path.c:62-75): fn gets
+ * one line per cached path -- "Found path <srcID>-><dstID> in cache:
+ * SourceIndex=.. DestinationIndex=.. Latency=%f Reliability=%f PacketCount=..
+ * isDirect=True|False" ("<->" on undirected graphs) -- in (source,
+ * destination) vertex order (the reference's order is glib's hash order).
+ * The cache is the release state (touched rows, released self paths, stored
+ * direct pairs) with the path packet counters.  A device-resident table is
+ * read back one row at a time. */
+typedef void (*ShdPathLogFn)(const char* line, void* user);
+int shd_topology_log_cached_paths(ShdTopology* top, ShdPathLogFn fn, void* user, uint64_t* nlines);
+
 /* n lookups in one call, in order, with the same side effects as n calls of
  * topology_getLatency (the pair's row touch, min-jump): lat_ms / rel (either
  * may be NULL) receive the answers.  For a device-resident table the answers

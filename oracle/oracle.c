@@ -407,6 +407,7 @@ struct OrcTopo {
     double min_lat;
     int min_updates;
     uint64_t next_min_jump_ns;
+    long long* v_ids; /* GML node ids (VERTEX_ATTR_ID) */
 };
 typedef struct PathE PathE;
 
@@ -608,6 +609,7 @@ void orc_topology_free(OrcTopo* t) {
     glist_free(&t->tree);
     free(t->efrom);
     free(t->eto);
+    free(t->v_ids);
     free(t->inc_off);
     free(t->inc);
     free(t->weight_ms);
@@ -736,7 +738,7 @@ OrcTopo* orc_topology_new(const char* text, int use_shortest_path) {
             t->eto[e] = sv;
         }
     }
-    free(ids);
+    t->v_ids = ids;
     free(byid);
     if (bad) {
         free(nodes);
@@ -1739,4 +1741,28 @@ int orc_codel_run(uint32_t nrouters, const uint32_t* op_offsets, const OrcCodelO
     }
     free(fifo);
     return rc;
+}
+
+/* _topology_logAllCachedPaths (topology.c:1860-1897) at topology_free
+ * (:2287), over the literal cache: "Found path <srcID><-> or -><dstID> in
+ * cache: " + path_toString (path.c:62-75).  Lines in (source, destination)
+ * vertex order (the reference's glib hash-table walk has no defined order). */
+size_t orc_topology_log_cached_paths(OrcTopo* t, char* buf, size_t cap) {
+    size_t used = 0;
+    char line[512];
+    for (int s = 0; s < t->V; s++) {
+        if (!t->cache[s]) continue;
+        for (int d = 0; d < t->V; d++) {
+            PathE* p = &t->cache[s][d];
+            if (!p->present) continue;
+            int k = snprintf(line, sizeof line,
+                             "Found path %li%s%li in cache: SourceIndex=%ld DestinationIndex=%ld Latency=%f "
+                             "Reliability=%f PacketCount=%lu isDirect=%s\n",
+                             (long)t->v_ids[s], t->directed ? "->" : "<->", (long)t->v_ids[d], (long)s, (long)d,
+                             p->lat, p->rel, (unsigned long)p->pkts, p->is_direct ? "True" : "False");
+            if (buf && used + (size_t)k < cap) memcpy(buf + used, line, (size_t)k + 1);
+            used += (size_t)k;
+        }
+    }
+    return used;
 }

@@ -128,6 +128,11 @@ size_t orc_round_mt(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint6
                     uint64_t bootstrap_end, const OrcPkt* pkts, size_t n, int nthreads, OrcDeliv* out,
                     uint8_t* status, uint64_t* min_time);
 
+/* _topology_logAllCachedPaths: every cached path as one '\n'-terminated line,
+ * in (source, destination) vertex order.  Writes at most cap bytes (NUL
+ * included) and returns the length the full log needs. */
+size_t orc_topology_log_cached_paths(OrcTopo* t, char* buf, size_t cap);
+
 /* Binary heap restating utility/priority_queue.c with event_compare
  * (core/work/event.c:109-152); exposed for the PQ golden test. */
 typedef struct OrcEvKey {

@@ -29,6 +29,7 @@ _u32p = C.POINTER(C.c_uint32)
 _u64p = C.POINTER(C.c_uint64)
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int)
+PATH_LOG_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
 
 PROTOS = {
     "shd_topology_new": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(_P)]),
@@ -76,6 +77,15 @@ PROTOS = {
     "shd_transport_rccl_new": (C.c_int, [C.c_int, C.c_int, _P, C.c_int, C.POINTER(_P)]),
     "shd_transport_rccl_free": (None, [_P]),
     "shd_memcpy": (C.c_int, [_P, _P, C.c_size_t]),
+    "shd_topology_log_cached_paths": (C.c_int, [_P, PATH_LOG_FN, _P, _u64p]),
+    "shd_dns_new": (C.c_int, [C.POINTER(_P)]),
+    "shd_dns_free": (None, [_P]),
+    "shd_dns_register": (C.c_int, [_P, C.c_char_p, C.c_char_p, _u32p, _u32p, _ip]),
+    "shd_dns_register_batch": (C.c_int, [_P, C.c_uint32, _P, _P, _P, _P, _P]),
+    "shd_dns_deregister": (C.c_int, [_P, C.c_uint32, C.c_char_p, C.c_int]),
+    "shd_dns_resolve_ip": (C.c_int, [_P, C.c_uint32, C.c_char_p, C.c_size_t, _u32p]),
+    "shd_dns_resolve_name": (C.c_int, [_P, C.c_char_p, _u32p, _u32p]),
+    "shd_dns_hosts_file": (C.c_int, [_P, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "shd_codel_run": (C.c_int, [C.c_uint32, _P, _P, _P, _P, C.c_uint32, _P, _P, _P]),
     "shd_parse_time_ns": (C.c_int, [C.c_char_p, _u64p]),
     "shd_parse_bandwidth_bits": (C.c_int, [C.c_char_p, _u64p]),

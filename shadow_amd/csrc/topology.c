@@ -436,10 +436,12 @@ static int load(ShdTopology* t, const char* text) {
     t->v_country = (const char**)calloc((size_t)V + 1, sizeof(char*));
     t->v_bw_down = (int64_t*)malloc(sizeof(int64_t) * ((size_t)V + 1));
     t->v_bw_up = (int64_t*)malloc(sizeof(int64_t) * ((size_t)V + 1));
+    t->v_id = (double*)malloc(sizeof(double) * ((size_t)V + 1));
     for (int v = 0; v < V; v++) {
         const GmlBlock* b = &d->nodes[v];
-        double idv;
+        double idv = 0;
         if (!num_attr(d, b, c_id, &idv)) rc = -EINVAL;
+        t->v_id[v] = idv;
         t->v_bw_down[v] = bw_kib(str_attr(d, b, c_bd));
         t->v_bw_up[v] = bw_kib(str_attr(d, b, c_bu));
         if (t->v_bw_down[v] <= 0 || t->v_bw_up[v] <= 0) rc = -EINVAL;
@@ -509,6 +511,7 @@ void shd_topology_free(ShdTopology* t) {
     free((void*)t->v_city);
     free((void*)t->v_country);
     free(t->v_bw_down);
+    free(t->v_id);
     free(t->v_bw_up);
     free(t->ipmap.slots);
     free(t->v_attached);
@@ -1054,6 +1057,106 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
     }
     pthread_mutex_unlock(&t->pkt_mu);
     return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* teardown path log (topology_free -> _topology_logAllCachedPaths)     */
+/* ------------------------------------------------------------------ */
+
+static uint64_t pkt_count_of(ShdTopology* t, int i, int j) {
+    uint64_t key = ((uint64_t)(uint32_t)i << 32) | (uint32_t)j, out = 0;
+    if (!t->pkt_cap) return 0;
+    uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20 & (t->pkt_cap - 1);
+    while (t->pkt_keys[h] != UINT64_MAX) {
+        if (t->pkt_keys[h] == key) {
+            out = t->pkt_vals[h];
+            break;
+        }
+        h = (h + 1) & (t->pkt_cap - 1);
+    }
+    return out;
+}
+
+/* isDirect of the self path (_topology_computeShortestPathToSelf,
+ * topology.c:1431-1575): is the minimum of the out-edges (latency doubled
+ * unless a self-loop, first minimum in incidence order) a self-loop. */
+static int self_is_direct(const ShdTopology* t, int v) {
+    double mn = -1;
+    int direct = 1; /* no edges: TRUE (:1516-1519) */
+    for (int k = t->inc_off[v]; k < t->inc_off[v + 1]; k++) {
+        const int loop = t->inc_nbr[k] == v;
+        double l = t->e_ms[t->inc_eid[k]];
+        if (!loop) l *= 2.0;
+        if (mn == -1 || l < mn) mn = l, direct = loop;
+    }
+    return direct;
+}
+
+static void log_line(ShdTopology* t, ShdPathLogFn fn, void* user, int i, int j, ShdEntry e, int direct) {
+    char line[512];
+    const int si = t->slot_vertex[i], di = t->slot_vertex[j];
+    snprintf(line, sizeof line,
+             "Found path %li%s%li in cache: SourceIndex=%ld DestinationIndex=%ld Latency=%f Reliability=%f "
+             "PacketCount=%lu isDirect=%s",
+             (long)t->v_id[si], t->directed ? "->" : "<->", (long)t->v_id[di], (long)si, (long)di, e.lat, e.rel,
+             (unsigned long)pkt_count_of(t, i, j), direct ? "True" : "False");
+    fn(line, user);
+}
+
+/* _topology_logAllCachedPaths (topology.c:1860-1897), called from
+ * topology_free (:2287): one line per path in the cache, formatted by
+ * path_toString (path.c:62-75) behind the helper's prefix.  The cache is the
+ * release state: row i's entries (i, y) for y touched after i (or never),
+ * released self paths, and stored direct pairs.  Lines come in (source,
+ * destination) vertex order; the reference walks glib hash tables, whose
+ * order is unspecified. */
+int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, uint64_t* nlines) {
+    if (!t || !fn) return -EINVAL;
+    uint64_t n = 0;
+    if (nlines) *nlines = 0;
+    if (!__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return 0;
+    const int A = t->A;
+    ShdEntry* row = NULL;
+    if (!t->h_tab) {
+        row = (ShdEntry*)malloc(sizeof(ShdEntry) * (size_t)A);
+        if (!row) return -ENOMEM;
+    }
+    int rc = 0;
+    pthread_mutex_lock(&t->pkt_mu);
+    for (int i = 0; i < A && !rc; i++) {
+        const uint32_t si = touch_of(t, i);
+        const int self = __atomic_load_n(&t->self_released[i], __ATOMIC_ACQUIRE);
+        int any = self;
+        if (t->use_sp) any |= si != SHD_UNTOUCHED;
+        else
+            for (int j = 0; j < A && !any; j++) any = pair_bit(t, i, j);
+        if (!any) continue;
+        const ShdEntry* r = t->h_tab ? t->h_tab + (size_t)i * (size_t)A : row;
+        if (!t->h_tab) {
+            if (i < t->tab_row_lo || i >= t->tab_row_hi) {
+                rc = shd_fail(-ENOTSUP, "row %d lives on another rank", i);
+                break;
+            }
+            if ((rc = shd_dev_init(t->device)) || (rc = shd_dev_d2h(row, t->d_tab + (size_t)i * (size_t)A,
+                                                                   sizeof(ShdEntry) * (size_t)A)))
+                break;
+        }
+        for (int j = 0; j < A; j++) {
+            if (t->use_sp) {
+                if (j == i) {
+                    if (self) log_line(t, fn, user, i, i, r[i], self_is_direct(t, t->slot_vertex[i])), n++;
+                } else if (si != SHD_UNTOUCHED && touch_of(t, j) > si && r[j].lat >= 0) {
+                    log_line(t, fn, user, i, j, r[j], 0), n++;
+                }
+            } else if (pair_bit(t, i, j)) {
+                log_line(t, fn, user, i, j, r[j], 1), n++;
+            }
+        }
+    }
+    pthread_mutex_unlock(&t->pkt_mu);
+    free(row);
+    if (nlines) *nlines = n;
+    return rc;
 }
 
 /* Device-resident table (no host mirror; C4's A = 86k table is 120 GB):

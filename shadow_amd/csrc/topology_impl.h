@@ -56,6 +56,7 @@ struct ShdTopology {
     int32_t *inc_off, *inc_nbr, *inc_eid; /* igraph_incident(OUT) CSR */
     const char **v_ip, **v_city, **v_country;
     int64_t *v_bw_down, *v_bw_up; /* KiB/s */
+    double* v_id;                 /* the GML node id (VERTEX_ATTR_ID) */
 
     /* attachment */
     IpMap ipmap;

@@ -132,6 +132,16 @@ class Topology:
         check(lib().shd_topology_get_path_packet_count(self._h, src_ip, dst_ip, C.byref(out)))
         return out.value
 
+    def cached_paths_log(self) -> list[str]:
+        """topology_free's teardown log (shd_topology_log_cached_paths)."""
+        from ._lib import PATH_LOG_FN
+        lines: list[str] = []
+        fn = PATH_LOG_FN(lambda line, _u: lines.append(line.decode()))
+        n = C.c_uint64(0)
+        check(lib().shd_topology_log_cached_paths(self._h, fn, None, C.byref(n)))
+        assert n.value == len(lines)
+        return lines
+
     def min_path_latency(self) -> float:
         out = C.c_double()
         check(lib().shd_topology_get_min_path_latency(self._h, C.byref(out)))

@@ -75,6 +75,8 @@ lib.orc_round_mt.restype = C.c_size_t
 lib.orc_round_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
                              C.c_void_p, C.c_size_t, C.c_int, C.c_void_p, C.c_void_p, u64p]
 lib.orc_pq_order.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
+lib.orc_topology_log_cached_paths.restype = C.c_size_t
+lib.orc_topology_log_cached_paths.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
 lib.orc_codel_run.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                               C.c_void_p]
 
@@ -136,6 +138,12 @@ class OracleTopology:
 
     def packet_count(self, s, d):
         return lib.orc_topology_path_packet_count(self.h, s, d)
+
+    def cached_paths_log(self):
+        n = lib.orc_topology_log_cached_paths(self.h, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        lib.orc_topology_log_cached_paths(self.h, buf, n + 1)
+        return buf.value.decode().splitlines()
 
     def min_path_latency(self):
         return lib.orc_topology_min_path_latency(self.h)

@@ -581,3 +581,25 @@ def test_lookup_batch_matches_single_lookups(resident):
         assert bits(lat[i]) == bits(orc.latency(int(s[i]), int(d[i])))
         assert bits(rel[i]) == bits(orc.reliability(int(s[i]), int(d[i])))
     assert bits(top.min_path_latency()) == bits(orc.min_path_latency())
+
+
+@pytest.mark.parametrize("name,use_sp", [("1_gbit_switch", True), ("complete30_ms", True), ("sparse300_ns", True),
+                                         ("sparse200_dir_ns", True), ("complete25_dir", False),
+                                         ("sparse5000_hbm", True)])
+def test_teardown_path_log_matches_reference(name, use_sp):
+    """topology_free's cached-path log after random lookups and counted
+    packets: the same lines (ids, indices, %f latency / reliability, packet
+    counts, isDirect) as the oracle's literal cache."""
+    gml, H = GRAPHS[name]
+    top, orc, ips, _ = make_pair(gml, H, use_sp)
+    rng = np.random.default_rng(11)
+    for _ in range(400):
+        a, b = (int(x) for x in rng.integers(0, H, 2))
+        s, d = int(ips[a]), int(ips[b])
+        assert bits(top.get_latency(s, d)) == bits(orc.latency(s, d))
+        if rng.random() < 0.5:
+            top.increment_path_packet_counter(s, d)
+            orc.increment(s, d)
+    got = top.cached_paths_log()
+    assert got == orc.cached_paths_log()
+    assert len(got) > 0

@@ -219,3 +219,18 @@ def test_round_mt_equals_serial_round():
     assert np.array_equal(status, status2) and mt == mt2 and np.array_equal(out, out2)
     for s, d in zip(ips[::37], ips[::53]):
         assert a.packet_count(int(s), int(d)) == b.packet_count(int(s), int(d))
+
+
+def test_teardown_log_known_answer_1_gbit_switch():
+    """1_gbit_switch: one vertex (id 0) with a 1 ms lossless self-loop; every
+    lookup is the self path, a direct one.  Three counted packets."""
+    t = O.OracleTopology(synth.ONE_GBIT_SWITCH_GML)
+    ips = synth.host_ips(4)
+    for h in range(4):
+        t.attach(h, int(ips[h]), h + 1)
+    assert t.latency(int(ips[0]), int(ips[1])) == 1.0
+    for _ in range(3):
+        t.increment(int(ips[2]), int(ips[3]))
+    assert t.cached_paths_log() == [
+        "Found path 0<->0 in cache: SourceIndex=0 DestinationIndex=0 Latency=1.000000 Reliability=1.000000 "
+        "PacketCount=3 isDirect=True"]
