@@ -355,6 +355,60 @@ enum { SHD_CODEL_QUEUED = 0, SHD_CODEL_DEQUEUED = 1, SHD_CODEL_DROPPED = 2 };
 int shd_codel_run(uint32_t nrouters, const uint32_t* d_op_offsets, const ShdCodelOp* d_ops, ShdCodelState* d_states,
                   ShdCodelEntry* d_rings, uint32_t ring_cap, uint32_t* d_deq_out, uint64_t* d_fate, void* stream);
 
+/* ---- network interfaces: router + CoDel + token buckets ----------------- */
+/* host/network_interface.c (buckets :33-41, 99-228; receivePackets :448-482;
+ * sendPackets :571-631; wantsSend :633-661) with the upstream router
+ * (routing/router.c:103-131, router_queue_codel.c).  One record per host;
+ * refill grid and router state included.  128 bytes. */
+typedef struct ShdNicState {
+    uint64_t recv_remaining, recv_refill, recv_capacity; /* bytes; refill per 1 ms */
+    uint64_t send_remaining, send_refill, send_capacity;
+    uint64_t refill_start; /* timeStartedRefillingBuckets */
+    uint64_t refill_time;  /* when the pending refill task runs */
+    uint32_t refill_pending, pad0;
+    uint64_t pad1;
+    ShdCodelState router; /* head/len index the host's entry ring */
+} ShdNicState;
+
+/* A packet a host's sockets offer to its interface (qdisc order), offered
+ * at `ready` (networkinterface_wantsSend); length = payload + header. */
+typedef struct ShdNicSend {
+    uint64_t ready;
+    uint32_t id, length;
+} ShdNicSend;
+
+enum { SHD_NIC_QUEUED = 0, SHD_NIC_RECEIVED = 1, SHD_NIC_DROPPED = 2 };
+
+/* _networkinterface_setupTokenBuckets + networkinterface_startRefillingTokenBuckets
+ * at start_time for nhosts interfaces (bandwidths in KiB/s, device arrays). */
+int shd_nic_init(uint32_t nhosts, const uint64_t* d_bw_down_kibps, const uint64_t* d_bw_up_kibps,
+                 uint64_t start_time, ShdNicState* d_states, void* stream);
+
+/* Per-event packet length = the record's payload_len + header_bytes (42 UDP,
+ * 66 TCP: CONFIG_HEADER_SIZE_*, definitions.h:173-180). */
+int shd_event_lengths(const ShdDeliv* d_events, size_t n, const ShdPkt* d_pkts, uint32_t header_bytes,
+                      uint32_t* d_lengths, void* stream);
+
+/* Runs hosts [host_base, host_base + nhosts) up to window_end (exclusive):
+ * host h's arrivals are d_events[d_event_offsets[h] .. [h+1]) in
+ * event_compare order (a round's per-destination segments, as produced),
+ * all with time < window_end; its send requests d_sends[d_send_offsets[h] ..
+ * [h+1]) (NULL offsets: none), in offer order.  Arrival k is packet id
+ * id_base + k: d_recv_time / d_recv_status[id] (arrays of fate_cap entries,
+ * also written for packets queued in earlier windows) get the receive time
+ * and SHD_NIC_RECEIVED, or SHD_NIC_DROPPED (CoDel), or stay
+ * SHD_NIC_QUEUED / ~0 (still in the router at window_end: the entry moves
+ * to the host's ring of ring_cap entries and is carried).  d_send_time[k]
+ * gets request k's send time (~0: not sent by window_end -- offer it again,
+ * first, in the next window).  Synchronous.  -ENOSPC on a ring overflow,
+ * -EINVAL on misaddressed, out-of-order or out-of-window inputs. */
+int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* d_events, const uint32_t* d_event_offsets,
+                const uint32_t* d_event_lengths, const ShdNicSend* d_sends, const uint32_t* d_send_offsets,
+                uint64_t window_end, uint64_t bootstrap_end, ShdNicState* d_states, ShdCodelEntry* d_rings,
+                uint32_t ring_cap, uint32_t id_base, uint64_t* d_recv_time, uint8_t* d_recv_status,
+                uint64_t fate_cap, uint64_t* d_send_time, void* stream);
+
+
 /* Copies between device and/or host memory (unified addressing), e.g. for a
  * transport that bounces device blocks through host memory. */
 int shd_memcpy(void* dst, const void* src, size_t bytes);

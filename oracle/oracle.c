@@ -1623,10 +1623,12 @@ typedef struct {
     uint64_t* fate;
     uint32_t op;
     int bad;
+    uint8_t* rstat; /* interface engine: drops are recorded per packet id here */
 } OrcRouter;
 
 static void orc_codel_drop(OrcRouter* R, uint32_t pkt) { /* :138-146 */
-    R->fate[pkt] = ((uint64_t)R->op << 2) | 2u;
+    if (R->rstat) R->rstat[pkt] = 2;
+    else R->fate[pkt] = ((uint64_t)R->op << 2) | 2u;
 }
 
 /* :148-196 */
@@ -1708,7 +1710,7 @@ int orc_codel_run(uint32_t nrouters, const uint32_t* op_offsets, const OrcCodelO
             fifo = malloc(fcap * sizeof *fifo);
             if (!fifo) return -3;
         }
-        OrcRouter R = {st, fifo, 0, 0, fcap, fate, 0, 0};
+        OrcRouter R = {st, fifo, 0, 0, fcap, fate, 0, 0, NULL};
         for (uint32_t k = 0; k < st->len; k++) fifo[R.wr++] = ring[(st->head + k) % ring_cap];
         int failed = 0;
         for (uint32_t i = op_offsets[r]; i < op_offsets[r + 1]; i++) {
@@ -1765,4 +1767,253 @@ size_t orc_topology_log_cached_paths(OrcTopo* t, char* buf, size_t cap) {
         }
     }
     return used;
+}
+
+/* ---------------------------------------------------------------------------
+ * Network interfaces (host/network_interface.c) with the upstream router,
+ * as the reference runs them: a per-host event queue ordered like
+ * event_compare (time, source host, then the source's event order), into
+ * which the arrivals and send requests are pushed up front and refill tasks
+ * are pushed when scheduled (worker_scheduleTask); each popped event runs its
+ * callback.  A refill and a send request of the same host at the same time:
+ * the send request first (the reference orders them by event id, which the
+ * inputs do not carry -- the same assumption as libshdnet's). */
+
+#define ORC_NIC_INTERVAL 1000000ull /* _networkinterface_getRefillInterval, :99-101 */
+
+typedef struct {
+    uint64_t time;
+    uint32_t src;
+    uint32_t cls; /* 0 arrival, 1 send request, 2 refill */
+    uint64_t idx; /* input order within (time, src, cls) */
+} OrcNicEv;
+
+static int orc_nicev_less(const OrcNicEv* a, const OrcNicEv* b) {
+    if (a->time != b->time) return a->time < b->time;
+    if (a->src != b->src) return a->src < b->src;
+    if (a->cls != b->cls) return a->cls < b->cls;
+    return a->idx < b->idx;
+}
+
+typedef struct {
+    OrcNicEv* h;
+    size_t n, cap;
+} OrcNicHeap;
+
+static int orc_nicheap_push(OrcNicHeap* H, OrcNicEv e) {
+    if (H->n == H->cap) {
+        size_t nc = H->cap ? H->cap * 2 : 64;
+        OrcNicEv* nh = (OrcNicEv*)realloc(H->h, nc * sizeof *nh);
+        if (!nh) return -1;
+        H->h = nh;
+        H->cap = nc;
+    }
+    size_t i = H->n++;
+    H->h[i] = e;
+    while (i && orc_nicev_less(&H->h[i], &H->h[(i - 1) / 2])) {
+        OrcNicEv t = H->h[i];
+        H->h[i] = H->h[(i - 1) / 2];
+        H->h[(i - 1) / 2] = t;
+        i = (i - 1) / 2;
+    }
+    return 0;
+}
+
+static OrcNicEv orc_nicheap_pop(OrcNicHeap* H) {
+    OrcNicEv top = H->h[0];
+    H->h[0] = H->h[--H->n];
+    size_t i = 0;
+    for (;;) {
+        size_t l = 2 * i + 1, r = l + 1, m = i;
+        if (l < H->n && orc_nicev_less(&H->h[l], &H->h[m])) m = l;
+        if (r < H->n && orc_nicev_less(&H->h[r], &H->h[m])) m = r;
+        if (m == i) break;
+        OrcNicEv t = H->h[i];
+        H->h[i] = H->h[m];
+        H->h[m] = t;
+        i = m;
+    }
+    return top;
+}
+
+typedef struct {
+    OrcNicState* s;
+    OrcRouter R;
+    OrcNicHeap* H;
+    uint32_t self;
+    uint64_t boot_end;
+    const OrcNicSend* sends;
+    size_t sq, sk; /* offered, not yet sent: [sq, sk) */
+    uint64_t* stime;
+    uint64_t* rtime;
+    uint8_t* rstat;
+    int oom;
+} OrcNic;
+
+static void orc_nic_consume(uint64_t* rem, uint64_t bytes) { /* :117-125 */
+    if (bytes >= *rem) *rem = 0;
+    else *rem -= bytes;
+}
+
+/* _networkinterface_scheduleNextRefillIfNeeded + scheduleNextRefill (:135-164) */
+static void orc_nic_schedule(OrcNic* N, uint64_t now) {
+    OrcNicState* s = N->s;
+    int need = s->send_remaining < s->send_capacity || s->recv_remaining < s->recv_capacity;
+    if (!need || s->refill_pending) return;
+    uint64_t offset = now - s->refill_start;
+    uint64_t since = offset % ORC_NIC_INTERVAL;
+    s->refill_time = now + (ORC_NIC_INTERVAL - since);
+    s->refill_pending = 1; /* _networkinterface_scheduleRefillTask (:127-133) */
+    OrcNicEv e = {s->refill_time, N->self, 2, 0};
+    if (orc_nicheap_push(N->H, e)) N->oom = 1;
+}
+
+/* networkinterface_receivePackets (:448-482) */
+static void orc_nic_receive(OrcNic* N, uint64_t now) {
+    int boot = now < N->boot_end;
+    while (boot || N->s->recv_remaining >= ORC_CODEL_MTU) {
+        int64_t p = orc_codel_dequeue(&N->R, now); /* router_dequeue (router.c:123-131) */
+        if (p < 0) break;
+        uint32_t len = N->R.q[N->R.rd - 1].length;
+        N->rtime[p] = now;
+        N->rstat[p] = 1;
+        if (!boot) {
+            orc_nic_consume(&N->s->recv_remaining, len);
+            orc_nic_schedule(N, now);
+        }
+    }
+}
+
+/* _networkinterface_sendPackets (:571-631) */
+static void orc_nic_send(OrcNic* N, uint64_t now) {
+    int boot = now < N->boot_end;
+    while (N->s->send_remaining >= ORC_CODEL_MTU) {
+        if (N->sq == N->sk) break; /* no socket has a packet */
+        const OrcNicSend* p = &N->sends[N->sq];
+        N->stime[N->sq] = now;
+        N->sq++;
+        if (!boot) {
+            orc_nic_consume(&N->s->send_remaining, p->length);
+            orc_nic_schedule(N, now);
+        }
+    }
+}
+
+/* _networkinterface_refillTokenBucketsCB (:166-186) */
+static void orc_nic_refill(OrcNic* N, uint64_t now) {
+    OrcNicState* s = N->s;
+    s->refill_pending = 0;
+    s->recv_remaining += s->recv_refill; /* :108-115 */
+    if (s->recv_remaining > s->recv_capacity) s->recv_remaining = s->recv_capacity;
+    s->send_remaining += s->send_refill;
+    if (s->send_remaining > s->send_capacity) s->send_remaining = s->send_capacity;
+    orc_nic_receive(N, now);
+    orc_nic_send(N, now);
+    orc_nic_schedule(N, now);
+}
+
+int orc_nic_init(uint32_t n, const uint64_t* down, const uint64_t* up, uint64_t start, OrcNicState* st) {
+    for (uint32_t h = 0; h < n; h++) {
+        OrcNicState* s = &st[h];
+        memset(s, 0, sizeof *s);
+        uint64_t factor = 1000000000ull / ORC_NIC_INTERVAL; /* _networkinterface_setupTokenBuckets (:196-228) */
+        s->recv_refill = down[h] * 1024 / factor;
+        s->send_refill = up[h] * 1024 / factor;
+        s->recv_capacity = s->recv_refill + ORC_CODEL_MTU;
+        s->send_capacity = s->send_refill + ORC_CODEL_MTU;
+        /* networkinterface_startRefillingTokenBuckets (:188-194) -> refillCB on empty buckets */
+        s->refill_start = start;
+        s->recv_remaining = s->recv_refill < s->recv_capacity ? s->recv_refill : s->recv_capacity;
+        s->send_remaining = s->send_refill < s->send_capacity ? s->send_refill : s->send_capacity;
+        int need = s->send_remaining < s->send_capacity || s->recv_remaining < s->recv_capacity;
+        if (need) {
+            s->refill_time = start + ORC_NIC_INTERVAL;
+            s->refill_pending = 1;
+        }
+    }
+    return 0;
+}
+
+int orc_nic_run(uint32_t nhosts, uint32_t host_base, const OrcDeliv* ev, const uint32_t* eoff, const uint32_t* elen,
+                const OrcNicSend* sends, const uint32_t* soff, uint64_t window_end, uint64_t boot_end,
+                OrcNicState* states, OrcCodelEntry* rings, uint32_t ring_cap, uint32_t id_base, uint64_t* rtime,
+                uint8_t* rstat, uint64_t fate_cap, uint64_t* stime) {
+    int rc = 0;
+    OrcNicHeap H = {0};
+    for (uint32_t k = eoff[0]; k < eoff[nhosts]; k++) {
+        if ((uint64_t)id_base + k >= fate_cap) return -3;
+        rtime[id_base + k] = UINT64_MAX;
+        rstat[id_base + k] = 0;
+    }
+    if (soff)
+        for (uint32_t k = soff[0]; k < soff[nhosts]; k++) stime[k] = UINT64_MAX;
+    for (uint32_t h = 0; h < nhosts && !rc; h++) {
+        OrcNicState* s = &states[h];
+        const uint32_t self = host_base + h;
+        size_t na = eoff[h + 1] - eoff[h], ns = soff ? soff[h + 1] - soff[h] : 0;
+        size_t fcap = (size_t)s->router.len + na + 1;
+        OrcCodelEntry* fifo = (OrcCodelEntry*)malloc(fcap * sizeof *fifo);
+        if (!fifo) return -3;
+        OrcCodelEntry* ring = rings + (size_t)h * ring_cap;
+        OrcNic N;
+        memset(&N, 0, sizeof N);
+        N.s = s;
+        N.R = (OrcRouter){(OrcCodelState*)&s->router, fifo, 0, 0, fcap, NULL, 0, 0, rstat};
+        for (uint32_t k = 0; k < s->router.len; k++) fifo[N.R.wr++] = ring[(s->router.head + k) % ring_cap];
+        N.H = &H;
+        N.self = self;
+        N.boot_end = boot_end;
+        N.sends = sends;
+        N.sq = N.sk = soff ? soff[h] : 0;
+        N.stime = stime;
+        N.rtime = rtime;
+        N.rstat = rstat;
+        H.n = 0;
+        for (size_t k = 0; k < na; k++) {
+            const OrcDeliv* d = &ev[eoff[h] + k];
+            if (d->dst_host != self || d->time >= window_end) rc = -1;
+            OrcNicEv e = {d->time, d->src_host, 0, k};
+            if (orc_nicheap_push(&H, e)) rc = -3;
+        }
+        for (size_t k = 0; k < ns; k++) {
+            if (sends[soff[h] + k].ready >= window_end) rc = -1;
+            OrcNicEv e = {sends[soff[h] + k].ready, self, 1, k};
+            if (orc_nicheap_push(&H, e)) rc = -3;
+        }
+        if (s->refill_pending) {
+            OrcNicEv e = {s->refill_time, self, 2, 0};
+            if (orc_nicheap_push(&H, e)) rc = -3;
+        }
+        uint64_t last = 0;
+        while (!rc && H.n && H.h[0].time < window_end) {
+            OrcNicEv e = orc_nicheap_pop(&H);
+            if (e.cls == 0) { /* packet arrival: router_enqueue (router.c:103-121) */
+                const uint32_t k = eoff[h] + (uint32_t)e.idx;
+                if (e.time < last) rc = -1;
+                last = e.time;
+                int buffered = N.R.rd != N.R.wr; /* queueHooks->peek */
+                N.R.q[N.R.wr++] = (OrcCodelEntry){ev[k].time, id_base + k, elen[k]};
+                s->router.total_size += elen[k];
+                if (!buffered) orc_nic_receive(&N, e.time);
+            } else if (e.cls == 1) { /* networkinterface_wantsSend (:633-661) */
+                N.sk = soff[h] + (size_t)e.idx + 1;
+                orc_nic_send(&N, e.time);
+            } else {
+                orc_nic_refill(&N, e.time);
+            }
+            if (N.R.bad) rc = -1;
+            if (N.oom) rc = -3;
+        }
+        /* still queued: back into the ring */
+        uint32_t left = (uint32_t)(N.R.wr - N.R.rd);
+        if (!rc && left > ring_cap) rc = -2;
+        if (!rc) {
+            s->router.head = (uint32_t)((s->router.head + (N.R.rd < s->router.len ? N.R.rd : s->router.len)) % ring_cap);
+            for (uint32_t k = 0; k < left; k++) ring[(s->router.head + k) % ring_cap] = fifo[N.R.rd + k];
+            s->router.len = left;
+        }
+        free(fifo);
+    }
+    free(H.h);
+    return rc;
 }

@@ -166,6 +166,29 @@ typedef struct OrcCodelOp {
 int orc_codel_run(uint32_t nrouters, const uint32_t* op_offsets, const OrcCodelOp* ops, OrcCodelState* states,
                   OrcCodelEntry* rings, uint32_t ring_cap, uint32_t* deq_out, uint64_t* fate);
 
+/* Network interfaces with the upstream router (host/network_interface.c,
+ * routing/router.c, router_queue_codel.c), as an event-driven simulation per
+ * host.  Same records and arguments as include/shdnet.h's shd_nic_*
+ * (host arrays).  Returns 0, -1 bad input, -2 ring overflow, -3 no memory. */
+typedef struct OrcNicState {
+    uint64_t recv_remaining, recv_refill, recv_capacity;
+    uint64_t send_remaining, send_refill, send_capacity;
+    uint64_t refill_start, refill_time;
+    uint32_t refill_pending, pad0;
+    uint64_t pad1;
+    OrcCodelState router;
+} OrcNicState;
+typedef struct OrcNicSend {
+    uint64_t ready;
+    uint32_t id, length;
+} OrcNicSend;
+int orc_nic_init(uint32_t n, const uint64_t* down, const uint64_t* up, uint64_t start, OrcNicState* st);
+int orc_nic_run(uint32_t nhosts, uint32_t host_base, const OrcDeliv* ev, const uint32_t* eoff, const uint32_t* elen,
+                const OrcNicSend* sends, const uint32_t* soff, uint64_t window_end, uint64_t boot_end,
+                OrcNicState* states, OrcCodelEntry* rings, uint32_t ring_cap, uint32_t id_base, uint64_t* rtime,
+                uint8_t* rstat, uint64_t fate_cap, uint64_t* stime);
+
+
 #ifdef __cplusplus
 }
 #endif

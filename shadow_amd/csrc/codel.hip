@@ -16,95 +16,29 @@
 #include <cerrno>
 #include <cmath>
 
+#include "codel_dev.h"
 #include "shd_internal.h"
 
 namespace {
 
-constexpr uint64_t kTarget = 10ull * 1000000ull;    // CODEL_PARAM_TARGET_DELAY_SIMTIME (:38)
-constexpr uint64_t kInterval = 100ull * 1000000ull; // CODEL_PARAM_INTERVAL_SIMTIME (:45)
-constexpr uint64_t kMtu = 1500;                     // CONFIG_MTU (definitions.h:185)
-
 struct Router {
-    ShdCodelState s;
     ShdCodelEntry* ring;
     uint32_t cap;
     uint64_t* fate;
     uint32_t op; // index of the operation being run (fate records)
-    bool bad;    // a dequeue ran at a time before an entry's enqueue (utility_assert(now >= ts), :172)
+    bool bad;    // a dequeue before an entry's enqueue time (utility_assert(now >= ts), :172)
+    uint32_t head, len;
+
+    __device__ __forceinline__ bool pop(ShdCodelEntry& e) {
+        if (len == 0) return false;
+        e = ring[head];
+        head = head + 1 == cap ? 0 : head + 1;
+        len--;
+        return true;
+    }
+    // _routerqueuecodel_drop (:138-146): PDS_ROUTER_DROPPED
+    __device__ __forceinline__ void drop(uint32_t pkt) { fate[pkt] = ((uint64_t)op << 2) | SHD_CODEL_DROPPED; }
 };
-
-__device__ __forceinline__ bool pop_head(Router& q, ShdCodelEntry& e) {
-    if (q.s.len == 0) return false;
-    e = q.ring[q.s.head];
-    q.s.head = q.s.head + 1 == q.cap ? 0 : q.s.head + 1;
-    q.s.len--;
-    return true;
-}
-
-// _routerqueuecodel_drop (:139-147): PDS_ROUTER_DROPPED
-__device__ __forceinline__ void drop(Router& q, uint32_t pkt) {
-    q.fate[pkt] = ((uint64_t)q.op << 2) | SHD_CODEL_DROPPED;
-}
-
-// _routerqueuecodel_dequeueHelper (:149-196); returns the packet or -1
-__device__ int64_t dequeue_helper(Router& q, uint64_t now, bool* ok_to_drop) {
-    *ok_to_drop = false;
-    ShdCodelEntry e;
-    if (!pop_head(q, e)) {
-        q.s.interval_expire = 0; // empty: cannot be above target
-        return -1;
-    }
-    q.s.total_size -= e.length;
-    if (now < e.enqueue_ts) q.bad = true;
-    const uint64_t sojourn = now - e.enqueue_ts;
-    if (sojourn < kTarget || q.s.total_size < kMtu) {
-        q.s.interval_expire = 0;
-    } else if (q.s.interval_expire == 0) {
-        q.s.interval_expire = now + kInterval;
-    } else if (now >= q.s.interval_expire) {
-        *ok_to_drop = true;
-    }
-    return e.pkt;
-}
-
-// _routerqueuecodel_controlLaw (:198-204), as written (not RFC 8289's
-// ts + interval / sqrt(count))
-__device__ __forceinline__ uint64_t control_law(uint32_t count, uint64_t ts) {
-    const uint64_t new_ts = ts + kInterval;
-    const double result = (double)new_ts / sqrt((double)count);
-    return (uint64_t)round(result);
-}
-
-// _routerqueuecodel_dequeue (:206-265)
-__device__ int64_t dequeue(Router& q, uint64_t now) {
-    bool ok = false;
-    int64_t pkt = dequeue_helper(q, now, &ok);
-    if (pkt < 0) {
-        q.s.mode = 0; // empty queue: leave dropping state
-        return pkt;
-    }
-    if (q.s.mode == 1) {
-        if (!ok) q.s.mode = 0; // delays low again
-        while (now >= q.s.next_drop && q.s.mode == 1) {
-            drop(q, (uint32_t)pkt);
-            q.s.drop_count++;
-            pkt = dequeue_helper(q, now, &ok);
-            if (ok) q.s.next_drop = control_law(q.s.drop_count, q.s.next_drop);
-            else q.s.mode = 0;
-        }
-    } else if (ok) {
-        drop(q, (uint32_t)pkt);
-        pkt = dequeue_helper(q, now, &ok);
-        q.s.mode = 1;
-        const uint32_t delta = q.s.drop_count - q.s.drop_count_last;
-        q.s.drop_count = 1;
-        const bool recently = now < q.s.next_drop + 16 * kInterval;
-        if (recently && delta > 1) q.s.drop_count = delta;
-        q.s.next_drop = control_law(q.s.drop_count, now);
-        q.s.drop_count_last = q.s.drop_count;
-    }
-    return pkt;
-}
 
 __global__ __launch_bounds__(256) void k_codel(uint32_t nrouters, const uint32_t* __restrict__ op_off,
                                                const ShdCodelOp* __restrict__ ops, ShdCodelState* __restrict__ states,
@@ -113,32 +47,36 @@ __global__ __launch_bounds__(256) void k_codel(uint32_t nrouters, const uint32_t
                                                int* __restrict__ err) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nrouters) return;
-    Router q{states[r], rings + (size_t)r * ring_cap, ring_cap, fate, 0, false};
+    ShdCodelState st = states[r];
+    Router q{rings + (size_t)r * ring_cap, ring_cap, fate, 0, false, st.head, st.len};
     for (uint32_t i = op_off[r]; i < op_off[r + 1]; i++) {
         const ShdCodelOp o = ops[i];
         q.op = i;
         if (o.kind == 0) { // router_enqueue -> _routerqueuecodel_enqueue (:113-137)
-            if (q.s.len == q.cap) {
+            if (q.len == q.cap) {
                 atomicOr(err, 1); // the caller's ring is too small (the reference queue is unbounded)
                 break;
             }
-            uint32_t tail = q.s.head + q.s.len;
+            uint32_t tail = q.head + q.len;
             if (tail >= q.cap) tail -= q.cap;
             q.ring[tail] = ShdCodelEntry{o.time, o.pkt, o.length};
-            q.s.len++;
-            q.s.total_size += o.length;
+            q.len++;
+            st.total_size += o.length;
             deq_out[i] = o.pkt; // PDS_ROUTER_ENQUEUED
         } else { // router_dequeue
-            const int64_t p = dequeue(q, o.time);
-            deq_out[i] = p < 0 ? 0xffffffffu : (uint32_t)p;
-            if (p >= 0) fate[p] = ((uint64_t)i << 2) | SHD_CODEL_DEQUEUED; // PDS_ROUTER_DEQUEUED
+            ShdCodelEntry e;
+            const bool got = shd_codel::dequeue(q, st, o.time, e);
+            deq_out[i] = got ? e.pkt : 0xffffffffu;
+            if (got) fate[e.pkt] = ((uint64_t)i << 2) | SHD_CODEL_DEQUEUED; // PDS_ROUTER_DEQUEUED
             if (q.bad) {
                 atomicOr(err, 2);
                 break;
             }
         }
     }
-    states[r] = q.s;
+    st.head = q.head;
+    st.len = q.len;
+    states[r] = st;
 }
 
 int hip_status(hipError_t e, const char* what) {

@@ -1,0 +1,340 @@
+// nic.hip -- the hosts' network interfaces on gfx950:
+// the upstream router with CoDel (routing/router.c:103-131,
+// router_queue_codel.c:113-267) feeding the receive token bucket, and the
+// send token bucket shaping the sender side (host/network_interface.c:
+// 99-194 buckets and refills, :448-482 receivePackets, :571-631 sendPackets,
+// :633-661 wantsSend).  One lane per host, every host of a window at once.
+//
+// A host's interface is a sequential state machine driven by three event
+// streams, merged here in the order the host's event queue would run them
+// (event_compare, core/work/event.c:109-152: time, then source host, then
+// the source's event id):
+//   - arrivals: the host's delivered events from the hand-off, already in
+//     event_compare order (shd_round_process_device / shd_deliv_sort_device
+//     segments, read in place) -> router_enqueue, and receivePackets when
+//     the router queue was empty;
+//   - send requests: packets the host's sockets offer to the interface, in
+//     qdisc order, each with the time it was offered (wantsSend) ->
+//     sendPackets;
+//   - refill tasks (every 1 ms on the grid started at
+//     networkinterface_startRefillingTokenBuckets, scheduled only while a
+//     bucket is below capacity) -> refill both buckets, receivePackets,
+//     sendPackets.
+// Refill tasks and send requests are the host's own events (source = the
+// host); arrivals come from other hosts, so at equal times the source host
+// id decides.  Between a refill and a send request at the same nanosecond
+// the source event ids decide in the reference; they are not in the inputs,
+// and the send request goes first (documented assumption).
+//
+// Router queue layout: the entries a window leaves queued are kept in a
+// per-host ring (ShdCodelEntry); the window's own arrivals are queued in
+// place -- the FIFO tail is always a contiguous run of the host's arrival
+// segment -- so no entry is copied unless it outlives the window.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+
+#include "codel_dev.h"
+#include "shd_internal.h"
+
+namespace {
+
+constexpr uint64_t kRefillInterval = 1000000ull; // _networkinterface_getRefillInterval (:99-101): 1 ms
+constexpr uint64_t kMtu = shd_codel::kMtu;
+constexpr uint64_t kNever = ~0ull;
+
+enum { kErrRing = 1, kErrOrder = 2, kErrHost = 4, kErrId = 8, kErrWindow = 16, kErrAssert = 32 };
+
+struct RouterQ {
+    // carried entries (ring) first, then the window's arrivals [qhead, qtail)
+    ShdCodelEntry* ring;
+    uint32_t cap, head, len;
+    const ShdDeliv* ev;
+    const uint32_t* evlen;
+    uint32_t qhead, qtail, id_base;
+    uint64_t* rtime;
+    uint8_t* rstat;
+    bool bad;
+
+    __device__ __forceinline__ bool empty() const { return len == 0 && qhead == qtail; }
+    __device__ __forceinline__ bool pop(ShdCodelEntry& e) {
+        if (len) {
+            e = ring[head];
+            head = head + 1 == cap ? 0 : head + 1;
+            len--;
+            return true;
+        }
+        if (qhead == qtail) return false;
+        e = ShdCodelEntry{ev[qhead].time, id_base + qhead, evlen[qhead]};
+        qhead++;
+        return true;
+    }
+    __device__ __forceinline__ void drop(uint32_t id) { // PDS_ROUTER_DROPPED
+        rstat[id] = SHD_NIC_DROPPED;
+    }
+};
+
+// _networkinterface_consumeTokenBucket (:117-125)
+__device__ __forceinline__ void consume(uint64_t& remaining, uint64_t bytes) {
+    remaining = bytes >= remaining ? 0 : remaining - bytes;
+}
+
+// _networkinterface_scheduleNextRefillIfNeeded (:151-164)
+__device__ __forceinline__ void schedule_if_needed(ShdNicState& s, uint64_t now) {
+    const bool need = s.send_remaining < s.send_capacity || s.recv_remaining < s.recv_capacity;
+    if (need && !s.refill_pending) {
+        const uint64_t since = (now - s.refill_start) % kRefillInterval;
+        s.refill_time = now + (kRefillInterval - since);
+        s.refill_pending = 1;
+    }
+}
+
+struct Host {
+    ShdNicState s;
+    RouterQ q;
+    const ShdNicSend* sends;
+    uint32_t sq, sk; // send queue: offered but not sent [sq, sk)
+    uint64_t* stime;
+    uint64_t boot_end;
+
+    // networkinterface_receivePackets (:448-482)
+    __device__ void receive(uint64_t now) {
+        const bool boot = now < boot_end;
+        while (boot || s.recv_remaining >= kMtu) {
+            ShdCodelEntry e;
+            if (!shd_codel::dequeue(q, s.router, now, e)) break; // router_dequeue (router.c:123-131)
+            q.rtime[e.pkt] = now;
+            q.rstat[e.pkt] = SHD_NIC_RECEIVED;
+            if (!boot) {
+                consume(s.recv_remaining, e.length);
+                schedule_if_needed(s, now);
+            }
+        }
+    }
+    // _networkinterface_sendPackets (:571-631); no bootstrap term in the loop
+    // condition, but no consumption while bootstrapping
+    __device__ void send(uint64_t now) {
+        const bool boot = now < boot_end;
+        while (s.send_remaining >= kMtu && sq < sk) {
+            const ShdNicSend p = sends[sq];
+            stime[sq] = now;
+            sq++;
+            if (!boot) {
+                consume(s.send_remaining, p.length);
+                schedule_if_needed(s, now);
+            }
+        }
+    }
+    // _networkinterface_refillTokenBucketsCB (:166-186)
+    __device__ void refill(uint64_t now) {
+        s.refill_pending = 0;
+        s.recv_remaining += s.recv_refill; // _networkinterface_refillTokenBucket (:108-115)
+        if (s.recv_remaining > s.recv_capacity) s.recv_remaining = s.recv_capacity;
+        s.send_remaining += s.send_refill;
+        if (s.send_remaining > s.send_capacity) s.send_remaining = s.send_capacity;
+        receive(now);
+        send(now);
+        schedule_if_needed(s, now);
+    }
+};
+
+__global__ __launch_bounds__(256) void k_nic_init(uint32_t n, const uint64_t* __restrict__ down,
+                                                  const uint64_t* __restrict__ up, uint64_t start,
+                                                  ShdNicState* __restrict__ st) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n) return;
+    // _networkinterface_setupTokenBuckets (:196-228): capacity = refill + MTU
+    const uint64_t factor = 1000000000ull / kRefillInterval;
+    ShdNicState s{};
+    s.recv_refill = down[h] * 1024 / factor;
+    s.send_refill = up[h] * 1024 / factor;
+    s.recv_capacity = s.recv_refill + kMtu;
+    s.send_capacity = s.send_refill + kMtu;
+    // networkinterface_startRefillingTokenBuckets (:188-194): the first
+    // refill runs at once on empty buckets
+    s.refill_start = start;
+    s.refill_pending = 0;
+    s.recv_remaining = s.recv_refill;
+    s.send_remaining = s.send_refill;
+    schedule_if_needed(s, start);
+    st[h] = s;
+}
+
+__global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, const ShdDeliv* __restrict__ ev,
+                                                const uint32_t* __restrict__ eoff, const uint32_t* __restrict__ elen,
+                                                const ShdNicSend* __restrict__ sends,
+                                                const uint32_t* __restrict__ soff, uint64_t window_end,
+                                                uint64_t boot_end, ShdNicState* __restrict__ states,
+                                                ShdCodelEntry* __restrict__ rings, uint32_t ring_cap,
+                                                uint32_t id_base, uint64_t* __restrict__ rtime,
+                                                uint8_t* __restrict__ rstat, uint64_t fate_cap,
+                                                uint64_t* __restrict__ stime, int* __restrict__ err) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n) return;
+    const uint32_t self = host_base + h;
+    Host H;
+    H.s = states[h];
+    uint32_t i = eoff[h];
+    const uint32_t iend = eoff[h + 1];
+    H.q = RouterQ{rings + (size_t)h * ring_cap, ring_cap, H.s.router.head, H.s.router.len, ev, elen, i, i, id_base,
+                  rtime, rstat, false};
+    H.sends = sends;
+    H.sq = H.sk = soff ? soff[h] : 0;
+    const uint32_t kend = soff ? soff[h + 1] : 0;
+    H.stime = stime;
+    H.boot_end = boot_end;
+    int bad = 0;
+    if ((uint64_t)id_base + iend > fate_cap) bad |= kErrId;
+    uint64_t last = 0;
+    // every lane ends: at most this many events (a host whose bucket refills
+    // by 0 bytes per ms schedules a refill every ms for ever, as the reference)
+    uint64_t budget = (uint64_t)(iend - i) + (kend - H.sk) + (1ull << 24);
+    while (!bad) {
+        if (budget-- == 0) {
+            bad |= kErrWindow;
+            break;
+        }
+        const bool have_a = i < iend;
+        const bool have_s = H.sk < kend;
+        const bool have_r = H.s.refill_pending && H.s.refill_time < window_end;
+        if (!have_a && !have_s && !have_r) break;
+        ShdDeliv a;
+        if (have_a) a = ev[i];
+        const uint64_t ta = have_a ? a.time : kNever;
+        const uint64_t ts = have_s ? sends[H.sk].ready : kNever;
+        const uint64_t tr = have_r ? H.s.refill_time : kNever;
+        // the host's own next event: a send request before a refill at equal times
+        const bool own_is_send = have_s && (!have_r || ts <= tr);
+        const uint64_t town = own_is_send ? ts : tr;
+        const bool own_exists = have_s || have_r;
+        if (have_a && (!own_exists || ta < town || (ta == town && a.src_host < self))) {
+            if (a.dst_host != self) bad |= kErrHost;
+            if (ta < last) bad |= kErrOrder;
+            if (ta >= window_end) bad |= kErrWindow;
+            if (bad) break;
+            last = ta;
+            // router_enqueue (router.c:103-121): peek, enqueue, receive if it was empty
+            const bool buffered = !H.q.empty();
+            H.q.qtail = ++i;
+            H.s.router.total_size += elen[i - 1]; // _routerqueuecodel_enqueue (:113-136)
+            if (!buffered) H.receive(ta);
+        } else if (own_is_send) {
+            if (ts >= window_end) {
+                bad |= kErrWindow;
+                break;
+            }
+            H.sk++; // networkinterface_wantsSend (:633-661)
+            H.send(ts);
+        } else {
+            H.refill(tr);
+        }
+        if (H.q.bad) bad |= kErrAssert;
+    }
+    // the window's arrivals still queued move to the ring
+    while (!bad && H.q.qhead < H.q.qtail) {
+        if (H.q.len == H.q.cap) {
+            bad |= kErrRing;
+            break;
+        }
+        const uint32_t k = H.q.qhead++;
+        uint32_t tail = H.q.head + H.q.len;
+        if (tail >= H.q.cap) tail -= H.q.cap;
+        H.q.ring[tail] = ShdCodelEntry{ev[k].time, id_base + k, elen[k]};
+        H.q.len++;
+    }
+    if (bad) atomicOr(err, bad);
+    H.s.router.head = H.q.head;
+    H.s.router.len = H.q.len;
+    states[h] = H.s;
+}
+
+__global__ void k_event_lengths(size_t n, const ShdDeliv* __restrict__ ev, const ShdPkt* __restrict__ pk,
+                                uint32_t header, uint32_t* __restrict__ len) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) len[i] = pk[ev[i].pkt_index].payload_len + header;
+}
+
+int hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+} // namespace
+
+extern "C" int shd_nic_init(uint32_t nhosts, const uint64_t* d_bw_down_kibps, const uint64_t* d_bw_up_kibps,
+                            uint64_t start_time, ShdNicState* d_states, void* stream) {
+    if (!nhosts) return 0;
+    if (!d_bw_down_kibps || !d_bw_up_kibps || !d_states) return -EINVAL;
+    hipLaunchKernelGGL(k_nic_init, dim3((nhosts + 255) / 256), dim3(256), 0, (hipStream_t)stream, nhosts,
+                       d_bw_down_kibps, d_bw_up_kibps, start_time, d_states);
+    return hip_status(hipGetLastError(), "k_nic_init launch");
+}
+
+extern "C" int shd_event_lengths(const ShdDeliv* d_events, size_t n, const ShdPkt* d_pkts, uint32_t header_bytes,
+                                 uint32_t* d_lengths, void* stream) {
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_event_lengths, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+                       d_events, d_pkts, header_bytes, d_lengths);
+    return hip_status(hipGetLastError(), "k_event_lengths launch");
+}
+
+extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* d_events,
+                           const uint32_t* d_event_offsets, const uint32_t* d_event_lengths, const ShdNicSend* d_sends,
+                           const uint32_t* d_send_offsets, uint64_t window_end, uint64_t bootstrap_end,
+                           ShdNicState* d_states, ShdCodelEntry* d_rings, uint32_t ring_cap, uint32_t id_base,
+                           uint64_t* d_recv_time, uint8_t* d_recv_status, uint64_t fate_cap, uint64_t* d_send_time,
+                           void* stream) {
+    if (!nhosts) return 0;
+    if (!d_event_offsets || !d_states || !d_rings || !ring_cap || !d_recv_time || !d_recv_status)
+        return shd_fail(-EINVAL, "missing buffer");
+    if (d_send_offsets && (!d_sends || !d_send_time)) return shd_fail(-EINVAL, "send offsets without sends");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t range[2];
+    int rc = hip_status(hipMemcpyAsync(range, d_event_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+    if (!rc) rc = hip_status(hipMemcpyAsync(range + 1, d_event_offsets + nhosts, sizeof(uint32_t),
+                                            hipMemcpyDeviceToHost, s), "D2H");
+    uint32_t srange[2] = {0, 0};
+    if (!rc && d_send_offsets) {
+        rc = hip_status(hipMemcpyAsync(srange, d_send_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
+        if (!rc) rc = hip_status(hipMemcpyAsync(srange + 1, d_send_offsets + nhosts, sizeof(uint32_t),
+                                                hipMemcpyDeviceToHost, s), "D2H");
+    }
+    if (!rc) rc = hip_status(hipStreamSynchronize(s), "offsets");
+    if (rc) return rc;
+    if (range[1] > range[0] && (!d_events || !d_event_lengths)) return shd_fail(-EINVAL, "events without lengths");
+    if ((uint64_t)id_base + range[1] > fate_cap) return shd_fail(-ERANGE, "packet ids exceed the fate arrays");
+    int* d_err = nullptr;
+    if ((rc = hip_status(hipMalloc((void**)&d_err, sizeof(int)), "hipMalloc nic"))) return rc;
+    int h_err = 0;
+    // the window's arrivals start as "queued"; unsent requests keep ~0
+    rc = hip_status(hipMemsetAsync(d_err, 0, sizeof(int), s), "memset");
+    if (!rc && range[1] > range[0])
+        rc = hip_status(hipMemsetAsync(d_recv_status + id_base + range[0], SHD_NIC_QUEUED, range[1] - range[0], s),
+                        "memset");
+    if (!rc && range[1] > range[0])
+        rc = hip_status(hipMemsetAsync(d_recv_time + id_base + range[0], 0xff,
+                                       sizeof(uint64_t) * (range[1] - range[0]), s), "memset");
+    if (!rc && srange[1] > srange[0])
+        rc = hip_status(hipMemsetAsync(d_send_time + srange[0], 0xff, sizeof(uint64_t) * (srange[1] - srange[0]), s),
+                        "memset");
+    if (!rc) {
+        hipLaunchKernelGGL(k_nic_run, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base, d_events,
+                           d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end, bootstrap_end,
+                           d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status, fate_cap, d_send_time,
+                           d_err);
+        rc = hip_status(hipGetLastError(), "k_nic_run launch");
+    }
+    if (!rc) rc = hip_status(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s), "D2H");
+    if (!rc) rc = hip_status(hipStreamSynchronize(s), "k_nic_run");
+    (void)hipFree(d_err);
+    if (rc) return rc;
+    if (h_err & kErrRing) return shd_fail(-ENOSPC, "a router queue outgrew its ring (capacity %u)", ring_cap);
+    if (h_err & kErrHost) return shd_fail(-EINVAL, "an event in a host's segment is addressed to another host");
+    if (h_err & kErrOrder) return shd_fail(-EINVAL, "a host's events are not in time order");
+    if (h_err & kErrWindow)
+        return shd_fail(-EINVAL, "an event or send request at or after the window end, or more than 2^24 refills "
+                                 "in one window");
+    if (h_err & kErrId) return shd_fail(-ERANGE, "packet ids exceed the fate arrays");
+    if (h_err & kErrAssert) return shd_fail(-EINVAL, "router dequeue before an entry's enqueue time");
+    return 0;
+}

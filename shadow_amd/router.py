@@ -102,3 +102,72 @@ def trace_from_arrivals(router: np.ndarray, arrival: np.ndarray, length: np.ndar
     off = np.zeros(nrouters + 1, dtype=np.uint32)
     np.cumsum(np.bincount(r2, minlength=nrouters), out=off[1:])
     return off, ops
+
+
+# ---- network interfaces (shd_nic_*) -------------------------------------
+
+NIC_STATE_DTYPE = np.dtype([("recv_remaining", "<u8"), ("recv_refill", "<u8"), ("recv_capacity", "<u8"),
+                            ("send_remaining", "<u8"), ("send_refill", "<u8"), ("send_capacity", "<u8"),
+                            ("refill_start", "<u8"), ("refill_time", "<u8"), ("refill_pending", "<u4"),
+                            ("pad0", "<u4"), ("pad1", "<u8"), ("router", STATE_DTYPE)])
+SEND_DTYPE = np.dtype([("ready", "<u8"), ("id", "<u4"), ("length", "<u4")])
+NIC_QUEUED, NIC_RECEIVED, NIC_DROPPED = 0, 1, 2
+NEVER = 0xFFFFFFFFFFFFFFFF
+HEADER_UDP, HEADER_TCP = 42, 66  # CONFIG_HEADER_SIZE_UDPIPETH / _TCPIPETH (definitions.h:173-180)
+assert NIC_STATE_DTYPE.itemsize == 128
+
+
+class Interfaces:
+    """Network interfaces of hosts [host_base, host_base + n): token buckets,
+    refill grid and upstream CoDel router per host, resident on the device
+    (host/network_interface.c + routing/router.c)."""
+
+    def __init__(self, n: int, bw_down_kibps, bw_up_kibps, start_time: int, ring_cap: int, fate_cap: int,
+                 host_base: int = 0, device="cuda"):
+        self.n, self.base, self.cap, self.device = n, host_base, ring_cap, torch.device(device)
+        self.states = torch.zeros(n * NIC_STATE_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+        self.rings = torch.zeros(n * ring_cap * ENTRY_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+        self.recv_time = torch.full((fate_cap,), -1, dtype=torch.int64, device=self.device)
+        self.recv_status = torch.zeros(fate_cap, dtype=torch.uint8, device=self.device)
+        self.fate_cap = fate_cap
+        dn = torch.as_tensor(np.asarray(bw_down_kibps, dtype=np.uint64).view(np.int64), device=self.device)
+        up = torch.as_tensor(np.asarray(bw_up_kibps, dtype=np.uint64).view(np.int64), device=self.device)
+        check(lib().shd_nic_init(n, dn.data_ptr(), up.data_ptr(), start_time, self.states.data_ptr(), None))
+        torch.cuda.synchronize(self.device)
+
+    def run_device(self, d_events: int, d_offsets: int, d_lengths: int, window_end: int, bootstrap_end: int = 0,
+                   id_base: int = 0, d_sends: int = 0, d_send_offsets: int = 0, d_send_time: int = 0, stream=0):
+        """shd_nic_run on device buffers (raw pointers)."""
+        check(lib().shd_nic_run(self.n, self.base, d_events or None, d_offsets, d_lengths or None, d_sends or None,
+                                d_send_offsets or None, window_end, bootstrap_end, self.states.data_ptr(),
+                                self.rings.data_ptr(), self.cap, id_base, self.recv_time.data_ptr(),
+                                self.recv_status.data_ptr(), self.fate_cap, d_send_time or None, stream))
+
+    def run(self, events: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, window_end: int,
+            bootstrap_end: int = 0, id_base: int = 0, sends: np.ndarray | None = None,
+            send_offsets: np.ndarray | None = None):
+        """Host arrays in, send times out (receive fates stay in
+        recv_time / recv_status, indexed by packet id)."""
+        d_ev = _dev(events, self.device) if len(events) else None
+        d_off = _dev(np.asarray(offsets, dtype=np.uint32), self.device)
+        d_len = _dev(np.asarray(lengths, dtype=np.uint32), self.device) if len(events) else None
+        d_s = d_so = d_st = None
+        if sends is not None:
+            d_s = _dev(sends.astype(SEND_DTYPE), self.device) if len(sends) else torch.empty(16, dtype=torch.uint8,
+                                                                                             device=self.device)
+            d_so = _dev(np.asarray(send_offsets, dtype=np.uint32), self.device)
+            d_st = torch.empty(max(len(sends), 1), dtype=torch.int64, device=self.device)
+        torch.cuda.synchronize(self.device)
+        self.run_device(d_ev.data_ptr() if d_ev is not None else 0, d_off.data_ptr(),
+                        d_len.data_ptr() if d_len is not None else 0, window_end, bootstrap_end, id_base,
+                        d_s.data_ptr() if d_s is not None else 0, d_so.data_ptr() if d_so is not None else 0,
+                        d_st.data_ptr() if d_st is not None else 0)
+        if d_st is None:
+            return None
+        return d_st.cpu().numpy().view(np.uint64)[:len(sends)].copy()
+
+    def state(self) -> np.ndarray:
+        return self.states.cpu().numpy().view(NIC_STATE_DTYPE).copy()
+
+    def fates(self):
+        return (self.recv_time.cpu().numpy().view(np.uint64).copy(), self.recv_status.cpu().numpy().copy())

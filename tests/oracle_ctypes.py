@@ -77,6 +77,10 @@ lib.orc_round_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c
 lib.orc_pq_order.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p]
 lib.orc_topology_log_cached_paths.restype = C.c_size_t
 lib.orc_topology_log_cached_paths.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+lib.orc_nic_init.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+lib.orc_nic_run.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                            C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p,
+                            C.c_void_p, C.c_uint64, C.c_void_p]
 lib.orc_codel_run.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                               C.c_void_p]
 
@@ -245,6 +249,40 @@ class OracleRouters:
         st = self.states[r]
         ring = self.rings[r * self.cap:(r + 1) * self.cap]
         return ring[(int(st["head"]) + np.arange(int(st["len"]))) % self.cap].copy()
+
+
+class OracleInterfaces:
+    """orc_nic_*: the same records as shadow_amd.router.Interfaces, on the host."""
+
+    def __init__(self, n, bw_down_kibps, bw_up_kibps, start_time, ring_cap, fate_cap, host_base=0):
+        from shadow_amd.router import ENTRY_DTYPE, NIC_STATE_DTYPE
+        self.n, self.base, self.cap, self.fate_cap = n, host_base, ring_cap, fate_cap
+        self.states = np.zeros(n, dtype=NIC_STATE_DTYPE)
+        self.rings = np.zeros(n * ring_cap, dtype=ENTRY_DTYPE)
+        self.recv_time = np.full(fate_cap, np.uint64(0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+        self.recv_status = np.zeros(fate_cap, dtype=np.uint8)
+        dn = np.ascontiguousarray(bw_down_kibps, dtype=np.uint64)
+        up = np.ascontiguousarray(bw_up_kibps, dtype=np.uint64)
+        lib.orc_nic_init(n, dn.ctypes.data, up.ctypes.data, start_time, self.states.ctypes.data)
+
+    def run(self, events, offsets, lengths, window_end, bootstrap_end=0, id_base=0, sends=None, send_offsets=None):
+        from shadow_amd.router import SEND_DTYPE
+        events = np.ascontiguousarray(events)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        st = None
+        sp = sop = stp = None
+        if sends is not None:
+            sends = np.ascontiguousarray(sends.astype(SEND_DTYPE))
+            send_offsets = np.ascontiguousarray(send_offsets, dtype=np.uint32)
+            st = np.zeros(max(len(sends), 1), dtype=np.uint64)
+            sp, sop, stp = sends.ctypes.data, send_offsets.ctypes.data, st.ctypes.data
+        rc = lib.orc_nic_run(self.n, self.base, events.ctypes.data, offsets.ctypes.data, lengths.ctypes.data, sp, sop,
+                             window_end, bootstrap_end, self.states.ctypes.data, self.rings.ctypes.data, self.cap,
+                             id_base, self.recv_time.ctypes.data, self.recv_status.ctypes.data, self.fate_cap, stp)
+        if rc:
+            raise ValueError(f"orc_nic_run: {rc}")
+        return None if st is None else st[:len(sends)]
 
 
 def parse_time_ns(s):
