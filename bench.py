@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--vertices", type=int, default=20_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-routing", action="store_true")
+    ap.add_argument("--no-nic", action="store_true", help="skip the receive-side interface leg (§8f-2/-4)")
     ap.add_argument("--c4", type=int, default=1, help="1: also time the C4 routing build (V=100k, H=200k)")
     ap.add_argument("--c4-vertices", type=int, default=100_000)
     ap.add_argument("--c4-hosts", type=int, default=200_000)
@@ -283,6 +284,10 @@ def main():
         "gpu_state": {"before_timed": state_before, "after_timed": gpu_state(local) if rank == 0 else None},
     }
 
+    # ------------------------------------------- receive side (§8f-2 / -4)
+    if not args.no_nic and world == 1:
+        result["nic"] = nic_leg(lib, top, d_recs, d_out, d_off, delivered, H, dev, stream)
+
     # ------------------------------------------------------------ C1 routing
     if not args.no_routing:
         g1 = synth.complete_graph_gml(1000, 0x5EED0001)
@@ -431,6 +436,54 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+BYTES_NIC_PER_EVENT = 32 + 4 + 8 + 1  # event record + length in; receive time + status out
+BYTES_NIC_PER_HOST = 2 * 128            # interface state read + written
+
+
+def nic_leg(lib, top, d_recs, d_out, d_off, delivered, H, dev, stream, reps=5):
+    """The round's delivered events, per destination segment in place, run
+    through every host's interface (upstream CoDel router + receive token
+    bucket + refill grid; shd_nic_run), 1 Gbit/s links, UDP headers."""
+    import torch
+
+    from shadow_amd.router import HEADER_UDP, Interfaces
+    _lib_check = __import__("shadow_amd._lib", fromlist=["check"]).check
+    sptr = stream.cuda_stream
+    d_len = torch.empty(max(delivered, 1), dtype=torch.int32, device=dev)
+    _lib_check(lib.shd_event_lengths(d_out.data_ptr(), delivered, d_recs.data_ptr(), HEADER_UDP, d_len.data_ptr(),
+                                     sptr))
+    times = d_out.view(torch.int64).view(-1, 4)[:delivered, 0]
+    tmax = int(times.max().item()) if delivered else 0
+    gbit = 1_000_000_000 // 8 // 1024  # KiB/s
+    bw = np.full(H, gbit, dtype=np.uint64)
+    nic = Interfaces(H, bw, bw, 100_000_000, 4096, max(delivered, 1), device=dev)
+    states0 = nic.states.clone()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = []
+    for r in range(reps + 1):
+        nic.states.copy_(states0)
+        torch.cuda.synchronize(dev)
+        ev0.record(stream)
+        nic.run_device(d_out.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), tmax + 1, 0, 0, stream=sptr)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        if r:
+            ms.append(ev0.elapsed_time(ev1))
+    t = float(np.mean(ms))
+    _, stat = nic.fates()
+    alg = BYTES_NIC_PER_EVENT * delivered + BYTES_NIC_PER_HOST * H
+    return {
+        "config": "C3 round output (%d events over %d hosts), 1 Gbit/s interfaces, UDP headers, window to the last "
+                  "arrival" % (delivered, H),
+        "ms_per_round": t, "events_per_s": delivered / (t * 1e-3),
+        "received": int((stat[:delivered] == 1).sum()), "router_dropped": int((stat[:delivered] == 2).sum()),
+        "kernel": "k_nic_run (one lane per host; shd_nic_run incl. its memsets and offset reads)",
+        "roofline": {"bound": "hbm", "achieved": alg / (t * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
+                     "alg_bytes": "45 B per event (32 record + 4 length in, 8 time + 1 status out) + 256 B per host"},
+    }
 
 
 def cpu_rows_parallel(orc, sources, targets, threads):

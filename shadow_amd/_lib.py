@@ -78,6 +78,10 @@ PROTOS = {
     "shd_transport_rccl_free": (None, [_P]),
     "shd_memcpy": (C.c_int, [_P, _P, C.c_size_t]),
     "shd_topology_log_cached_paths": (C.c_int, [_P, PATH_LOG_FN, _P, _u64p]),
+    "shd_nic_init": (C.c_int, [C.c_uint32, _P, _P, C.c_uint64, _P, _P]),
+    "shd_event_lengths": (C.c_int, [_P, C.c_size_t, _P, C.c_uint32, _P, _P]),
+    "shd_nic_run": (C.c_int, [C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint64, C.c_uint64, _P, _P, C.c_uint32,
+                              C.c_uint32, _P, _P, C.c_uint64, _P, _P]),
     "shd_dns_new": (C.c_int, [C.POINTER(_P)]),
     "shd_dns_free": (None, [_P]),
     "shd_dns_register": (C.c_int, [_P, C.c_char_p, C.c_char_p, _u32p, _u32p, _ip]),
