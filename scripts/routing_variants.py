@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Times the slab routing kernel's measurement variants (same exact
-algorithm: SHD_SSSP_LAZYPOS, SHD_SSSP_SINK, SHD_SSSP_WAVES) on the C2 (and
-optionally C4) build and checks every variant's table is bitwise equal to
-the first one's.  Usage: routing_variants.py [--c4] VARIANT...
-VARIANT = "lazy=1,sink=5[,waves=N]"."""
+algorithm: SHD_SSSP_TOP = LDS heap positions per wave, SHD_SSSP_WAVES) on
+the C2 (and optionally C4) build and checks every variant's table is bitwise
+equal to the first one's.  Usage: routing_variants.py [--c4] VARIANT...
+VARIANT = "top=256[,waves=N]"."""
 import argparse
 import os
 import sys
@@ -32,8 +32,7 @@ def main():
         tab = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
         for v in a.variants:
             kv = dict(x.split("=") for x in v.split(","))
-            os.environ["SHD_SSSP_LAZYPOS"] = kv.get("lazy", "1")
-            os.environ["SHD_SSSP_SINK"] = kv.get("sink", "5")
+            os.environ["SHD_SSSP_TOP"] = kv.get("top", "256")
             if "waves" in kv:
                 os.environ["SHD_SSSP_WAVES"] = kv["waves"]
             else:

@@ -65,11 +65,18 @@ static uint64_t name_hash(const char* s) {
     return h;
 }
 
-static uint32_t slot_of(uint64_t key, uint32_t cap) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 32) & (cap - 1); }
+static uint32_t slot_of(uint64_t key, uint32_t cap) { /* splitmix64 finaliser */
+    key ^= key >> 30;
+    key *= 0xbf58476d1ce4e5b9ull;
+    key ^= key >> 27;
+    key *= 0x94d049bb133111ebull;
+    key ^= key >> 31;
+    return (uint32_t)key & (cap - 1);
+}
 
-static int map_grow(DnsMap* m) {
+static int map_grow_to(DnsMap* m, uint32_t want) {
     uint32_t ncap = m->cap ? m->cap * 2 : 1024;
-    while ((uint64_t)(m->n + 1) * 2 > ncap) ncap *= 2;
+    while ((uint64_t)(want + 1) * 2 > ncap) ncap *= 2;
     DnsSlot* ns = (DnsSlot*)malloc(sizeof(DnsSlot) * ncap);
     if (!ns) return -ENOMEM;
     for (uint32_t i = 0; i < ncap; i++) ns[i].idx = -1;
@@ -85,6 +92,8 @@ static int map_grow(DnsMap* m) {
     m->tomb = 0;
     return 0;
 }
+
+static int map_grow(DnsMap* m) { return map_grow_to(m, m->n); }
 
 /* the slot holding an entry accepted by `match`, or NULL */
 typedef int (*MatchFn)(const struct ShdDns* d, int32_t idx, const void* want);
@@ -216,6 +225,17 @@ int shd_dns_register_batch(ShdDns* d, uint32_t n, const char* const* names, cons
         if (!names[i]) return shd_fail(-EINVAL, "name %u is NULL", i);
     pthread_mutex_lock(&d->mu);
     int rc = 0;
+    /* size the maps and the address array for the whole batch up front */
+    const uint64_t want = (uint64_t)d->naddr + n;
+    if (want > UINT32_MAX / 4) rc = shd_fail(-ENOMEM, "too many addresses");
+    if (!rc && (uint64_t)(d->by_ip.n + d->by_ip.tomb + n) * 2 > d->by_ip.cap) rc = map_grow_to(&d->by_ip, d->by_ip.n + n);
+    if (!rc && (uint64_t)(d->by_name.n + d->by_name.tomb + n) * 2 > d->by_name.cap)
+        rc = map_grow_to(&d->by_name, d->by_name.n + n);
+    if (!rc && want > d->capaddr) {
+        DnsAddr* na = (DnsAddr*)realloc(d->addr, sizeof(DnsAddr) * want);
+        if (!na) rc = -ENOMEM;
+        else d->addr = na, d->capaddr = (uint32_t)want;
+    }
     for (uint32_t i = 0; i < n && !rc; i++) {
         int local = 0;
         rc = register_locked(d, names[i], requested_ips ? requested_ips[i] : NULL, ip_net ? &ip_net[i] : NULL,

@@ -95,9 +95,22 @@ static int prepare(ShdTopology* t) {
             rc = -ENOMEM;
             goto fail;
         }
-        for (int v = 0; v < t->V; v++) soff[v] = t->inc_off[v] + v;
+        /* a list handle packs the start (24 bits) with the number of entries
+         * a first read needs, sentinel included (8 bits; 255 = "255 or more":
+         * read whole batches) */
+        if (SM >= (1u << 24)) {
+            free(snb);
+            free(swr);
+            free(soff);
+            rc = shd_fail(-ENOTSUP, "graph too large for 24-bit incidence list handles (%zu entries)", SM);
+            goto fail;
+        }
         for (int v = 0; v < t->V; v++) {
-            size_t o = (size_t)soff[v];
+            const int32_t cnt = t->inc_off[v + 1] - t->inc_off[v] + 1;
+            soff[v] = ((t->inc_off[v] + v) << 8) | (cnt < 255 ? cnt : 255);
+        }
+        for (int v = 0; v < t->V; v++) {
+            size_t o = (size_t)(soff[v] >> 8);
             for (int32_t k = t->inc_off[v]; k < t->inc_off[v + 1]; k++, o++) {
                 snb[2 * o] = t->inc_nbr[k];
                 snb[2 * o + 1] = soff[t->inc_nbr[k]];

@@ -46,7 +46,7 @@
 
 namespace {
 
-constexpr int kTop = 256;       // heap positions in LDS for the slab kernel (levels 0..7)
+constexpr int kTopDefault = 256; // heap positions in LDS for the slab kernel (levels 0..7)
 constexpr int kSlabWaves = 4;   // independent waves per slab-kernel block
 constexpr int kWavesPerCU = 32; // gfx950: resident waves per CU
 constexpr int kLdsMaxV = 4096;  // 36 B per vertex -> 144 KiB of the 160 KiB LDS
@@ -88,7 +88,7 @@ __device__ __forceinline__ HNode uni_n(const HNode& x) { return HNode{uni_d(x.ke
 // most kTop) top positions.  The slab kernel's pop does not clear pos: a
 // popped vertex is never decreased again (alt = dist[u] + w >= dist[v] for
 // every popped v, weights > 0).  Neither changes a heap operation.
-template <bool kAll>
+template <bool kAll, int kTop = kTopDefault>
 struct Heap {
     HNode* top;
     HNode* rest;
@@ -346,13 +346,15 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
             const double ru = rel[u];
             // the list's first kRelax batches are loaded before the root is
             // removed: their latency overlaps the (LDS) sink
-            int b = t.so;
+            int b = t.so >> 8;
+            const int lim = (t.so & 255) == 255 ? 64 * kRelax : (t.so & 255); // entries worth reading
             int2 nb[kRelax];
             double2 wr[kRelax];
 #pragma unroll
-            for (int q = 0; q < kRelax; q++) {
-                nb[q] = snb[b + q * 64 + lane];
-                wr[q] = swr[b + q * 64 + lane];
+            for (int q = 0; q < kRelax; q++) { // (entries past the sentinel re-read it)
+                const int k = q * 64 + lane < lim ? q * 64 + lane : lim - 1;
+                nb[q] = snb[b + k];
+                wr[q] = swr[b + k];
             }
             h.pop_top(u);
             // kRelax batches are relaxed together (dist reads, then the
@@ -424,6 +426,7 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
 // g.soff[v], entries {nbr, soff[nbr]} in g.snb and {w, 1 - loss} in g.swr,
 // closed by {-1 or -2 (v attached), 0}; the arrays are padded by 64 x 16 entries,
 // so a 64-lane batch never reads past them.
+template <int kTop>
 __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80))) void k_sssp_slab(ShdGraphDev g, int row_lo, int row_hi,
                                                               ShdEntry* __restrict__ tab, char* __restrict__ slab,
                                                               size_t slab_stride) {
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
         const int src = g.slot_vertex[row];
         for (int v = lane; v < V; v += 64) dr[v].x = -1.0;
         wave_fence();
-        Heap<false> h{top, rest, pos, 0, lane};
+        Heap<false, kTop> h{top, rest, pos, 0, lane};
         dr[src] = make_double2(0.0, 1.0);
         h.push(src, 0.0, uni(g.soff[src]));
         int to_reach = A;
@@ -453,11 +456,15 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
             const HNode t = h.top_node(); // LDS
             const int u = t.v;
             const double mindist = -t.key;
-            int b = t.so;
-            // issued together: u's first 64 incidence entries, the last heap
-            // node (the removal sinks it) and rel[u]
-            int2 nb = snb[b + lane];
-            double2 wr = swr[b + lane];
+            int b = t.so >> 8;
+            // issued together: u's incidence entries (only as many lanes as
+            // the list has entries, sentinel included), the last heap node
+            // (the removal sinks it) and rel[u]
+            // lanes past the sentinel re-read it: their loads fall on lines
+            // the list already fetches, so a short list costs 1-2 requests
+            const int li = lane < (t.so & 255) ? lane : (t.so & 255) - 1;
+            int2 nb = snb[b + li];
+            double2 wr = swr[b + li];
             const int last = --h.n;
             const HNode xl = h.ld_raw(last);
             const double ru_l = dr[u].y;
@@ -595,7 +602,10 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         (rc = hip_status(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
                          "hipDeviceGetAttribute")))
         return rc;
-    long waves = (long)cus * kWavesPerCU;
+    // heap positions kept in LDS per wave (256: 32 waves/CU; 512: 20)
+    int top_n = kTopDefault;
+    if (const char* e = getenv("SHD_SSSP_TOP")) top_n = atoi(e) == 512 ? 512 : kTopDefault;
+    long waves = (long)cus * (top_n == 512 ? 20 : kWavesPerCU);
     if (const char* e = getenv("SHD_SSSP_WAVES")) {
         const long x = atol(e);
         if (x > 0) waves = x;
@@ -608,8 +618,20 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         if (grid <= 16) return shd_fail(-ENOMEM, "cannot allocate SSSP workspace");
         grid /= 2;
     }
-    hipLaunchKernelGGL(k_sssp_slab, dim3(grid), dim3(64 * kSlabWaves), sizeof(HNode) * kTop * kSlabWaves, nullptr,
-                       g, row_lo, row_hi, tab, slab, stride);
+    if (top_n == 512) {
+        const size_t lds = sizeof(HNode) * 512 * kSlabWaves;
+        if ((rc = hip_status(hipFuncSetAttribute((const void*)k_sssp_slab<512>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                             "hipFuncSetAttribute"))) {
+            (void)hipFree(slab);
+            return rc;
+        }
+        hipLaunchKernelGGL(k_sssp_slab<512>, dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo, row_hi, tab,
+                           slab, stride);
+    } else {
+        hipLaunchKernelGGL(k_sssp_slab<kTopDefault>, dim3(grid), dim3(64 * kSlabWaves),
+                           sizeof(HNode) * kTopDefault * kSlabWaves, nullptr, g, row_lo, row_hi, tab, slab, stride);
+    }
     rc = hip_status(hipGetLastError(), "k_sssp_slab launch");
     if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_slab");
     (void)hipFree(slab);

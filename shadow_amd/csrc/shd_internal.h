@@ -62,10 +62,12 @@ typedef struct {
     const double* inc_r;    /* M, 1 - packet_loss */
     const int32_t* slot_vertex; /* A */
     const int32_t* vertex_slot; /* V, -1 = not attached */
-    /* sentinel-terminated copy of the incidence lists for the slab kernel:
-     * v's list starts at soff[v] = inc_off[v] + v; entries {nbr, soff[nbr]}
-     * (snb, int2) and {w_ms, 1 - loss} (swr, double2), closed by {-1, 0}
-     * (-2 when v is attached); both padded by 64 x 16 entries */
+    /* sentinel-terminated copy of the incidence lists for the SSSP kernels:
+     * v's list handle soff[v] = (start << 8) | n, start = inc_off[v] + v and
+     * n = min(degree + 1, 255) entries to read first (sentinel included; 255
+     * = read whole batches); entries {nbr, soff[nbr]} (snb, int2) and
+     * {w_ms, 1 - loss} (swr, double2), closed by {-1, 0} (-2 when v is
+     * attached); both padded by 64 x 16 entries */
     const void* snb;
     const void* swr;
     const int32_t* soff; /* V */
