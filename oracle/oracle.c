@@ -1181,7 +1181,7 @@ int orc_compute_row(OrcTopo* t, int src, const int* targets, int ntargets, doubl
 static PathE* cache_get(OrcTopo* t, int s, int d) {
     if (!t->cache[s]) return NULL;
     PathE* p = &t->cache[s][d];
-    return p->present ? p : NULL;
+    return __atomic_load_n(&p->present, __ATOMIC_ACQUIRE) ? p : NULL;
 }
 
 /* controller_updateMinTimeJump (controller.c:141-153) */
@@ -1196,11 +1196,11 @@ static void cache_store(OrcTopo* t, int isDirect, int s, int d, double lat, doub
     if (!isDirect && !t->use_sp && get_eid(t, s, d) >= 0) return;
     if (!t->cache[s]) t->cache[s] = (PathE*)calloc((size_t)t->V, sizeof(PathE));
     PathE* p = &t->cache[s][d];
-    p->present = 1;
     p->is_direct = (unsigned char)isDirect;
     p->lat = lat;
     p->rel = rel;
     p->pkts = 0;
+    __atomic_store_n(&p->present, 1, __ATOMIC_RELEASE); /* last: orc_round_mt readers */
     if (t->min_lat == 0 || lat < t->min_lat) {
         t->min_lat = lat;
         t->min_updates++;
@@ -1300,15 +1300,17 @@ int orc_topology_preload_table(OrcTopo* t, const int* slots, int nslots, const d
     for (int v = 0; v < t->V && empty; v++) empty = t->cache[v] == NULL;
     if (empty) {
         /* Same stores, same order, without the lookups: on an empty cache
-         * row i's store of (s_i, s_j) succeeds exactly for j >= i (the
-         * reverse (s_j, s_i), j < i, was stored by the earlier row j). */
+         * row i's store of (s_i, s_j) succeeds exactly for j > i (the
+         * reverse (s_j, s_i), j < i, was stored by the earlier row j).  A row
+         * never stores its own vertex (topology.c:1744-1752): the self path
+         * is computed and stored by the first (X, X) lookup only. */
         for (int i = 0; i < nslots; i++) {
             int s = slots[i];
             if (!t->cache[s]) t->cache[s] = (PathE*)calloc((size_t)t->V, sizeof(PathE));
-            for (int j = i; j < nslots; j++) {
+            for (int j = i + 1; j < nslots; j++) {
                 PathE* p = &t->cache[s][slots[j]];
                 p->present = 1;
-                p->is_direct = (unsigned char)(i == j);
+                p->is_direct = 0;
                 p->lat = lat[(size_t)i * nslots + j];
                 p->rel = rel[(size_t)i * nslots + j];
                 p->pkts = 0;
@@ -1324,12 +1326,8 @@ int orc_topology_preload_table(OrcTopo* t, const int* slots, int nslots, const d
     for (int i = 0; i < nslots; i++) {
         int s = slots[i];
         for (int j = 0; j < nslots; j++) {
-            int d = slots[j];
-            if (i == j) {
-                cache_store(t, 1, s, s, lat[(size_t)i * nslots + j], rel[(size_t)i * nslots + j]);
-            } else {
-                cache_store(t, 0, s, d, lat[(size_t)i * nslots + j], rel[(size_t)i * nslots + j]);
-            }
+            if (i == j) continue; /* self paths: first (X, X) lookup only */
+            cache_store(t, 0, s, slots[j], lat[(size_t)i * nslots + j], rel[(size_t)i * nslots + j]);
         }
     }
     return 0;
@@ -1344,8 +1342,8 @@ int orc_topology_preload_rows(OrcTopo* t, const int* rows, int nrows, const int*
                               const double* rel) {
     for (int i = 0; i < nrows; i++)
         for (int j = 0; j < ncols; j++)
-            cache_store(t, rows[i] == cols[j], rows[i], cols[j], lat[(size_t)i * ncols + j],
-                        rel[(size_t)i * ncols + j]);
+            if (rows[i] != cols[j]) /* self paths: first (X, X) lookup only */
+                cache_store(t, 0, rows[i], cols[j], lat[(size_t)i * ncols + j], rel[(size_t)i * ncols + j]);
     return 0;
 }
 
@@ -1487,6 +1485,7 @@ typedef struct {
     int nthreads;
     size_t* qoff;
     OrcDeliv* out;
+    pthread_mutex_t miss_mu; /* a missing path (a first self path) is computed serially */
 } RoundMt;
 
 typedef struct {
@@ -1513,6 +1512,11 @@ static void* round_mt_send(void* arg) {
         const OrcPkt* p = &r->pkts[i];
         if ((int)(p->src_host % (uint32_t)r->nthreads) != a->tid) continue; /* this worker's hosts */
         PathE* e = cached_entry(r->t, r->host_ips[p->src_host], r->host_ips[p->dst_host]);
+        if (!e) { /* the reference's lookup (its writer lock): first (X, X) lookups */
+            pthread_mutex_lock(&r->miss_mu);
+            e = get_path_entry(r->t, r->host_ips[p->src_host], r->host_ips[p->dst_host]);
+            pthread_mutex_unlock(&r->miss_mu);
+        }
         if (!e) {
             a->missing++;
             continue;
@@ -1556,13 +1560,15 @@ static void* round_mt_pop(void* arg) {
 }
 
 /* Returns the number of delivered events, or (size_t)-1 if a packet's path
- * is not cached (preload first). */
+ * cannot be resolved.  Paths are expected to be preloaded; a missing one (a
+ * first self path: rows never store their own vertex) is computed by the
+ * serial lookup under miss_mu, as the reference's writer lock would. */
 size_t orc_round_mt(OrcTopo* t, const uint32_t* host_ips, uint32_t nhosts, uint64_t barrier, uint64_t end_time,
                     uint64_t bootstrap_end, const OrcPkt* pkts, size_t n, int nthreads, OrcDeliv* out,
                     uint8_t* status, uint64_t* min_time) {
     if (nthreads < 1) nthreads = 1;
     RoundMt r = {t, host_ips, nhosts, barrier, end_time, bootstrap_end, pkts, n, status, NULL, NULL, NULL, nthreads,
-                 NULL, out};
+                 NULL, out, PTHREAD_MUTEX_INITIALIZER};
     r.keys = (OrcEvKey*)malloc(sizeof(OrcEvKey) * (n ? n : 1));
     r.qs = (Pq*)calloc(nhosts ? nhosts : 1, sizeof(Pq));
     r.qlock = (pthread_mutex_t*)malloc(sizeof(pthread_mutex_t) * (nhosts ? nhosts : 1));

@@ -75,6 +75,7 @@ def test_batches_carry_state_on_device():
     off, ops = trace_from_arrivals(router, arr, length, nr, 15_000.0)
     G, R = CodelRouters(nr, 512), O.OracleRouters(nr, 512)
     cuts = [off[:-1] + (off[1:] - off[:-1]) * k // 3 for k in range(4)]
+    carried = False
     for b in range(3):
         idx = np.concatenate([np.arange(cuts[b][r], cuts[b + 1][r]) for r in range(nr)]).astype(np.int64)
         o = np.r_[0, np.cumsum(cuts[b + 1].astype(np.int64) - cuts[b])].astype(np.uint32)
@@ -82,7 +83,9 @@ def test_batches_carry_state_on_device():
         rc, deq_o, fate_o = R.run(o, ops[idx], len(router))
         assert rc == 0
         _compare(G, R, deq_g, fate_g, deq_o, fate_o)
-    assert (G.state()["len"] > 0).any()
+        if b < 2:  # packets queued at a batch boundary carry over (the trace drains by its end)
+            carried |= bool((G.state()["len"] > 0).any())
+    assert carried
 
 
 def test_errors_fail_loudly():
