@@ -3,7 +3,7 @@
 algorithm: SHD_SSSP_TOP = LDS heap positions per wave, SHD_SSSP_WAVES) on
 the C2 (and optionally C4) build and checks every variant's table is bitwise
 equal to the first one's.  Usage: routing_variants.py [--c4] VARIANT...
-VARIANT = "top=256[,waves=N]"."""
+VARIANT = "kern=blk|slab[,top=256|512][,wpe=7|8][,waves=N]"."""
 import argparse
 import os
 import sys
@@ -33,6 +33,8 @@ def main():
         for v in a.variants:
             kv = dict(x.split("=") for x in v.split(","))
             os.environ["SHD_SSSP_TOP"] = kv.get("top", "256")
+            os.environ["SHD_SSSP_KERNEL"] = kv.get("kern", "blk")
+            os.environ["SHD_SSSP_WPE"] = kv.get("wpe", "8")
             if "waves" in kv:
                 os.environ["SHD_SSSP_WAVES"] = kv["waves"]
             else:

@@ -208,9 +208,73 @@ struct Heap {
         }
         st(e, x, from);
     }
+    // Sink by blocks, data-parallel (slab kernel): the 62 nodes of the next
+    // 5 levels under e are loaded one per lane as in sink_blocks; the lanes
+    // then make every level's comparisons at once -- each left child lane
+    // compares with its sibling (DPP swap), every lane compares with x --
+    // and three ballots hand the scalar unit what the sequential walk would
+    // read: which children exist, which sibling is the larger one (the left
+    // on equality), which children x is smaller than.  The walk down the
+    // larger children is then a few scalar bit operations per level, and the
+    // nodes it moves are stored by their own lanes, each one level up, in one
+    // store instruction (plus one for their pos).  Same moves as sink_seq.
+    __device__ __forceinline__ void sink_dp(int e, const HNode& x, int from) {
+        const int j = 31 - __builtin_clz((unsigned)lane + 2);
+        const int bi = lane + 2 - (1 << j);
+        const bool inblk = lane < (2 << kSinkLevels) - 2;
+        for (;;) {
+            if (2 * e + 1 >= n) break;
+            const int p = (e + 1) * (1 << j) - 1 + bi;
+            const bool valid = inblk && p < n;
+            HNode c = HNode{0.0, 0, 0};
+            if (valid) {
+                if (p < kTop) {
+                    c = top[p];
+                    __asm__ volatile("; sink lds" ::: "memory");
+                } else {
+                    c = rest[p + 1];
+                    __asm__ volatile("; sink hbm" ::: "memory");
+                }
+            }
+            // the sibling's key: quad_perm(1, 0, 3, 2) swaps lanes 2i, 2i + 1
+            const long long kb = __double_as_longlong(c.key);
+            const unsigned slo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(kb & 0xffffffffll), 0xB1, 0xF, 0xF, false);
+            const unsigned shi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(kb >> 32), 0xB1, 0xF, 0xF, false);
+            const double ks = __longlong_as_double((long long)(((unsigned long long)shi << 32) | slo));
+            const unsigned long long vm = __ballot(valid);
+            const unsigned long long rm =
+                __ballot(valid && (lane & 1) == 0 && ((vm >> (lane + 1)) & 1ull) && !(c.key >= ks));
+            const unsigned long long lm = __ballot(valid && x.key < c.key);
+            unsigned long long mv = 0;
+            int lv = 0, li = 0;
+            for (; lv < kSinkLevels; lv++) {
+                const int cl = (2 << lv) - 2 + 2 * li; // lane of the left child
+                if (!((vm >> cl) & 1ull)) break;        // no child: x stays
+                const int cc = cl + (int)((rm >> cl) & 1ull);
+                if (!((lm >> cc) & 1ull)) break;        // x >= the larger child: x stays
+                mv |= 1ull << cc;
+                li = 2 * li + (cc - cl);
+            }
+            if ((mv >> lane) & 1ull) { // each moved node goes one level up
+                const int q = (p - 1) >> 1;
+                if (q < kTop) {
+                    top[q] = c;
+                    __asm__ volatile("; sink mv lds" ::: "memory");
+                } else {
+                    rest[q + 1] = c;
+                    __asm__ volatile("; sink mv hbm" ::: "memory");
+                }
+                if (q >= kTop) pos[c.v] = q + 2;
+                else if (p >= kTop) pos[c.v] = 1; // entered the LDS top
+            }
+            e = ((e + 1) << lv) - 1 + li; // the hole: the last moved node's old position
+            if (lv < kSinkLevels) break;
+        }
+        st(e, x, from);
+    }
     __device__ __forceinline__ void sink(int e, const HNode& x, int from) {
         if (kAll) sink_seq(e, x, from); // a level of LDS is a short round trip (C1 4.99 vs 5.17 ms)
-        else sink_blocks(e, x, from);
+        else sink_dp(e, x, from);
     }
     __device__ __forceinline__ void push(int v, double key, int so) {
         const int e = n++;
@@ -247,6 +311,301 @@ struct Heap {
             e = pv == 1 ? uni(find_top(v)) : pv - 2;
         }
         shift_up(e, HNode{key, v, so}, e);
+    }
+};
+
+// ---- blocked slab heap (k_sssp_blk) ----------------------------------------
+// The same igraph_2wheap (every comparison, move and tie rule of Heap above),
+// stored so that a heap operation costs few HBM requests.  Positions
+// [0, kBlkTop) -- levels 0..7 -- live in LDS.  Below, the heap is cut into
+// 3-level subtrees ("blocks": a root at level 8, 11, 14, ... with its 2
+// children and 4 grandchildren) of 7 nodes, stored BFS-ordered in one
+// 128-byte line (slot 7 unused).  A sink or shift-up then reads a level
+// triple with one line request and writes it back with one full-line store
+// (8 lanes x 16 B, no partial-line write), where the flat layout costs a
+// request per level for the node and another for its position.
+// pos[v]: 0 not queued / popped, 1 in the LDS top, b + 2 in block b: a node
+// moving inside its block keeps its pos (only moves across blocks write it);
+// a decrease-key loads the block and finds v among its 7 slots.
+// Lane-resident working set: lane L holds slot (L & 7) of one block in a
+// 16-lane region (a sibling pair of blocks: the children of a level-7 node or
+// of a block's bottom node are the roots of two consecutive blocks).
+constexpr int kBlkTop = 255;   // LDS heap positions (levels 0..7)
+constexpr int kBlkTopLv = 8;   // first HBM level
+
+__host__ __device__ __forceinline__ int blk_base(int k) { return (256 * ((1 << (3 * k)) - 1)) / 7; }
+
+// number of 128-B blocks that positions [kBlkTop, P] occupy (+1: pair loads)
+__host__ __forceinline__ size_t blk_count(long P) {
+    if (P < kBlkTop) return 2;
+    int L = 0;
+    while ((2L << L) <= P + 1) L++;
+    const int k = (L - kBlkTopLv) / 3, Lr = kBlkTopLv + 3 * k;
+    const long roots = P - (1L << Lr) + 2; // roots at level Lr with position <= P
+    return (size_t)blk_base(k) + (size_t)(roots < (1L << Lr) ? roots : (1L << Lr)) + 1;
+}
+
+struct BHeap {
+    HNode* top;   // LDS, kBlkTop (+1) nodes
+    HNode* blk;   // HBM blocks, 8 nodes each, 128-B aligned
+    int* pos;
+    int n;
+    int lane;
+    // this lane's slot of an operation's working blocks (local to each
+    // operation, so that it holds no registers between them)
+    struct W {
+        double k;
+        int v, s;
+    };
+
+    // position p >= kBlkTop -> block id and slot
+    __device__ __forceinline__ static void locate(int p, int& bid, int& idx) {
+        const int L = 31 - __builtin_clz((unsigned)p + 1);
+        const int k = (L - kBlkTopLv) / 3, Lr = kBlkTopLv + 3 * k, d = L - Lr;
+        const int r1 = (p + 1) >> d;
+        bid = blk_base(k) + r1 - (1 << Lr);
+        idx = (1 << d) - 1 + ((p + 1) & ((1 << d) - 1));
+    }
+    // position of the root of block bid
+    __device__ __forceinline__ static int root_pos(int bid) {
+        int k = 0;
+        while (blk_base(k + 1) <= bid) k++;
+        return bid - blk_base(k) + (1 << (kBlkTopLv + 3 * k)) - 1;
+    }
+    __device__ __forceinline__ static int slot_pos(int root, int idx) {
+        const int d = 31 - __builtin_clz((unsigned)idx + 1);
+        return ((root + 1) << d) + (idx - ((1 << d) - 1)) - 1;
+    }
+    // node in working lane l (uniform)
+    __device__ __forceinline__ static HNode lane_node(const W& w, int l) {
+        return HNode{readlane_d(w.k, l), __builtin_amdgcn_readlane(w.v, l), __builtin_amdgcn_readlane(w.s, l)};
+    }
+    __device__ __forceinline__ void set_lane(W& w, int l, const HNode& x) const {
+        if (lane == l) w.k = x.key, w.v = x.v, w.s = x.so;
+    }
+    // lanes [rb, rb + 8 * nb) <- blocks bid, bid + 1 (nb = 1 or 2)
+    __device__ __forceinline__ void load_blocks(W& w, int bid, int rb, int nb) const {
+        __asm__ volatile("" ::: "memory");
+        if (lane >= rb && lane < rb + 8 * nb) {
+            const HNode x = blk[(size_t)bid * 8 + (lane - rb)];
+            w.k = x.key, w.v = x.v, w.s = x.so;
+        }
+        __asm__ volatile("; blk load" ::: "memory");
+    }
+    // one full-line store of the block in lanes [cb, cb + 8)
+    __device__ __forceinline__ void store_block(const W& w, int bid, int cb) const {
+        __asm__ volatile("" ::: "memory");
+        if (lane >= cb && lane < cb + 8) blk[(size_t)bid * 8 + (lane - cb)] = HNode{w.k, w.v, w.s};
+        __asm__ volatile("; blk store" ::: "memory");
+    }
+    __device__ __forceinline__ void set_pos(int v, int x) {
+        pos[v] = x;
+        __asm__ volatile("; pos store" ::: "memory");
+    }
+    __device__ __forceinline__ HNode ld_raw(int p) const {
+        HNode x;
+        if (p < kBlkTop) {
+            x = top[p];
+            __asm__ volatile("; heap lds" ::: "memory");
+        } else {
+            int b, i;
+            locate(p, b, i);
+            x = blk[(size_t)b * 8 + i];
+            __asm__ volatile("; heap hbm" ::: "memory");
+        }
+        return x;
+    }
+    __device__ __forceinline__ HNode top_node() const { return uni_n(top[0]); }
+
+    // LDS-only shift-up from e < kBlkTop; x enters the top (pos 1) unless it
+    // was there already
+    __device__ __forceinline__ void up_lds(int e, const HNode& x, bool was_top) {
+        while (e > 0) {
+            const int p = ((e + 1) >> 1) - 1;
+            const HNode pn = uni_n(top[p]);
+            if (x.key < pn.key) break;
+            top[e] = pn;
+            e = p;
+        }
+        top[e] = x;
+        if (!was_top) set_pos(x.v, 1);
+    }
+
+    // shift-up of x from position e (>= kBlkTop) whose block is in lanes
+    // [0, 8) already (block cbid, x's slot idx); from_bid = block x was in
+    // (-1: new or from the LDS)
+    __device__ __forceinline__ void up_blk(W& w, int cbid, int idx, const HNode& x, int from_bid) {
+        int cb = 0;
+        for (;;) {
+            if (idx > 0) {
+                const int pi = (idx - 1) >> 1;
+                const HNode pn = lane_node(w, cb + pi);
+                if (x.key < pn.key) break;
+                set_lane(w, cb + idx, pn); // same block: pos unchanged
+                idx = pi;
+                continue;
+            }
+            const int rp = root_pos(cbid);
+            const int pp = ((rp + 1) >> 1) - 1;
+            if (pp < kBlkTop) { // parent in the LDS top
+                const HNode pn = uni_n(top[pp]);
+                if (x.key < pn.key) break;
+                set_lane(w, cb, pn);
+                set_pos(pn.v, cbid + 2);
+                store_block(w, cbid, cb);
+                up_lds(pp, x, false);
+                return;
+            }
+            int pb, pidx;
+            locate(pp, pb, pidx);
+            const int ob = cb ^ 16;
+            load_blocks(w, pb, ob, 1);
+            const HNode pn = lane_node(w, ob + pidx);
+            if (x.key < pn.key) break;
+            set_lane(w, cb, pn);
+            set_pos(pn.v, cbid + 2);
+            store_block(w, cbid, cb);
+            cb = ob, cbid = pb, idx = pidx;
+        }
+        set_lane(w, cb + idx, x);
+        if (from_bid != cbid) set_pos(x.v, cbid + 2);
+        store_block(w, cbid, cb);
+    }
+
+    __device__ __forceinline__ void push(int v, double key, int so) {
+        const int e = n++;
+        const HNode x{key, v, so};
+        if (e < kBlkTop) {
+            up_lds(e, x, false);
+            return;
+        }
+        int b, i;
+        locate(e, b, i);
+        W w{0.0, 0, 0};
+        if (i) load_blocks(w, b, 0, 1); // (a new block root: no slot of its block is live)
+        up_blk(w, b, i, x, -1);
+    }
+
+    // igraph_2wheap_modify with a larger key: a shift-up at v's position
+    __device__ __forceinline__ void raise(int v, double key, int so) {
+        const HNode x{key, v, so};
+        const int pv = uni(pos[v]);
+        if (pv == 1) {
+            const int m = n < kBlkTop ? n : kBlkTop;
+            int found = -1;
+            for (int q = lane; q < m; q += 64)
+                if (top[q].v == v) found = q;
+            const unsigned long long b = __ballot(found >= 0);
+            const int e = uni(__builtin_amdgcn_readlane(found, b ? __builtin_ctzll(b) : 0));
+            up_lds(e, x, true);
+            return;
+        }
+        const int bid = pv - 2;
+        W w{0.0, 0, 0};
+        load_blocks(w, bid, 0, 1);
+        const int root = root_pos(bid);
+        const bool mine = lane < 8 && w.v == v && slot_pos(root, lane) < n;
+        const unsigned long long m = __ballot(mine);
+        up_blk(w, bid, __builtin_ctzll(m), x, bid);
+    }
+
+    // delete_max's sink of x (the old last node, from position `from`) from
+    // the root: LDS levels by blocks of up to 5 levels, then HBM block pairs
+    __device__ __forceinline__ void sink(const HNode& x, int from) {
+        int e = 0;
+        const int j = 31 - __builtin_clz((unsigned)lane + 2);
+        const int bi = lane + 2 - (1 << j);
+        for (;;) { // LDS phase
+            if (2 * e + 1 >= n) {
+                top[e] = x;
+                if (from >= kBlkTop) set_pos(x.v, 1);
+                return;
+            }
+            if (2 * e + 1 >= kBlkTop) break;
+            const int p = (e + 1) * (1 << j) - 1 + bi;
+            double ck_l = 0.0;
+            int cv_l = 0, cs_l = 0;
+            if (lane < (2 << kSinkLevels) - 2 && p < n && p < kBlkTop) {
+                const HNode c = top[p];
+                ck_l = c.key, cv_l = c.v, cs_l = c.so;
+            }
+            int lv = 0, li = 0;
+            for (; lv < kSinkLevels; lv++) {
+                const int l = 2 * e + 1;
+                if (l >= n || l >= kBlkTop) break;
+                int cl = (2 << lv) - 2 + 2 * li;
+                double ck = readlane_d(ck_l, cl);
+                int ci = l;
+                if (l + 1 < n) {
+                    const double rk = readlane_d(ck_l, cl + 1);
+                    if (!(ck >= rk)) ck = rk, cl += 1, ci = l + 1;
+                }
+                if (!(x.key < ck)) {
+                    top[e] = x;
+                    if (from >= kBlkTop) set_pos(x.v, 1);
+                    return;
+                }
+                top[e] = HNode{ck, __builtin_amdgcn_readlane(cv_l, cl), __builtin_amdgcn_readlane(cs_l, cl)};
+                li = 2 * li + (ci - l);
+                e = ci;
+            }
+        }
+        // HBM phase: e is a level-7 hole whose children root blocks cb0, cb0 + 1
+        int from_bid = -1;
+        if (from >= kBlkTop) {
+            int fi;
+            locate(from, from_bid, fi);
+        }
+        int rb = 0;
+        W w{0.0, 0, 0};
+        load_blocks(w, 2 * e + 2 - 256, rb, 2);
+        int cbid = -1, cb = 0, idx = 0; // the hole: top[e] (cbid < 0) or slot idx of block cbid
+        for (;;) {
+            const int l = 2 * e + 1;
+            if (l >= n) break;
+            int lc, step; // lanes of the two children
+            const bool down = cbid < 0 || idx >= 3; // children are the roots of the loaded pair
+            if (down) lc = rb, step = 8;
+            else lc = cb + 2 * idx + 1, step = 1;
+            HNode c = lane_node(w, lc);
+            int ci = l;
+            if (l + 1 < n) {
+                const double rk = readlane_d(w.k, lc + step);
+                if (!(c.key >= rk)) c = lane_node(w, lc + step), lc += step, ci = l + 1;
+            }
+            if (!(x.key < c.key)) break;
+            if (cbid < 0) { // into the LDS top
+                top[e] = c;
+                set_pos(c.v, 1);
+            } else {
+                set_lane(w, cb + idx, c);
+                if (down) set_pos(c.v, cbid + 2);
+            }
+            e = ci;
+            if (down) {
+                if (cbid >= 0) store_block(w, cbid, cb);
+                cb = lc;
+                int i2;
+                locate(ci, cbid, i2);
+                idx = 0;
+            } else {
+                idx = 2 * idx + 1 + (ci - l);
+            }
+            if (idx >= 3 && 2 * e + 1 < n) { // bottom of the block: next pair
+                rb = (cb & ~15) ^ 16;
+                int b2, i2;
+                locate(2 * e + 1, b2, i2);
+                load_blocks(w, b2, rb, 2);
+            }
+        }
+        if (cbid < 0) {
+            top[e] = x;
+            if (from >= kBlkTop) set_pos(x.v, 1);
+            return;
+        }
+        set_lane(w, cb + idx, x);
+        if (from_bid != cbid) set_pos(x.v, cbid + 2);
+        store_block(w, cbid, cb);
     }
 };
 
@@ -427,7 +786,7 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
 // closed by {-1 or -2 (v attached), 0}; the arrays are padded by 64 x 16 entries,
 // so a 64-lane batch never reads past them.
 template <int kTop>
-__global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80))) void k_sssp_slab(ShdGraphDev g, int row_lo, int row_hi,
+__global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_sssp_slab(ShdGraphDev g, int row_lo, int row_hi,
                                                               ShdEntry* __restrict__ tab, char* __restrict__ slab,
                                                               size_t slab_stride) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -524,6 +883,88 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
     }
 }
 
+// ---- blocked-slab kernel: k_sssp_slab's pop loop over BHeap -----------------
+// Slab per wave: nblk 128-B heap blocks, then one 16-B {dist, rel} record per
+// vertex, then pos.  Same overlap of the pop's round trips as k_sssp_slab.
+template <int kWpe> // waves per SIMD the register allocation is held to (8: 32 per CU)
+__global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(kWpe, kWpe))) void k_sssp_blk(
+    ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab, char* __restrict__ slab, size_t slab_stride,
+    size_t nblk) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int gw = (int)blockIdx.x * wpb + w, nw = (int)gridDim.x * wpb;
+    const int V = g.V, A = g.A;
+    HNode* top = reinterpret_cast<HNode*>(smem) + w * (kBlkTop + 1);
+    HNode* blk = reinterpret_cast<HNode*>(slab + (size_t)gw * slab_stride);
+    double2* dr = reinterpret_cast<double2*>(blk + nblk * 8);
+    int* pos = reinterpret_cast<int*>(dr + V);
+    const int2* __restrict__ snb = static_cast<const int2*>(g.snb);
+    const double2* __restrict__ swr = static_cast<const double2*>(g.swr);
+
+    for (int row = row_lo + gw; row < row_hi; row += nw) {
+        const int src = g.slot_vertex[row];
+        for (int v = lane; v < V; v += 64) dr[v].x = -1.0;
+        wave_fence();
+        BHeap h{top, blk, pos, 0, lane};
+        dr[src] = make_double2(0.0, 1.0);
+        h.push(src, 0.0, uni(g.soff[src]));
+        int to_reach = A;
+        while (h.n > 0 && to_reach > 0) {
+            const HNode t = h.top_node(); // LDS
+            const int u = t.v;
+            const double mindist = -t.key;
+            int b = t.so >> 8;
+            const int li = lane < (t.so & 255) ? lane : (t.so & 255) - 1;
+            int2 nb = snb[b + li];
+            double2 wr = swr[b + li];
+            const int last = --h.n;
+            const HNode xl = h.ld_raw(last);
+            const double ru_l = dr[u].y;
+            bool first = true;
+            double ru = 0.0;
+            for (;;) {
+                const unsigned long long sm = __ballot(nb.x < 0);
+                const int fs = sm ? __builtin_ctzll(sm) : 64;
+                const bool ok = lane < fs && nb.x != u;
+                double cur = ok ? dr[nb.x].x : 0.0;
+                if (first) {
+                    if (last > 0) h.sink(uni_n(xl), last);
+                    ru = uni_d(ru_l);
+                    first = false;
+                }
+                __asm__ volatile("" : "+v"(cur));
+                if (fs < 64 && __builtin_amdgcn_readlane(nb.x, fs) == -2) --to_reach;
+                const double alt = mindist + wr.x;
+                const double rv = ru * wr.y;
+                const bool fresh = ok && cur < 0;
+                unsigned long long m = __ballot(ok && (cur < 0 || alt < cur));
+                const unsigned long long fm = __ballot(fresh);
+                while (m) {
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const int vv = __builtin_amdgcn_readlane(nb.x, l);
+                    const int vs = __builtin_amdgcn_readlane(nb.y, l);
+                    const double aa = readlane_d(alt, l);
+                    dr[vv] = make_double2(aa, readlane_d(rv, l));
+                    if ((fm >> l) & 1ull) h.push(vv, -aa, vs);
+                    else h.raise(vv, -aa, vs);
+                }
+                if (fs < 64) break;
+                b += 64;
+                nb = snb[b + lane];
+                wr = swr[b + lane];
+            }
+        }
+        wave_fence();
+        write_row(g, row, src, tab, lane, [&](int v, double& l, double& r) {
+            const double2 x = dr[v];
+            l = x.x;
+            r = x.y;
+        });
+        wave_fence();
+    }
+}
+
 // _topology_lookupDirectPath (topology.c:1816-1858): the (s,d) edge itself.
 __global__ __launch_bounds__(256) void k_direct_rows(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab) {
     const int A = g.A;
@@ -594,6 +1035,43 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         return hip_status(hipDeviceSynchronize(), "k_sssp_lds");
     }
     if (!g.snb || !g.swr || !g.soff) return shd_fail(-EINVAL, "slab kernel needs the sentinel incidence arrays");
+    const char* kern = getenv("SHD_SSSP_KERNEL");
+    if (kern && strcmp(kern, "blk") == 0) { // SHD_SSSP_KERNEL=blk: the blocked slab heap
+        const size_t nblk = blk_count((long)g.V + 1);
+        const size_t bstride = (nblk * 128 + 20 * (size_t)g.V + 255) & ~(size_t)255;
+        int dev = 0, cus = 0;
+        if ((rc = hip_status(hipGetDevice(&dev), "hipGetDevice")) ||
+            (rc = hip_status(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
+                             "hipDeviceGetAttribute")))
+            return rc;
+        // SHD_SSSP_WPE=7: 7 waves per SIMD (no register spills) instead of 8
+        int wpe = 8;
+        if (const char* e = getenv("SHD_SSSP_WPE")) wpe = atoi(e) == 7 ? 7 : 8;
+        long waves = (long)cus * 4 * wpe;
+        if (const char* e = getenv("SHD_SSSP_WAVES")) {
+            const long x = atol(e);
+            if (x > 0) waves = x;
+        }
+        if (waves > rows) waves = rows;
+        int grid = (int)((waves + kSlabWaves - 1) / kSlabWaves);
+        char* slab = nullptr;
+        while (hipMalloc((void**)&slab, bstride * kSlabWaves * (size_t)grid) != hipSuccess) {
+            (void)hipGetLastError();
+            if (grid <= 16) return shd_fail(-ENOMEM, "cannot allocate SSSP workspace");
+            grid /= 2;
+        }
+        const size_t lds = sizeof(HNode) * (kBlkTop + 1) * kSlabWaves;
+        if (wpe == 7)
+            hipLaunchKernelGGL(k_sssp_blk<7>, dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo, row_hi, tab,
+                               slab, bstride, nblk);
+        else
+            hipLaunchKernelGGL(k_sssp_blk<8>, dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo, row_hi, tab,
+                               slab, bstride, nblk);
+        rc = hip_status(hipGetLastError(), "k_sssp_blk launch");
+        if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_blk");
+        (void)hipFree(slab);
+        return rc;
+    }
     // large graphs: persistent waves, one HBM slab each (heap V+2 nodes,
     // {dist, rel}, pos); SHD_SSSP_WAVES overrides the wave count
     const size_t stride = (sizeof(HNode) * ((size_t)g.V + 2) + 20 * (size_t)g.V + 255) & ~(size_t)255;

@@ -60,6 +60,20 @@ def test_routing_table_bit_exact(name):
         assert np.all(np.abs(rel[i][nz] - orl[nz]) <= REL_TOL * np.abs(orl[nz]))
 
 
+@pytest.mark.parametrize("name", ["sparse5000_hbm", "sparse4500_dir_ns_hbm", "dense4400_hbm"])
+def test_flat_slab_kernel_bit_exact(name, monkeypatch):
+    """The flat-slab heap (SHD_SSSP_KERNEL=slab, heap position p at rest[p + 1])
+    kept beside the default blocked-slab heap: same rows, bit for bit."""
+    monkeypatch.setenv("SHD_SSSP_KERNEL", "slab")
+    gml, H = GRAPHS[name]
+    top, orc, _, _ = make_pair(gml, H)
+    lat, rel, sv = top.table()
+    for i, s in enumerate(sv):
+        ol, orl = orc.row(int(s), sv)
+        assert np.array_equal(bits(lat[i]), bits(ol)), (name, i)
+        assert np.array_equal(bits(rel[i]), bits(orl)), (name, i)
+
+
 @pytest.mark.parametrize("waves", [1, 6])
 def test_slab_kernel_persistent_rows(waves, monkeypatch):
     """Fewer slab waves than rows (SHD_SSSP_WAVES): each wave reuses its slab
