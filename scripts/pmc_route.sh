@@ -9,6 +9,6 @@ i=0
 for GROUP in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" \
              "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAVES SQ_BUSY_CYCLES"; do
   i=$((i+1))
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $GROUP -f csv -d $D/p$i -o p -- python3 $GRAFT_REPO_ROOT/scripts/routing_variants.py --reps 1 kern=slab kern=blk > $D/p$i.log 2>&1) || { echo "pass $i failed"; tail -5 $D/p$i.log; exit 1; }
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $GROUP -f csv -d $D/p$i -o p -- python3 $GRAFT_REPO_ROOT/scripts/routing_variants.py --reps 1 ${VARIANTS:-kern=slab kern=blk} > $D/p$i.log 2>&1) || { echo "pass $i failed"; tail -5 $D/p$i.log; exit 1; }
   echo "pass $i ok"
 done

@@ -144,6 +144,52 @@ struct Heap {
         }
         st(e, x, from);
     }
+    // Shift-up, data-parallel (slab kernel): lane j loads the j-th ancestor
+    // of e -- at most 2 from the HBM slab per round (a climb is usually 0-2
+    // levels), every LDS one up to the root -- and one ballot says which
+    // ancestors x is not smaller than.  The heap order makes that set the
+    // nearest c ancestors (parent >= child all the way up), so x climbs c
+    // levels: those ancestors each move one level down along the path, by
+    // their own lanes in one store (+ one for pos), exactly the moves of
+    // shift_up.
+    __device__ __forceinline__ void shift_up_dp(int e, const HNode& x, int from) {
+        for (;;) {
+            if (e == 0) break;
+            const int lvl = 31 - __builtin_clz((unsigned)e + 1); // ancestors of e: lvl
+            constexpr int kTopLv = kTop >= 512 ? 9 : 8;          // levels wholly in the LDS top
+            const int nh = lvl > kTopLv ? lvl - kTopLv : 0;      // ancestors at deeper levels (slab)
+            const int K = nh > 2 ? 2 : lvl;                      // loaded this round
+            const int a = ((e + 1) >> (lane + 1)) - 1;           // lane's ancestor
+            const bool ld = lane < K;
+            HNode c = HNode{0.0, 0, 0};
+            if (ld) {
+                if (a < kTop) {
+                    c = top[a];
+                    __asm__ volatile("; up lds" ::: "memory");
+                } else {
+                    c = rest[a + 1];
+                    __asm__ volatile("; up hbm" ::: "memory");
+                }
+            }
+            const unsigned long long m = __ballot(ld && !(x.key < c.key)); // x climbs past these
+            const int cnt = (int)__builtin_ctzll(~m);
+            if (lane < cnt) { // each passed ancestor moves one level down the path
+                const int d = ((e + 1) >> lane) - 1;
+                if (d < kTop) {
+                    top[d] = c;
+                    __asm__ volatile("; up mv lds" ::: "memory");
+                } else {
+                    rest[d + 1] = c;
+                    __asm__ volatile("; up mv hbm" ::: "memory");
+                    pos[c.v] = d + 2;
+                }
+            }
+            if (cnt == 0) break;
+            e = ((e + 1) >> cnt) - 1;
+            if (cnt < K) break;
+        }
+        st(e, x, from);
+    }
     // descend towards the larger child (the left one when left >= right)
     // while x < child, one level at a time
     __device__ __forceinline__ void sink_seq(int e, const HNode& x, int from) {
@@ -278,7 +324,8 @@ struct Heap {
     }
     __device__ __forceinline__ void push(int v, double key, int so) {
         const int e = n++;
-        shift_up(e, HNode{key, v, so}, -1);
+        if (kAll) shift_up(e, HNode{key, v, so}, -1);
+        else shift_up_dp(e, HNode{key, v, so}, -1);
     }
     // delete_max in two halves: the root is read first (top_node), then
     // removed (the last node takes the root and sinks)
@@ -310,7 +357,8 @@ struct Heap {
             const int pv = uni(pos[v]);
             e = pv == 1 ? uni(find_top(v)) : pv - 2;
         }
-        shift_up(e, HNode{key, v, so}, e);
+        if (kAll) shift_up(e, HNode{key, v, so}, e);
+        else shift_up_dp(e, HNode{key, v, so}, e);
     }
 };
 
