@@ -265,21 +265,29 @@ struct Heap {
     // nodes it moves are stored by their own lanes, each one level up, in one
     // store instruction (plus one for their pos).  Same moves as sink_seq.
     __device__ __forceinline__ void sink_dp(int e, const HNode& x, int from) {
-        const int j = 31 - __builtin_clz((unsigned)lane + 2);
-        const int bi = lane + 2 - (1 << j);
+        const int j = 31 - __builtin_clz((unsigned)lane + 2); // this lane's level under e (1..5)
+        const int bi = lane + 2 - (1 << j);                    // ... and index in that level
         const bool inblk = lane < (2 << kSinkLevels) - 2;
         for (;;) {
             if (2 * e + 1 >= n) break;
             const int p = (e + 1) * (1 << j) - 1 + bi;
             const bool valid = inblk && p < n;
             HNode c = HNode{0.0, 0, 0};
-            if (valid) {
+            // (uniform tests first: a block is wholly in LDS or in the slab
+            // except the one that straddles kTop)
+            if (32 * e + 62 < kTop) {
+                if (valid) c = top[p];
+                __asm__ volatile("; sink lds" ::: "memory");
+            } else if (2 * e + 1 >= kTop) {
+                if (valid) c = rest[p + 1];
+                __asm__ volatile("; sink hbm" ::: "memory");
+            } else if (valid) {
                 if (p < kTop) {
                     c = top[p];
-                    __asm__ volatile("; sink lds" ::: "memory");
+                    __asm__ volatile("; sink lds/hbm" ::: "memory");
                 } else {
                     c = rest[p + 1];
-                    __asm__ volatile("; sink hbm" ::: "memory");
+                    __asm__ volatile("; sink hbm/lds" ::: "memory");
                 }
             }
             // the sibling's key: quad_perm(1, 0, 3, 2) swaps lanes 2i, 2i + 1
@@ -288,20 +296,20 @@ struct Heap {
             const unsigned shi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(kb >> 32), 0xB1, 0xF, 0xF, false);
             const double ks = __longlong_as_double((long long)(((unsigned long long)shi << 32) | slo));
             const unsigned long long vm = __ballot(valid);
+            // rm bit at a left child: its right sibling exists and is larger
             const unsigned long long rm =
                 __ballot(valid && (lane & 1) == 0 && ((vm >> (lane + 1)) & 1ull) && !(c.key >= ks));
-            const unsigned long long lm = __ballot(valid && x.key < c.key);
-            unsigned long long mv = 0;
-            int lv = 0, li = 0;
-            for (; lv < kSinkLevels; lv++) {
-                const int cl = (2 << lv) - 2 + 2 * li; // lane of the left child
-                if (!((vm >> cl) & 1ull)) break;        // no child: x stays
-                const int cc = cl + (int)((rm >> cl) & 1ull);
-                if (!((lm >> cc) & 1ull)) break;        // x >= the larger child: x stays
-                mv |= 1ull << cc;
-                li = 2 * li + (cc - cl);
-            }
-            if ((mv >> lane) & 1ull) { // each moved node goes one level up
+            // g: this lane is the larger child of its pair and x < it -- the
+            // walk passes it iff every ancestor of it in the block is g too
+            const bool larger = (int)((rm >> (lane & ~1)) & 1ull) == (lane & 1);
+            const unsigned long long g = __ballot(valid && larger && x.key < c.key);
+            bool mvl = (g >> lane) & 1ull;
+#pragma unroll
+            for (int i = 1; i < kSinkLevels; i++) // ancestor at level i (lanes at levels > i)
+                if (i < j) mvl = mvl && ((g >> ((2 << (i - 1)) - 2 + (bi >> (j - i)))) & 1ull);
+            const unsigned long long mv = __ballot(mvl); // one lane per level, levels 1..lv
+            const int lv = __builtin_popcountll(mv);
+            if (mvl) { // each moved node goes one level up
                 const int q = (p - 1) >> 1;
                 if (q < kTop) {
                     top[q] = c;
@@ -310,10 +318,12 @@ struct Heap {
                     rest[q + 1] = c;
                     __asm__ volatile("; sink mv hbm" ::: "memory");
                 }
-                if (q >= kTop) pos[c.v] = q + 2;
-                else if (p >= kTop) pos[c.v] = 1; // entered the LDS top
+                if (p >= kTop) pos[c.v] = q >= kTop ? q + 2 : 1; // (1: entered the LDS top)
             }
-            e = ((e + 1) << lv) - 1 + li; // the hole: the last moved node's old position
+            if (lv == 0) break;
+            // the hole: the deepest moved node's old position
+            const int hl = 63 - __builtin_clzll(mv);
+            e = ((e + 1) << lv) - 1 + (hl + 2 - (1 << lv));
             if (lv < kSinkLevels) break;
         }
         st(e, x, from);
