@@ -17,15 +17,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--c4", action="store_true")
+    ap.add_argument("--c1", action="store_true", help="the C1 complete graph (LDS kernel) instead of C2")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
 
     from shadow_amd import Topology, scenario, synth
-    cfgs = [("C2", 20_000, 100_000, 0x5EED0002)] + ([("C4", 100_000, 200_000, 0x5EED0004)] if a.c4 else [])
+    cfgs = ([("C1", 1000, 5000, 0x5EED0001)] if a.c1 else [("C2", 20_000, 100_000, 0x5EED0002)]) + \
+        ([("C4", 100_000, 200_000, 0x5EED0004)] if a.c4 else [])
     for name, V, H, seed in cfgs:
-        top = Topology(synth.sparse_graph_gml(V, seed))
+        gml = synth.complete_graph_gml(V, seed) if name == "C1" else synth.sparse_graph_gml(V, seed)
+        top = Topology(gml)
         scenario.register_hosts(top, H, seed=1)
         A = top.slot_count()
         ref = None
@@ -35,12 +38,13 @@ def main():
             os.environ["SHD_SSSP_TOP"] = kv.get("top", "256")
             os.environ["SHD_SSSP_KERNEL"] = kv.get("kern", "blk")
             os.environ["SHD_SSSP_WPE"] = kv.get("wpe", "8")
+            os.environ["SHD_SSSP_LDS_SEQ"] = kv.get("seq", "0")
             if "waves" in kv:
                 os.environ["SHD_SSSP_WAVES"] = kv["waves"]
             else:
                 os.environ.pop("SHD_SSSP_WAVES", None)
             ts = []
-            for _ in range(a.reps if name == "C2" else 1):
+            for _ in range(a.reps if name != "C4" else 1):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 top.build_rows_device(0, A, tab.data_ptr())
@@ -51,7 +55,7 @@ def main():
             sig = (int(h[::997].sum().item()), int(h[1::1009].sum().item()), int((h[: A * 2 * 64]).sum().item()))
             if ref is None:
                 ref = sig
-            print(f"{name} {v}: {min(ts):.3f}s (all {', '.join(f'{t:.3f}' for t in ts)}) "
+            print(f"{name} {v}: {min(ts):.5f}s (all {', '.join(f'{t:.5f}' for t in ts)}) "
                   f"{'same' if sig == ref else 'DIFFERENT'}", flush=True)
             if sig != ref:
                 sys.exit(1)

@@ -88,7 +88,9 @@ __device__ __forceinline__ HNode uni_n(const HNode& x) { return HNode{uni_d(x.ke
 // most kTop) top positions.  The slab kernel's pop does not clear pos: a
 // popped vertex is never decreased again (alt = dist[u] + w >= dist[v] for
 // every popped v, weights > 0).  Neither changes a heap operation.
-template <bool kAll, int kTop = kTopDefault>
+// kDp: sink and shift-up by the data-parallel block forms (sink_dp,
+// shift_up_dp) rather than level by level; always on for the slab kernel.
+template <bool kAll, int kTop = kTopDefault, bool kDp = !kAll>
 struct Heap {
     HNode* top;
     HNode* rest;
@@ -158,12 +160,12 @@ struct Heap {
             const int lvl = 31 - __builtin_clz((unsigned)e + 1); // ancestors of e: lvl
             constexpr int kTopLv = kTop >= 512 ? 9 : 8;          // levels wholly in the LDS top
             const int nh = lvl > kTopLv ? lvl - kTopLv : 0;      // ancestors at deeper levels (slab)
-            const int K = nh > 2 ? 2 : lvl;                      // loaded this round
+            const int K = (!kAll && nh > 2) ? 2 : lvl;           // loaded this round
             const int a = ((e + 1) >> (lane + 1)) - 1;           // lane's ancestor
             const bool ld = lane < K;
             HNode c = HNode{0.0, 0, 0};
             if (ld) {
-                if (a < kTop) {
+                if (kAll || a < kTop) {
                     c = top[a];
                     __asm__ volatile("; up lds" ::: "memory");
                 } else {
@@ -175,7 +177,10 @@ struct Heap {
             const int cnt = (int)__builtin_ctzll(~m);
             if (lane < cnt) { // each passed ancestor moves one level down the path
                 const int d = ((e + 1) >> lane) - 1;
-                if (d < kTop) {
+                if (kAll) {
+                    top[d] = c;
+                    pos[c.v] = d + 2;
+                } else if (d < kTop) {
                     top[d] = c;
                     __asm__ volatile("; up mv lds" ::: "memory");
                 } else {
@@ -208,52 +213,6 @@ struct Heap {
         }
         st(e, x, from);
     }
-    // Sink by blocks (slab kernel): a level of the HBM slab costs a ~us
-    // round trip, so the wave loads the 62 nodes of the next 5 levels at
-    // once (lane t: level j = log2(t + 2), index t + 2 - 2^j under e, only
-    // positions < n) and makes the same comparisons and moves on readlane'd
-    // copies, reloading every 5 levels (5 levels per block measured fastest
-    // against 3, 2 and level by level on C2 and C4).  Moved nodes are stored
-    // above the next block, so a block never reads a position this sink has
-    // written.
-    __device__ __forceinline__ void sink_blocks(int e, const HNode& x, int from) {
-        const int j = 31 - __builtin_clz((unsigned)lane + 2);
-        const int bi = lane + 2 - (1 << j);
-        for (;;) {
-            if (2 * e + 1 >= n) break;
-            const int p = (e + 1) * (1 << j) - 1 + bi;
-            double ck_l = 0.0;
-            int cv_l = 0, cs_l = 0;
-            if (lane < (2 << kSinkLevels) - 2 && p < n) {
-                const HNode c = (kAll || p < kTop) ? top[p] : rest[p + 1];
-                ck_l = c.key;
-                cv_l = c.v;
-                cs_l = c.so;
-            }
-            int lv = 0, li = 0; // block level and index of e
-            for (; lv < kSinkLevels; lv++) {
-                const int l = 2 * e + 1;
-                if (l >= n) break;
-                int cl = (2 << lv) - 2 + 2 * li; // lane of the left child
-                double ck = readlane_d(ck_l, cl);
-                int ci = l;
-                if (l + 1 < n) {
-                    const double rk = readlane_d(ck_l, cl + 1);
-                    if (!(ck >= rk)) {
-                        ck = rk;
-                        cl += 1;
-                        ci = l + 1;
-                    }
-                }
-                if (!(x.key < ck)) break;
-                st(e, HNode{ck, __builtin_amdgcn_readlane(cv_l, cl), __builtin_amdgcn_readlane(cs_l, cl)}, ci);
-                li = 2 * li + (ci - l);
-                e = ci;
-            }
-            if (lv < kSinkLevels) break;
-        }
-        st(e, x, from);
-    }
     // Sink by blocks, data-parallel (slab kernel): the 62 nodes of the next
     // 5 levels under e are loaded one per lane as in sink_blocks; the lanes
     // then make every level's comparisons at once -- each left child lane
@@ -275,7 +234,7 @@ struct Heap {
             HNode c = HNode{0.0, 0, 0};
             // (uniform tests first: a block is wholly in LDS or in the slab
             // except the one that straddles kTop)
-            if (32 * e + 62 < kTop) {
+            if (kAll || 32 * e + 62 < kTop) {
                 if (valid) c = top[p];
                 __asm__ volatile("; sink lds" ::: "memory");
             } else if (2 * e + 1 >= kTop) {
@@ -311,14 +270,17 @@ struct Heap {
             const int lv = __builtin_popcountll(mv);
             if (mvl) { // each moved node goes one level up
                 const int q = (p - 1) >> 1;
-                if (q < kTop) {
+                if (kAll) {
+                    top[q] = c;
+                    pos[c.v] = q + 2;
+                } else if (q < kTop) {
                     top[q] = c;
                     __asm__ volatile("; sink mv lds" ::: "memory");
                 } else {
                     rest[q + 1] = c;
                     __asm__ volatile("; sink mv hbm" ::: "memory");
                 }
-                if (p >= kTop) pos[c.v] = q >= kTop ? q + 2 : 1; // (1: entered the LDS top)
+                if (!kAll && p >= kTop) pos[c.v] = q >= kTop ? q + 2 : 1; // (1: entered the LDS top)
             }
             if (lv == 0) break;
             // the hole: the deepest moved node's old position
@@ -329,13 +291,13 @@ struct Heap {
         st(e, x, from);
     }
     __device__ __forceinline__ void sink(int e, const HNode& x, int from) {
-        if (kAll) sink_seq(e, x, from); // a level of LDS is a short round trip (C1 4.99 vs 5.17 ms)
-        else sink_dp(e, x, from);
+        if (kDp) sink_dp(e, x, from);
+        else sink_seq(e, x, from);
     }
     __device__ __forceinline__ void push(int v, double key, int so) {
         const int e = n++;
-        if (kAll) shift_up(e, HNode{key, v, so}, -1);
-        else shift_up_dp(e, HNode{key, v, so}, -1);
+        if (kDp) shift_up_dp(e, HNode{key, v, so}, -1);
+        else shift_up(e, HNode{key, v, so}, -1);
     }
     // delete_max in two halves: the root is read first (top_node), then
     // removed (the last node takes the root and sinks)
@@ -367,8 +329,8 @@ struct Heap {
             const int pv = uni(pos[v]);
             e = pv == 1 ? uni(find_top(v)) : pv - 2;
         }
-        if (kAll) shift_up(e, HNode{key, v, so}, e);
-        else shift_up_dp(e, HNode{key, v, so}, e);
+        if (kDp) shift_up_dp(e, HNode{key, v, so}, e);
+        else shift_up(e, HNode{key, v, so}, e);
     }
 };
 
@@ -736,6 +698,7 @@ __device__ __forceinline__ void write_row(const ShdGraphDev& g, int row, int src
 // loads: kRelax batches of 64 entries are issued together (a complete
 // graph's lists are 24 MB: Infinity-Cache round trips); the list's sentinel
 // also says whether u is attached.
+template <bool kDp>
 __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
@@ -751,7 +714,7 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
         const int src = g.slot_vertex[row];
         for (int v = lane; v < V; v += 64) dist[v] = -1.0;
         wave_fence();
-        Heap<true> h{top, nullptr, pos, 0, lane};
+        Heap<true, kTopDefault, kDp> h{top, nullptr, pos, 0, lane};
         dist[src] = 0.0;
         rel[src] = 1.0;
         h.push(src, 0.0, g.soff[src]);
@@ -1083,12 +1046,16 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
     }
     if (g.V <= kLdsMaxV) {
         const size_t lds = sizeof(HNode) * ((size_t)g.V + 1) + 20 * (size_t)g.V;
+        // SHD_SSSP_LDS_SEQ=1: level-by-level sink and shift-up
+        const char* sq = getenv("SHD_SSSP_LDS_SEQ");
+        const bool dp = !(sq && atoi(sq) == 1);
+        const void* kf = dp ? (const void*)k_sssp_lds<true> : (const void*)k_sssp_lds<false>;
         if (lds > 65536 &&
-            (rc = hip_status(hipFuncSetAttribute((const void*)k_sssp_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)lds),
+            (rc = hip_status(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
                              "hipFuncSetAttribute")))
             return rc;
-        hipLaunchKernelGGL(k_sssp_lds, dim3(rows), dim3(64), lds, nullptr, g, row_lo, row_hi, tab);
+        if (dp) hipLaunchKernelGGL(k_sssp_lds<true>, dim3(rows), dim3(64), lds, nullptr, g, row_lo, row_hi, tab);
+        else hipLaunchKernelGGL(k_sssp_lds<false>, dim3(rows), dim3(64), lds, nullptr, g, row_lo, row_hi, tab);
         if ((rc = hip_status(hipGetLastError(), "k_sssp_lds launch"))) return rc;
         return hip_status(hipDeviceSynchronize(), "k_sssp_lds");
     }
