@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02d_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
@@ -157,18 +157,22 @@ def main():
     log(f"C2 graph V={V} H={H} A={A} ready in {time.perf_counter() - t0:.1f}s")
 
     # routing rows sharded by source slot, assembled by RCCL all-gather (§8e)
+    # The resident table the rounds gather from is placed as the library
+    # places its own (shd_device_alloc_table: physically contiguous when
+    # granted); at N>1 the rows are all-gathered in a torch tensor and copied in.
     rows_per = (A + world - 1) // world
-    full = torch.empty(rows_per * world * A * 2, dtype=torch.float64, device=dev)
-    shard = full.narrow(0, rank * rows_per * A * 2, rows_per * A * 2)
+    table = top.alloc_table(A * A * 16)
     lo, hi = min(A, rank * rows_per), min(A, (rank + 1) * rows_per)
+    full = torch.empty(rows_per * world * A * 2, dtype=torch.float64, device=dev) if world > 1 else None
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     if hi > lo:
-        # rows are written at their absolute offsets inside `full`
-        top.build_rows_device(lo, hi, full.data_ptr())
+        # rows are written at their absolute offsets
+        top.build_rows_device(lo, hi, full.data_ptr() if world > 1 else table.ptr)
     torch.cuda.synchronize(dev)
     t_rows_c2 = time.perf_counter() - t0
     if world > 1:
+        shard = full.narrow(0, rank * rows_per * A * 2, rows_per * A * 2)
         if cdev == dev:
             dist.all_gather_into_tensor(full, shard.clone())
         else:
@@ -176,7 +180,10 @@ def main():
             dist.all_gather_into_tensor(host, host.narrow(0, rank * rows_per * A * 2, rows_per * A * 2).clone())
             full.copy_(host)
         torch.cuda.synchronize(dev)
-    top.adopt_table_device(full.data_ptr())
+        table.copy_from(full.data_ptr(), A * A * 16)
+        del full, shard
+        torch.cuda.empty_cache()
+    top.adopt_table_device(table.ptr)
     top.touch_all()  # steady state: every row released (slot order)
     log(f"C2 table {A}x{A} rows {lo}:{hi} in {t_rows_c2:.2f}s; touched")
 
@@ -334,13 +341,13 @@ def main():
         log(f"C4 graph V={args.c4_vertices} H={args.c4_hosts} A={A4} ready in {time.perf_counter() - t0:.1f}s")
         per4 = (A4 + world - 1) // world
         l4, h4 = min(A4, rank * per4), min(A4, (rank + 1) * per4)
-        shard4 = torch.empty(max(h4 - l4, 1) * A4 * 2, dtype=torch.float64, device=dev)
+        shard4 = t4.alloc_table(max(h4 - l4, 1) * A4 * 16)  # placed as the library places tables
         barrier()
         torch.cuda.synchronize(dev)
         s0 = time.perf_counter()
         if h4 > l4:
             # rows land at absolute offsets from the base: base = shard - l4 rows
-            t4.build_rows_device(l4, h4, shard4.data_ptr() - l4 * A4 * 16)
+            t4.build_rows_device(l4, h4, shard4.ptr - l4 * A4 * 16)
         torch.cuda.synchronize(dev)
         barrier()
         tr4 = max_over_ranks(time.perf_counter() - s0)
@@ -362,13 +369,13 @@ def main():
         # (shd_round_exchange).  Weak scaling: c4_packets per rank per round.
         if args.c4_rounds > 0:
             if world == 1:
-                t4.adopt_table_device_resident(shard4.data_ptr())  # no 120 GB host mirror
+                t4.adopt_table_device_resident(shard4.ptr)  # no 120 GB host mirror
             else:
-                mn = torch.tensor([t4.shard_min_latency(shard4.data_ptr(), l4, h4) if h4 > l4 else -1.0],
+                mn = torch.tensor([t4.shard_min_latency(shard4.ptr, l4, h4) if h4 > l4 else -1.0],
                                   dtype=torch.float64, device=cdev)
                 mn[mn < 0] = float("inf")
                 dist.all_reduce(mn, op=dist.ReduceOp.MIN)
-                t4.adopt_table_shard_device_resident(shard4.data_ptr(), l4, h4, float(mn.item()))
+                t4.adopt_table_shard_device_resident(shard4.ptr, l4, h4, float(mn.item()))
             P4 = args.c4_packets
             H4 = args.c4_hosts
             s_lo, s_hi = rank * H4 // world, (rank + 1) * H4 // world

@@ -154,6 +154,18 @@ int shd_topology_copy_table(ShdTopology* top, double* lat_ms, double* rel, int32
  * all-gather completes), then adopt the completed table as the resident one
  * (the caller keeps it alive for the topology's lifetime). */
 int shd_topology_slot_count(ShdTopology* top, int* slots);
+/* Device memory for a routing table (or any randomly gathered array):
+ * physically contiguous when the driver grants it (hipDeviceMallocContiguous:
+ * few, large translation fragments, so uniformly random 16-B gathers over a
+ * multi-GB table do not depend on how the allocation happened to be
+ * fragmented), else an ordinary device allocation.  *contiguous (may be NULL)
+ * says which.  Free with shd_device_free.  The library's own tables
+ * (shd_topology_build_routes) are allocated this way. */
+int shd_device_alloc_table(int device, size_t bytes, void** d_out, int* contiguous);
+int shd_device_free(int device, void* d_ptr);
+/* Device-to-device copy (e.g. an all-gathered table into one from
+ * shd_device_alloc_table); synchronous. */
+int shd_device_copy(int device, void* d_dst, const void* d_src, size_t bytes);
 int shd_topology_build_rows_device(ShdTopology* top, int row_lo, int row_hi, void* d_table);
 int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
 /* Adopts a device table WITHOUT a host mirror (tables larger than host RAM

@@ -11,7 +11,7 @@ import re
 import sys
 
 STAGE = {"k_pkt_scatter": "packet_scatter", "k_place_rank": "place", "k_place_bucket": "place",
-         "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_rows<false>": "routing_slab", "k_sssp_rows<true>": "routing_lds"}
+         "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_slab<256>": "routing_slab", "k_sssp_lds<true>": "routing_lds"}
 
 
 def kname(n):

@@ -117,6 +117,20 @@ int main() {
         for (size_t k = 0; k < tabs.size(); k++)
             printf("allocation %zu (pass %d): %.3f ms\n", k, r, run(d_idx, n, tabs[k], c3, d_out));
     for (auto t : tabs) CHECK(hipFree(t));
+    // (d) physically contiguous allocations of the C3 size
+    for (auto& t : tabs) {
+        if (hipExtMallocWithFlags((void**)&t, c3 * 16, hipDeviceMallocContiguous) != hipSuccess) {
+            printf("contiguous allocation refused: %s\n", hipGetErrorString(hipGetLastError()));
+            t = nullptr;
+            continue;
+        }
+        CHECK(hipMemset(t, 0, c3 * 16));
+    }
+    for (int r = 0; r < 2; r++)
+        for (size_t k = 0; k < tabs.size(); k++)
+            if (tabs[k]) printf("contiguous allocation %zu (pass %d): %.3f ms\n", k, r, run(d_idx, n, tabs[k], c3, d_out));
+    for (auto t : tabs)
+        if (t) CHECK(hipFree(t));
     CHECK(hipFree(d_idx));
     CHECK(hipFree(d_out));
     CHECK(hipFree(d_sorted));

@@ -51,6 +51,9 @@ PROTOS = {
     "shd_topology_vertex_of_host": (C.c_int, [_P, C.c_uint32, _ip]),
     "shd_topology_copy_table": (C.c_int, [_P, _P, _P, _P, C.c_int]),
     "shd_topology_slot_count": (C.c_int, [_P, _ip]),
+    "shd_device_alloc_table": (C.c_int, [C.c_int, C.c_size_t, C.POINTER(_P), _ip]),
+    "shd_device_free": (C.c_int, [C.c_int, _P]),
+    "shd_device_copy": (C.c_int, [C.c_int, _P, _P, C.c_size_t]),
     "shd_topology_build_rows_device": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "shd_topology_adopt_table_device": (C.c_int, [_P, _P]),
     "shd_topology_adopt_table_device_resident": (C.c_int, [_P, _P]),

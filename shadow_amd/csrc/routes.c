@@ -201,7 +201,7 @@ static int build_routes_locked(ShdTopology* t) {
     int rc = prepare(t);
     if (rc) return rc;
     ShdEntry* d_tab = NULL;
-    rc = shd_dev_malloc((void**)&d_tab, sizeof(ShdEntry) * (size_t)t->A * (size_t)t->A);
+    rc = shd_dev_malloc_table((void**)&d_tab, sizeof(ShdEntry) * (size_t)t->A * (size_t)t->A, NULL);
     if (rc) return rc;
     ShdGraphDev g = graph_dev(t);
     rc = shd_dev_build_rows(&g, t->use_sp, 0, t->A, d_tab);
@@ -299,4 +299,22 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->row_hi = t->tab_row_hi;
     if (!t->ws) shd_dev_ws_new(&t->ws); /* (a failure leaves ws NULL: the launch reports -ENOMEM) */
     c->ws = t->ws;
+}
+
+int shd_device_alloc_table(int device, size_t bytes, void** d_out, int* contiguous) {
+    if (!d_out) return -EINVAL;
+    *d_out = NULL;
+    int rc = shd_dev_init(device);
+    return rc ? rc : shd_dev_malloc_table(d_out, bytes, contiguous);
+}
+
+int shd_device_free(int device, void* d_ptr) {
+    int rc = shd_dev_init(device);
+    return rc ? rc : shd_dev_free(d_ptr);
+}
+
+int shd_device_copy(int device, void* d_dst, const void* d_src, size_t bytes) {
+    if ((!d_dst || !d_src) && bytes) return -EINVAL;
+    int rc = shd_dev_init(device);
+    return rc ? rc : shd_dev_d2d(d_dst, d_src, bytes);
 }

@@ -81,6 +81,9 @@ typedef struct {
 int shd_dev_init(int device);
 int shd_dev_malloc(void** p, size_t bytes);
 int shd_dev_free(void* p);
+/* physically contiguous when granted, else hipMalloc; *contig says which */
+int shd_dev_malloc_table(void** p, size_t bytes, int* contig);
+int shd_dev_d2d(void* d, const void* s, size_t bytes);
 int shd_dev_h2d(void* d, const void* h, size_t bytes);
 int shd_dev_d2h(void* h, const void* d, size_t bytes);
 int shd_dev_memset(void* d, int v, size_t bytes);

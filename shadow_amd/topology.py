@@ -16,15 +16,42 @@ import numpy as np
 from ._lib import MINJUMP_FN, ShdError, check, lib
 from .synth import DELIV_DTYPE, PKT_DTYPE
 
-__all__ = ["Topology", "ShdError"]
+__all__ = ["Topology", "ShdError", "DeviceTable"]
 
 
 def _s(x):
     return None if x is None else x.encode()
 
 
+class DeviceTable:
+    """A device allocation from shd_device_alloc_table (freed on close/GC).
+    ``ptr`` is the device address, ``contiguous`` whether the driver granted
+    physically contiguous memory."""
+
+    def __init__(self, device: int, nbytes: int):
+        p, c = C.c_void_p(), C.c_int()
+        check(lib().shd_device_alloc_table(device, nbytes, C.byref(p), C.byref(c)))
+        self.device, self.nbytes, self.ptr, self.contiguous = device, nbytes, p.value, bool(c.value)
+
+    def copy_from(self, d_src_ptr: int, nbytes: int):
+        assert nbytes <= self.nbytes
+        check(lib().shd_device_copy(self.device, C.c_void_p(self.ptr), C.c_void_p(d_src_ptr), nbytes))
+
+    def close(self):
+        if self.ptr:
+            check(lib().shd_device_free(self.device, C.c_void_p(self.ptr)))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Topology:
     def __init__(self, gml: str, use_shortest_path: bool = True, device: int = 0, from_file: bool = False):
+        self.device = device
         h = C.c_void_p()
         fn = lib().shd_topology_new if from_file else lib().shd_topology_new_from_text
         check(fn(gml.encode(), 1 if use_shortest_path else 0, device, C.byref(h)))
@@ -84,6 +111,12 @@ class Topology:
         sv = np.empty(A, dtype=np.int32)
         check(lib().shd_topology_copy_table(self._h, lat.ctypes.data, rel.ctypes.data, sv.ctypes.data, A))
         return lat, rel, sv
+
+    def alloc_table(self, nbytes: int) -> "DeviceTable":
+        """Device memory for a caller-owned table, placed as the library
+        places its own (shd_device_alloc_table: physically contiguous when
+        granted)."""
+        return DeviceTable(self.device, nbytes)
 
     def build_rows_device(self, row_lo: int, row_hi: int, d_table_ptr: int):
         check(lib().shd_topology_build_rows_device(self._h, row_lo, row_hi, C.c_void_p(d_table_ptr)))

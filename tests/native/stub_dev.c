@@ -21,12 +21,20 @@ int shd_dev_malloc(void** p, size_t bytes) {
     *p = malloc(bytes ? bytes : 4);
     return *p ? 0 : -ENOMEM;
 }
+int shd_dev_malloc_table(void** p, size_t bytes, int* contig) {
+    if (contig) *contig = 0;
+    return shd_dev_malloc(p, bytes);
+}
 int shd_dev_free(void* p) {
     free(p);
     return 0;
 }
 int shd_dev_h2d(void* d, const void* h, size_t bytes) {
     if (bytes) memcpy(d, h, bytes);
+    return 0;
+}
+int shd_dev_d2d(void* d, const void* s, size_t bytes) {
+    if (bytes) memcpy(d, s, bytes);
     return 0;
 }
 int shd_dev_d2h(void* h, const void* d, size_t bytes) {
