@@ -597,7 +597,7 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
 
 template <int E, typename Load>
 __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* __restrict__ out, uint32_t o,
-                                  int lane) {
+                                  int lane, unsigned long long* lk = nullptr) {
     Ev v[E];
     uint32_t rank[E];
 #pragma unroll
@@ -625,14 +625,37 @@ __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* _
 #pragma unroll
     for (int e = 0; e < E; e++)
         key[e] = (e * 64 + lane < (int)n) ? (packed ? ((v[e].t - tmin) << 24) | v[e].s : v[e].t) : ~0ull;
-    // pass 1: one 64-bit compare per pair (rank = number of smaller keys)
+    // pass 1: one 64-bit compare per pair (rank = number of smaller keys).
+    // With a per-wave LDS key array (lk: 64 * E + 8 slots) the other keys
+    // come two at a time by broadcast reads (every lane reads the same
+    // address) instead of two readlanes each; slots past n hold the maximum
+    // key, which is never smaller.
+    if (lk) {
 #pragma unroll
-    for (int ej = 0; ej < E; ej++) {
-        const int lim = (int)n - ej * 64 < 64 ? (int)n - ej * 64 : 64; // wave-uniform
-        for (int l = 0; l < lim; l++) {
-            const unsigned long long kj = readlane_u64(key[ej], l);
+        for (int e = 0; e < E; e++) lk[e * 64 + lane] = key[e]; // (padding lanes hold ~0ull)
+        if (lane < 8) lk[64 * E + lane] = ~0ull;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const ulonglong2* lk2 = reinterpret_cast<const ulonglong2*>(lk);
+        for (uint32_t j = 0; j < n; j += 8) {
+            ulonglong2 kk[4];
 #pragma unroll
-            for (int e = 0; e < E; e++) rank[e] += (uint32_t)(kj < key[e]);
+            for (int u = 0; u < 4; u++) kk[u] = lk2[(j >> 1) + u];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int e = 0; e < E; e++) rank[e] += (uint32_t)(kk[u].x < key[e]) + (uint32_t)(kk[u].y < key[e]);
+        }
+    } else {
+#pragma unroll
+        for (int ej = 0; ej < E; ej++) {
+            const int lim = (int)n - ej * 64 < 64 ? (int)n - ej * 64 : 64; // wave-uniform
+            for (int l = 0; l < lim; l++) {
+                const unsigned long long kj = readlane_u64(key[ej], l);
+#pragma unroll
+                for (int e = 0; e < E; e++) rank[e] += (uint32_t)(kj < key[e]);
+            }
         }
     }
     // Ties: the ranks are a permutation of [0, n) -- sum n(n-1)/2 -- iff all
@@ -734,15 +757,15 @@ __device__ void wave_sort_segment(const ShdDeliv* __restrict__ src, uint32_t b, 
 __device__ __forceinline__ void sort_segment(uint32_t algo, const ShdDeliv* __restrict__ src, uint32_t b,
                                              const uint16_t* perm, uint32_t n, uint32_t d,
                                              ShdDeliv* __restrict__ out, uint32_t o, int lane,
-                                             uint32_t stride = 1) {
+                                             uint32_t stride = 1, unsigned long long* lk = nullptr) {
     if (algo == 1) {
         auto load = [&](uint32_t i) {
             const ShdDeliv r = ld_ev(&src[b + (perm ? (uint32_t)perm[i] : i * stride)]);
             return Ev{r.time, r.seq, r.src_host, r.pkt_index};
         };
-        if (n <= 64) wave_rank_segment<1>(load, n, d, out, o, lane);
-        else if (n <= 128) wave_rank_segment<2>(load, n, d, out, o, lane);
-        else wave_rank_segment<4>(load, n, d, out, o, lane);
+        if (n <= 64) wave_rank_segment<1>(load, n, d, out, o, lane, lk);
+        else if (n <= 128) wave_rank_segment<2>(load, n, d, out, o, lane, lk);
+        else wave_rank_segment<4>(load, n, d, out, o, lane, lk);
     } else {
         if (n <= 64) wave_sort_segment<1>(src, b, perm, stride, n, d, out, o, lane);
         else if (n <= 128) wave_sort_segment<2>(src, b, perm, stride, n, d, out, o, lane);
@@ -1064,10 +1087,14 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
                                                      uint32_t H, uint32_t host_lo, ShdDeliv* __restrict__ out,
                                                      uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
                                                      uint32_t rsort, uint32_t flo, uint32_t fhi,
-                                                     const ShdDeliv* __restrict__ slab, uint32_t slab_rm) {
+                                                     const ShdDeliv* __restrict__ slab, uint32_t slab_rm,
+                                                     uint32_t lds_keys) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    // per-wave pass-1 key array of the rank sort (SHD_SEGSORT_LDS=0: readlanes)
+    __shared__ unsigned long long keys[4][64 * 4 + 8];
+    unsigned long long* lk = lds_keys ? keys[threadIdx.x >> 6] : nullptr;
     for (uint32_t d = flo + wave; d < fhi; d += nwaves) {
         const uint32_t b = off[d], n = off[d + 1] - b;
         const uint32_t dh = d + host_lo;
@@ -1075,13 +1102,13 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
         if (slab) {
             const uint32_t base = slab_rm ? d : d * kSlab, stride = slab_rm ? H : 1u;
             if (n <= kSlab) {
-                sort_segment(rsort, slab, base, nullptr, n, dh, out, b, lane, stride);
+                sort_segment(rsort, slab, base, nullptr, n, dh, out, b, lane, stride, lk);
             } else {
                 for (uint32_t i = lane; i < kSlab; i += 64) st_ev(&scr[b + i], ld_ev(&slab[base + (size_t)i * stride]));
                 if (lane == 0) big[atomicAdd(nbig, 1u)] = d;
             }
         } else if (n <= (uint32_t)kSmallSeg) {
-            sort_segment(rsort, scr, b, nullptr, n, dh, out, b, lane);
+            sort_segment(rsort, scr, b, nullptr, n, dh, out, b, lane, 1u, lk);
         } else if (lane == 0) {
             big[atomicAdd(nbig, 1u)] = d;
         }
@@ -1210,6 +1237,11 @@ bool staged_partition() {
 }
 
 // SHD_SEGSORT=bitonic selects the bitonic segment network, else rank sort
+// SHD_SEGSORT_LDS=0: pass-1 keys by readlane instead of LDS broadcast reads
+uint32_t lds_keys() {
+    const char* v = getenv("SHD_SEGSORT_LDS");
+    return !(v && strcmp(v, "0") == 0);
+}
 uint32_t rank_sort() {
     const char* v = getenv("SHD_SEGSORT");
     if (v && strcmp(v, "bitonic") == 0) return 0;
@@ -1323,7 +1355,7 @@ int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const 
                            n, host_lo, H, offsets, w.st1, 0u, H);
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, w.st1, offsets, H, host_lo, out,
-                       w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm);
+                       w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm, lds_keys());
     if (int rc = mid_attr()) return rc;
     hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, w.st1, offsets, w.big, w.nbig,
                        out);
