@@ -17,8 +17,10 @@
 //   k_place_ovf    overflow events only (grid-stride over a device count).
 //   k_segsort_dst  one wave per destination: register rank sort of its slab
 //                  by (time, src host, srcHostEventID), written at off[dst].
-//   k_segsort_mid  listed segments up to 4096 events: LDS bitonic, one workgroup each.
-//   k_segsort_big  larger segments: padded all-ascending bitonic network in HBM.
+//   k_segsort_mid  listed segments (> 256 events): 4096-event runs, LDS bitonic, one
+//                  workgroup each (a segment up to 4096 events is one run).
+//   k_segsort_merge  segments above 4096 events: merge-path passes over the runs,
+//                  tiles claimed by persistent workgroups (skewed destinations).
 // Alternatives, all bit-exact and parity-tested: "rank" (events in record
 // order, then k_place_rank over the whole batch) and "bucket" (LDS
 // histograms over destination buckets, k_place_bucket, k_bucket_sort; no
@@ -782,7 +784,8 @@ __device__ __forceinline__ void sort_segment(uint32_t algo, const ShdDeliv* __re
 // list (the bucket region was just read: L2 / Infinity-Cache resident) and
 // writing each segment contiguously to its final place.  Segments above
 // kSmallSeg events, and every segment of a bucket above kBucketCap events,
-// are copied unsorted to their final place and listed for k_segsort_big.
+// are copied unsorted to their final place and listed for k_segsort_mid /
+// k_segsort_merge.
 __global__ __launch_bounds__(kSortBlock) void k_bucket_sort(const ShdDeliv* __restrict__ stage, Bucketing bk,
                                                             const uint32_t* __restrict__ off1,
                                                             uint32_t* __restrict__ offsets,
@@ -873,7 +876,7 @@ __global__ __launch_bounds__(kSortBlock) void k_bucket_sort(const ShdDeliv* __re
         }
     } else {
         // oversized bucket (skewed destinations): unsorted placement through
-        // LDS cursors, every segment sorted in place by k_segsort_big
+        // LDS cursors, every segment then sorted by k_segsort_mid / _merge
         for (uint32_t j = threadIdx.x; j < nd; j += kSortBlock)
             if (cnt[j] > 0) big[atomicAdd(nbig, 1u)] = d0 + j;
         __syncthreads();
@@ -894,107 +897,354 @@ __device__ __forceinline__ bool ev_less(const ShdDeliv& a, const ShdDeliv& b) {
     return a.seq < b.seq;
 }
 
-__device__ __forceinline__ void cmpx(ShdDeliv* v, uint32_t a, uint32_t b) {
-    const ShdDeliv x = v[a], y = v[b];
-    if (ev_less(y, x)) {
-        v[a] = y;
-        v[b] = x;
-    }
+
+// ---- listed segments (above kSmallSeg events) ----
+// Segments of up to kChunk events: one workgroup sorts the segment in LDS
+// (k_segsort_mid).  Larger segments (skewed destinations: a popular server
+// can receive a sizeable share of a round) are cut into kChunk-event runs,
+// each sorted in LDS by the same kernel, then merged pairwise by
+// k_segsort_merge: merge-path tiles of kMergeTile outputs, claimed from a
+// global work counter in (pass, segment, tile) order by persistent
+// workgroups; a tile of pass p waits only for its segment's pass p-1 tiles,
+// which were claimed before it and so are being processed by running
+// workgroups -- no co-residency assumption, no grid barrier.  Runs ping-pong
+// between `out` and `scratch`; the chunk sort writes to whichever makes the
+// last pass land in `out`.  event_compare is a total order on distinct
+// events, so every merge is exact.
+constexpr uint32_t kMidSeg = 4096;      // 96 KiB of dynamic LDS
+constexpr uint32_t kChunk = kMidSeg;    // sorted runs of the chunk sort
+constexpr uint32_t kMergeTile = 2048;   // outputs per merge tile: 256 threads x 8
+constexpr uint32_t kMaxPasses = 24;     // 4096 << 24 events per segment
+constexpr uint32_t kMidThreads = 1024;
+
+__device__ __forceinline__ uint32_t merge_passes(uint32_t n) {
+    const uint32_t c = (n + kChunk - 1) / kChunk;
+    uint32_t p = 0;
+    while ((1u << p) < c) p++;
+    return p;
 }
 
-// Segments above kSmallSeg events: copy (skipped when sorting in place),
-// then an all-ascending bitonic network over the next power of two with
-// virtual +inf padding (pairs that touch the padding are skipped, which is
-// exact for this network form).
-// Listed segments of up to kMidSeg events: one workgroup loads the segment
-// into LDS (24 B per event: time, srcHostEventID, src, index), runs a
-// bitonic network over the next power of two with +inf padding (event_compare
-// is total on real events, padding sorts last) and writes the segment back in
-// order -- in place when stage2 == out.  Larger segments stay with
-// k_segsort_big.
-constexpr uint32_t kMidSeg = 4096; // 96 KiB of dynamic LDS
-__global__ __launch_bounds__(1024) void k_segsort_mid(const ShdDeliv* stage2, const uint32_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ big,
-                                                      const uint32_t* __restrict__ nbig, ShdDeliv* out) {
-    extern __shared__ __attribute__((aligned(16))) char mid_smem[];
-    Ev* sv = reinterpret_cast<Ev*>(mid_smem);
-    const uint32_t nb = *nbig;
-    for (uint32_t q = blockIdx.x; q < nb; q += gridDim.x) {
-        const uint32_t d = big[q];
-        const uint32_t b = off[d], n = off[d + 1] - b;
-        if (n == 0 || n > kMidSeg) continue; // block-uniform
-        const uint32_t dh = stage2[b].dst_host;
-        uint32_t N = 1;
-        while (N < n) N <<= 1;
-        for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
-            if (i < n) {
-                const ShdDeliv r = ld_ev(&stage2[b + i]);
-                sv[i] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
-            } else {
-                sv[i] = Ev{~0ull, ~0ull, ~0u, ~0u};
-            }
+// Merge metadata (one u32 array in the workspace, shd_dev_ws): header, then
+// per merge segment {b, n, dst host, passes} sorted by passes descending (so
+// the segments taking part in pass p are a prefix), their tile prefix, and
+// per (segment, pass) a count of finished tiles.
+struct MergeMeta {
+    uint32_t* hdr;   // [0] segments, [1] items, [2] work counter, [3] spin-limit hits,
+                     // [4 + p] first item of pass p (p <= kMaxPasses), [32 + p] segments in pass p
+    uint4* seg;      // cap
+    uint32_t* tpre;  // cap + 1
+    uint32_t* done;  // cap * kMaxPasses
+    uint32_t cap;
+};
+constexpr uint32_t kMetaHdr = 64;
+
+// Block-uniform value read from LDS or memory, made wave-uniform for the
+// compiler (an SGPR): loops and branches around barriers must be uniform in
+// its divergence analysis too, or the structurizer may split a loop between
+// lanes and the waves reach different barriers.
+__device__ __forceinline__ uint32_t bu(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+// Barrier for global memory written by one wave and read by another in the
+// same workgroup: __syncthreads() does not wait for vector stores to land
+// (MI355X_MICROARCH.md, hand-off forms), so every wave drains first.
+__device__ __forceinline__ void vm_sync() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// block-wide exclusive scan for kMidThreads threads
+__device__ __forceinline__ uint32_t block_excl_scan_1k(uint32_t v, uint32_t* total, uint32_t* ws) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int k = 0; k < (int)(kMidThreads / 64); k++) {
+        if (k < w) base += ws[k];
+        tot += ws[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// LDS bitonic sort of n <= kChunk events read from src[b ...], written to
+// dst[b ...] (in place when src == dst: the whole range is in LDS first).
+__device__ void lds_sort_run(const ShdDeliv* src, ShdDeliv* dst, uint32_t b, uint32_t n, uint32_t dh, Ev* sv) {
+    uint32_t N = 1;
+    while (N < n) N <<= 1;
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+        if (i < n) {
+            const ShdDeliv r = ld_ev(&src[b + i]);
+            sv[i] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
+        } else {
+            sv[i] = Ev{~0ull, ~0ull, ~0u, ~0u};
         }
-        __syncthreads();
-        for (uint32_t k = 2; k <= N; k <<= 1) {
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
-                    const uint32_t l = i ^ j;
-                    if (l > i) {
-                        const Ev x = sv[i], y = sv[l];
-                        const bool up = (i & k) == 0;
-                        if (up ? ev_lt(y, x) : ev_lt(x, y)) {
-                            sv[i] = y;
-                            sv[l] = x;
-                        }
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= N; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const Ev x = sv[i], y = sv[l];
+                    const bool up = (i & k) == 0;
+                    if (up ? ev_lt(y, x) : ev_lt(x, y)) {
+                        sv[i] = y;
+                        sv[l] = x;
                     }
                 }
-                __syncthreads();
-            }
-        }
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
-            st_ev(&out[b + i], ShdDeliv{sv[i].t, sv[i].q, sv[i].s, dh, sv[i].ix, 0u});
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(256) void k_segsort_big(const ShdDeliv* stage2,
-                                                     const uint32_t* __restrict__ off,
-                                                     const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig,
-                                                     ShdDeliv* out) {
-    const uint32_t nb = *nbig;
-    for (uint32_t q = blockIdx.x; q < nb; q += gridDim.x) {
-        const uint32_t d = big[q];
-        const uint32_t b = off[d], n = off[d + 1] - b;
-        if (n <= kMidSeg) continue; // k_segsort_mid
-        ShdDeliv* v = out + b;
-        if (stage2 != out) {
-            for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) {
-                ShdDeliv r = ld_ev(&stage2[b + k]);
-                r.pad = 0;
-                v[k] = r;
-            }
-        }
-        __syncthreads();
-        uint32_t N = 1;
-        while (N < n) N <<= 1;
-        for (uint32_t k = 2; k <= N; k <<= 1) {
-            const uint32_t half = k >> 1;
-            for (uint32_t i = threadIdx.x; i < N / 2; i += blockDim.x) {
-                const uint32_t blk = i / half, o = i % half;
-                const uint32_t x = blk * k + o, y = blk * k + k - 1 - o;
-                if (y < n) cmpx(v, x, y);
             }
             __syncthreads();
-            for (uint32_t j = k >> 2; j >= 1; j >>= 1) {
-                for (uint32_t i = threadIdx.x; i < N / 2; i += blockDim.x) {
-                    const uint32_t blk = i / j, o = i % j;
-                    const uint32_t x = blk * 2 * j + o, y = x + j;
-                    if (y < n) cmpx(v, x, y);
-                }
-                __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x)
+        st_ev(&dst[b + i], ShdDeliv{sv[i].t, sv[i].q, sv[i].s, dh, sv[i].ix, 0u});
+    __syncthreads();
+}
+
+// Every listed segment's kChunk-event runs, dealt round-robin over the
+// workgroups (a segment of up to kChunk events is one run, sorted straight
+// into `out`).  Workgroup 0 also builds the merge metadata.
+__global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* unsorted,
+                                                             const uint32_t* __restrict__ off,
+                                                             const uint32_t* __restrict__ big,
+                                                             const uint32_t* __restrict__ nbig, ShdDeliv* out,
+                                                             ShdDeliv* scratch, MergeMeta mm) {
+    extern __shared__ __attribute__((aligned(16))) char mid_smem[];
+    Ev* sv = reinterpret_cast<Ev*>(mid_smem);
+    __shared__ uint32_t sb[kMidThreads], sn[kMidThreads], sst[kMidThreads + 1];
+    __shared__ uint32_t ws[kMidThreads / 64];
+    __shared__ uint32_t hp[kMaxPasses + 1], cur[kMaxPasses + 1], s_part[kMaxPasses], s_ns;
+    const uint32_t nb = *nbig, tid = threadIdx.x, grid = gridDim.x;
+    uint32_t base = 0;
+    for (uint32_t qb = 0; qb < nb; qb += kMidThreads) {
+        const uint32_t q = qb + tid;
+        uint32_t b = 0, n = 0;
+        if (q < nb) {
+            const uint32_t d = big[q];
+            b = off[d];
+            n = off[d + 1] - b;
+        }
+        const uint32_t nch = (n + kChunk - 1) / kChunk;
+        uint32_t total;
+        const uint32_t st = block_excl_scan_1k(nch, &total, ws);
+        total = bu(total);
+        sb[tid] = b;
+        sn[tid] = n;
+        sst[tid] = st;
+        if (tid == 0) sst[kMidThreads] = total;
+        __syncthreads();
+        for (uint32_t i = base + (blockIdx.x + grid - base % grid) % grid; i < base + total; i += grid) {
+            const uint32_t loc = i - base;
+            uint32_t lo = 0, hi = kMidThreads; // last t with sst[t] <= loc (block-uniform search)
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (bu(sst[mid]) <= loc) lo = mid;
+                else hi = mid;
             }
+            const uint32_t c = loc - bu(sst[lo]), sbb = bu(sb[lo]), snn = bu(sn[lo]);
+            const uint32_t cb = sbb + c * kChunk, cn = snn - c * kChunk < kChunk ? snn - c * kChunk : kChunk;
+            ShdDeliv* dst = (snn <= kChunk || (merge_passes(snn) & 1u) == 0) ? out : scratch;
+            lds_sort_run(unsorted, dst, cb, cn, bu(unsorted[cb].dst_host), sv);
+        }
+        base += total;
+        __syncthreads();
+    }
+    if (blockIdx.x != 0) return;
+    // ---- merge metadata (workgroup 0): segments above kChunk by passes, descending
+    for (uint32_t k = tid; k <= kMaxPasses; k += kMidThreads) hp[k] = 0;
+    __syncthreads();
+    for (uint32_t q = tid; q < nb; q += kMidThreads) {
+        const uint32_t d = big[q], n = off[d + 1] - off[d];
+        if (n > kChunk) atomicAdd(&hp[merge_passes(n)], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int p = (int)kMaxPasses; p >= 1; p--) { // descending passes
+            cur[p] = acc;
+            acc += hp[p];
+        }
+        s_ns = acc < mm.cap ? acc : mm.cap; // (read back through LDS: see vm_sync)
+        mm.hdr[0] = s_ns;
+        if (acc > mm.cap) mm.hdr[3] |= 0x80000000u; // (cannot happen: cap covers n / (kChunk + 1))
+        // segments taking part in pass p: those with more than p passes
+        uint32_t part = 0;
+        for (int p = (int)kMaxPasses - 1; p >= 0; p--) {
+            part += hp[p + 1];
+            s_part[p] = part;
+            mm.hdr[32 + p] = part;
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < nb; q += kMidThreads) {
+        const uint32_t d = big[q], b = off[d], n = off[d + 1] - b;
+        if (n <= kChunk) continue;
+        const uint32_t k = atomicAdd(&cur[merge_passes(n)], 1u);
+        if (k < mm.cap) mm.seg[k] = make_uint4(b, n, unsorted[b].dst_host, merge_passes(n));
+    }
+    vm_sync(); // other waves read these entries next
+    // tile prefix over the sorted segments, then the per-pass item bases
+    const uint32_t ns = bu(s_ns);
+    uint32_t run = 0;
+    for (uint32_t kb = 0; kb < ns; kb += kMidThreads) {
+        const uint32_t k = kb + tid;
+        const uint32_t nt = k < ns ? (mm.seg[k].y + kMergeTile - 1) / kMergeTile : 0u;
+        uint32_t total;
+        const uint32_t st = block_excl_scan_1k(nt, &total, ws);
+        if (k < ns) mm.tpre[k] = run + st;
+        run += bu(total);
+    }
+    vm_sync(); // (thread 0 reads other threads' tpre entries)
+    if (tid == 0) {
+        mm.tpre[ns] = run;
+        uint32_t item = 0;
+        for (uint32_t p = 0; p < kMaxPasses; p++) {
+            mm.hdr[4 + p] = item;
+            item += s_part[p] == ns ? run : mm.tpre[s_part[p]]; // (tpre[ns]: this thread's own store)
+        }
+        mm.hdr[4 + kMaxPasses] = item;
+        mm.hdr[1] = item;
+        mm.hdr[2] = 0;
+    }
+    for (uint32_t k = tid; k < ns * kMaxPasses; k += kMidThreads) mm.done[k] = 0;
+}
+
+// Merge-path split for output diagonal `diag` of A (la) and B (lb) in
+// global memory: the number of outputs taken from A, i.e. the first m in
+// [lo, hi) with B[diag - 1 - m] < A[m] (else hi).  The workgroup probes up
+// to blockDim positions per step: one dependent load pair per step, log_256
+// of the range.  Block-uniform; sh: one LDS word.
+__device__ uint32_t coop_split(const ShdDeliv* A, uint32_t la, const ShdDeliv* B, uint32_t lb, uint32_t diag,
+                               uint32_t* sh) {
+    uint32_t lo = diag > lb ? diag - lb : 0u, hi = diag < la ? diag : la;
+    const uint32_t nt = blockDim.x;
+    while (lo < hi) {
+        const uint32_t span = hi - lo;
+        const bool dense = span <= nt; // probes lo + k, k < span: this step decides
+        const uint32_t k = threadIdx.x;
+        const uint32_t m = dense ? lo + k : lo + (uint32_t)(((unsigned long long)span * k) / nt);
+        bool pred = false;
+        if (!dense || k < span) pred = ev_less(ld_ev(&B[diag - 1 - m]), ld_ev(&A[m]));
+        if (threadIdx.x == 0) sh[0] = nt;
+        __syncthreads();
+        if (pred) atomicMin(&sh[0], k);
+        __syncthreads();
+        const uint32_t f = bu(sh[0]); // first probe that is true (nt: none)
+        __syncthreads();
+        if (dense) return f == nt ? hi : lo + f;
+        auto mk = [&](uint32_t q) { return lo + (uint32_t)(((unsigned long long)span * q) / nt); };
+        if (f == nt) {
+            lo = mk(nt - 1) + 1;
+        } else {
+            const uint32_t nlo = f ? mk(f - 1) + 1 : lo;
+            hi = mk(f);
+            lo = nlo;
+        }
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_segsort_merge(ShdDeliv* out, ShdDeliv* scratch, MergeMeta mm) {
+    __shared__ Ev tile[kMergeTile];
+    __shared__ uint32_t sh[8];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t items = bu(mm.hdr[1]);
+    uint32_t done_slot = ~0u; // the previous tile's (segment, pass) counter, published at the next claim
+    for (;;) {
+        // one lane: publish the previous tile (its stores were drained before
+        // the barrier that ended it), then claim the next -- a single lane
+        // region between barriers (a second one at the end of the body let
+        // the compiler split the loop between lanes)
+        if (tid == 0) {
+            if (done_slot != ~0u) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                atomicAdd(&mm.done[done_slot], 1u);
+            }
+            sh[1] = atomicAdd(&mm.hdr[2], 1u);
         }
         __syncthreads();
+        const uint32_t item = bu(sh[1]);
+        __syncthreads();
+        if (item >= items) break;
+        uint32_t p = 0;
+        while (p + 1 < kMaxPasses && bu(mm.hdr[4 + p + 1]) <= item) p++;
+        const uint32_t loc = item - bu(mm.hdr[4 + p]);
+        uint32_t lo = 0, hi = bu(mm.hdr[32 + p]); // the segment: last k with tpre[k] <= loc
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (bu(mm.tpre[mid]) <= loc) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t sgi = lo;
+        const uint4 sg = mm.seg[sgi];
+        const uint32_t b = bu(sg.x), n = bu(sg.y), dh = bu(sg.z), P = bu(sg.w);
+        const uint32_t t = loc - bu(mm.tpre[sgi]);
+        const uint32_t ntile = (n + kMergeTile - 1) / kMergeTile;
+        if (p > 0) { // the segment's previous pass must be complete (its tiles were claimed before this one)
+            if (tid == 0) {
+                uint32_t spins = 0;
+                while (__hip_atomic_load(&mm.done[sgi * kMaxPasses + p - 1], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) < ntile) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins == (1u << 22)) { // every wave ends (inputs that never complete would be a bug)
+                        atomicAdd(&mm.hdr[3], 1u);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // drops this CU's stale lines
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (holds the barrier for the invalidate)
+            }
+            __syncthreads();
+        }
+        // pass p reads the buffer the chunk sort (p = 0) or pass p - 1 wrote
+        ShdDeliv* x0 = (P & 1u) ? scratch : out;
+        ShdDeliv* x1 = (P & 1u) ? out : scratch;
+        const ShdDeliv* src = ((p & 1u) ? x1 : x0) + b;
+        ShdDeliv* dst = ((p & 1u) ? x0 : x1) + b;
+        const uint32_t L = kChunk << p;
+        const uint32_t o0 = t * kMergeTile;            // tile outputs [o0, o1) of the segment
+        const uint32_t a0 = o0 / (2 * L) * (2 * L);   // its run pair (a tile never straddles two)
+        const uint32_t la = n - a0 < L ? n - a0 : L;
+        const uint32_t lb = n - a0 - la < L ? n - a0 - la : L;
+        const uint32_t d0 = o0 - a0, d1 = (o0 + kMergeTile < n ? o0 + kMergeTile : n) - a0;
+        const ShdDeliv* A = src + a0;
+        const ShdDeliv* B = A + la;
+        const uint32_t s0 = lb ? coop_split(A, la, B, lb, d0, sh + 4) : d0;
+        const uint32_t s1 = lb ? coop_split(A, la, B, lb, d1, sh + 4) : d1;
+        const uint32_t ta = s1 - s0, tb = (d1 - d0) - ta;
+        for (uint32_t i = tid; i < ta + tb; i += blockDim.x) {
+            const ShdDeliv r = i < ta ? ld_ev(&A[s0 + i]) : ld_ev(&B[d0 - s0 + (i - ta)]);
+            tile[i] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
+        }
+        __syncthreads();
+        const uint32_t k0 = tid * (kMergeTile / 256);
+        if (k0 < ta + tb) {
+            // this thread's split inside the tile (A part = tile[0, ta), B part = tile[ta, ta + tb))
+            uint32_t lo2 = k0 > tb ? k0 - tb : 0u, hi2 = k0 < ta ? k0 : ta;
+            while (lo2 < hi2) {
+                const uint32_t m = (lo2 + hi2) >> 1;
+                if (ev_lt(tile[ta + k0 - 1 - m], tile[m])) hi2 = m;
+                else lo2 = m + 1;
+            }
+            uint32_t i = lo2, j = k0 - lo2;
+            const uint32_t kend = k0 + kMergeTile / 256 < ta + tb ? k0 + kMergeTile / 256 : ta + tb;
+            for (uint32_t k = k0; k < kend; k++) {
+                const bool takeA = j >= tb || (i < ta && !ev_lt(tile[ta + j], tile[i]));
+                const Ev e = takeA ? tile[i] : tile[ta + j];
+                if (takeA) i++;
+                else j++;
+                st_ev(&dst[a0 + d0 + k], ShdDeliv{e.t, e.q, e.s, dh, e.ix, 0u});
+            }
+        }
+        // the tile is published at the next claim (MI355X_MICROARCH.md, valid
+        // hand-off forms): every storing wave drains its stores, barrier, then
+        // one lane's agent release, drain, and the counter add consumers poll
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        done_slot = sgi * kMaxPasses + p;
     }
 }
 
@@ -1137,6 +1387,8 @@ struct Ws {
     uint32_t* nbig = nullptr; // [0] big segments, [1] slab overflow events
     size_t cap_slab = 0;      // slab pipeline: H x kSlab event slots
     ShdDeliv* slab = nullptr;
+    uint32_t* meta = nullptr; // big-segment merge metadata (MergeMeta)
+    uint32_t cap_meta = 0;    // merge segments it holds
 };
 
 int hip_status(hipError_t e, const char* what) {
@@ -1169,6 +1421,20 @@ int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
             (rc = hip_status(hipMalloc((void**)&w.st2, sizeof(ShdDeliv) * cap), "hipMalloc ws.st2")))
             return rc;
         w.cap_n = cap;
+    }
+    // merge metadata: segments above kChunk events are at most n / (kChunk + 1)
+    const uint32_t cm = (uint32_t)((n + n / 8 + 1024) / (kChunk + 1) + 2);
+    if (!w.meta || cm > w.cap_meta) {
+        if ((rc = ws_quiesce(w))) return rc;
+        (void)hipFree(w.meta);
+        w.meta = nullptr;
+        w.cap_meta = 0;
+        if ((rc = hip_status(hipMalloc((void**)&w.meta, 4 * ((size_t)kMetaHdr + 4ull * cm + cm + 1 +
+                                                               (size_t)cm * kMaxPasses)),
+                             "hipMalloc ws.meta")))
+            return rc;
+        if ((rc = hip_status(hipMemset(w.meta, 0, 4 * (size_t)kMetaHdr), "hipMemset ws.meta"))) return rc;
+        w.cap_meta = cm;
     }
     if (m + 1 > w.cap_m) {
         (void)hipFree(w.cnt1);
@@ -1211,6 +1477,16 @@ int slab_reserve(Ws& w, uint32_t H) {
     return rc;
 }
 
+MergeMeta merge_meta(const Ws& w) {
+    MergeMeta m;
+    m.hdr = w.meta;
+    m.seg = reinterpret_cast<uint4*>(w.meta + kMetaHdr);
+    m.tpre = w.meta + kMetaHdr + 4ull * w.cap_meta;
+    m.done = m.tpre + w.cap_meta + 1;
+    m.cap = w.cap_meta;
+    return m;
+}
+
 // k_segsort_mid's dynamic LDS (above the 64 KiB default), set once per process
 constexpr size_t kMidLds = sizeof(Ev) * kMidSeg;
 int mid_attr() {
@@ -1221,6 +1497,17 @@ int mid_attr() {
                         "hipFuncSetAttribute k_segsort_mid");
     done = rc == 0;
     return rc;
+}
+
+// listed segments: LDS runs, then the merge passes of the larger ones
+int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDeliv* out, hipStream_t s) {
+    if (int rc = mid_attr()) return rc;
+    const MergeMeta mm = merge_meta(w);
+    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(kMidThreads), kMidLds, s, unsorted, offsets, w.big, w.nbig,
+                       out, w.st1, mm);
+    if (int rc = hip_status(hipGetLastError(), "k_segsort_mid launch")) return rc;
+    hipLaunchKernelGGL(k_segsort_merge, dim3(512), dim3(256), 0, s, out, w.st1, mm);
+    return hip_status(hipGetLastError(), "k_segsort_merge launch");
 }
 
 unsigned grid_for(size_t n, unsigned block, unsigned cap) {
@@ -1325,9 +1612,7 @@ int group_and_sort(Ws& w, const ShdDeliv* in, const uint8_t* status, const uint3
     mark(3, s);
     hipLaunchKernelGGL(k_bucket_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, w.st1, bk, w.off1, offsets, out,
                        w.big, w.nbig);
-    if (int rc = mid_attr()) return rc;
-    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, out, offsets, w.big, w.nbig, out);
-    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, out, offsets, w.big, w.nbig, out);
+    if (int rc = sort_listed(w, out, offsets, out, s)) return rc; // placed unsorted in out; st1 is free now
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort launch");
@@ -1356,10 +1641,7 @@ int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const 
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, w.st1, offsets, H, host_lo, out,
                        w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm, lds_keys());
-    if (int rc = mid_attr()) return rc;
-    hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(1024), kMidLds, s, w.st1, offsets, w.big, w.nbig,
-                       out);
-    hipLaunchKernelGGL(k_segsort_big, dim3(1024), dim3(256), 0, s, w.st1, offsets, w.big, w.nbig, out);
+    if (int rc = sort_listed(w, w.st1, offsets, out, s)) return rc;
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort_rank launch");
@@ -1421,6 +1703,7 @@ extern "C" void shd_dev_ws_free(void* p) {
     (void)hipFree(w->big);
     (void)hipFree(w->nbig);
     (void)hipFree(w->slab);
+    (void)hipFree(w->meta);
     if (w->done) (void)hipEventDestroy(w->done);
     delete w;
 }

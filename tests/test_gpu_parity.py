@@ -285,6 +285,39 @@ def test_deliv_sort_device_against_lexsort(pipeline):
     assert offs[-1] == n and np.array_equal(np.diff(offs), np.bincount(ev["dst_host"] - lo, minlength=hi - lo))
 
 
+def test_deliv_sort_skewed_destinations_merge_passes(pipeline):
+    """Skewed destinations (a popular server): segments of 150k, 40k, 9k, 5k,
+    4097 and 4096 events -- 6, 4, 2, 1, 1 and 0 merge passes over the
+    4096-event LDS runs -- beside thousands of small ones; every event must
+    come out in event_compare order (the keys are distinct: exact compare)."""
+    import torch
+    top, _, _, _ = make_pair(synth.complete_graph_gml(5, 3), 5)
+    rng = np.random.default_rng(11)
+    lo, hi = 500, 4500
+    sizes = [150_000, 40_000, 9_000, 5_000, 4_097, 4_096]
+    hot = np.concatenate([np.full(k, lo + 3 * i, dtype=np.int64) for i, k in enumerate(sizes)])
+    rest = rng.integers(lo, hi, 100_000)
+    dst = np.concatenate([hot, rest])
+    n = len(dst)
+    ev = np.zeros(n, dtype=synth.DELIV_DTYPE)
+    ev["dst_host"] = rng.permutation(dst)
+    ev["time"] = 110_000_000 + rng.integers(0, 2_000, n) * 1_000  # many equal times
+    ev["src_host"] = rng.integers(0, 300, n)                       # many equal (time, src)
+    ev["seq"] = rng.permutation(n)                                 # distinct: a total order
+    ev["pkt_index"] = np.arange(n)
+    d_in = torch.from_numpy(ev.view(np.uint8)).cuda()
+    d_out = torch.empty_like(d_in)
+    d_off = torch.empty(hi - lo + 1, dtype=torch.int32, device="cuda")
+    for _ in range(2):  # the second call reuses the workspace and its merge metadata
+        top.deliv_sort_device(d_in.data_ptr(), n, lo, hi, d_out.data_ptr(), d_off.data_ptr(), 0)
+        torch.cuda.synchronize()
+        got = d_out.cpu().numpy().view(synth.DELIV_DTYPE)
+        want = ev[np.lexsort((ev["seq"], ev["src_host"], ev["time"], ev["dst_host"]))]
+        assert np.array_equal(got, want)
+        offs = d_off.cpu().numpy()
+        assert np.array_equal(np.diff(offs), np.bincount(ev["dst_host"] - lo, minlength=hi - lo))
+
+
 def test_multi_gpu_row_shards_assemble():
     """Rows built in shards into a caller-owned (torch) table == one-shot build."""
     import torch
