@@ -157,9 +157,9 @@ def main():
     log(f"C2 graph V={V} H={H} A={A} ready in {time.perf_counter() - t0:.1f}s")
 
     # routing rows sharded by source slot, assembled by RCCL all-gather (§8e)
-    # The resident table the rounds gather from is placed as the library
-    # places its own (shd_device_alloc_table: physically contiguous when
-    # granted); at N>1 the rows are all-gathered in a torch tensor and copied in.
+    # The resident table the rounds gather from is allocated as the library
+    # allocates its own (shd_device_alloc_table); at N>1 the rows are
+    # all-gathered in a torch tensor and copied in.
     rows_per = (A + world - 1) // world
     table = top.alloc_table(A * A * 16)
     lo, hi = min(A, rank * rows_per), min(A, (rank + 1) * rows_per)
@@ -343,7 +343,7 @@ def main():
         log(f"C4 graph V={args.c4_vertices} H={args.c4_hosts} A={A4} ready in {time.perf_counter() - t0:.1f}s")
         per4 = (A4 + world - 1) // world
         l4, h4 = min(A4, rank * per4), min(A4, (rank + 1) * per4)
-        shard4 = t4.alloc_table(max(h4 - l4, 1) * A4 * 16)  # placed as the library places tables
+        shard4 = t4.alloc_table(max(h4 - l4, 1) * A4 * 16)  # allocated as the library allocates tables
         barrier()
         torch.cuda.synchronize(dev)
         s0 = time.perf_counter()

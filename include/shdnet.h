@@ -154,13 +154,11 @@ int shd_topology_copy_table(ShdTopology* top, double* lat_ms, double* rel, int32
  * all-gather completes), then adopt the completed table as the resident one
  * (the caller keeps it alive for the topology's lifetime). */
 int shd_topology_slot_count(ShdTopology* top, int* slots);
-/* Device memory for a routing table (or any randomly gathered array):
- * physically contiguous when the driver grants it (hipDeviceMallocContiguous:
- * few, large translation fragments, so uniformly random 16-B gathers over a
- * multi-GB table do not depend on how the allocation happened to be
- * fragmented), else an ordinary device allocation.  *contiguous (may be NULL)
- * says which.  Free with shd_device_free.  The library's own tables
- * (shd_topology_build_routes) are allocated this way. */
+/* Device memory for a caller-owned routing table (or any device array the
+ * library should own the placement of): the allocation the library uses for
+ * its own tables (shd_topology_build_routes).  *contiguous (may be NULL)
+ * reports whether it is physically contiguous (currently never: measured
+ * slower for the table build).  Free with shd_device_free. */
 int shd_device_alloc_table(int device, size_t bytes, void** d_out, int* contiguous);
 int shd_device_free(int device, void* d_ptr);
 /* Device-to-device copy (e.g. an all-gathered table into one from

@@ -36,21 +36,14 @@ extern "C" int shd_dev_malloc(void** p, size_t bytes) {
     return hip_err(hipMalloc(p, bytes ? bytes : 4), "hipMalloc");
 }
 
-// Randomly gathered tables: a physically contiguous allocation keeps the
-// gather rate independent of how an ordinary allocation happens to be
-// fragmented (scripts/ubench_tlb.hip: 10M random 16-B gathers over 6.3 GB
-// take 0.253-0.272 ms on hipMalloc'd tables depending on the allocation,
-// 0.251-0.255 ms on contiguous ones).  Not for the per-wave routing slabs:
-// their strided partitions run slower on contiguous memory.
+// Tables: an ordinary device allocation.  (Physically contiguous memory,
+// hipDeviceMallocContiguous, was measured: 10M random 16-B gathers over
+// 6.3 GB took 0.251-0.255 ms on it vs 0.253-0.272 ms depending on the
+// hipMalloc'd allocation, but the write-heavy users were slower -- the C4
+// table build 10.3 vs 9.0-9.2 s, per-wave routing slabs and packet slabs far
+// more)
 extern "C" int shd_dev_malloc_table(void** p, size_t bytes, int* contig) {
-    *p = nullptr;
     if (contig) *contig = 0;
-    if (bytes && hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
-        if (contig) *contig = 1;
-        return 0;
-    }
-    (void)hipGetLastError();
-    *p = nullptr;
     return shd_dev_malloc(p, bytes);
 }
 

@@ -113,9 +113,8 @@ class Topology:
         return lat, rel, sv
 
     def alloc_table(self, nbytes: int) -> "DeviceTable":
-        """Device memory for a caller-owned table, placed as the library
-        places its own (shd_device_alloc_table: physically contiguous when
-        granted)."""
+        """Device memory for a caller-owned table, allocated as the library
+        allocates its own (shd_device_alloc_table)."""
         return DeviceTable(self.device, nbytes)
 
     def build_rows_device(self, row_lo: int, row_hi: int, d_table_ptr: int):
