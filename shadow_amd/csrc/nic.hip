@@ -45,6 +45,36 @@ constexpr uint64_t kNever = ~0ull;
 
 enum { kErrRing = 1, kErrOrder = 2, kErrHost = 4, kErrId = 8, kErrWindow = 16, kErrAssert = 32 };
 
+// A lane's packet fates (receive time, status) go out in runs: the ids a
+// router pops are consecutive (FIFO over the carried run, then over the
+// window's arrival segment), so up to kStage of them are staged in LDS and
+// stored back to back, where one store per pop left each 128-B line to be
+// written back from L2 many times over.  A dropped packet's time is written
+// as ~0, the value its slot already holds (shd_nic_run's memset / the
+// window that queued it).
+constexpr uint32_t kStage = 16;
+struct FateStage {
+    uint64_t* rtime;
+    uint8_t* rstat;
+    uint64_t* lt; // this lane's column of the wave's [kStage][64] LDS arrays
+    uint8_t* ls;
+    uint32_t id0, n;
+    __device__ __forceinline__ void flush() {
+        for (uint32_t k = 0; k < n; k++) {
+            rtime[id0 + k] = lt[64 * k];
+            rstat[id0 + k] = ls[64 * k];
+        }
+        n = 0;
+    }
+    __device__ __forceinline__ void put(uint32_t id, uint64_t t, uint8_t st) {
+        if (n && id != id0 + n) flush();
+        if (!n) id0 = id;
+        lt[64 * n] = t;
+        ls[64 * n] = st;
+        if (++n == kStage) flush();
+    }
+};
+
 struct RouterQ {
     // carried entries (ring) first, then the window's arrivals [qhead, qtail)
     ShdCodelEntry* ring;
@@ -52,9 +82,11 @@ struct RouterQ {
     const ShdDeliv* ev;
     const uint32_t* evlen;
     uint32_t qhead, qtail, id_base;
-    uint64_t* rtime;
-    uint8_t* rstat;
+    FateStage* out;
     bool bad;
+    uint32_t cidx;   // arrival index whose time / length are cached (~0: none)
+    uint64_t ctime;
+    uint32_t clen;
 
     __device__ __forceinline__ bool empty() const { return len == 0 && qhead == qtail; }
     __device__ __forceinline__ bool pop(ShdCodelEntry& e) {
@@ -65,12 +97,14 @@ struct RouterQ {
             return true;
         }
         if (qhead == qtail) return false;
-        e = ShdCodelEntry{ev[qhead].time, id_base + qhead, evlen[qhead]};
+        // (the arrival just enqueued is usually the one popped: no re-read)
+        e = qhead == cidx ? ShdCodelEntry{ctime, id_base + qhead, clen}
+                          : ShdCodelEntry{ev[qhead].time, id_base + qhead, evlen[qhead]};
         qhead++;
         return true;
     }
     __device__ __forceinline__ void drop(uint32_t id) { // PDS_ROUTER_DROPPED
-        rstat[id] = SHD_NIC_DROPPED;
+        out->put(id, ~0ull, SHD_NIC_DROPPED);
     }
 };
 
@@ -103,8 +137,7 @@ struct Host {
         while (boot || s.recv_remaining >= kMtu) {
             ShdCodelEntry e;
             if (!shd_codel::dequeue(q, s.router, now, e)) break; // router_dequeue (router.c:123-131)
-            q.rtime[e.pkt] = now;
-            q.rstat[e.pkt] = SHD_NIC_RECEIVED;
+            q.out->put(e.pkt, now, SHD_NIC_RECEIVED);
             if (!boot) {
                 consume(s.recv_remaining, e.length);
                 schedule_if_needed(s, now);
@@ -169,15 +202,18 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
                                                 uint32_t id_base, uint64_t* __restrict__ rtime,
                                                 uint8_t* __restrict__ rstat, uint64_t fate_cap,
                                                 uint64_t* __restrict__ stime, int* __restrict__ err) {
+    __shared__ uint64_t stage_t[kStage * 64];
+    __shared__ uint8_t stage_s[kStage * 64];
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= n) return;
     const uint32_t self = host_base + h;
+    FateStage out{rtime, rstat, stage_t + threadIdx.x, stage_s + threadIdx.x, 0u, 0u};
     Host H;
     H.s = states[h];
     uint32_t i = eoff[h];
     const uint32_t iend = eoff[h + 1];
     H.q = RouterQ{rings + (size_t)h * ring_cap, ring_cap, H.s.router.head, H.s.router.len, ev, elen, i, i, id_base,
-                  rtime, rstat, false};
+                  &out, false, ~0u, 0, 0};
     H.sends = sends;
     H.sq = H.sk = soff ? soff[h] : 0;
     const uint32_t kend = soff ? soff[h + 1] : 0;
@@ -189,6 +225,17 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
     // every lane ends: at most this many events (a host whose bucket refills
     // by 0 bytes per ms schedules a refill every ms for ever, as the reference)
     uint64_t budget = (uint64_t)(iend - i) + (kend - H.sk) + (1ull << 24);
+    // the next arrival and its length in registers, the one after it in flight
+    ShdDeliv a_cur{}, a_nxt{};
+    uint32_t l_cur = 0, l_nxt = 0;
+    if (i < iend) {
+        a_cur = ev[i];
+        l_cur = elen[i];
+    }
+    if (i + 1 < iend) {
+        a_nxt = ev[i + 1];
+        l_nxt = elen[i + 1];
+    }
     while (!bad) {
         if (budget-- == 0) {
             bad |= kErrWindow;
@@ -198,8 +245,7 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
         const bool have_s = H.sk < kend;
         const bool have_r = H.s.refill_pending && H.s.refill_time < window_end;
         if (!have_a && !have_s && !have_r) break;
-        ShdDeliv a;
-        if (have_a) a = ev[i];
+        const ShdDeliv a = a_cur;
         const uint64_t ta = have_a ? a.time : kNever;
         const uint64_t ts = have_s ? sends[H.sk].ready : kNever;
         const uint64_t tr = have_r ? H.s.refill_time : kNever;
@@ -215,8 +261,17 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
             last = ta;
             // router_enqueue (router.c:103-121): peek, enqueue, receive if it was empty
             const bool buffered = !H.q.empty();
+            H.q.cidx = i;
+            H.q.ctime = ta;
+            H.q.clen = l_cur;
             H.q.qtail = ++i;
-            H.s.router.total_size += elen[i - 1]; // _routerqueuecodel_enqueue (:113-136)
+            H.s.router.total_size += l_cur; // _routerqueuecodel_enqueue (:113-136)
+            a_cur = a_nxt;
+            l_cur = l_nxt;
+            if (i + 1 < iend) {
+                a_nxt = ev[i + 1];
+                l_nxt = elen[i + 1];
+            }
             if (!buffered) H.receive(ta);
         } else if (own_is_send) {
             if (ts >= window_end) {
@@ -242,6 +297,7 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
         H.q.ring[tail] = ShdCodelEntry{ev[k].time, id_base + k, elen[k]};
         H.q.len++;
     }
+    out.flush();
     if (bad) atomicOr(err, bad);
     H.s.router.head = H.q.head;
     H.s.router.len = H.q.len;
