@@ -130,6 +130,7 @@ struct Bucketing {
     uint32_t xcd;     // 1: XCD-grouped column order (see col_of)
     uint32_t rsort;   // segment sort: 1 rank (default), 0 bitonic (see sort_segment)
     uint32_t slab_rm; // slab layout: 1 rank-major (slot r of host d at r * H + d), 0 host-major (d * kSlab + r)
+    uint32_t agg;     // wave-aggregated destination slots (dest_slot); SHD_DEST_AGG=0 turns them off
 };
 
 // Matrix column of chunk g.  Workgroups are dealt to the 8 XCDs round-robin
@@ -142,6 +143,65 @@ __device__ __forceinline__ uint32_t col_of(const Bucketing& bk, uint32_t g) {
     if (!bk.xcd) return g;
     const uint32_t q = bk.ntiles >> 3, r = bk.ntiles & 7, x = g & 7;
     return x * q + (x < r ? x : r) + (g >> 3);
+}
+
+// Per-destination slot counters, wave-aggregated.  Every lane that takes a
+// slot hashes its destination to one of 64 per-wave LDS slots and writes its
+// lane id there; the lanes whose slot holds a lane of the same destination
+// form a group: one global atomic per group (by that lane) hands the group a
+// base, and each member adds its rank inside the group (an LDS atomic).
+// Lanes whose slot was taken by another destination add alone.  With
+// uniform destinations every group has one member (a few LDS operations
+// more per event); with a hot destination -- a popular server, Zipf -- its
+// lanes share one atomic, where one per event serialised on one address.
+// The slots a destination's events get are a permutation of [0, count) in
+// any arrangement; the segment sort orders them.
+struct DestAgg {
+    uint32_t* owner; // [64] per wave
+    uint32_t* cnt;   // [64] per wave, zero between uses
+    uint32_t* base;  // [64] per wave
+    uint32_t on;     // 0: one atomic per event (SHD_DEST_AGG=0)
+};
+__device__ __forceinline__ void agg_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// called by every lane of the wave (want: this lane takes a slot of d)
+__device__ __forceinline__ uint32_t dest_slot(bool want, uint32_t d, uint32_t* __restrict__ gcnt, const DestAgg& a,
+                                              int lane) {
+    if (!a.on) return want ? atomicAdd(&gcnt[d], 1u) : 0u;
+    const uint32_t slot = (d * 2654435761u) >> 26;
+    if (want) a.owner[slot] = (uint32_t)lane;
+    agg_fence();
+    const uint32_t ol = want ? a.owner[slot] : (uint32_t)lane;
+    const uint32_t od = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ol << 2), (int)d);
+    const bool grp = want && od == d;
+    uint32_t r = 0;
+    if (grp) r = atomicAdd(&a.cnt[slot], 1u);
+    agg_fence();
+    if (grp && ol == (uint32_t)lane) {
+        const uint32_t c = a.cnt[slot];
+        a.base[slot] = atomicAdd(&gcnt[d], c);
+        a.cnt[slot] = 0;
+    }
+    agg_fence();
+    if (grp) return a.base[slot] + r;
+    return want ? atomicAdd(&gcnt[d], 1u) : 0u;
+}
+
+// One atomic per wave for the lanes that want a slot of a shared counter
+// (the slab overflow list: with a hot destination most of its events
+// overflow, and one atomic per event on one address serialised them).
+// Called by every lane; returns this lane's slot (want) or 0.
+__device__ __forceinline__ uint32_t wave_alloc(bool want, uint32_t* counter, int lane) {
+    const unsigned long long m = __ballot(want);
+    if (!m) return 0u;
+    const int first = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(counter, (uint32_t)__builtin_popcountll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, first);
+    return base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
 }
 
 // kMode 1 ("rank" pipeline): each delivered event takes its slot in its
@@ -166,6 +226,11 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
     constexpr bool kRank = kMode != 0;
     __shared__ uint32_t hist[kRank ? 1 : kMaxBuckets];
     __shared__ unsigned long long wmin[kBlock / 64];
+    __shared__ uint32_t agg_s[kRank ? 3 * kBlock : 1];
+    const int lane = threadIdx.x & 63;
+    const DestAgg agg{agg_s + 3 * (threadIdx.x & ~63u), agg_s + 3 * (threadIdx.x & ~63u) + 64,
+                      agg_s + 3 * (threadIdx.x & ~63u) + 128, bk.agg};
+    if (kRank) agg.cnt[lane] = 0;
     if (!kRank)
         for (uint32_t b = threadIdx.x; b < bk.nb; b += kBlock) hist[b] = 0;
     __syncthreads();
@@ -221,35 +286,46 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
 #pragma unroll
         for (int k = 0; k < kB; k++)
             if (si[k] >= 0 && di[k] >= 0) e[k] = tab[ei[k]];
+        uint8_t st[kB];
+        uint64_t tt[kB];
 #pragma unroll
         for (int k = 0; k < kB; k++) {
-            if (!live[k]) continue;
-            uint8_t st = 0xff; // unregistered host: not delivered
-            if (si[k] >= 0 && di[k] >= 0) {
+            st[k] = 0xff; // unregistered host: not delivered
+            tt[k] = 0;
+            if (live[k] && si[k] >= 0 && di[k] >= 0) {
                 uint32_t rs = p[k].rng_state;
                 const double chance = (double)glibc_rand_r(&rs) / 2147483647.0; // random_nextDouble
-                st = SHD_DROPPED_LOSS;
+                st[k] = SHD_DROPPED_LOSS;
                 if (p[k].now < boot_end || chance <= e[k].rel || p[k].payload_len == 0) { // worker.c:545
                     uint64_t t = p[k].now + (uint64_t)ceil(e[k].lat * 1000000.0);     // worker.c:548-549
                     if (t >= end_time) {                                              // scheduler.c:236-239
-                        st = SHD_DROPPED_END;
+                        st[k] = SHD_DROPPED_END;
                     } else {
                         if (p[k].src_host != p[k].dst_host && t < barrier) t = barrier; // host_single.c:187-192
-                        st = SHD_DELIVERED;
-                        uint32_t rank;
-                        if (kRank) rank = atomicAdd(&cnt1[p[k].dst_host], 1u);
-                        else rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
-                        const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
-                        if (kMode < 2) st_ev(&tmp[idx[k]], ev);
-                        else if (rank < kSlab)
-                            st_ev(&tmp[bk.slab_rm ? (size_t)rank * bk.H + p[k].dst_host
-                                                  : (size_t)p[k].dst_host * kSlab + rank], ev);
-                        else st_ev(&ovf[atomicAdd(novf, 1u)], ev); // rare: segments above kSlab
-                        if (t >= barrier && t < mn) mn = t; // worker.c:350-363
+                        st[k] = SHD_DELIVERED;
+                        tt[k] = t;
                     }
                 }
             }
-            status[idx[k]] = st;
+        }
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            const bool dl = st[k] == SHD_DELIVERED;
+            uint32_t rank = 0;
+            if (kRank) rank = dest_slot(dl, p[k].dst_host, cnt1, agg, lane); // (every lane: wave-level groups)
+            const uint32_t oslot = kMode == 2 ? wave_alloc(dl && rank >= kSlab, novf, lane) : 0u;
+            if (dl) {
+                const uint64_t t = tt[k];
+                if (!kRank) rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
+                const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
+                if (kMode < 2) st_ev(&tmp[idx[k]], ev);
+                else if (rank < kSlab)
+                    st_ev(&tmp[bk.slab_rm ? (size_t)rank * bk.H + p[k].dst_host
+                                          : (size_t)p[k].dst_host * kSlab + rank], ev);
+                else st_ev(&ovf[oslot], ev); // segments above kSlab
+                if (t >= barrier && t < mn) mn = t; // worker.c:350-363
+            }
+            if (live[k]) status[idx[k]] = st[k];
         }
     }
     mn = wave_min_u64(mn);
@@ -1252,10 +1328,18 @@ __global__ __launch_bounds__(256) void k_segsort_merge(ShdDeliv* out, ShdDeliv* 
 
 // Regroup path: rank of each event inside its destination (counter old value).
 __global__ __launch_bounds__(256) void k_hist_rank(const ShdDeliv* __restrict__ in, size_t n, uint32_t host_lo,
-                                                   uint32_t H, uint32_t* __restrict__ cnt, uint32_t* __restrict__ rank) {
+                                                   uint32_t H, uint32_t* __restrict__ cnt, uint32_t* __restrict__ rank,
+                                                   uint32_t agg_on) {
+    __shared__ uint32_t agg_s[3 * 256];
+    const int lane = threadIdx.x & 63;
+    const DestAgg agg{agg_s + 3 * (threadIdx.x & ~63u), agg_s + 3 * (threadIdx.x & ~63u) + 64,
+                      agg_s + 3 * (threadIdx.x & ~63u) + 128, agg_on};
+    agg.cnt[lane] = 0;
+    __syncthreads();
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t d = in[i].dst_host - host_lo; // out-of-range events are dropped
-        rank[i] = d < H ? atomicAdd(&cnt[d], 1u) : ~0u;
+        const uint32_t r = dest_slot(d < H, d, cnt, agg, lane);
+        rank[i] = d < H ? r : ~0u;
     }
 }
 
@@ -1306,7 +1390,13 @@ __global__ __launch_bounds__(256) void k_place_ovf(const ShdDeliv* __restrict__ 
 __global__ __launch_bounds__(256) void k_hist_slab(const ShdDeliv* __restrict__ in, size_t n, uint32_t host_lo,
                                                    uint32_t H, uint32_t* __restrict__ cnt, ShdDeliv* __restrict__ slab,
                                                    uint32_t slab_rm, ShdDeliv* __restrict__ ovf,
-                                                   uint32_t* __restrict__ novf) {
+                                                   uint32_t* __restrict__ novf, uint32_t agg_on) {
+    __shared__ uint32_t agg_s[3 * 256];
+    const int lane = threadIdx.x & 63;
+    const DestAgg agg{agg_s + 3 * (threadIdx.x & ~63u), agg_s + 3 * (threadIdx.x & ~63u) + 64,
+                      agg_s + 3 * (threadIdx.x & ~63u) + 128, agg_on};
+    agg.cnt[lane] = 0;
+    __syncthreads();
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += stride * kBatch) {
         ShdDeliv r[kBatch];
@@ -1316,15 +1406,18 @@ __global__ __launch_bounds__(256) void k_hist_slab(const ShdDeliv* __restrict__ 
             const size_t i = i0 + (size_t)k * stride;
             ok[k] = i < n;
             if (ok[k]) r[k] = ld_ev(&in[i]);
+            else r[k].dst_host = host_lo + H; // (out of range: takes no slot)
         }
 #pragma unroll
         for (int k = 0; k < kBatch; k++) {
             const uint32_t d = r[k].dst_host - host_lo;
-            if (!ok[k] || d >= H) continue;
-            const uint32_t rank = atomicAdd(&cnt[d], 1u);
+            const bool in = ok[k] && d < H;
+            const uint32_t rank = dest_slot(in, d, cnt, agg, lane);
+            const uint32_t oslot = wave_alloc(in && rank >= kSlab, novf, lane);
+            if (!in) continue;
             r[k].pad = rank;
             if (rank < kSlab) st_ev(&slab[slab_rm ? (size_t)rank * H + d : (size_t)d * kSlab + rank], r[k]);
-            else st_ev(&ovf[atomicAdd(novf, 1u)], r[k]);
+            else st_ev(&ovf[oslot], r[k]);
         }
     }
 }
@@ -1562,6 +1655,8 @@ int make_bucketing(uint32_t host_lo, uint32_t H, size_t n, Bucketing* out) {
     bk.xcd = !(x && strcmp(x, "0") == 0);
     const char* sl = getenv("SHD_SLAB_LAYOUT");
     bk.slab_rm = sl && strcmp(sl, "rank") == 0;
+    const char* ag = getenv("SHD_DEST_AGG");
+    bk.agg = !(ag && strcmp(ag, "0") == 0);
     bk.rsort = rank_sort();
     *out = bk;
     return 0;
@@ -1816,10 +1911,10 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
     if (n) {
         if (pipe == kSlabPipe)
             hipLaunchKernelGGL(k_hist_slab, dim3(grid_for(n, 256 * kBatch, 1u << 20)), dim3(256), 0, s, d_in, n,
-                               host_lo, H, w.cnt1, w.slab, bk.slab_rm, w.st2, w.nbig + 1);
+                               host_lo, H, w.cnt1, w.slab, bk.slab_rm, w.st2, w.nbig + 1, bk.agg);
         else if (rk)
             hipLaunchKernelGGL(k_hist_rank, dim3(grid_for(n, 256, 1u << 20)), dim3(256), 0, s, d_in, n, host_lo, H,
-                               w.cnt1, w.rnk);
+                               w.cnt1, w.rnk, bk.agg);
         else
             hipLaunchKernelGGL(k_hist_tiles, dim3(bk.ntiles), dim3(kBlock), 0, s, d_in, n, bk, w.cnt1, w.rnk);
     }
