@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02d_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02z_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
@@ -361,7 +361,8 @@ def main():
             "vertex_pairs_per_s": float(A4) * A4 / tr4, "build_s": tr4,
             "kernel": "k_sssp_slab (igraph-exact Dijkstra, 1 wave/source, persistent)",
             "roofline": routing_roofline(A4, tr4, 20.0 * 2 * t4.info()["edges"] + 4 * (args.c4_vertices + 1),
-                                         max(h4 - l4, 0), args.c4_vertices, tj.get("routing_slab_c4")),
+                                         max(h4 - l4, 0), args.c4_vertices,
+                                         tj.get("routing_slab_c4") if world == 1 else None),
         }
         # C4 packet delivery: 1,000 rounds on the 100k-vertex table.  N=1: the
         # whole table is resident (A4^2 x 16 B = 120 GB of the 288 GB).  N>1:
