@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""A/B of the wave-aggregated destination slots (SHD_DEST_AGG, read per
-launch) on the C3 round in ONE process (no allocation / box variance between
-the arms): alternating blocks of 20 rounds, live per-stage timing, outputs
-compared."""
+"""In-process A/B of a per-launch knob on the C3 round (no allocation / box
+variance between the arms): alternating blocks of 20 rounds, live per-stage
+timing, outputs compared.  Usage: agg_probe.py [ENV_NAME VALUE VALUE ...]
+(default: SHD_DEST_AGG 1 0)."""
 import ctypes as C
 import os
 import sys
@@ -33,9 +33,10 @@ def main():
     d_cnt = torch.empty(2, dtype=torch.int64, device=dev)
     lib = _lib.lib()
     outs = {}
+    name, vals = (sys.argv[1], sys.argv[2:]) if len(sys.argv) > 2 else ("SHD_DEST_AGG", ["1", "0"])
     for rep in range(3):
-        for agg in ("1", "0"):
-            os.environ["SHD_DEST_AGG"] = agg
+        for agg in vals:
+            os.environ[name] = agg
             for _ in range(2):
                 top.process_device(d_recs.data_ptr(), P, 110_000_000, 10**15, 0, d_out.data_ptr(),
                                    d_off.data_ptr(), d_status.data_ptr(), d_cnt.data_ptr(), 0)
@@ -51,9 +52,9 @@ def main():
             nl = C.c_int()
             _lib.check(lib.shd_round_timing_read(st, 4, C.byref(nl)))
             _lib.check(lib.shd_round_timing_enable(0))
-            print(f"agg={agg} rep {rep}: round {dt:.4f} ms, scatter {st[0] / max(nl.value, 1):.4f} ms", flush=True)
+            print(f"{name}={agg} rep {rep}: round {dt:.4f} ms, scatter {st[0] / max(nl.value, 1):.4f} ms", flush=True)
             outs[agg] = (d_out.clone(), d_off.clone(), d_status.clone())
-    same = all(torch.equal(a, b) for a, b in zip(outs["1"], outs["0"]))
+    same = all(all(torch.equal(a, b) for a, b in zip(outs[vals[0]], outs[v])) for v in vals[1:])
     print(f"outputs identical: {same}", flush=True)
 
 

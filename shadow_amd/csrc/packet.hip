@@ -43,7 +43,10 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kBatch = 4;          // records per thread in flight through the gather chain
-constexpr int kChunks = 1024;      // scatter workgroups per launch (columns of the count matrix)
+constexpr int kChunks = 1536;      // scatter workgroups per launch (columns of the count matrix);
+                                   // 1.5 per CU at 4 waves each = 24 of the 20..32 resident waves a
+                                   // CU holds at 88 VGPRs, tails of small chunks overlap better
+                                   // than 1024 (profiles/r02s_chunks.log: -1% round time)
 constexpr int kMaxBuckets = 4096;  // destination buckets (LDS histogram size)
 constexpr int kScanTile = 4096;    // 256 threads x 16
 constexpr int kSmallSeg = 256;     // wave register sort up to 4 events per lane
@@ -1632,7 +1635,8 @@ constexpr uint32_t kMaxShift = 11; // 2^11 = kMaxPerBucket destinations per buck
 
 // Buckets: the fewest (widest) that keep a uniform batch's expected events
 // per bucket within half the LDS capacity of k_bucket_sort; chunks: about
-// kChunks scatter workgroups, each a multiple of one batch of records.
+// kChunks scatter workgroups of whole kBlock-record rows (the last batch of a
+// chunk may be partial: the scatter masks it).
 int make_bucketing(uint32_t host_lo, uint32_t H, size_t n, Bucketing* out) {
     Bucketing bk;
     bk.host_lo = host_lo;
@@ -1644,8 +1648,14 @@ int make_bucketing(uint32_t host_lo, uint32_t H, size_t n, Bucketing* out) {
         bk.shift++;
     bk.nb = (uint32_t)(((size_t)H + (1u << bk.shift) - 1) >> bk.shift);
     if (bk.nb == 0) bk.nb = 1;
-    const size_t unit = (size_t)kBlock * kBatch;
-    size_t chunk = (n + kChunks - 1) / kChunks;
+    // SHD_SCATTER_CHUNKS=k (64..65536): measurement knob for the workgroup count
+    const size_t unit = kBlock;
+    size_t nchunks = kChunks;
+    if (const char* sc = getenv("SHD_SCATTER_CHUNKS")) {
+        const long v = atol(sc);
+        if (v >= 64 && v <= 65536) nchunks = (size_t)v;
+    }
+    size_t chunk = (n + nchunks - 1) / nchunks;
     chunk = (chunk + unit - 1) / unit * unit;
     if (chunk < unit) chunk = unit;
     bk.chunk = (uint32_t)chunk;
