@@ -275,8 +275,8 @@ def main():
         "dtype": "u64+f64",
         "data": "synthetic (seeded splitmix64 graph, hosts, packets; no datasets)",
         "config": {
-            "workload": "C3 per-round packet hand-off: 10M packets/round/GPU over 100k hosts on the C2 sparse "
-                        "graph (V=20k); dst-sharded with RCCL all-to-all at N>1",
+            "workload": f"C3 per-round packet hand-off: {P / 1e6:g}M packets/round/GPU over {H / 1e3:g}k hosts on "
+                        f"the C2 sparse graph (V={V / 1e3:g}k); dst-sharded with RCCL all-to-all at N>1",
             "packets_per_round_per_gpu": P, "hosts": H, "vertices": V, "attached_vertices": A,
             "delivered_per_round_rank0": delivered, "parallelism": f"dst-shard x{world}",
         },
