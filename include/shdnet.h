@@ -167,14 +167,37 @@ int shd_device_copy(int device, void* d_dst, const void* d_src, size_t bytes);
 int shd_topology_build_rows_device(ShdTopology* top, int row_lo, int row_hi, void* d_table);
 int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
 /* Adopts a device table WITHOUT a host mirror (tables larger than host RAM
- * wants: A = 86k slots is 120 GB) and releases every row in slot order (the
- * touch_all steady state).  Host lookups then read single entries from the
- * device.  use_shortest_path graphs only (-ENOTSUP), before any row was
- * released (-EBUSY).  Replaces nothing in the reference: topology.c keeps
- * its paths in host hash tables (topology.c:1217-1265). */
+ * wants: A = 86k slots is 120 GB).  Nothing is released at adoption: as in
+ * the reference, the first lookup or send that misses row i releases it
+ * (topology.c:1189-1265, 1900-1981) -- here a device pass over row i that
+ * finds what the reference's store loop would store (columns whose row was
+ * not touched before i) and feeds their minimum to the min-jump callback.
+ * Host lookups read single entries from the device.  use_shortest_path
+ * graphs only (-ENOTSUP), before any lookup (-EBUSY).  The caller keeps
+ * d_table alive for the topology's lifetime. */
 int shd_topology_adopt_table_device_resident(ShdTopology* top, void* d_table);
-/* Marks every attached vertex row touched, in slot order (steady state of a
- * long simulation; used by benchmarks before timing). */
+/* Single-process multi-GPU table (Shadow is one process with one manager,
+ * core/manager.c:543-577): shard k holds rows [row_bounds[k],
+ * row_bounds[k+1]) (nshards + 1 slot ids, host memory) in d_rows[k], a device
+ * allocation of (row_bounds[k+1] - row_bounds[k]) * A entries on
+ * devices[k] (e.g. built by shd_topology_build_rows_device on that device's
+ * topology copy, or shd_topology_build_shards).  One release state for the
+ * whole table: lookups from any worker thread read the owning shard's
+ * device, a row release reduces the row on its shard's device.  Destination
+ * hosts are split evenly over the shards for the rounds
+ * (shd_topology_set_host_bounds).  Same conditions as above. */
+int shd_topology_adopt_table_shards(ShdTopology* top, int nshards, const int* devices, void* const* d_rows,
+                                    const int* row_bounds);
+/* Builds every row of a single-process multi-GPU table: shard k's rows are
+ * computed on devices[k] into d_rows[k] (caller-owned, sized as above), all
+ * shards concurrently (one host thread per shard). */
+int shd_topology_build_shards(ShdTopology* top, int nshards, const int* devices, void* const* d_rows,
+                              const int* row_bounds);
+/* Destination hosts owned by each shard of a multi-shard table in its rounds
+ * (nshards + 1 host ids, [0, nhosts)); default: an even split. */
+int shd_topology_set_host_bounds(ShdTopology* top, const uint32_t* host_bounds);
+/* Touches every untouched attached vertex row, in slot order (steady state
+ * of a long simulation; used by benchmarks before timing). */
 int shd_topology_touch_all(ShdTopology* top);
 /* Release state, for tests and tooling: per table slot, the touch sequence
  * number of its row (UINT32_MAX = never touched) and whether its self pair
@@ -307,12 +330,15 @@ int shd_round_exchange(ShdTopology* top, const ShdTransport* xport, const ShdDel
 int shd_round_route_records(ShdTopology* top, const ShdTransport* xport, const ShdPkt* d_recs, size_t n,
                             const uint32_t* row_bounds, ShdPkt* d_scratch, ShdPkt* d_recv, size_t recv_cap,
                             size_t* n_recv, void* stream);
-/* Adopts rows [row_lo, row_hi) of the table (d_rows: (row_hi - row_lo) * A
- * entries) as this rank's device-resident shard and releases every row in
- * slot order (the touch_all steady state); lookups and rounds on this
- * topology may then only use pairs whose answering row is in the shard.
- * global_min_ms: the released minimum over the whole table (min over ranks
- * of shd_topology_shard_min_latency), or < 0 to use this shard's. */
+/* Multi-process jobs (one process per GPU): adopts rows [row_lo, row_hi) of
+ * the table (d_rows: (row_hi - row_lo) * A entries) as this rank's
+ * device-resident shard and releases every row in slot order (the
+ * touch_all steady state of a long simulation); lookups and rounds on this
+ * topology may then only use pairs whose answering row is in the shard
+ * (-EXDEV otherwise).  global_min_ms: the released minimum over the whole
+ * table (min over ranks of shd_topology_shard_min_latency), or < 0 to use
+ * this shard's.  The lazy release of a single process is
+ * shd_topology_adopt_table_shards. */
 int shd_topology_adopt_table_shard_device_resident(ShdTopology* top, void* d_rows, int row_lo, int row_hi,
                                                    double global_min_ms);
 /* Released minimum over this shard's rows (pairs i < j), -1 if none. */

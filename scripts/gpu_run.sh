@@ -1,0 +1,44 @@
+#!/bin/bash
+# GPU-box recipe (run through gpurun from the repo root):
+#   scripts/gpu_run.sh TAG STEP [STEP ...]
+# STEP: test[:EXPR]  pytest -m gpu (optionally -k EXPR), full output in gpurun_out/TAG/
+#       smoke        __graft_entry__.smoke()
+#       bench[:ARGS] bench.py (ARGS: extra arguments, commas for spaces)
+#       prof[:ARGS]  rocprofv3 --kernel-trace --stats of bench.py
+# Every GPU step runs under its own time limit and the first failure ends
+# the call (no further GPU work after a fault, abort or timeout).
+set -o pipefail
+T=$1
+shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+D=$R/gpurun_out/$T
+mkdir -p $D
+export TMPDIR=/tmp
+for step in "$@"; do
+    kind=${step%%:*}
+    arg=""
+    [[ $step == *:* ]] && arg=${step#*:}
+    case $kind in
+    test)
+        if [ -n "$arg" ]; then
+            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread -k "$arg" \
+                > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
+        else
+            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread \
+                > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
+        fi
+        tail -3 $D/pytest.log ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1 \
+            || { tail -20 $D/smoke.log; exit 1; }
+        tail -1 $D/smoke.log ;;
+    bench)
+        timeout -k 10 900 python -u $R/bench.py ${arg//,/ } > $D/bench.json 2> $D/bench.err || { tail -30 $D/bench.err; exit 1; }
+        cat $D/bench.json ;;
+    prof)
+        (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $D/prof -o prof -- \
+            python3 $R/bench.py ${arg//,/ } > $D/prof_bench.json 2> $D/prof_bench.err) || { tail -30 $D/prof_bench.err; exit 1; }
+        find $D/prof -name "*kernel_stats.csv" | head -1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done

@@ -57,6 +57,9 @@ PROTOS = {
     "shd_topology_build_rows_device": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "shd_topology_adopt_table_device": (C.c_int, [_P, _P]),
     "shd_topology_adopt_table_device_resident": (C.c_int, [_P, _P]),
+    "shd_topology_adopt_table_shards": (C.c_int, [_P, C.c_int, _P, _P, _P]),
+    "shd_topology_build_shards": (C.c_int, [_P, C.c_int, _P, _P, _P]),
+    "shd_topology_set_host_bounds": (C.c_int, [_P, _u32p]),
     "shd_topology_touch_all": (C.c_int, [_P]),
     "shd_topology_touch_order": (C.c_int, [_P, _P, _P, C.c_int]),
     "shd_topology_host_count": (C.c_int, [_P, _u32p]),

@@ -66,3 +66,16 @@ extern "C" int shd_dev_memset(void* d, int v, size_t bytes) {
 }
 
 extern "C" int shd_dev_sync(void) { return hip_err(hipDeviceSynchronize(), "hipDeviceSynchronize"); }
+
+extern "C" int shd_dev_stream_new(void** s) {
+    hipStream_t h = nullptr;
+    const int rc = hip_err(hipStreamCreate(&h), "hipStreamCreate");
+    *s = rc ? nullptr : (void*)h;
+    return rc;
+}
+
+extern "C" int shd_dev_stream_sync(void* s) { return hip_err(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize"); }
+
+extern "C" void shd_dev_stream_free(void* s) {
+    if (s) (void)hipStreamDestroy((hipStream_t)s);
+}

@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
             if (dl) {
                 const uint64_t t = tt[k];
                 if (!kRank) rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
-                const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k], rank};
+                const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k] + c.idx_base, rank};
                 if (kMode < 2) st_ev(&tmp[idx[k]], ev);
                 else if (rank < kSlab)
                     st_ev(&tmp[bk.slab_rm ? (size_t)rank * bk.H + p[k].dst_host
@@ -1147,7 +1147,10 @@ __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* uns
         }
         s_ns = acc < mm.cap ? acc : mm.cap; // (read back through LDS: see vm_sync)
         mm.hdr[0] = s_ns;
-        if (acc > mm.cap) mm.hdr[3] |= 0x80000000u; // (cannot happen: cap covers n / (kChunk + 1))
+        // this round's fault word: spin-limit hits of the merge (counted by
+        // k_segsort_merge) and the metadata overflow bit (cannot happen: cap
+        // covers n / (kChunk + 1)); read back by the host (ws_faults)
+        mm.hdr[3] = acc > mm.cap ? 0x80000000u : 0u;
         // segments taking part in pass p: those with more than p passes
         uint32_t part = 0;
         for (int p = (int)kMaxPasses - 1; p >= 0; p--) {
@@ -1485,6 +1488,7 @@ struct Ws {
     ShdDeliv* slab = nullptr;
     uint32_t* meta = nullptr; // big-segment merge metadata (MergeMeta)
     uint32_t cap_meta = 0;    // merge segments it holds
+    uint32_t* fault = nullptr; // pinned host copy of the last round's merge fault word (meta hdr[3])
 };
 
 int hip_status(hipError_t e, const char* what) {
@@ -1595,7 +1599,10 @@ int mid_attr() {
     return rc;
 }
 
-// listed segments: LDS runs, then the merge passes of the larger ones
+// listed segments: LDS runs, then the merge passes of the larger ones.  The
+// round's merge fault word (hdr[3]: tiles that gave up waiting for their
+// segment's previous pass, or a metadata overflow) is copied to pinned host
+// memory behind the merge; ws_faults reports it.
 int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDeliv* out, hipStream_t s) {
     if (int rc = mid_attr()) return rc;
     const MergeMeta mm = merge_meta(w);
@@ -1603,7 +1610,26 @@ int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDel
                        out, w.st1, mm);
     if (int rc = hip_status(hipGetLastError(), "k_segsort_mid launch")) return rc;
     hipLaunchKernelGGL(k_segsort_merge, dim3(512), dim3(256), 0, s, out, w.st1, mm);
-    return hip_status(hipGetLastError(), "k_segsort_merge launch");
+    if (int rc = hip_status(hipGetLastError(), "k_segsort_merge launch")) return rc;
+    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
+        w.fault = nullptr;
+        return shd_fail(-ENOMEM, "hipHostMalloc fault word");
+    }
+    return hip_status(hipMemcpyAsync(w.fault, mm.hdr + 3, 4, hipMemcpyDeviceToHost, s), "fault word D2H");
+}
+
+// The merge fault word of the workspace's last completed round (non-blocking:
+// a round still running is checked by a later call).  -EIO: a merge tile hit
+// its spin limit (its input may have been incomplete: the destination
+// segment may be mis-sorted) or the merge metadata overflowed.
+int ws_faults(Ws& w, bool completed) {
+    if (!w.used || !w.fault) return 0;
+    if (!completed && hipEventQuery(w.done) != hipSuccess) return 0;
+    const uint32_t f = __atomic_load_n(w.fault, __ATOMIC_ACQUIRE);
+    if (!f) return 0;
+    *w.fault = 0;
+    return shd_fail(-EIO, "segment merge fault word %#x in a previous round (%u spin-limit hits%s)", f,
+                    f & 0x7fffffffu, (f & 0x80000000u) ? ", metadata overflow" : "");
 }
 
 unsigned grid_for(size_t n, unsigned block, unsigned cap) {
@@ -1774,6 +1800,7 @@ int ws_begin(Ws& w, hipStream_t s) {
     if (rc) return rc;
     if (w.device >= 0 && w.device != dev) return shd_fail(-EINVAL, "workspace of device %d used on device %d", w.device, dev);
     w.device = dev;
+    if ((rc = ws_faults(w, false))) return rc;
     if (!w.done && (rc = hip_status(hipEventCreateWithFlags(&w.done, hipEventDisableTiming), "hipEventCreate ws")))
         return rc;
     if (w.used && w.last != s) return hip_status(hipStreamWaitEvent(s, w.done, 0), "hipStreamWaitEvent ws");
@@ -1809,6 +1836,7 @@ extern "C" void shd_dev_ws_free(void* p) {
     (void)hipFree(w->nbig);
     (void)hipFree(w->slab);
     (void)hipFree(w->meta);
+    if (w->fault) (void)hipHostFree(w->fault);
     if (w->done) (void)hipEventDestroy(w->done);
     delete w;
 }
@@ -1869,7 +1897,9 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
               : group_and_sort(w, w.tmp, d_status, nullptr, n, bk, d_out, d_dst_offsets, counters, s);
     if (!rc) rc = ws_end(w, s);
     if (rc) return rc;
-    return stream ? 0 : hip_status(hipStreamSynchronize(s), "packet round");
+    if (stream) return 0;
+    if ((rc = hip_status(hipStreamSynchronize(s), "packet round"))) return rc;
+    return ws_faults(w, true);
 }
 
 extern "C" int shd_round_timing_enable(int enable) {
@@ -1936,5 +1966,7 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
               : group_and_sort(w, d_in, nullptr, w.rnk, n, bk, d_out, d_dst_offsets, nullptr, s);
     if (!rc) rc = ws_end(w, s);
     if (rc) return rc;
-    return stream ? 0 : hip_status(hipStreamSynchronize(s), "deliv sort");
+    if (stream) return 0;
+    if ((rc = hip_status(hipStreamSynchronize(s), "deliv sort"))) return rc;
+    return ws_faults(w, true);
 }

@@ -81,14 +81,17 @@ int shd_round_append_worker(ShdTopology* t, int worker, const ShdPkt* recs, size
         b->recs = s;
         b->cap = nc;
     }
-    for (size_t i = 0; i < n; i++) {
+    ShdRelBatch rb = {0};
+    for (size_t i = 0; i < n && !rc; i++) {
         rec_slots(t, &recs[i], &si, &di);
         int oi, oj;
-        rc = shd_resolve(t, si, di, &oi, &oj); /* topology_getReliability's lookup, at send time */
-        if (rc) return rc;                     /* (unreachable on a validated graph) */
-        b->recs[b->n++] = recs[i];
+        rc = shd_resolve_b(t, si, di, &oi, &oj, &rb); /* topology_getReliability's lookup, at send time */
+        if (!rc) b->recs[b->n++] = recs[i];
     }
-    return 0;
+    /* device-resident rows this batch touched, released in touch order */
+    const int rcf = shd_release_flush(t, &rb);
+    shd_relbatch_free(&rb);
+    return rc ? rc : rcf;
 }
 
 int shd_round_append(ShdTopology* t, const ShdPkt* recs, size_t n) { return shd_round_append_worker(t, 0, recs, n); }
@@ -118,6 +121,24 @@ static int gather_staged(ShdTopology* t, size_t* n_out) {
     }
     *n_out = n;
     return 0;
+}
+
+/* topology_incrementPathPacketCounter for every kept packet of the staged
+ * batch (worker.c:551), delivered or discarded at the end time alike; the
+ * lookups were made at append, so this only resolves owners and counts.
+ * Only an allocation failure of the counter map stops it halfway; the
+ * caller has already consumed the batch, so a retry cannot count twice. */
+static int count_kept(ShdTopology* t, size_t n, const uint8_t* status) {
+    int rc = 0;
+    pthread_mutex_lock(&t->pkt_mu);
+    for (size_t i = 0; i < n && !rc; i++)
+        if (status[i] != SHD_DROPPED_LOSS) {
+            int si, di, oi, oj;
+            rec_slots(t, &t->staged[i], &si, &di);
+            if (!(rc = shd_resolve(t, si, di, &oi, &oj))) rc = shd_count_packet_locked(t, oi, oj, 1);
+        }
+    pthread_mutex_unlock(&t->pkt_mu);
+    return rc;
 }
 
 static int collect_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_out, uint32_t* dst_offsets,
@@ -159,19 +180,10 @@ static int collect_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_o
         goto done;
     }
     if ((rc = shd_dev_d2h(h_status, d_status, n))) goto done;
-    /* topology_incrementPathPacketCounter for every kept packet (worker.c:551),
-     * delivered or discarded at the end time alike; the lookups were already
-     * made at append, so this only resolves owners and counts */
-    pthread_mutex_lock(&t->pkt_mu);
-    for (size_t i = 0; i < n && !rc; i++)
-        if (h_status[i] != SHD_DROPPED_LOSS) {
-            int si, di, oi, oj;
-            rec_slots(t, &t->staged[i], &si, &di);
-            if (!(rc = shd_resolve(t, si, di, &oi, &oj))) rc = shd_count_packet_locked(t, oi, oj, 1);
-        }
-    pthread_mutex_unlock(&t->pkt_mu);
-    if (!rc)
-        for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0;
+    /* the round is decided: its records leave the staging buffers whatever
+     * happens below (a retried collect must not count them twice) */
+    for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0;
+    rc = count_kept(t, n, h_status);
 done:
     if (h_status != status) free(h_status);
     shd_dev_free(d_recs);
@@ -182,11 +194,203 @@ done:
     return rc;
 }
 
+/* ---- single-process multi-GPU round (a multi-shard table) ----
+ * The batch is split by the shard holding each record's answering row (the
+ * owner row of the touch order, resolved here on the host from the same
+ * state the kernel reads); every shard decides its records on its own device
+ * and stream, concurrently; the decided events of each shard are cut by
+ * destination owner (shard m owns hosts [host_bounds[m], host_bounds[m+1]))
+ * and copied device to device (xGMI between GPUs) to the owner, which
+ * regroups them into event_compare order (shd_dev_deliv_sort).  The union is
+ * the single-GPU round: event_compare is a total order. */
+
+#define GROW(ptr, cap_field, need, elem)                                                      \
+    do {                                                                                      \
+        if ((need) > (cap_field)) {                                                           \
+            shd_dev_free(ptr);                                                                \
+            (ptr) = NULL;                                                                     \
+            if ((rc = shd_dev_malloc((void**)&(ptr), (elem) * ((need) + (need) / 4 + 64)))) goto done; \
+        }                                                                                     \
+    } while (0)
+
+/* Uploads the release state to shard s's device if it changed (caller holds round_mu). */
+static int sync_shard_touch(ShdTopology* t, ShdShard* s) {
+    const uint64_t gen = __atomic_load_n(&t->touch_gen, __ATOMIC_ACQUIRE);
+    if (s->d_touch && s->synced_gen == gen && gen) return 0;
+    int rc = 0;
+    if (!s->d_touch && (rc = shd_dev_malloc((void**)&s->d_touch, sizeof(uint32_t) * (size_t)t->A))) return rc;
+    if (!s->d_host_info && (rc = shd_dev_malloc((void**)&s->d_host_info, sizeof(uint32_t) * 2 * ((size_t)t->nhosts + 1))))
+        return rc;
+    uint32_t* snap = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)t->A);
+    uint32_t* hs = (uint32_t*)malloc(sizeof(uint32_t) * 2 * ((size_t)t->nhosts + 1));
+    if (!snap || !hs) rc = -ENOMEM;
+    for (int i = 0; !rc && i < t->A; i++) snap[i] = __atomic_load_n(&t->touch[i], __ATOMIC_ACQUIRE);
+    for (uint32_t h = 0; !rc && h < t->nhosts; h++) {
+        hs[2 * h] = t->h_host_info[2 * h];
+        hs[2 * h + 1] = hs[2 * h] != SHD_UNTOUCHED ? snap[hs[2 * h]] : SHD_UNTOUCHED;
+    }
+    if (!rc) rc = shd_dev_h2d(s->d_touch, snap, sizeof(uint32_t) * (size_t)t->A);
+    if (!rc) rc = shd_dev_h2d(s->d_host_info, hs, sizeof(uint32_t) * 2 * (size_t)t->nhosts);
+    free(snap);
+    free(hs);
+    if (!rc) s->synced_gen = gen;
+    return rc;
+}
+
+static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_out, uint32_t* dst_offsets,
+                                 uint8_t* status, uint64_t* min_time) {
+    const int S = t->nshards;
+    const uint32_t H = t->nhosts;
+    size_t n = 0;
+    int rc = gather_staged(t, &n);
+    if (rc) return rc;
+    if (cap < n && out) return shd_fail(-ENOSPC, "output capacity %zu < %zu records", cap, n);
+    const size_t nn = n ? n : 1;
+    uint32_t* perm = (uint32_t*)malloc(sizeof(uint32_t) * nn);    /* partition position -> record */
+    uint16_t* owner = (uint16_t*)malloc(sizeof(uint16_t) * nn);   /* record -> shard */
+    ShdPkt* part = (ShdPkt*)malloc(sizeof(ShdPkt) * nn);
+    uint8_t* pst = (uint8_t*)malloc(nn);
+    uint32_t* offk = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)H + 1) * (size_t)S);
+    size_t pbeg[SHD_MAX_SHARDS + 1] = {0};
+    uint64_t cnt[SHD_MAX_SHARDS][2];
+    if (!perm || !owner || !part || !pst || !offk) {
+        rc = -ENOMEM;
+        goto done;
+    }
+    /* owner shard of every record: its answering row (use_shortest_path:
+     * touch order, as k_pkt_scatter resolves it); unattached -> shard 0,
+     * which reports them undelivered */
+    for (size_t i = 0; i < n; i++) {
+        const ShdPkt* p = &t->staged[i];
+        int si, di, k = 0;
+        if (!rec_slots(t, p, &si, &di)) {
+            int oi = si;
+            if (si != di && __atomic_load_n(&t->touch[di], __ATOMIC_ACQUIRE) <
+                                __atomic_load_n(&t->touch[si], __ATOMIC_ACQUIRE))
+                oi = di;
+            ShdShard* s = shd_shard_of(t, oi);
+            k = s ? (int)(s - t->shards) : 0;
+        }
+        owner[i] = (uint16_t)k;
+        pbeg[k + 1]++;
+    }
+    for (int k = 0; k < S; k++) pbeg[k + 1] += pbeg[k];
+    {
+        size_t fill[SHD_MAX_SHARDS];
+        for (int k = 0; k < S; k++) fill[k] = pbeg[k];
+        for (size_t i = 0; i < n; i++) {
+            const size_t q = fill[owner[i]]++;
+            perm[q] = (uint32_t)i;
+            part[q] = t->staged[i];
+        }
+    }
+    /* decide: every shard on its device and stream, concurrently */
+    for (int k = 0; k < S && !rc; k++) {
+        ShdShard* s = &t->shards[k];
+        const size_t nk = pbeg[k + 1] - pbeg[k];
+        if ((rc = shd_dev_init(s->device))) break;
+        if (!s->stream && (rc = shd_dev_stream_new(&s->stream))) break;
+        if (!s->ws && (rc = shd_dev_ws_new(&s->ws))) break;
+        if ((rc = sync_shard_touch(t, s))) break;
+        GROW(s->d_recs, s->cap_n, nk, sizeof(ShdPkt));
+        GROW(s->d_out, s->cap_n, nk, sizeof(ShdDeliv));
+        GROW(s->d_status, s->cap_n, nk, 1);
+        if (nk > s->cap_n) s->cap_n = nk + nk / 4 + 64;
+        GROW(s->d_off, s->cap_h, (size_t)H + 1, sizeof(uint32_t));
+        GROW(s->d_fin_off, s->cap_h, (size_t)H + 1, sizeof(uint32_t));
+        if (!s->d_cnt && (rc = shd_dev_malloc((void**)&s->d_cnt, 16))) break;
+        if ((size_t)H + 1 > s->cap_h) s->cap_h = H + 1 + (H + 1) / 4 + 64;
+        if (nk && (rc = shd_dev_h2d(s->d_recs, part + pbeg[k], sizeof(ShdPkt) * nk))) break;
+        ShdPktCtx c;
+        c.tab = s->base;
+        c.A = t->A;
+        c.mode = 0;
+        c.touch = s->d_touch;
+        c.pair_bits = NULL;
+        c.host_info = s->d_host_info;
+        c.nhosts = H;
+        c.ws = s->ws;
+        c.row_lo = s->lo;
+        c.row_hi = s->hi;
+        c.idx_base = (uint32_t)pbeg[k];
+        rc = shd_dev_packet_round(&c, s->d_recs, nk, t->barrier, t->end_time, t->bootstrap_end, s->d_out, s->d_off,
+                                  s->d_status, s->d_cnt, s->stream);
+    }
+    for (int k = 0; k < S && !rc; k++) {
+        ShdShard* s = &t->shards[k];
+        const size_t nk = pbeg[k + 1] - pbeg[k];
+        if (!(rc = shd_dev_init(s->device)) && !(rc = shd_dev_stream_sync(s->stream)) &&
+            !(rc = shd_dev_d2h(cnt[k], s->d_cnt, 16)) &&
+            !(rc = shd_dev_d2h(offk + ((size_t)H + 1) * (size_t)k, s->d_off, sizeof(uint32_t) * ((size_t)H + 1))))
+            rc = shd_dev_d2h(pst + pbeg[k], s->d_status, nk);
+    }
+    /* destination-owner exchange (device to device) and regroup */
+    size_t obase = 0;
+    for (int m = 0; m < S && !rc; m++) {
+        ShdShard* sm = &t->shards[m];
+        const uint32_t lo = t->host_bounds[m], hi = t->host_bounds[m + 1];
+        size_t tot = 0;
+        for (int k = 0; k < S; k++) {
+            const uint32_t* o = offk + ((size_t)H + 1) * (size_t)k;
+            tot += o[hi] - o[lo];
+        }
+        if ((rc = shd_dev_init(sm->device))) break;
+        GROW(sm->d_recv, sm->cap_r, tot, sizeof(ShdDeliv));
+        GROW(sm->d_fin, sm->cap_r, tot, sizeof(ShdDeliv));
+        if (tot > sm->cap_r) sm->cap_r = tot + tot / 4 + 64;
+        size_t at = 0;
+        for (int k = 0; k < S && !rc; k++) {
+            const uint32_t* o = offk + ((size_t)H + 1) * (size_t)k;
+            const size_t b = o[hi] - o[lo];
+            if (b) rc = shd_dev_d2d(sm->d_recv + at, t->shards[k].d_out + o[lo], sizeof(ShdDeliv) * b);
+            at += b;
+        }
+        if (!rc) rc = shd_dev_init(sm->device);
+        if (!rc) rc = shd_dev_deliv_sort(sm->ws, sm->d_recv, tot, lo, hi, sm->d_fin, sm->d_fin_off, sm->stream);
+        if (!rc) rc = shd_dev_stream_sync(sm->stream);
+        if (!rc && out && tot) rc = shd_dev_d2h(out + obase, sm->d_fin, sizeof(ShdDeliv) * tot);
+        if (!rc && dst_offsets) {
+            if ((rc = shd_dev_d2h(dst_offsets + lo, sm->d_fin_off, sizeof(uint32_t) * ((size_t)(hi - lo) + 1))))
+                break;
+            for (uint32_t h = lo; h <= hi; h++) dst_offsets[h] += (uint32_t)obase;
+        }
+        obase += tot;
+    }
+    if (rc) goto done;
+    uint64_t mt = UINT64_MAX;
+    for (int k = 0; k < S; k++)
+        if (pbeg[k + 1] > pbeg[k] && cnt[k][1] < mt) mt = cnt[k][1];
+    if (n_out) *n_out = obase;
+    if (min_time) *min_time = mt;
+    if (out)
+        for (size_t i = 0; i < obase; i++) out[i].pkt_index = perm[out[i].pkt_index];
+    {
+        uint8_t* st = status ? status : (uint8_t*)malloc(nn);
+        if (!st) {
+            rc = -ENOMEM;
+            goto done;
+        }
+        for (size_t q = 0; q < n; q++) st[perm[q]] = pst[q]; /* partition order -> record order */
+        for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0; /* decided (see collect_locked) */
+        rc = count_kept(t, n, st);
+        if (st != status) free(st);
+    }
+done:
+    free(perm);
+    free(owner);
+    free(part);
+    free(pst);
+    free(offk);
+    shd_dev_init(t->device);
+    return rc;
+}
+
 int shd_round_collect(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_out, uint32_t* dst_offsets,
                       uint8_t* status, uint64_t* min_time) {
     if (!t) return -EINVAL;
     pthread_mutex_lock(&t->round_mu);
-    int rc = collect_locked(t, out, cap, n_out, dst_offsets, status, min_time);
+    int rc = t->nshards > 1 ? collect_shards_locked(t, out, cap, n_out, dst_offsets, status, min_time)
+                            : collect_locked(t, out, cap, n_out, dst_offsets, status, min_time);
     pthread_mutex_unlock(&t->round_mu);
     return rc;
 }
@@ -198,6 +402,7 @@ int shd_round_process_device(ShdTopology* t, const ShdPkt* d_recs, size_t n, uin
     int rc = shd_ensure_routes(t);
     if (rc) return rc;
     if (!__atomic_load_n(&t->lookups_started, __ATOMIC_RELAXED)) __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
+    if (t->nshards > 1) return shd_fail(-ENOTSUP, "a multi-shard table runs its rounds with shd_round_process_shards");
     pthread_mutex_lock(&t->round_mu);
     if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t))) {
         ShdPktCtx c;

@@ -10,12 +10,14 @@
  * for the CPU-side lookups of the drop-in API.
  */
 #include <errno.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "topology_impl.h"
 
 void shd_topology_release_device(ShdTopology* t) {
+    shd_shards_clear(t);
     if (t->d_tab && t->d_tab_owned) shd_dev_free(t->d_tab);
     shd_dev_free(t->d_inc_off);
     shd_dev_free(t->d_inc_nbr);
@@ -181,6 +183,7 @@ static ShdGraphDev graph_dev(const ShdTopology* t) {
 
 static int adopt(ShdTopology* t, ShdEntry* d_tab, int owned) {
     size_t n = (size_t)t->A * (size_t)t->A;
+    shd_shards_clear(t); /* (a device-resident table adopted before) */
     free(t->h_tab);
     t->h_tab = (ShdEntry*)malloc(sizeof(ShdEntry) * n);
     if (!t->h_tab) return -ENOMEM;
@@ -245,6 +248,81 @@ int shd_topology_build_rows_device(ShdTopology* t, int row_lo, int row_hi, void*
     return rc;
 }
 
+/* ---- single-process multi-GPU build (shd_topology_build_shards) ---- */
+
+/* The device graph arrays of prepare(), with their sizes (bytes). */
+static void graph_arrays(ShdTopology* t, const void* src[9], size_t bytes[9]) {
+    const size_t M = (size_t)t->M, V = (size_t)t->V, SM = M + V + 64 * 16;
+    const void* s[9] = {t->d_inc_off, t->d_inc_nbr, t->d_inc_w, t->d_inc_r, t->d_slot_vertex,
+                        t->d_vertex_slot, t->d_snb, t->d_swr, t->d_soff};
+    const size_t b[9] = {4 * (V + 1), 4 * M, 8 * M, 8 * M, 4 * (size_t)t->A, 4 * V, 8 * SM, 16 * SM, 4 * V};
+    for (int k = 0; k < 9; k++) src[k] = s[k], bytes[k] = b[k];
+}
+
+typedef struct {
+    ShdTopology* t;
+    int device, lo, hi;
+    ShdEntry* base;
+    int rc;
+    char err[256];
+} ShardJob;
+
+static void* build_shard(void* arg) {
+    ShardJob* j = (ShardJob*)arg;
+    ShdTopology* t = j->t;
+    const void* src[9];
+    size_t bytes[9];
+    void* dst[9] = {0};
+    graph_arrays(t, src, bytes);
+    int rc = shd_dev_init(j->device);
+    ShdGraphDev g = graph_dev(t);
+    if (!rc && j->device != t->device) { /* the graph on this shard's device (peer copies) */
+        for (int k = 0; k < 9 && !rc; k++)
+            if (!(rc = shd_dev_malloc(&dst[k], bytes[k]))) rc = shd_dev_d2d(dst[k], src[k], bytes[k]);
+        g.inc_off = (const int32_t*)dst[0];
+        g.inc_nbr = (const int32_t*)dst[1];
+        g.inc_w = (const double*)dst[2];
+        g.inc_r = (const double*)dst[3];
+        g.slot_vertex = (const int32_t*)dst[4];
+        g.vertex_slot = (const int32_t*)dst[5];
+        g.snb = dst[6];
+        g.swr = dst[7];
+        g.soff = (const int32_t*)dst[8];
+    }
+    if (!rc) rc = shd_dev_build_rows(&g, t->use_sp, j->lo, j->hi, j->base);
+    for (int k = 0; k < 9; k++) shd_dev_free(dst[k]);
+    j->rc = rc;
+    if (rc) snprintf(j->err, sizeof j->err, "%s", shd_last_error());
+    return NULL;
+}
+
+int shd_topology_build_shards(ShdTopology* t, int n, const int* devices, void* const* d_rows, const int* row_bounds) {
+    if (!t || n < 1 || n > SHD_MAX_SHARDS || !devices || !d_rows || !row_bounds)
+        return shd_fail(-EINVAL, "bad shard arguments");
+    pthread_mutex_lock(&t->setup_mu);
+    int rc = prepare(t);
+    if (!rc && (row_bounds[0] != 0 || row_bounds[n] != t->A)) rc = shd_fail(-EINVAL, "row bounds must cover [0, %d)", t->A);
+    for (int k = 0; k < n && !rc; k++)
+        if (row_bounds[k + 1] < row_bounds[k]) rc = shd_fail(-EINVAL, "row bounds not ascending");
+    ShardJob jobs[SHD_MAX_SHARDS];
+    pthread_t th[SHD_MAX_SHARDS];
+    int started[SHD_MAX_SHARDS] = {0};
+    for (int k = 0; k < n && !rc; k++) {
+        jobs[k] = (ShardJob){t, devices[k], row_bounds[k], row_bounds[k + 1],
+                             (ShdEntry*)d_rows[k] - (ptrdiff_t)row_bounds[k] * (ptrdiff_t)t->A, 0, {0}};
+        if (row_bounds[k + 1] > row_bounds[k]) started[k] = pthread_create(&th[k], NULL, build_shard, &jobs[k]) == 0;
+        if (row_bounds[k + 1] > row_bounds[k] && !started[k]) rc = shd_fail(-EAGAIN, "cannot start a build thread");
+    }
+    for (int k = 0; k < n; k++)
+        if (started[k]) {
+            pthread_join(th[k], NULL);
+            if (!rc && jobs[k].rc) rc = shd_fail(jobs[k].rc, "shard %d: %s", k, jobs[k].err);
+        }
+    pthread_mutex_unlock(&t->setup_mu);
+    shd_dev_init(t->device);
+    return rc;
+}
+
 int shd_topology_adopt_table_device(ShdTopology* t, void* d_table) {
     if (!t || !d_table) return -EINVAL;
     pthread_mutex_lock(&t->setup_mu);
@@ -297,6 +375,7 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->nhosts = t->nhosts;
     c->row_lo = t->tab_row_lo;
     c->row_hi = t->tab_row_hi;
+    c->idx_base = 0;
     if (!t->ws) shd_dev_ws_new(&t->ws); /* (a failure leaves ws NULL: the launch reports -ENOMEM) */
     c->ws = t->ws;
 }

@@ -88,6 +88,10 @@ int shd_dev_h2d(void* d, const void* h, size_t bytes);
 int shd_dev_d2h(void* h, const void* d, size_t bytes);
 int shd_dev_memset(void* d, int v, size_t bytes);
 int shd_dev_sync(void);
+/* a stream on the calling thread's device (hipStream_t behind void*) */
+int shd_dev_stream_new(void** s);
+int shd_dev_stream_sync(void* s);
+void shd_dev_stream_free(void* s);
 
 /* Routing rows [row_lo, row_hi) of the A x A table (tab already sized A*A
  * on device; rows outside the range are not written).
@@ -97,6 +101,15 @@ int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi,
 /* min latency over the entries (i, j), i < j, lat >= 0, of rows [row_lo,
  * row_hi) of an A-column table (rows: row i at rows + (i - row_lo) * A); -1 if none */
 int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out);
+/* Lazy row release (release.hip): for each listed row rows[r] (absolute slot,
+ * row r at base + rows[r] * A) with touch sequence seqs[r], the minimum
+ * latency over columns j != rows[r] with touch[j] > seqs[r] and lat >= 0;
+ * out[r] = -1 if none.  rows / seqs / touch / out are host arrays; runs on the
+ * calling thread's device, synchronously.  *scratch: grow-only device buffers
+ * of the caller (NULL the first time), freed with shd_dev_release_scratch_free. */
+int shd_dev_release_min(const ShdEntry* base, int A, const int32_t* rows, const uint32_t* seqs, int n,
+                        const uint32_t* touch, double* out, void** scratch);
+void shd_dev_release_scratch_free(void* scratch);
 
 /* Packet round on device arrays (see shd_round_process_device). */
 typedef struct {
@@ -109,6 +122,7 @@ typedef struct {
     uint32_t nhosts;
     void* ws;                  /* the topology's device workspace (shd_dev_ws_new) */
     int row_lo, row_hi;        /* rows of tab present (a shard: others are never read) */
+    uint32_t idx_base;         /* added to the record index an event carries (pkt_index) */
 } ShdPktCtx;
 
 /* Round-pipeline workspace (grow-only device buffers + the event that marks
@@ -121,7 +135,8 @@ int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uin
 int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                        uint32_t* d_dst_offsets, void* stream);
 
-/* out[i] = tab[idx[i]] for n entries (device pointers; synchronous) */
+/* out[i] = tab[idx[i]] for n entries (device pointers; synchronous; on the
+ * calling thread's device) */
 int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n, ShdEntry* d_out);
 
 /* multi-GPU rounds (xchg.hip) */

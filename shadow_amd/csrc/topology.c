@@ -790,24 +790,156 @@ static void note_released(ShdTopology* t, double lat) {
     pthread_mutex_unlock(&t->min_mu);
 }
 
-/* Entry k of the table: from the host mirror, or one 16-byte read of the
- * device table when it is device-resident (no mirror). */
-static ShdEntry ent(const ShdTopology* t, size_t k) {
-    if (t->h_tab) return t->h_tab[k];
-    ShdEntry e = {-1.0, 0.0};
-    const size_t row = k / (size_t)t->A;
-    if (row < (size_t)t->tab_row_lo || row >= (size_t)t->tab_row_hi) return e; /* another rank's row */
-    if (shd_dev_init(t->device) || shd_dev_d2h(&e, t->d_tab + k, sizeof e)) e.lat = -1.0;
-    return e;
+ShdShard* shd_shard_of(ShdTopology* t, int row) {
+    for (int k = 0; k < t->nshards; k++)
+        if (row >= t->shards[k].lo && row < t->shards[k].hi) return &t->shards[k];
+    return NULL;
+}
+
+/* Entry k of the table: from the host mirror, or one 16-byte read from the
+ * device of the shard that holds its row (device-resident tables).  -EXDEV
+ * for a row no shard of this process holds (a multi-process rank's table). */
+static int ent_read(ShdTopology* t, size_t k, ShdEntry* e) {
+    if (t->h_tab) {
+        *e = t->h_tab[k];
+        return 0;
+    }
+    const int row = (int)(k / (size_t)t->A);
+    ShdShard* s = shd_shard_of(t, row);
+    if (!s) return shd_fail(-EXDEV, "row %d of the table lives on another rank", row);
+    int rc = shd_dev_init(s->device);
+    if (!rc) rc = shd_dev_d2h(e, s->base + k, sizeof *e);
+    return rc;
+}
+
+int shd_read_entries(ShdTopology* t, const uint64_t* idx, size_t n, ShdEntry* out) {
+    if (!n) return 0;
+    if (t->h_tab) {
+        for (size_t i = 0; i < n; i++) out[i] = t->h_tab[idx[i]];
+        return 0;
+    }
+    /* device-resident: one gather per shard instead of n 16-byte PCIe reads */
+    size_t* pos = (size_t*)malloc(sizeof(size_t) * n);
+    uint64_t* sub = (uint64_t*)malloc(sizeof(uint64_t) * n);
+    ShdEntry* e = (ShdEntry*)malloc(sizeof(ShdEntry) * n);
+    int rc = (pos && sub && e) ? 0 : -ENOMEM;
+    size_t covered = 0;
+    for (int k = 0; k < t->nshards && !rc; k++) {
+        ShdShard* s = &t->shards[k];
+        size_t m = 0;
+        for (size_t i = 0; i < n; i++) {
+            const int row = (int)(idx[i] / (uint64_t)t->A);
+            if (row >= s->lo && row < s->hi) pos[m] = i, sub[m++] = idx[i];
+        }
+        if (!m) continue;
+        uint64_t* d_idx = NULL;
+        ShdEntry* d_e = NULL;
+        if (!(rc = shd_dev_init(s->device)) && !(rc = shd_dev_malloc((void**)&d_idx, 8 * m)) &&
+            !(rc = shd_dev_malloc((void**)&d_e, sizeof(ShdEntry) * m)) && !(rc = shd_dev_h2d(d_idx, sub, 8 * m)) &&
+            !(rc = shd_dev_gather_entries(s->base, d_idx, m, d_e)))
+            rc = shd_dev_d2h(e, d_e, sizeof(ShdEntry) * m);
+        shd_dev_free(d_idx);
+        shd_dev_free(d_e);
+        if (!rc)
+            for (size_t x = 0; x < m; x++) out[pos[x]] = e[x];
+        covered += m;
+    }
+    if (!rc && covered != n) rc = shd_fail(-EXDEV, "%zu entries live on another rank's rows", n - covered);
+    free(pos);
+    free(sub);
+    free(e);
+    return rc;
+}
+
+/* ---- row releases ---- */
+
+static int relbatch_push(ShdRelBatch* b, int row, uint32_t seq) {
+    if (b->n == b->cap) {
+        int nc = b->cap ? 2 * b->cap : 64;
+        int32_t* r = (int32_t*)realloc(b->rows, sizeof(int32_t) * (size_t)nc);
+        if (r) b->rows = r;
+        uint32_t* s = r ? (uint32_t*)realloc(b->seqs, sizeof(uint32_t) * (size_t)nc) : NULL;
+        if (s) b->seqs = s;
+        if (!r || !s) return -ENOMEM;
+        b->cap = nc;
+    }
+    b->rows[b->n] = row;
+    b->seqs[b->n++] = seq;
+    return 0;
+}
+
+void shd_relbatch_free(ShdRelBatch* b) {
+    free(b->rows);
+    free(b->seqs);
+    b->rows = NULL;
+    b->seqs = NULL;
+    b->n = b->cap = 0;
+}
+
+/* Releases the rows of b (device-resident table), in their order: one
+ * reduction per shard over the rows it holds (release.hip), with a snapshot
+ * of the touch sequences taken after every row of b drew its number -- a row
+ * touched before row i has a smaller number and was published before i's was
+ * drawn, every other row compares greater than i's either way, so the
+ * snapshot selects exactly the columns the serial store loop would.  Self
+ * entries (rows encoded -1 - slot, sequence unused) carry their value. */
+int shd_release_flush(ShdTopology* t, ShdRelBatch* b) {
+    if (!b || !b->n) return 0;
+    const int A = t->A, n = b->n;
+    uint32_t* snap = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)A);
+    double* mn = (double*)malloc(sizeof(double) * (size_t)n);
+    int32_t* rk = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    uint32_t* sk = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+    int* pos = (int*)malloc(sizeof(int) * (size_t)n);
+    double* ok = (double*)malloc(sizeof(double) * (size_t)n);
+    int rc = (snap && mn && rk && sk && pos && ok) ? 0 : -ENOMEM;
+    if (!rc)
+        for (int j = 0; j < A; j++) snap[j] = touch_of(t, j);
+    int covered = 0;
+    for (int r = 0; r < n && !rc; r++)
+        if (b->rows[r] < 0) { /* a self pair: its one entry */
+            ShdEntry e;
+            const size_t s = (size_t)(-1 - b->rows[r]);
+            rc = ent_read(t, s * (size_t)A + s, &e);
+            mn[r] = e.lat;
+            covered++;
+        }
+    for (int k = 0; k < t->nshards && !rc; k++) {
+        ShdShard* s = &t->shards[k];
+        int m = 0;
+        for (int r = 0; r < n; r++)
+            if (b->rows[r] >= s->lo && b->rows[r] < s->hi) rk[m] = b->rows[r], sk[m] = b->seqs[r], pos[m++] = r;
+        if (!m) continue;
+        pthread_mutex_lock(&s->mu);
+        if (!(rc = shd_dev_init(s->device)))
+            rc = shd_dev_release_min(s->base, A, rk, sk, m, snap, ok, &s->rel_scratch);
+        pthread_mutex_unlock(&s->mu);
+        if (!rc)
+            for (int x = 0; x < m; x++) mn[pos[x]] = ok[x];
+        covered += m;
+    }
+    if (!rc && covered != n) rc = shd_fail(-EXDEV, "a touched row lives on another rank");
+    if (!rc)
+        for (int r = 0; r < n; r++)
+            if (mn[r] >= 0) note_released(t, mn[r]);
+    b->n = 0;
+    free(snap);
+    free(mn);
+    free(rk);
+    free(sk);
+    free(pos);
+    free(ok);
+    return rc;
 }
 
 /* Releases row i (a touch).  The row's sequence number is drawn and
  * published under touch_mu; the entries it releases are then every (i, y)
  * whose y is untouched or was touched later (sequence > i's) -- exactly the
  * pairs the serial execution in sequence order stores from row i, whatever
- * the interleaving with other touches.  Device-resident tables release every
- * row at adoption, so they never get here. */
-static void touch_row(ShdTopology* t, int i) {
+ * the interleaving with other touches.  A host-mirrored row is reduced right
+ * here; a device-resident one by shd_release_flush, now (b == NULL) or at the
+ * end of the caller's batch. */
+static int touch_row(ShdTopology* t, int i, ShdRelBatch* b) {
     pthread_mutex_lock(&t->touch_mu);
     uint32_t seq = t->touch[i];
     const int mine = seq == SHD_UNTOUCHED;
@@ -815,9 +947,18 @@ static void touch_row(ShdTopology* t, int i) {
         seq = t->next_touch++;
         __atomic_store_n(&t->touch[i], seq, __ATOMIC_RELEASE);
         __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
+        __atomic_add_fetch(&t->touch_gen, 1, __ATOMIC_RELEASE);
     }
     pthread_mutex_unlock(&t->touch_mu);
-    if (!mine || !t->h_tab) return;
+    if (!mine) return 0;
+    if (!t->h_tab) {
+        if (b) return relbatch_push(b, i, seq);
+        ShdRelBatch one = {0};
+        int rc = relbatch_push(&one, i, seq);
+        if (!rc) rc = shd_release_flush(t, &one);
+        shd_relbatch_free(&one);
+        return rc;
+    }
     const ShdEntry* row = t->h_tab + (size_t)i * (size_t)t->A;
     double mn = 0;
     int any = 0;
@@ -827,6 +968,17 @@ static void touch_row(ShdTopology* t, int i) {
             any = 1;
         }
     if (any) note_released(t, mn);
+    return 0;
+}
+
+/* First (X, X) lookup: releases the self path (topology.c:1597-1599). */
+static int release_self(ShdTopology* t, int si, ShdRelBatch* b) {
+    if (__atomic_exchange_n(&t->self_released[si], 1, __ATOMIC_ACQ_REL)) return 0;
+    if (b && !t->h_tab) return relbatch_push(b, -1 - si, 0); /* after the rows the batch touched before it */
+    ShdEntry e;
+    int rc = ent_read(t, (size_t)si * (size_t)t->A + (size_t)si, &e);
+    if (!rc && e.lat >= 0) note_released(t, e.lat);
+    return rc;
 }
 
 static int pair_bit(const ShdTopology* t, int i, int j) {
@@ -838,22 +990,25 @@ static void set_pair_bit(ShdTopology* t, int i, int j) {
     size_t b = (size_t)i * (size_t)t->A + (size_t)j;
     __atomic_fetch_or(&t->pair_bits[b >> 5], 1u << (b & 31), __ATOMIC_ACQ_REL);
     __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
+    __atomic_add_fetch(&t->touch_gen, 1, __ATOMIC_RELEASE);
 }
 
 /* _topology_getPathEntry (topology.c:1900-1981) for slots (si, di): applies
  * the side effects and returns the slot pair whose entry answers.  Lock-free
  * on a hit; safe to call from any number of threads. */
-int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) {
+int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) { return shd_resolve_b(t, si, di, oi, oj, NULL); }
+
+int shd_resolve_b(ShdTopology* t, int si, int di, int* oi, int* oj, ShdRelBatch* b) {
     size_t A = (size_t)t->A;
+    int rc = 0;
     if (t->use_sp) {
         if (si == di) {
-            if (!__atomic_exchange_n(&t->self_released[si], 1, __ATOMIC_ACQ_REL))
-                note_released(t, ent(t, (size_t)si * A + (size_t)si).lat);
+            if ((rc = release_self(t, si, b))) return rc;
             *oi = *oj = si;
         } else {
             uint32_t ts = touch_of(t, si), td = touch_of(t, di);
             int hit = t->directed ? (ts != SHD_UNTOUCHED && ts < td) : (ts != SHD_UNTOUCHED || td != SHD_UNTOUCHED);
-            if (!hit && ts == SHD_UNTOUCHED) touch_row(t, si);
+            if (!hit && ts == SHD_UNTOUCHED && (rc = touch_row(t, si, b))) return rc;
             /* re-read both: a concurrent touch of di with a smaller sequence
              * was published before ours (touch_mu), so it is visible here */
             ts = touch_of(t, si);
@@ -866,13 +1021,17 @@ int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) {
         if (!hit && !pair_bit(t, di, si)) {
             pthread_mutex_lock(&t->pair_mu); /* the reference's writer lock (topology.c:1217-1265) */
             if (!pair_bit(t, si, di) && !pair_bit(t, di, si)) {
-                const double lat = ent(t, (size_t)si * A + (size_t)di).lat;
-                if (lat < 0) {
+                ShdEntry e;
+                if ((rc = ent_read(t, (size_t)si * A + (size_t)di, &e))) {
+                    pthread_mutex_unlock(&t->pair_mu);
+                    return rc;
+                }
+                if (e.lat < 0) {
                     pthread_mutex_unlock(&t->pair_mu);
                     return shd_fail(-EHOSTUNREACH, "no direct edge");
                 }
                 set_pair_bit(t, si, di);
-                note_released(t, lat);
+                note_released(t, e.lat);
             }
             pthread_mutex_unlock(&t->pair_mu);
         }
@@ -905,8 +1064,7 @@ static int entry_of(ShdTopology* t, uint32_t sip, uint32_t dip, ShdEntry* e, int
     if (rc) return rc;
     rc = shd_resolve(t, si, di, oi, oj);
     if (rc) return rc;
-    *e = ent(t, (size_t)*oi * (size_t)t->A + (size_t)*oj);
-    return 0;
+    return ent_read(t, (size_t)*oi * (size_t)t->A + (size_t)*oj, e);
 }
 
 int shd_topology_get_latency(ShdTopology* t, uint32_t s, uint32_t d, double* out) {
@@ -949,27 +1107,19 @@ int shd_topology_lookup_batch(ShdTopology* t, const uint32_t* sips, const uint32
     if (!idx) return -ENOMEM;
     int rc = 0;
     size_t done = 0;
+    ShdRelBatch b = {0};
     for (; done < n; done++) { /* the side effects, in call order */
         int si, di, oi, oj;
-        if ((rc = slots_of(t, sips[done], dips[done], &si, &di)) || (rc = shd_resolve(t, si, di, &oi, &oj))) break;
+        if ((rc = slots_of(t, sips[done], dips[done], &si, &di)) || (rc = shd_resolve_b(t, si, di, &oi, &oj, &b)))
+            break;
         idx[done] = (uint64_t)oi * (uint64_t)t->A + (uint64_t)oj;
     }
+    int rcf = shd_release_flush(t, &b); /* the rows this batch touched, in touch order */
+    shd_relbatch_free(&b);
+    if (!rc) rc = rcf;
     if (done && (lat || rel)) {
         ShdEntry* e = (ShdEntry*)malloc(sizeof(ShdEntry) * done);
-        int rc2 = e ? 0 : -ENOMEM;
-        if (!rc2 && t->h_tab) {
-            for (size_t i = 0; i < done; i++) e[i] = t->h_tab[idx[i]];
-        } else if (!rc2) { /* device-resident: one gather instead of `done` PCIe reads */
-            uint64_t* d_idx = NULL;
-            ShdEntry* d_e = NULL;
-            if (!(rc2 = shd_dev_init(t->device)) && !(rc2 = shd_dev_malloc((void**)&d_idx, 8 * done)) &&
-                !(rc2 = shd_dev_malloc((void**)&d_e, sizeof(ShdEntry) * done)) &&
-                !(rc2 = shd_dev_h2d(d_idx, idx, 8 * done)) &&
-                !(rc2 = shd_dev_gather_entries(t->d_tab, d_idx, done, d_e)))
-                rc2 = shd_dev_d2h(e, d_e, sizeof(ShdEntry) * done);
-            shd_dev_free(d_idx);
-            shd_dev_free(d_e);
-        }
+        int rc2 = e ? shd_read_entries(t, idx, done, e) : -ENOMEM;
         if (!rc2)
             for (size_t i = 0; i < done; i++) {
                 if (lat) lat[i] = e[i].lat;
@@ -982,11 +1132,13 @@ int shd_topology_lookup_batch(ShdTopology* t, const uint32_t* sips, const uint32
     return rc;
 }
 
-/* per stored pair packet counters (path.c:58-61); caller holds pkt_mu */
-int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc) {
-    uint64_t key = ((uint64_t)(uint32_t)oi << 32) | (uint32_t)oj;
-    if ((t->pkt_n + 1) * 2 > t->pkt_cap) {
+/* Grows the packet counter map so that `more` new keys fit without a
+ * rehash; caller holds pkt_mu. */
+int shd_count_reserve_locked(ShdTopology* t, uint64_t more) {
+    if ((t->pkt_n + more) * 2 <= t->pkt_cap) return 0;
+    {
         uint64_t ncap = t->pkt_cap ? t->pkt_cap * 2 : 4096;
+        while ((t->pkt_n + more) * 2 > ncap) ncap *= 2;
         uint64_t* nk = (uint64_t*)malloc(sizeof(uint64_t) * ncap);
         uint64_t* nv = (uint64_t*)calloc(ncap, sizeof(uint64_t));
         if (!nk || !nv) {
@@ -1008,6 +1160,14 @@ int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc) {
         t->pkt_vals = nv;
         t->pkt_cap = ncap;
     }
+    return 0;
+}
+
+/* per stored pair packet counters (path.c:58-61); caller holds pkt_mu */
+int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc) {
+    uint64_t key = ((uint64_t)(uint32_t)oi << 32) | (uint32_t)oj;
+    int rc = shd_count_reserve_locked(t, 1);
+    if (rc) return rc;
     uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20 & (t->pkt_cap - 1);
     while (t->pkt_keys[h] != UINT64_MAX && t->pkt_keys[h] != key) h = (h + 1) & (t->pkt_cap - 1);
     if (t->pkt_keys[h] == UINT64_MAX) {
@@ -1133,12 +1293,13 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
         if (!any) continue;
         const ShdEntry* r = t->h_tab ? t->h_tab + (size_t)i * (size_t)A : row;
         if (!t->h_tab) {
-            if (i < t->tab_row_lo || i >= t->tab_row_hi) {
-                rc = shd_fail(-ENOTSUP, "row %d lives on another rank", i);
+            ShdShard* s = shd_shard_of(t, i);
+            if (!s) {
+                rc = shd_fail(-EXDEV, "row %d lives on another rank", i);
                 break;
             }
-            if ((rc = shd_dev_init(t->device)) || (rc = shd_dev_d2h(row, t->d_tab + (size_t)i * (size_t)A,
-                                                                   sizeof(ShdEntry) * (size_t)A)))
+            if ((rc = shd_dev_init(s->device)) ||
+                (rc = shd_dev_d2h(row, s->base + (size_t)i * (size_t)A, sizeof(ShdEntry) * (size_t)A)))
                 break;
         }
         for (int j = 0; j < A; j++) {
@@ -1159,48 +1320,152 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
     return rc;
 }
 
-/* Device-resident table (no host mirror; C4's A = 86k table is 120 GB):
- * adopts d_table and releases every row in slot order, as touch_all does.
- * The released minimum is one device reduction over the pairs (i < j) that
- * the row-by-row release would store; the min-jump callback fires once with
- * the final value instead of once per decreasing row. */
+/* ------------------------------------------------------------------ */
+/* device-resident tables: shards, lazy release                         */
+/* ------------------------------------------------------------------ */
+
+void shd_shards_clear(ShdTopology* t) {
+    for (int k = 0; k < t->nshards; k++) {
+        ShdShard* s = &t->shards[k];
+        shd_dev_init(s->device);
+        shd_dev_release_scratch_free(s->rel_scratch);
+        shd_dev_free(s->d_host_info);
+        shd_dev_free(s->d_touch);
+        shd_dev_free(s->d_pair_bits);
+        shd_dev_ws_free(s->ws);
+        shd_dev_free(s->d_recs);
+        shd_dev_free(s->d_out);
+        shd_dev_free(s->d_recv);
+        shd_dev_free(s->d_fin);
+        shd_dev_free(s->d_status);
+        shd_dev_free(s->d_off);
+        shd_dev_free(s->d_fin_off);
+        shd_dev_free(s->d_cnt);
+        shd_dev_stream_free(s->stream);
+        pthread_mutex_destroy(&s->mu);
+        memset(s, 0, sizeof *s);
+    }
+    t->nshards = 0;
+    free(t->host_bounds);
+    t->host_bounds = NULL;
+}
+
+/* Installs the device-resident shards (caller holds setup_mu and checked the
+ * arguments).  The table on the topology's own device keeps its single-GPU
+ * fields (d_tab, tab_row_lo/hi) for the packet path of one shard. */
+static int set_shards(ShdTopology* t, int n, const int* devices, ShdEntry* const* bases, const int* bounds) {
+    shd_shards_clear(t);
+    free(t->h_tab);
+    t->h_tab = NULL;
+    if (t->d_tab && t->d_tab_owned) shd_dev_free(t->d_tab);
+    t->d_tab = NULL;
+    t->d_tab_owned = 0;
+    t->tab_row_lo = t->tab_row_hi = 0;
+    for (int k = 0; k < n; k++) {
+        ShdShard* s = &t->shards[k];
+        memset(s, 0, sizeof *s);
+        s->device = devices[k];
+        s->base = bases[k];
+        s->lo = bounds[k];
+        s->hi = bounds[k + 1];
+        pthread_mutex_init(&s->mu, NULL);
+    }
+    t->nshards = n;
+    if (n == 1) {
+        t->d_tab = bases[0];
+        t->tab_row_lo = bounds[0];
+        t->tab_row_hi = bounds[1];
+    }
+    t->built = 1;
+    return 0;
+}
+
+static int adopt_checks(ShdTopology* t, int* A) {
+    int rc = shd_topology_slot_count(t, A); /* prepares the device graph */
+    if (!rc && !t->use_sp) rc = shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
+    if (!rc && (t->next_touch || __atomic_load_n(&t->lookups_started, __ATOMIC_ACQUIRE)))
+        rc = shd_fail(-EBUSY, "lookups were already made on this topology");
+    return rc;
+}
+
+/* Device-resident table (no host mirror; C4's A = 86k table is 120 GB).
+ * Nothing is released at adoption: rows are released lazily, by the first
+ * lookup or send that touches them, as in the reference (topology.c:
+ * 1189-1265, 1900-1981); shd_topology_touch_all reaches the all-touched
+ * steady state. */
 int shd_topology_adopt_table_device_resident(ShdTopology* t, void* d_table) {
     int A = 0;
     if (!t || !d_table) return -EINVAL;
     pthread_mutex_lock(&t->setup_mu);
-    int rc = shd_topology_slot_count(t, &A); /* prepares the device graph */
-    if (!rc && !t->use_sp) rc = shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
-    if (!rc && t->next_touch) rc = shd_fail(-EBUSY, "rows were already released");
-    double mn = -1.0;
-    if (!rc) rc = shd_dev_min_upper((const ShdEntry*)d_table, A, 0, A, &mn);
+    int rc = adopt_checks(t, &A);
     if (!rc) {
-        free(t->h_tab);
-        t->h_tab = NULL;
-        if (t->d_tab && t->d_tab_owned && t->d_tab != (ShdEntry*)d_table) shd_dev_free(t->d_tab);
-        t->d_tab = (ShdEntry*)d_table;
-        t->d_tab_owned = 0;
-        t->tab_row_lo = 0;
-        t->tab_row_hi = A;
-        t->built = 1;
-        pthread_mutex_lock(&t->touch_mu);
-        for (int i = 0; i < A; i++) __atomic_store_n(&t->touch[i], t->next_touch++, __ATOMIC_RELEASE);
-        __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
-        pthread_mutex_unlock(&t->touch_mu);
-        __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE);
-        if (mn >= 0) note_released(t, mn);
+        ShdEntry* base = (ShdEntry*)d_table;
+        const int bounds[2] = {0, A};
+        rc = set_shards(t, 1, &t->device, &base, bounds);
     }
+    if (!rc) __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE);
     pthread_mutex_unlock(&t->setup_mu);
     return rc;
 }
 
+/* Single-process multi-GPU table (Shadow runs one process, core/manager.c:
+ * 543-577): shard k = rows [row_bounds[k], row_bounds[k+1]) in d_rows[k]
+ * on devices[k].  One release state for all of them. */
+int shd_topology_adopt_table_shards(ShdTopology* t, int n, const int* devices, void* const* d_rows,
+                                    const int* row_bounds) {
+    int A = 0;
+    if (!t || n < 1 || n > SHD_MAX_SHARDS || !devices || !d_rows || !row_bounds)
+        return shd_fail(-EINVAL, "bad shard arguments");
+    pthread_mutex_lock(&t->setup_mu);
+    int rc = adopt_checks(t, &A);
+    if (!rc && (row_bounds[0] != 0 || row_bounds[n] != A)) rc = shd_fail(-EINVAL, "row bounds must cover [0, %d)", A);
+    ShdEntry* bases[SHD_MAX_SHARDS];
+    for (int k = 0; k < n && !rc; k++) {
+        if (row_bounds[k + 1] < row_bounds[k]) rc = shd_fail(-EINVAL, "row bounds not ascending");
+        else if (row_bounds[k + 1] > row_bounds[k] && !d_rows[k]) rc = shd_fail(-EINVAL, "shard %d has no rows", k);
+        else if ((rc = shd_dev_init(devices[k]))) break;
+        /* shard k's first row is row_bounds[k]: keep the base of row 0 */
+        bases[k] = (ShdEntry*)d_rows[k] - (ptrdiff_t)row_bounds[k] * (ptrdiff_t)A;
+    }
+    if (!rc) rc = set_shards(t, n, devices, bases, row_bounds);
+    if (!rc) {
+        t->host_bounds = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)n + 1));
+        if (!t->host_bounds) rc = -ENOMEM;
+        else
+            for (int k = 0; k <= n; k++) t->host_bounds[k] = (uint32_t)((uint64_t)k * t->nhosts / (uint64_t)n);
+    }
+    if (!rc) __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&t->setup_mu);
+    shd_dev_init(t->device);
+    return rc;
+}
+
+int shd_topology_set_host_bounds(ShdTopology* t, const uint32_t* bounds) {
+    if (!t || !bounds) return -EINVAL;
+    if (t->nshards < 2 || !t->host_bounds) return shd_fail(-EINVAL, "not a multi-shard table");
+    if (bounds[0] != 0 || bounds[t->nshards] != t->nhosts) return shd_fail(-EINVAL, "host bounds must cover [0, %u)", t->nhosts);
+    for (int k = 0; k < t->nshards; k++)
+        if (bounds[k + 1] < bounds[k]) return shd_fail(-EINVAL, "host bounds not ascending");
+    pthread_mutex_lock(&t->round_mu);
+    memcpy(t->host_bounds, bounds, sizeof(uint32_t) * ((size_t)t->nshards + 1));
+    pthread_mutex_unlock(&t->round_mu);
+    return 0;
+}
+
+/* Every attached row touched, untouched ones in slot order (the steady state
+ * of a long simulation; benchmarks use it before timing). */
 int shd_topology_touch_all(ShdTopology* t) {
     if (!t) return -EINVAL;
     int rc = shd_ensure_routes(t);
     if (rc) return rc;
     __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
     if (t->use_sp) {
-        for (int i = 0; i < t->A; i++)
-            if (touch_of(t, i) == SHD_UNTOUCHED) touch_row(t, i);
+        ShdRelBatch b = {0};
+        for (int i = 0; i < t->A && !rc; i++)
+            if (touch_of(t, i) == SHD_UNTOUCHED) rc = touch_row(t, i, &b);
+        int rcf = shd_release_flush(t, &b);
+        shd_relbatch_free(&b);
+        if (!rc) rc = rcf;
     } else {
         for (int i = 0; i < t->A; i++)
             for (int j = 0; j < t->A; j++) {
@@ -1208,7 +1473,7 @@ int shd_topology_touch_all(ShdTopology* t) {
                 shd_resolve(t, i, j, &oi, &oj);
             }
     }
-    return 0;
+    return rc;
 }
 
 int shd_topology_touch_order(ShdTopology* t, uint32_t* seq, uint8_t* self, int cap) {
@@ -1222,10 +1487,9 @@ int shd_topology_touch_order(ShdTopology* t, uint32_t* seq, uint8_t* self, int c
     return 0;
 }
 
-/* Row shard of a device-resident table (C4 at N > 1): d_rows holds rows
- * [row_lo, row_hi); every row counts as released in slot order (as
- * adopt_table_device_resident), the min-jump feed gets the whole table's
- * minimum from the caller (a min over ranks of shd_topology_shard_min_latency). */
+/* Row shard of a device-resident table held by one rank of a multi-process
+ * job (C4 at N > 1).  Released minimum of the shard's pairs i < j (the
+ * all-touched-in-slot-order state). */
 int shd_topology_shard_min_latency(ShdTopology* t, const void* d_rows, int row_lo, int row_hi, double* min_ms) {
     int A = 0;
     if (!t || !d_rows || !min_ms) return -EINVAL;
@@ -1236,32 +1500,32 @@ int shd_topology_shard_min_latency(ShdTopology* t, const void* d_rows, int row_l
     return shd_dev_min_upper((const ShdEntry*)d_rows, A, row_lo, row_hi, min_ms);
 }
 
+/* The multi-process steady state: this rank holds rows [row_lo, row_hi) and
+ * every row counts as released in slot order; the min-jump feed gets the
+ * whole table's minimum from the caller (a min over ranks of
+ * shd_topology_shard_min_latency). */
 int shd_topology_adopt_table_shard_device_resident(ShdTopology* t, void* d_rows, int row_lo, int row_hi,
                                                    double global_min_ms) {
     int A = 0;
     if (!t || !d_rows) return -EINVAL;
     pthread_mutex_lock(&t->setup_mu);
-    int rc = shd_topology_slot_count(t, &A);
+    int rc = adopt_checks(t, &A);
     if (!rc && (row_lo < 0 || row_hi > A || row_lo > row_hi)) rc = shd_fail(-EINVAL, "row range out of bounds");
-    if (!rc && !t->use_sp) rc = shd_fail(-ENOTSUP, "a device-resident table needs use_shortest_path (touch order)");
-    if (!rc && t->next_touch) rc = shd_fail(-EBUSY, "rows were already released");
     double mn = global_min_ms;
     if (!rc && mn < 0) rc = shd_dev_min_upper((const ShdEntry*)d_rows, A, row_lo, row_hi, &mn);
     if (!rc) {
-        free(t->h_tab);
-        t->h_tab = NULL;
-        if (t->d_tab && t->d_tab_owned) shd_dev_free(t->d_tab);
-        /* row i lives at d_rows + (i - row_lo) * A: keep the base of row 0 */
-        t->d_tab = (ShdEntry*)d_rows - (ptrdiff_t)row_lo * (ptrdiff_t)A;
-        t->d_tab_owned = 0;
-        t->tab_row_lo = row_lo;
-        t->tab_row_hi = row_hi;
-        t->built = 1;
+        ShdEntry* base = (ShdEntry*)d_rows - (ptrdiff_t)row_lo * (ptrdiff_t)A;
+        const int bounds[2] = {row_lo, row_hi};
+        rc = set_shards(t, 1, &t->device, &base, bounds);
+    }
+    if (!rc) {
         pthread_mutex_lock(&t->touch_mu);
         for (int i = 0; i < A; i++) __atomic_store_n(&t->touch[i], t->next_touch++, __ATOMIC_RELEASE);
         __atomic_store_n(&t->touch_dirty, 1, __ATOMIC_RELEASE);
+        __atomic_add_fetch(&t->touch_gen, 1, __ATOMIC_RELEASE);
         pthread_mutex_unlock(&t->touch_mu);
         __atomic_store_n(&t->ready, 1, __ATOMIC_RELEASE);
+        __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
         if (mn >= 0) note_released(t, mn);
     }
     pthread_mutex_unlock(&t->setup_mu);

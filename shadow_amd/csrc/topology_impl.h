@@ -44,6 +44,44 @@ typedef struct {
     uint32_t cap, n, tomb;
 } IpMap;
 
+/* A device-resident piece of the routing table (no host mirror): rows [lo,
+ * hi) on `device`, row r at base + r * A.  One shard for a single-GPU table,
+ * several for a single-process multi-GPU table (shd_topology_adopt_table_shards);
+ * a multi-process rank holds one shard and no other rows.  mu serialises the
+ * shard's release scratch and its round buffers. */
+#define SHD_MAX_SHARDS 64
+typedef struct {
+    int device;
+    ShdEntry* base;
+    int lo, hi;
+    void* rel_scratch; /* shd_dev_release_min buffers */
+    pthread_mutex_t mu;
+    /* per-shard packet-round state (multi-shard topologies, round.c) */
+    uint32_t *d_host_info, *d_touch, *d_pair_bits;
+    uint64_t synced_gen;
+    void* ws;
+    void* stream;
+    ShdPkt* d_recs;
+    ShdDeliv *d_out, *d_recv, *d_fin;
+    uint8_t* d_status;
+    uint32_t *d_off, *d_fin_off;
+    uint64_t* d_cnt;
+    size_t cap_n, cap_r;
+    uint32_t cap_h;
+} ShdShard;
+
+/* Rows a thread touched in one batch call (append / lookup batch), released
+ * together after the batch: one device pass instead of one per row.  The
+ * reference's min-jump side effect only matters at the next round boundary
+ * (controller.c:141-153, 390-422), so releasing at the end of the call is
+ * indistinguishable to Shadow; the rows are released in their sequence
+ * order, so the callback sees the serial sequence of minima. */
+typedef struct {
+    int32_t* rows;
+    uint32_t* seqs;
+    int n, cap;
+} ShdRelBatch;
+
 struct ShdTopology {
     int device;
     int use_sp;
@@ -92,6 +130,12 @@ struct ShdTopology {
     uint8_t* self_released;
     uint32_t* pair_bits; /* use_shortest_path = 0: (i,j) stored, A*A bits */
     int touch_dirty;
+    uint64_t touch_gen; /* bumped by every touch (multi-shard uploads) */
+
+    /* device-resident table (h_tab == NULL): its shards */
+    int nshards;
+    ShdShard shards[SHD_MAX_SHARDS];
+    uint32_t* host_bounds; /* nshards + 1: destination hosts owned per shard (multi-shard rounds) */
     double min_lat;
     ShdMinJumpFn cb;
     void* cb_user;
@@ -116,9 +160,19 @@ struct ShdTopology {
 };
 
 void shd_topology_release_device(ShdTopology* t);
+void shd_shards_clear(ShdTopology* t);
 int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj);
+/* shd_resolve with the row releases deferred into b (flush with shd_release_flush) */
+int shd_resolve_b(ShdTopology* t, int si, int di, int* oi, int* oj, ShdRelBatch* b);
+int shd_release_flush(ShdTopology* t, ShdRelBatch* b);
+void shd_relbatch_free(ShdRelBatch* b);
+/* the shard holding row `row` of a device-resident table (NULL: another rank's) */
+ShdShard* shd_shard_of(ShdTopology* t, int row);
+/* n table entries by flat index (host mirror or the owning shards' devices) */
+int shd_read_entries(ShdTopology* t, const uint64_t* idx, size_t n, ShdEntry* out);
 int shd_count_packet(ShdTopology* t, int oi, int oj, uint64_t inc);
 int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc);
+int shd_count_reserve_locked(ShdTopology* t, uint64_t more);
 int shd_sync_touch(ShdTopology* t);
 void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c);
 int shd_ensure_routes(ShdTopology* t);

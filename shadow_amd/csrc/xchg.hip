@@ -149,7 +149,17 @@ int exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* s
         sb[r] = send_elems[r] * elem_bytes;
         rb[r] = recv_elems[r] * elem_bytes;
     }
-    if (total > recv_cap) return shd_fail(-ENOSPC, "receive %llu elements > capacity %zu", (unsigned long long)total, recv_cap);
+    // The capacity verdict is collective: a rank that returned here alone
+    // would leave its peers waiting in the payload exchange.  Every rank
+    // sends its overflow flag to every peer, and all of them fail together.
+    const uint64_t over = total > recv_cap ? 1 : 0;
+    std::vector<uint64_t> flags(W, over), peer(W);
+    rc = x->alltoall_u64(x->user, flags.data(), peer.data());
+    if (rc) return rc < 0 ? rc : -EIO;
+    uint64_t any = 0;
+    for (int r = 0; r < W; r++) any |= peer[r];
+    if (over) return shd_fail(-ENOSPC, "receive %llu elements > capacity %zu", (unsigned long long)total, recv_cap);
+    if (any) return shd_fail(-ENOSPC, "a peer's receive capacity is too small for this exchange");
     rc = x->alltoallv(x->user, d_send, sb.data(), d_recv, rb.data(), (void*)s);
     if (rc) return rc < 0 ? rc : -EIO;
     *n_recv = (size_t)total;

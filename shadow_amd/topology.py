@@ -124,8 +124,28 @@ class Topology:
         check(lib().shd_topology_adopt_table_device(self._h, C.c_void_p(d_table_ptr)))
 
     def adopt_table_device_resident(self, d_table_ptr: int):
-        """Adopt without a host mirror; every row released in slot order."""
+        """Adopt without a host mirror; rows are released lazily by the
+        lookups and sends that first touch them (touch_all: steady state)."""
         check(lib().shd_topology_adopt_table_device_resident(self._h, C.c_void_p(d_table_ptr)))
+
+    @staticmethod
+    def _shard_args(devices, d_rows, row_bounds):
+        n = len(devices)
+        assert len(d_rows) == n and len(row_bounds) == n + 1
+        return (n, (C.c_int * n)(*[int(x) for x in devices]), (C.c_void_p * n)(*[int(x) for x in d_rows]),
+                (C.c_int * (n + 1))(*[int(x) for x in row_bounds]))
+
+    def build_shards(self, devices, d_rows, row_bounds):
+        """Rows [row_bounds[k], row_bounds[k+1]) into d_rows[k] on devices[k], shards concurrently."""
+        check(lib().shd_topology_build_shards(self._h, *self._shard_args(devices, d_rows, row_bounds)))
+
+    def adopt_table_shards(self, devices, d_rows, row_bounds):
+        """Single-process multi-GPU table: one release state over the shards."""
+        check(lib().shd_topology_adopt_table_shards(self._h, *self._shard_args(devices, d_rows, row_bounds)))
+
+    def set_host_bounds(self, host_bounds):
+        hb = (C.c_uint32 * len(host_bounds))(*[int(x) for x in host_bounds])
+        check(lib().shd_topology_set_host_bounds(self._h, hb))
 
     def touch_all(self):
         check(lib().shd_topology_touch_all(self._h))

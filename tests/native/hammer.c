@@ -12,7 +12,10 @@
  *   - every appended record is staged, in its worker's append order.
  * Built twice by tests/test_threads_cpu.py: plain and -fsanitize=thread,
  * against the product host C and tests/native/stub_dev.c.
- * Usage: hammer GML_PATH USE_SP NHOSTS THREADS OPS
+ * Usage: hammer GML_PATH USE_SP NHOSTS THREADS OPS [SHARDS]
+ *   SHARDS 0 (default): host-mirrored table; 1: device-resident table
+ *   (lazy release through shd_release_flush); 2: a two-shard table
+ *   (shd_topology_build_shards + adopt_table_shards, both on device 0).
  */
 #include <arpa/inet.h>
 #include <pthread.h>
@@ -35,11 +38,16 @@ static int g_nhosts, g_ops, g_use_sp;
 static uint32_t* g_ip;
 static Op** g_log;
 
+static void* g_extra;
 static double g_cb_last = 0;
 static int g_cb_calls = 0, g_cb_bad = 0;
+static uint64_t g_cb_hash = 1469598103934665603ull; /* FNV-1a over the reported values, in call order */
 static void on_min_jump(double ms, void* user) {
     (void)user;
     /* called under the topology's min lock: plain accesses are ordered */
+    uint64_t b;
+    memcpy(&b, &ms, 8);
+    for (int k = 0; k < 8; k++) g_cb_hash = (g_cb_hash ^ ((b >> (8 * k)) & 0xff)) * 1099511628211ull;
     if (g_cb_calls && !(ms < g_cb_last)) g_cb_bad++;
     g_cb_last = ms;
     g_cb_calls++;
@@ -105,6 +113,27 @@ int main(int argc, char** argv) {
     int A = 0, V = 0;
     shd_topology_info(g_top, &V, NULL, NULL, NULL, NULL);
     shd_topology_slot_count(g_top, &A);
+    const int shards = argc > 6 ? atoi(argv[6]) : 0;
+    void* d_tab = NULL;
+    if (shards == 1) {
+        if (shd_device_alloc_table(0, (size_t)A * A * 16, &d_tab, NULL) ||
+            shd_topology_build_rows_device(g_top, 0, A, d_tab) || shd_topology_adopt_table_device_resident(g_top, d_tab)) {
+            fprintf(stderr, "device-resident: %s\n", shd_last_error());
+            return 3;
+        }
+    } else if (shards == 2) {
+        const int bounds[3] = {0, A / 3, A}, devs[2] = {0, 0};
+        void* rows[2] = {NULL, NULL};
+        if (shd_device_alloc_table(0, (size_t)(A / 3 + 1) * A * 16, &rows[0], NULL) ||
+            shd_device_alloc_table(0, (size_t)(A - A / 3) * A * 16, &rows[1], NULL) ||
+            shd_topology_build_shards(g_top, 2, devs, rows, bounds) ||
+            shd_topology_adopt_table_shards(g_top, 2, devs, rows, bounds)) {
+            fprintf(stderr, "shards: %s\n", shd_last_error());
+            return 3;
+        }
+        d_tab = rows[0];
+        g_extra = rows[1];
+    }
     int* slot_of_v = malloc(sizeof(int) * (size_t)V);
     for (int v = 0; v < V; v++) slot_of_v[v] = -1;
     for (int h = 0; h < g_nhosts; h++) slot_of_v[host_vertex[h]] = 1;
@@ -184,8 +213,10 @@ int main(int argc, char** argv) {
     shd_round_staged(g_top, &staged);
     int bads = staged != appended;
     if (bads) fprintf(stderr, "staged %zu appended %zu\n", staged, appended);
-    printf("threads %d ops %d slots %d touched %d min %.17g cb_calls %d staged %zu bad %d %d %d %d\n", T, g_ops, A,
-           touched, got, g_cb_calls, staged, bad, badc, badm, bads);
+    printf("threads %d ops %d slots %d touched %d min %.17g cb_calls %d cb_hash %016llx staged %zu bad %d %d %d %d\n",
+           T, g_ops, A, touched, got, g_cb_calls, (unsigned long long)g_cb_hash, staged, bad, badc, badm, bads);
     shd_topology_free(g_top);
+    if (d_tab) shd_device_free(0, d_tab);
+    if (g_extra) shd_device_free(0, g_extra);
     return (bad || badc || badm || bads) ? 1 : 0;
 }

@@ -46,6 +46,12 @@ int shd_dev_memset(void* d, int v, size_t bytes) {
     return 0;
 }
 int shd_dev_sync(void) { return 0; }
+int shd_dev_stream_new(void** s) {
+    *s = malloc(1);
+    return *s ? 0 : -ENOMEM;
+}
+int shd_dev_stream_sync(void* s) { return 0; }
+void shd_dev_stream_free(void* s) { free(s); }
 
 /* entry (i, j) of the synthetic table */
 void stub_entry(int i, int j, double* lat, double* rel) {
@@ -73,6 +79,19 @@ int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, doubl
         }
     return 0;
 }
+
+int shd_dev_release_min(const ShdEntry* base, int A, const int32_t* rows, const uint32_t* seqs, int n,
+                        const uint32_t* touch, double* out, void** scratch) {
+    for (int r = 0; r < n; r++) {
+        const ShdEntry* row = base + (size_t)rows[r] * (size_t)A;
+        out[r] = -1.0;
+        for (int j = 0; j < A; j++)
+            if (j != rows[r] && touch[j] > seqs[r] && row[j].lat >= 0 && (out[r] < 0 || row[j].lat < out[r]))
+                out[r] = row[j].lat;
+    }
+    return 0;
+}
+void shd_dev_release_scratch_free(void* scratch) { (void)scratch; }
 
 int shd_dev_ws_new(void** ws) {
     *ws = malloc(1);

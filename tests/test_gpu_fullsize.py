@@ -77,6 +77,7 @@ def test_c3_uniform_unrestricted_round_bit_exact():
     top.build_rows_device(0, A, full.data_ptr())
     torch.cuda.synchronize()
     top.adopt_table_device_resident(full.data_ptr())
+    top.touch_all()  # steady state: every row released, in slot order (the oracle's preload order)
     sv = np.unique(verts).astype(np.int32)
     assert len(sv) == A
     orc = O.OracleTopology(gml)
@@ -109,6 +110,7 @@ def c4():
     top.build_rows_device(0, A, full.data_ptr())
     torch.cuda.synchronize()
     top.adopt_table_device_resident(full.data_ptr())
+    top.touch_all()  # steady state (slot order); lazy release is tests/test_gpu_lazy_release.py
     sv = np.unique(verts).astype(np.int32)
     assert len(sv) == A
     orc = O.OracleTopology(gml)

@@ -462,9 +462,10 @@ def test_device_api_unknown_hosts_not_delivered(pipeline):
 
 @pytest.mark.parametrize("name", ["sparse300_ns", "sparse200_dir_ns", "sparse5000_hbm"])
 def test_device_resident_table_matches_mirrored(name, pipeline):
-    """adopt_table_device_resident (no host mirror, all rows released at
-    adoption) == adopt_table_device + touch_all: same released minimum, same
-    host lookups (single-entry device reads), same device round as the oracle."""
+    """adopt_table_device_resident (no host mirror) + touch_all ==
+    adopt_table_device + touch_all: same released minimum (touch_all's rows
+    released by the device pass in slot order), same host lookups
+    (single-entry device reads), same device round as the oracle."""
     import torch
     from shadow_amd import ShdError
     gml, H = GRAPHS[name]
@@ -479,6 +480,8 @@ def test_device_resident_table_matches_mirrored(name, pipeline):
     top2.build_rows_device(0, A, tab.data_ptr())
     torch.cuda.synchronize()
     top2.adopt_table_device_resident(tab.data_ptr())
+    assert top2.min_path_latency() == 0  # lazy: nothing released at adoption
+    top2.touch_all()
     assert bits(top2.min_path_latency()) == bits(top.min_path_latency())
     with pytest.raises(ShdError):
         top2.adopt_table_device_resident(tab.data_ptr())  # rows already released: -EBUSY
@@ -621,17 +624,15 @@ def test_lookup_batch_matches_single_lookups(resident):
         tab = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
         top.build_rows_device(0, A, tab.data_ptr())
         torch.cuda.synchronize()
-        top.adopt_table_device_resident(tab.data_ptr())
-        lat_t, rel_t, sv = top.table() if False else (None, None, None)
-        top2, orc2, _, _ = make_pair(gml, H)
-        top2.touch_all()
-        lat2, rel2, sv2 = top2.table()
-        orc.preload(sv2, lat2, rel2)  # every row released in slot order, as the resident adoption
+        top.adopt_table_device_resident(tab.data_ptr())  # lazy: the batch's touches release rows on the device
+    top.record_min_jump()
     lat, rel = top.lookup_batch(s, d)
     for i in range(len(s)):
         assert bits(lat[i]) == bits(orc.latency(int(s[i]), int(d[i])))
         assert bits(rel[i]) == bits(orc.reliability(int(s[i]), int(d[i])))
     assert bits(top.min_path_latency()) == bits(orc.min_path_latency())
+    assert top.next_min_jump_ns() == orc.next_min_jump_ns()
+    assert top.cached_paths_log() == orc.cached_paths_log()  # the same pairs from the same rows
 
 
 @pytest.mark.parametrize("name,use_sp", [("1_gbit_switch", True), ("complete30_ms", True), ("sparse300_ns", True),

@@ -48,19 +48,44 @@ CASES = {
 }
 
 
+def _run(exe, path, use_sp, hosts, threads, ops, shards):
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66 second_deadlock_stack=1")
+    return subprocess.run([exe, str(path), str(use_sp), str(hosts), str(threads), str(ops), str(shards)],
+                          capture_output=True, text=True, timeout=300, env=env)
+
+
+# table: 0 host-mirrored, 1 device-resident (lazy release by device pass,
+# here the stub's), 2 two shards of a single-process multi-GPU table
+@pytest.mark.parametrize("table", [0, 1, 2], ids=["mirror", "resident", "shards2"])
 @pytest.mark.parametrize("kind", ["plain", "tsan"])
 @pytest.mark.parametrize("case", list(CASES))
-def test_concurrent_lookups_serially_consistent(binaries, case, kind, tmp_path):
+def test_concurrent_lookups_serially_consistent(binaries, case, kind, table, tmp_path):
     gml, use_sp, hosts = CASES[case]
+    if table and not use_sp:
+        pytest.skip("device-resident tables need use_shortest_path")
     path = tmp_path / "g.gml"
     path.write_text(gml)
-    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66 second_deadlock_stack=1")
-    ops = "20000" if kind == "plain" else "4000"
-    r = subprocess.run([binaries[kind], str(path), str(use_sp), str(hosts), "8", ops], capture_output=True,
-                       text=True, timeout=300, env=env)
+    ops = 20000 if kind == "plain" else 4000
+    r = _run(binaries[kind], path, use_sp, hosts, 8, ops, table)
     assert "ThreadSanitizer" not in r.stderr, r.stderr[-3000:]
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     assert " bad 0 0 0 0" in r.stdout
     if use_sp:
         touched = int(r.stdout.split("touched ")[1].split()[0])
         assert touched > 10  # many rows were released concurrently
+
+
+@pytest.mark.parametrize("case", ["sparse200_undirected", "sparse150_directed_ns"])
+def test_single_worker_release_sequence_same_for_every_table(binaries, case, tmp_path):
+    """One worker (the reference's serial order): the device-resident and the
+    two-shard tables release exactly what the host-mirrored table releases --
+    same touch order, same min-jump callback sequence (value by value)."""
+    gml, use_sp, hosts = CASES[case]
+    path = tmp_path / "g.gml"
+    path.write_text(gml)
+    outs = []
+    for table in (0, 1, 2):
+        r = _run(binaries["plain"], path, use_sp, hosts, 1, 20000, table)
+        assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+        outs.append(r.stdout.split("cb_calls ")[1].split(" staged")[0] + r.stdout.split("touched ")[1].split()[0])
+    assert outs[0] == outs[1] == outs[2], outs
