@@ -288,21 +288,39 @@ int shd_deliv_sort_device(ShdTopology* top, const ShdDeliv* d_in, size_t n, uint
 
 /* The collectives a multi-GPU round needs, supplied by the caller: Shadow's
  * C host plugs in RCCL (shd_transport_rccl_new below: ncclSend/ncclRecv over
- * xGMI); tests plug in gloo.  Both calls are collective over `world` ranks.
+ * xGMI); tests plug in gloo.  Every call is collective over `world` ranks.
  *   alltoall_u64: host arrays of `world` values; recv[r] = what rank r sent
  *                 to this rank.
  *   alltoallv:    device buffers; this rank's block for peer r is
  *                 send_bytes[r] bytes, blocks contiguous in rank order in
  *                 d_send; the blocks received land contiguous in rank order
  *                 in d_recv.  Enqueued on `stream` (hipStream_t) or completed
- *                 before returning.  Return 0 or a negative errno. */
+ *                 before returning.
+ *   allgatherv:   in place on the device buffer d_buf: rank r contributes
+ *                 bytes [offsets[r], offsets[r+1]) (world + 1 host values,
+ *                 the same on every rank); afterwards every rank holds every
+ *                 block.  Enqueued on `stream` or completed before returning.
+ *                 Only shd_topology_allgather_rows needs it (may be NULL
+ *                 otherwise).
+ * Return 0 or a negative errno. */
 typedef struct ShdTransport {
     int rank, world;
     void* user;
     int (*alltoall_u64)(void* user, const uint64_t* send, uint64_t* recv);
     int (*alltoallv)(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
                      const uint64_t* recv_bytes, void* stream);
+    int (*allgatherv)(void* user, void* d_buf, const uint64_t* offsets, void* stream);
 } ShdTransport;
+
+/* Full-matrix export of a row-sharded table ("RCCL
+ * all-gather over xGMI only when a full matrix is requested"): d_table is
+ * this rank's A x A table (A = shd_topology_slot_count) in which rank r has
+ * built rows [row_bounds[r], row_bounds[r+1]) at their own offsets
+ * (shd_topology_build_rows_device); on return every rank's d_table holds
+ * every row, ready for shd_topology_adopt_table_device.  row_bounds: world +
+ * 1 slot ids covering [0, A).  Synchronous (stream: hipStream_t or NULL). */
+int shd_topology_allgather_rows(ShdTopology* top, const ShdTransport* xport, void* d_table, const uint32_t* row_bounds,
+                                void* stream);
 
 /* Destination-owner exchange of one round's delivered events: rank r owns
  * the destination hosts [host_bounds[r], host_bounds[r+1]) (host memory,

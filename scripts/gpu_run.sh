@@ -14,20 +14,23 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 D=$R/gpurun_out/$T
 mkdir -p $D
 export TMPDIR=/tmp
+i=0
 for step in "$@"; do
+    i=$((i + 1))
     kind=${step%%:*}
     arg=""
     [[ $step == *:* ]] && arg=${step#*:}
     case $kind in
     test)
+        L=$D/pytest$i.log
         if [ -n "$arg" ]; then
             timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread -k "$arg" \
-                > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
+                > $L 2>&1 || { tail -60 $L; exit 1; }
         else
             timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread \
-                > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
+                > $L 2>&1 || { tail -60 $L; exit 1; }
         fi
-        tail -3 $D/pytest.log ;;
+        tail -3 $L ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1 \
             || { tail -20 $D/smoke.log; exit 1; }

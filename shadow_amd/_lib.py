@@ -77,6 +77,7 @@ PROTOS = {
     "shd_round_exchange": (C.c_int, [_P, _P, _P, _P, _u32p, _P, C.c_size_t, _P, _P, C.POINTER(C.c_size_t), _P]),
     "shd_round_route_records": (C.c_int, [_P, _P, _P, C.c_size_t, _u32p, _P, _P, C.c_size_t,
                                           C.POINTER(C.c_size_t), _P]),
+    "shd_topology_allgather_rows": (C.c_int, [_P, _P, _P, _u32p, _P]),
     "shd_topology_adopt_table_shard_device_resident": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_double]),
     "shd_topology_shard_min_latency": (C.c_int, [_P, _P, C.c_int, C.c_int, _dp]),
     "shd_transport_rccl_unique_id": (C.c_int, [_P]),

@@ -1489,6 +1489,10 @@ struct Ws {
     uint32_t* meta = nullptr; // big-segment merge metadata (MergeMeta)
     uint32_t cap_meta = 0;    // merge segments it holds
     uint32_t* fault = nullptr; // pinned host copy of the last round's merge fault word (meta hdr[3])
+    void* xdev = nullptr;      // exchange scratch (xchg.hip: route counts / offsets, event cuts), grow-only
+    size_t cap_xdev = 0;
+    void* xhost = nullptr;     // its pinned host side (read back on the launch stream)
+    size_t cap_xhost = 0;
 };
 
 int hip_status(hipError_t e, const char* what) {
@@ -1837,8 +1841,42 @@ extern "C" void shd_dev_ws_free(void* p) {
     (void)hipFree(w->slab);
     (void)hipFree(w->meta);
     if (w->fault) (void)hipHostFree(w->fault);
+    (void)hipFree(w->xdev);
+    if (w->xhost) (void)hipHostFree(w->xhost);
     if (w->done) (void)hipEventDestroy(w->done);
     delete w;
+}
+
+// Grow-only scratch of the multi-GPU exchange (device + pinned host), so a
+// round allocates nothing: hipFree / hipHostFree synchronise the device.
+// Callers run on one stream and synchronise it before returning, so a grow
+// only waits for the workspace's last round.
+extern "C" int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, void** h) {
+    if (!ws) return shd_fail(-ENOMEM, "no round workspace");
+    Ws& w = *static_cast<Ws*>(ws);
+    int rc = 0;
+    if (dev_bytes > w.cap_xdev) {
+        if ((rc = ws_quiesce(w))) return rc;
+        (void)hipFree(w.xdev);
+        w.xdev = nullptr;
+        w.cap_xdev = 0;
+        const size_t cap = dev_bytes + dev_bytes / 4 + 256;
+        if ((rc = hip_status(hipMalloc(&w.xdev, cap), "hipMalloc exchange scratch"))) return rc;
+        w.cap_xdev = cap;
+    }
+    if (host_bytes > w.cap_xhost) {
+        if ((rc = ws_quiesce(w))) return rc;
+        if (w.xhost) (void)hipHostFree(w.xhost);
+        w.xhost = nullptr;
+        w.cap_xhost = 0;
+        const size_t cap = host_bytes + host_bytes / 4 + 256;
+        if ((rc = hip_status(hipHostMalloc(&w.xhost, cap, hipHostMallocDefault), "hipHostMalloc exchange scratch")))
+            return rc;
+        w.cap_xhost = cap;
+    }
+    if (d) *d = w.xdev;
+    if (h) *h = w.xhost;
+    return 0;
 }
 
 extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,

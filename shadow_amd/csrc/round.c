@@ -439,7 +439,11 @@ int shd_round_exchange(ShdTopology* t, const ShdTransport* x, const ShdDeliv* d_
     uint64_t* send = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)x->world);
     if (!send) return -ENOMEM;
     size_t nrecv = 0;
-    if (!(rc = shd_dev_event_cuts(d_dst_offsets, host_bounds, x->world, send, stream)) &&
+    pthread_mutex_lock(&t->round_mu);
+    if (!t->ws) rc = shd_dev_ws_new(&t->ws);
+    if (!rc) rc = shd_dev_event_cuts(t->ws, d_dst_offsets, host_bounds, x->world, send, stream);
+    pthread_mutex_unlock(&t->round_mu);
+    if (!rc &&
         !(rc = shd_dev_exchange_blocks(x, d_events, send, sizeof(ShdDeliv), d_recv, recv_cap, &nrecv, stream)))
         rc = shd_deliv_sort_device(t, d_recv, nrecv, host_bounds[x->rank], host_bounds[x->rank + 1], d_out,
                                    d_out_offsets, stream);
@@ -464,5 +468,30 @@ int shd_round_route_records(ShdTopology* t, const ShdTransport* x, const ShdPkt*
         rc = shd_dev_route_records(&c, x, d_recs, n, row_bounds, d_scratch, d_recv, recv_cap, n_recv, stream);
     }
     pthread_mutex_unlock(&t->round_mu);
+    return rc;
+}
+
+int shd_topology_allgather_rows(ShdTopology* t, const ShdTransport* x, void* d_table, const uint32_t* row_bounds,
+                                void* stream) {
+    if (!t || !x || !d_table || !row_bounds || x->world < 1 || x->rank < 0 || x->rank >= x->world)
+        return shd_fail(-EINVAL, "bad all-gather arguments");
+    if (!x->allgatherv) return shd_fail(-ENOTSUP, "the transport has no allgatherv");
+    int A = 0;
+    int rc = shd_topology_slot_count(t, &A);
+    if (rc) return rc;
+    if (row_bounds[0] != 0 || (int)row_bounds[x->world] != A) return shd_fail(-EINVAL, "row bounds must cover [0, %d)", A);
+    uint64_t* off = (uint64_t*)malloc(sizeof(uint64_t) * ((size_t)x->world + 1));
+    if (!off) return -ENOMEM;
+    for (int r = 0; r <= x->world && !rc; r++) {
+        if (r && row_bounds[r] < row_bounds[r - 1]) rc = shd_fail(-EINVAL, "row bounds not ascending");
+        off[r] = (uint64_t)row_bounds[r] * (uint64_t)A * sizeof(ShdEntry);
+    }
+    if (!rc) rc = shd_dev_init(t->device);
+    if (!rc) {
+        rc = x->allgatherv(x->user, d_table, off, stream);
+        if (rc > 0) rc = -EIO;
+    }
+    if (!rc) rc = stream ? shd_dev_stream_sync(stream) : shd_dev_sync();
+    free(off);
     return rc;
 }

@@ -129,6 +129,9 @@ typedef struct {
  * the end of its last use), one per topology; callers serialise its use. */
 int shd_dev_ws_new(void** ws);
 void shd_dev_ws_free(void* ws);
+/* grow-only exchange scratch of a workspace: dev_bytes of device memory and
+ * host_bytes of pinned host memory (either pointer may be NULL) */
+int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, void** h);
 int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                          uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets,
                          uint8_t* d_status, uint64_t* d_counters, void* stream);
@@ -143,8 +146,8 @@ int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n,
 int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
                           const uint32_t* row_bounds, ShdPkt* d_scratch, ShdPkt* d_recv, size_t recv_cap,
                           size_t* n_recv, void* stream);
-int shd_dev_event_cuts(const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world, uint64_t* send_elems,
-                       void* stream);
+int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world,
+                       uint64_t* send_elems, void* stream);
 int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
                             void* d_recv, size_t recv_cap, size_t* n_recv, void* stream);
 

@@ -171,28 +171,40 @@ struct Rccl {
     ShdTransport x;
     ncclComm_t comm;
     int device;
-    uint64_t* d_u64; // 2 x world staging for the count exchange
+    hipStream_t stream; // the count exchange's own stream (never the null stream)
+    uint64_t* d_u64;    // 2 x world staging for the count exchange
+    uint64_t* h_u64;    // its pinned host side
 };
 
 int nccl_status(ncclResult_t r, const char* what) {
     return r == ncclSuccess ? 0 : shd_fail(-EIO, "%s: %s", what, ncclGetErrorString(r));
 }
 
+// Counts: pinned staging, stream-ordered copies and the send/recv group on
+// the transport's own stream, one synchronisation of that stream (the host
+// needs the counts); nothing touches the null stream.
 int rccl_alltoall_u64(void* user, const uint64_t* send, uint64_t* recv) {
     Rccl* t = static_cast<Rccl*>(user);
     const int W = t->x.world;
-    int rc = hip_status(hipMemcpy(t->d_u64, send, 8 * (size_t)W, hipMemcpyHostToDevice), "hipMemcpy counts");
+    std::memcpy(t->h_u64, send, 8 * (size_t)W);
+    int rc = hip_status(hipMemcpyAsync(t->d_u64, t->h_u64, 8 * (size_t)W, hipMemcpyHostToDevice, t->stream),
+                        "counts H2D");
     if (rc) return rc;
     if ((rc = nccl_status(ncclGroupStart(), "ncclGroupStart"))) return rc;
     for (int r = 0; r < W; r++) {
-        if ((rc = nccl_status(ncclSend(t->d_u64 + r, 1, ncclUint64, r, t->comm, nullptr), "ncclSend")) ||
-            (rc = nccl_status(ncclRecv(t->d_u64 + W + r, 1, ncclUint64, r, t->comm, nullptr), "ncclRecv"))) {
+        if ((rc = nccl_status(ncclSend(t->d_u64 + r, 1, ncclUint64, r, t->comm, t->stream), "ncclSend")) ||
+            (rc = nccl_status(ncclRecv(t->d_u64 + W + r, 1, ncclUint64, r, t->comm, t->stream), "ncclRecv"))) {
             (void)ncclGroupEnd();
             return rc;
         }
     }
     if ((rc = nccl_status(ncclGroupEnd(), "ncclGroupEnd"))) return rc;
-    return hip_status(hipMemcpy(recv, t->d_u64 + W, 8 * (size_t)W, hipMemcpyDeviceToHost), "hipMemcpy counts");
+    if ((rc = hip_status(hipMemcpyAsync(t->h_u64 + W, t->d_u64 + W, 8 * (size_t)W, hipMemcpyDeviceToHost, t->stream),
+                         "counts D2H")) ||
+        (rc = hip_status(hipStreamSynchronize(t->stream), "counts sync")))
+        return rc;
+    std::memcpy(recv, t->h_u64 + W, 8 * (size_t)W);
+    return 0;
 }
 
 int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
@@ -217,6 +229,29 @@ int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, v
     return rc ? rc : rc2;
 }
 
+// All-gather of variable blocks, in place: rank r's block is bytes
+// [off[r], off[r+1]) of buf.  Every rank sends its block straight to every
+// peer (one send/recv group): on the fully connected xGMI mesh each block
+// crosses one link and the 7 links of a GPU run at once, where a ring would
+// pass every block through W - 1 hops.
+int rccl_allgatherv(void* user, void* d_buf, const uint64_t* off, void* stream) {
+    Rccl* t = static_cast<Rccl*>(user);
+    const int W = t->x.world, me = t->x.rank;
+    hipStream_t s = (hipStream_t)stream;
+    char* b = static_cast<char*>(d_buf);
+    const uint64_t mine = off[me + 1] - off[me];
+    int rc = nccl_status(ncclGroupStart(), "ncclGroupStart");
+    if (rc) return rc;
+    for (int r = 0; r < W && !rc; r++) {
+        if (r == me) continue;
+        if (mine) rc = nccl_status(ncclSend(b + off[me], mine, ncclChar, r, t->comm, s), "ncclSend");
+        if (!rc && off[r + 1] > off[r])
+            rc = nccl_status(ncclRecv(b + off[r], off[r + 1] - off[r], ncclChar, r, t->comm, s), "ncclRecv");
+    }
+    const int rc2 = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+    return rc ? rc : rc2;
+}
+
 } // namespace
 
 extern "C" int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
@@ -231,46 +266,43 @@ extern "C" int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, 
     if (nblocks > 1024) nblocks = 1024;
     const size_t chunk = n ? (n + nblocks - 1) / nblocks : 1;
     const size_t m = (size_t)W * nblocks;
-    uint32_t *d_cnt = nullptr, *d_off = nullptr;
-    std::vector<uint32_t> off(m + 1);
+    // counts and offsets in the workspace's persistent scratch (no per-round
+    // hipMalloc / hipFree), offsets read back into its pinned host side
+    void *dscr = nullptr, *hscr = nullptr;
+    if ((rc = shd_dev_ws_scratch(c->ws, 4 * (2 * m + 1), 4 * (m + 1), &dscr, &hscr))) return rc;
+    uint32_t* d_cnt = static_cast<uint32_t*>(dscr);
+    uint32_t* d_off = d_cnt + m;
+    const uint32_t* off = static_cast<const uint32_t*>(hscr);
     std::vector<uint64_t> send(W);
-    if ((rc = hip_status(hipMalloc((void**)&d_cnt, 4 * m), "hipMalloc route")) ||
-        (rc = hip_status(hipMalloc((void**)&d_off, 4 * (m + 1)), "hipMalloc route")))
-        goto done;
-    {
-        const uint2* hi = reinterpret_cast<const uint2*>(c->host_info);
-        hipLaunchKernelGGL(k_route<0>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
-                           d_cnt, nullptr, nullptr);
-        hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, d_cnt, (uint32_t)m, d_off);
-        hipLaunchKernelGGL(k_route<1>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
-                           nullptr, d_off, d_part);
-        if ((rc = hip_status(hipGetLastError(), "k_route launch"))) goto done;
-        if ((rc = hip_status(hipMemcpyAsync(off.data(), d_off, 4 * (m + 1), hipMemcpyDeviceToHost, s), "route D2H")) ||
-            (rc = hip_status(hipStreamSynchronize(s), "route sync")))
-            goto done;
-        for (int r = 0; r < W; r++) send[r] = off[(size_t)(r + 1) * nblocks] - off[(size_t)r * nblocks];
-        rc = exchange_blocks(x, d_part, send.data(), sizeof(ShdPkt), d_recv, recv_cap, n_recv, s);
-        if (!rc) rc = hip_status(hipStreamSynchronize(s), "route exchange");
-    }
-done:
-    (void)hipFree(d_cnt);
-    (void)hipFree(d_off);
+    const uint2* hi = reinterpret_cast<const uint2*>(c->host_info);
+    hipLaunchKernelGGL(k_route<0>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk, d_cnt,
+                       nullptr, nullptr);
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, d_cnt, (uint32_t)m, d_off);
+    hipLaunchKernelGGL(k_route<1>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
+                       nullptr, d_off, d_part);
+    if ((rc = hip_status(hipGetLastError(), "k_route launch"))) return rc;
+    if ((rc = hip_status(hipMemcpyAsync(hscr, d_off, 4 * (m + 1), hipMemcpyDeviceToHost, s), "route D2H")) ||
+        (rc = hip_status(hipStreamSynchronize(s), "route sync")))
+        return rc;
+    for (int r = 0; r < W; r++) send[r] = off[(size_t)(r + 1) * nblocks] - off[(size_t)r * nblocks];
+    rc = exchange_blocks(x, d_part, send.data(), sizeof(ShdPkt), d_recv, recv_cap, n_recv, s);
+    if (!rc) rc = hip_status(hipStreamSynchronize(s), "route exchange");
     return rc;
 }
 
-extern "C" int shd_dev_event_cuts(const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world,
+extern "C" int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world,
                                   uint64_t* send_elems, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     RouteArgs ra;
     int rc = make_args(host_bounds, world, &ra);
     if (rc) return rc;
-    uint32_t* d_cuts = nullptr;
-    uint32_t cuts[kMaxWorld + 1];
-    if ((rc = hip_status(hipMalloc((void**)&d_cuts, 4 * (kMaxWorld + 1)), "hipMalloc cuts"))) return rc;
+    void *dscr = nullptr, *hscr = nullptr;
+    if ((rc = shd_dev_ws_scratch(ws, 4 * (kMaxWorld + 1), 4 * (kMaxWorld + 1), &dscr, &hscr))) return rc;
+    uint32_t* d_cuts = static_cast<uint32_t*>(dscr);
+    const uint32_t* cuts = static_cast<const uint32_t*>(hscr);
     hipLaunchKernelGGL(k_cuts, dim3(1), dim3(kMaxWorld + 1), 0, s, d_dst_offsets, ra, d_cuts);
-    rc = hip_status(hipMemcpyAsync(cuts, d_cuts, 4 * (size_t)(world + 1), hipMemcpyDeviceToHost, s), "cuts D2H");
+    rc = hip_status(hipMemcpyAsync(hscr, d_cuts, 4 * (size_t)(world + 1), hipMemcpyDeviceToHost, s), "cuts D2H");
     if (!rc) rc = hip_status(hipStreamSynchronize(s), "cuts sync");
-    (void)hipFree(d_cuts);
     if (!rc)
         for (int r = 0; r < world; r++) send_elems[r] = cuts[r + 1] - cuts[r];
     return rc;
@@ -302,9 +334,14 @@ extern "C" int shd_transport_rccl_new(int rank, int world, const void* id128, in
     ncclUniqueId id;
     std::memcpy(&id, id128, sizeof id);
     t->device = device;
-    if ((rc = hip_status(hipMalloc((void**)&t->d_u64, 16 * (size_t)world), "hipMalloc transport")) ||
+    if ((rc = hip_status(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking), "hipStreamCreate transport")) ||
+        (rc = hip_status(hipMalloc((void**)&t->d_u64, 16 * (size_t)world), "hipMalloc transport")) ||
+        (rc = hip_status(hipHostMalloc((void**)&t->h_u64, 16 * (size_t)world, hipHostMallocDefault),
+                         "hipHostMalloc transport")) ||
         (rc = nccl_status(ncclCommInitRank(&t->comm, world, id, rank), "ncclCommInitRank"))) {
         (void)hipFree(t->d_u64);
+        if (t->h_u64) (void)hipHostFree(t->h_u64);
+        if (t->stream) (void)hipStreamDestroy(t->stream);
         delete t;
         return rc;
     }
@@ -313,6 +350,7 @@ extern "C" int shd_transport_rccl_new(int rank, int world, const void* id128, in
     t->x.user = t;
     t->x.alltoall_u64 = rccl_alltoall_u64;
     t->x.alltoallv = rccl_alltoallv;
+    t->x.allgatherv = rccl_allgatherv;
     *out = &t->x;
     return 0;
 }
@@ -322,6 +360,8 @@ extern "C" void shd_transport_rccl_free(ShdTransport* x) {
     Rccl* t = static_cast<Rccl*>(x->user);
     (void)ncclCommDestroy(t->comm);
     (void)hipFree(t->d_u64);
+    if (t->h_u64) (void)hipHostFree(t->h_u64);
+    if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
 

@@ -267,6 +267,16 @@ class Topology:
         check(rc)
         return nr.value
 
+    def allgather_rows(self, xport, d_table: int, row_bounds, stream: int = 0):
+        """shd_topology_allgather_rows: completes this rank's A x A table
+        (rows [row_bounds[rank], row_bounds[rank+1]) built in place) with
+        every other rank's rows over the transport's allgatherv."""
+        rb = (C.c_uint32 * len(row_bounds))(*[int(x) for x in row_bounds])
+        rc = lib().shd_topology_allgather_rows(self._h, xport.handle, C.c_void_p(d_table), rb, C.c_void_p(stream))
+        if rc and getattr(xport, "error", None) is not None:
+            raise xport.error
+        check(rc)
+
     def shard_min_latency(self, d_rows: int, row_lo: int, row_hi: int) -> float:
         out = C.c_double()
         check(lib().shd_topology_shard_min_latency(self._h, C.c_void_p(d_rows), row_lo, row_hi, C.byref(out)))

@@ -1,7 +1,8 @@
 """Transports for multi-GPU rounds (include/shdnet.h ``ShdTransport``).
 
-``shd_round_exchange`` / ``shd_round_route_records`` take the two collectives
-they need from the caller.  Shadow's C host plugs in RCCL
+``shd_round_exchange`` / ``shd_round_route_records`` /
+``shd_topology_allgather_rows`` take the collectives they need from the
+caller.  Shadow's C host plugs in RCCL
 (``RcclTransport``: ncclSend/ncclRecv over xGMI, inside libshdnet); these
 Python transports wrap ``torch.distributed`` for tests and the benchmark:
 ``TorchTransport`` runs the all-to-all(v) on device tensors with the
@@ -21,11 +22,12 @@ from ._lib import check, lib
 A2A_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64))
 A2AV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p, C.POINTER(C.c_uint64),
                       C.c_void_p)
+AGV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p)
 
 
 class ShdTransport(C.Structure):
     _fields_ = [("rank", C.c_int), ("world", C.c_int), ("user", C.c_void_p), ("alltoall_u64", A2A_FN),
-                ("alltoallv", A2AV_FN)]
+                ("alltoallv", A2AV_FN), ("allgatherv", AGV_FN)]
 
 
 class TorchTransport:
@@ -40,7 +42,8 @@ class TorchTransport:
         self.error: BaseException | None = None
         self._a2a = A2A_FN(self._alltoall_u64)
         self._a2av = A2AV_FN(self._alltoallv)
-        self.struct = ShdTransport(self.rank, self.world, None, self._a2a, self._a2av)
+        self._agv = AGV_FN(self._allgatherv)
+        self.struct = ShdTransport(self.rank, self.world, None, self._a2a, self._a2av, self._agv)
 
     def register(self, *tensors: torch.Tensor):
         """Device buffers the C calls will pass to alltoallv (by base pointer)."""
@@ -76,6 +79,30 @@ class TorchTransport:
                 out = torch.empty(sum(rb), dtype=torch.uint8)
                 dist.all_to_all_single(out, src.cpu(), rb, sb, group=self.group)
                 dst.copy_(out.to(dst.device))
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            return 0
+        except BaseException as e:
+            self.error = e
+            return -5
+
+    def _allgatherv(self, _user, d_buf, offsets, _stream):
+        """In place: rank r's block is bytes [offsets[r], offsets[r+1]) of the
+        registered buffer d_buf; afterwards every rank holds every block."""
+        try:
+            off = [int(offsets[r]) for r in range(self.world + 1)]
+            buf = self._buf(d_buf)[:off[-1]]
+            sizes = [off[r + 1] - off[r] for r in range(self.world)]
+            work = buf if self.backend == "nccl" else buf.cpu()
+            if len(set(sizes)) == 1 and sizes[0]:
+                mine = work[off[self.rank]:off[self.rank + 1]].clone()
+                dist.all_gather_into_tensor(work, mine, group=self.group)
+            else:
+                for r in range(self.world):
+                    if sizes[r]:
+                        dist.broadcast(work[off[r]:off[r + 1]], src=r, group=self.group)
+            if work is not buf:
+                buf.copy_(work)
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             return 0

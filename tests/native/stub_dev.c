@@ -98,6 +98,9 @@ int shd_dev_ws_new(void** ws) {
     return *ws ? 0 : -ENOMEM;
 }
 void shd_dev_ws_free(void* ws) { free(ws); }
+int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, void** h) {
+    return shd_fail(-ENOSYS, "stub device: no exchange scratch");
+}
 
 int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
                          uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,
@@ -115,8 +118,8 @@ int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPk
                           size_t* n_recv, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no exchange");
 }
-int shd_dev_event_cuts(const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world, uint64_t* send_elems,
-                       void* stream) {
+int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world,
+                       uint64_t* send_elems, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no exchange");
 }
 int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,

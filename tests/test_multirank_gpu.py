@@ -2,10 +2,13 @@
 world sizes 2 and 3 on one GPU (every rank on cuda:0, the gloo-backed
 TorchTransport; the 8-GPU node runs the same code over RCCL).
 
-replicated: every rank holds the whole table, decides its own senders'
-  packets (shd_round_process_device), then shd_round_exchange sends each
-  event to its destination's owner rank, which regroups it with
-  shd_deliv_sort_device.
+replicated: rank r builds rows [row_bounds[r], row_bounds[r+1]) of the
+  table and shd_topology_allgather_rows completes it on every rank (the
+  full-matrix all-gather of §8e, through the transport's allgatherv); every
+  rank then decides its own senders' packets (shd_round_process_device), and
+  shd_round_exchange sends each event to its destination's owner rank, which
+  regroups it with shd_deliv_sort_device.  The gathered table is checked
+  bitwise against the oracle's rows.
 sharded: rank r builds and holds only rows [row_bounds[r], row_bounds[r+1])
   (shd_topology_adopt_table_shard_device_resident); shd_round_route_records
   first moves every record to the rank holding the row that answers it,
@@ -62,7 +65,17 @@ def _worker(rank, world, port, mode, q):
         host_bounds = [r * H // world for r in range(world + 1)]
         pk = _packets(rank, world, st)
         xp = TorchTransport(device=torch.device("cuda", 0))
+        table = b""
         if mode == "replicated":
+            lo, hi = row_bounds[rank], row_bounds[rank + 1]
+            tab = torch.zeros(A * A * 2, dtype=torch.float64, device="cuda")
+            if hi > lo:
+                top.build_rows_device(lo, hi, tab.data_ptr())
+            torch.cuda.synchronize()
+            xp.register(tab)
+            top.allgather_rows(xp, tab.data_ptr(), row_bounds)
+            table = tab.cpu().numpy().tobytes()
+            top.adopt_table_device(tab.data_ptr())
             top.touch_all()
             recs = torch.from_numpy(pk.view(np.uint8)).cuda()
             n = len(pk)
@@ -106,11 +119,11 @@ def _worker(rank, world, port, mode, q):
         assert np.array_equal(np.diff(offs), np.bincount(got["dst_host"] - host_bounds[rank], minlength=mine))
         mt = torch.tensor([int(d_cnt.cpu().numpy().view(np.uint64)[1])], dtype=torch.float64)
         dist.all_reduce(mt, op=dist.ReduceOp.MIN)
-        q.put((rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), None))
+        q.put((rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), table, None))
         dist.destroy_process_group()
     except BaseException as e:  # report, then fail the process
         import traceback
-        q.put((rank, b"", 0.0, 0, traceback.format_exc()))
+        q.put((rank, b"", 0.0, 0, b"", traceback.format_exc()))
         raise
 
 
@@ -139,6 +152,9 @@ def test_multirank_round_through_c_abi(world, mode):
     ips, st, verts = scenario.register_hosts(orc, H, 1)
     sv = np.unique(verts).astype(np.int32)
     lat, rel = orc.rows_parallel(sv, sv, 8)
+    if mode == "replicated":  # every rank's all-gathered table == the oracle's rows
+        want = np.stack([lat, rel], axis=-1).tobytes()
+        assert all(r[4] == want for r in res)
     orc.preload(sv, lat, rel)  # every row released in slot order, as touch_all / the shard adoption
     allpk = np.concatenate([_packets(r, world, st) for r in range(world)])
     ref, status, mt = orc.round(ips, allpk, BARRIER, END)
