@@ -404,6 +404,12 @@ struct OrcTopo {
         double lat, rel;
         uint64_t pkts;
     }** cache;
+    /* rows already computed once: on a directed graph the reference recomputes
+     * row s on every (s, d) lookup whose pair was stored as (d, s)
+     * (topology.c:1940-1968, the (d, s) probe is undirected-only); that
+     * recomputation stores nothing (every (s, v) of the row is already stored
+     * either way, entries are never removed), so it is skipped here */
+    unsigned char* row_done;
     double min_lat;
     int min_updates;
     uint64_t next_min_jump_ns;
@@ -621,6 +627,7 @@ void orc_topology_free(OrcTopo* t) {
         for (int v = 0; v < t->V; v++) free(t->cache[v]);
         free(t->cache);
     }
+    free(t->row_done);
     free(t);
 }
 
@@ -769,6 +776,7 @@ OrcTopo* orc_topology_new(const char* text, int use_shortest_path) {
     }
     t->v_attached = (unsigned char*)calloc((size_t)t->V, 1);
     t->cache = (PathE**)calloc((size_t)t->V, sizeof(PathE*));
+    t->row_done = (unsigned char*)calloc((size_t)t->V, 1);
     return t;
 fail:
     orc_topology_free(t);
@@ -1217,6 +1225,7 @@ static int compute_source_paths(OrcTopo* t, int s, int d) {
         cache_store(t, dir, s, s, l, r);
         return 1;
     }
+    if (t->row_done[s]) return 1; /* a recomputation would store nothing (row_done) */
     int V = t->V, n = 0;
     int* targets = (int*)malloc(sizeof(int) * (size_t)V);
     for (int v = 0; v < V; v++)
@@ -1233,6 +1242,7 @@ static int compute_source_paths(OrcTopo* t, int s, int d) {
         if (l == 0) l = 1;
         cache_store(t, 0, s, v, l, r[v]);
     }
+    t->row_done[s] = 1;
     free(targets);
     free(is_t);
     free(dist);
@@ -1787,6 +1797,11 @@ size_t orc_topology_log_cached_paths(OrcTopo* t, char* buf, size_t cap) {
 
 #define ORC_NIC_INTERVAL 1000000ull /* _networkinterface_getRefillInterval, :99-101 */
 
+/* send requests that met a refill task of their host at the same nanosecond
+ * in the last orc_nic_run (how often the tie assumption above decided) */
+static uint64_t orc_nic_ties;
+uint64_t orc_nic_tie_count(void) { return orc_nic_ties; }
+
 typedef struct {
     uint64_t time;
     uint32_t src;
@@ -1946,6 +1961,7 @@ int orc_nic_run(uint32_t nhosts, uint32_t host_base, const OrcDeliv* ev, const u
                 uint8_t* rstat, uint64_t fate_cap, uint64_t* stime) {
     int rc = 0;
     OrcNicHeap H = {0};
+    orc_nic_ties = 0;
     for (uint32_t k = eoff[0]; k < eoff[nhosts]; k++) {
         if ((uint64_t)id_base + k >= fate_cap) return -3;
         rtime[id_base + k] = UINT64_MAX;
@@ -2002,6 +2018,9 @@ int orc_nic_run(uint32_t nhosts, uint32_t host_base, const OrcDeliv* ev, const u
                 s->router.total_size += elen[k];
                 if (!buffered) orc_nic_receive(&N, e.time);
             } else if (e.cls == 1) { /* networkinterface_wantsSend (:633-661) */
+                /* the documented assumption decided this order iff the host's
+                 * refill task is due at the very same nanosecond */
+                if (H.n && H.h[0].time == e.time && H.h[0].cls == 2) orc_nic_ties++;
                 N.sk = soff[h] + (size_t)e.idx + 1;
                 orc_nic_send(&N, e.time);
             } else {

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Builds the C4 routing table once (V=100k, H=200k, all 86,603 rows into a
-device table), as bench.py's C4 leg does -- a target for PMC passes over the
-C4 slab-kernel launch (scripts/r02_final_pmc.sh)."""
+"""Builds a routing table once, as bench.py's legs do -- a target for PMC
+passes over one slab-kernel launch (scripts/pmc_r03.sh).  Default: C4 (V=100k,
+H=200k, all 86,603 rows); `build_c4.py V H SEED` for another sparse config
+(C2: 20000 50000 0x5EED0002)."""
 import os
 import sys
 import time
@@ -12,15 +13,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     from shadow_amd import Topology, scenario, synth
     import torch
-    top = Topology(synth.sparse_graph_gml(100_000, 0x5EED0004))
-    scenario.register_hosts(top, 200_000, seed=1)
+    V, H, seed = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3], 0)) if len(sys.argv) > 3 else \
+        (100_000, 200_000, 0x5EED0004)
+    top = Topology(synth.sparse_graph_gml(V, seed))
+    scenario.register_hosts(top, H, seed=1)
     A = top.slot_count()
     tab = top.alloc_table(A * A * 16)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     top.build_rows_device(0, A, tab.ptr)
     torch.cuda.synchronize()
-    print(f"C4 build A={A}: {time.perf_counter() - t0:.2f}s", flush=True)
+    print(f"build V={V} H={H} A={A}: {time.perf_counter() - t0:.2f}s", flush=True)
 
 
 if __name__ == "__main__":

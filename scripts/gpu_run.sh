@@ -2,6 +2,7 @@
 # GPU-box recipe (run through gpurun from the repo root):
 #   scripts/gpu_run.sh TAG STEP [STEP ...]
 # STEP: test[:EXPR]  pytest -m gpu (optionally -k EXPR), full output in gpurun_out/TAG/
+#       probe:ARGS   scripts/agg_probe.py ARGS (commas for spaces): in-process A/B of a knob
 #       smoke        __graft_entry__.smoke()
 #       bench[:ARGS] bench.py (ARGS: extra arguments, commas for spaces)
 #       prof[:ARGS]  rocprofv3 --kernel-trace --stats of bench.py
@@ -38,6 +39,10 @@ for step in "$@"; do
     bench)
         timeout -k 10 900 python -u $R/bench.py ${arg//,/ } > $D/bench.json 2> $D/bench.err || { tail -30 $D/bench.err; exit 1; }
         cat $D/bench.json ;;
+    probe)
+        # scripts/agg_probe.py ENV V1 V2 ... (commas for spaces)
+        timeout -k 10 600 python -u $R/scripts/agg_probe.py ${arg//,/ } > $D/probe$i.log 2>&1 || { tail -30 $D/probe$i.log; exit 1; }
+        cat $D/probe$i.log ;;
     prof)
         (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $D/prof -o prof -- \
             python3 $R/bench.py ${arg//,/ } > $D/prof_bench.json 2> $D/prof_bench.err) || { tail -30 $D/prof_bench.err; exit 1; }

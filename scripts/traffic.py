@@ -4,14 +4,17 @@ stage, as MI355X_MICROARCH.md §HBM prescribes for gfx950: FETCH_SIZE counts
 64 B per TCC_EA0_RDREQ while the requests are 128-B lines (x2 correction,
 cross-checked against TCC_EA0_RDREQ_sum in the third pass); WRITE_SIZE is
 taken as is (it equals 64 B x WRREQ_64B + 32 B x the other write requests).
-Usage: scripts/traffic.py OUT.json PASS_CSV...   (profiles/r01_s5a_pmc_p*.csv)"""
+Usage: scripts/traffic.py OUT.json [--suffix S] [--source TEXT] PASS_CSV...
+(--suffix appends S to the routing keys and merges into an existing OUT.json,
+e.g. routing_slab_c4 from a C4 build's passes)"""
 import csv
 import json
 import re
 import sys
 
 STAGE = {"k_pkt_scatter": "packet_scatter", "k_place_rank": "place", "k_place_bucket": "place",
-         "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_slab<256>": "routing_slab", "k_sssp_lds<true>": "routing_lds"}
+         "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_slab<256>": "routing_slab",
+         "k_sssp_lds<true>": "routing_lds", "k_scan_one": "scan"}
 
 
 def kname(n):
@@ -20,7 +23,16 @@ def kname(n):
 
 
 def main():
-    out, files = sys.argv[1], sys.argv[2:]
+    out, args = sys.argv[1], sys.argv[2:]
+    suffix, source = "", None
+    while args and args[0].startswith("--"):
+        if args[0] == "--suffix":
+            suffix, args = args[1], args[2:]
+        elif args[0] == "--source":
+            source, args = args[1], args[2:]
+        else:
+            raise SystemExit(f"unknown option {args[0]}")
+    files = args
     agg = {}
     for f in files:
         for r in csv.DictReader(open(f)):
@@ -36,11 +48,23 @@ def main():
         wr = 1024 * sum(w) / len(w)
         rq = agg.get((k, "TCC_EA0_RDREQ_sum"))
         wq = agg.get((k, "TCC_EA0_WRREQ_sum"))
-        res[st] = {"bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
+        key = st + suffix if st.startswith("routing") else st
+        res[key] = {"bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
                    "rd_requests": sum(rq) / len(rq) if rq else None,
                    "wr_requests": sum(wq) / len(wq) if wq else None}
-    res["_source"] = "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | TCC_EA0_*REQ (separate passes) over " \
-                     "`bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline`; FETCH_SIZE x2 (gfx950)"
+    if suffix:
+        try:
+            base = json.load(open(out))
+        except OSError:
+            base = {}
+        base.update(res)
+        if source:
+            base.setdefault("_sources", {})[suffix] = source
+        res = base
+    else:
+        res["_source"] = source or ("rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | TCC_EA0_*REQ (separate passes) over "
+                                    "`bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline`; FETCH_SIZE x2 "
+                                    "(gfx950)")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

@@ -33,6 +33,7 @@
 
 #include <cerrno>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -62,6 +63,10 @@ constexpr int kStageItems = 4;
 constexpr int kStageTile = kStageBlock * kStageItems; // events staged in LDS per step
 constexpr int kMaxParts = 64;      // pass-1 fan-out limit (np <= kMaxParts - 1)
 constexpr uint32_t kPartsTarget = 32;
+// stage guards of a round (nbig[2], folded into the merge fault word's bits
+// 24..30 by k_segsort_mid): overflow event outside its segment, overflow
+// count above the list, big-segment list full, offsets above the staging area
+enum : uint32_t { kFaultOvfRange = 1u, kFaultOvfCap = 2u, kFaultBigCap = 4u, kFaultOff = 8u };
 
 __device__ __forceinline__ int glibc_rand_r(uint32_t* state) {
     uint32_t next = *state;
@@ -219,7 +224,18 @@ __device__ __forceinline__ uint32_t wave_alloc(bool want, uint32_t* counter, int
 // comes from the workgroup's LDS histogram (old value of an LDS atomic,
 // carried in pad) -- no global atomics per event; cnt1 is the bucket x tile
 // matrix.
-template <int kMode, int kB = kBatch>
+// Packet-path table entry (shd_dev_ptab_build): {delay_ns, keep threshold}.
+// keep_thr = max{r : (double)r / 2147483647.0 <= rel} over the 31-bit rand_r
+// outputs, so `chance <= rel` (worker.c:545) is exactly `r <= keep_thr`, and
+// delay_ns = (u64)ceil(lat * 1e6) (worker.c:548); an entry whose delay does
+// not fit (or whose rel has no such r) holds kPtabFallback and is decided
+// from the f64 entry.  8 B instead of 16: half the random-gather footprint.
+constexpr uint32_t kPtabFallback = 0xFFFFFFFFu;
+
+// kProbe (measurement only, SHD_SCATTER_PROBE; outputs are NOT the round's):
+// 1 skips the table gather, 2 the host->slot gathers, 3 the event store,
+// 4 the destination-slot atomic -- each stage's share of the kernel time.
+template <int kMode, int kB = kBatch, int kProbe = 0>
 __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
                                                         uint64_t barrier, uint64_t end_time, uint64_t boot_end,
                                                         Bucketing bk, ShdDeliv* __restrict__ tmp,
@@ -243,6 +259,7 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
     const size_t end = beg + bk.chunk < n ? beg + bk.chunk : n;
     const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
     const ShdEntry* __restrict__ tab = c.tab;
+    const uint2* __restrict__ ptab = reinterpret_cast<const uint2*>(c.ptab);
     // kB records per thread go through each gather level together, so a
     // wave keeps kB x 64 independent requests in flight per level
     for (size_t b0 = beg; b0 < end; b0 += (size_t)kBlock * kB) {
@@ -260,8 +277,13 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
 #pragma unroll
         for (int k = 0; k < kB; k++) {
             const bool known = live[k] && p[k].src_host < c.nhosts && p[k].dst_host < c.nhosts;
-            const uint2 hs = known ? host_info[p[k].src_host] : make_uint2(~0u, ~0u);
-            const uint2 hd = known ? host_info[p[k].dst_host] : make_uint2(~0u, ~0u);
+            uint2 hs = make_uint2(~0u, ~0u), hd = make_uint2(~0u, ~0u);
+            if (kProbe == 2) {
+                if (known) hs = make_uint2(p[k].src_host % c.A, 0u), hd = make_uint2(p[k].dst_host % c.A, 1u);
+            } else if (known) {
+                hs = host_info[p[k].src_host];
+                hd = host_info[p[k].dst_host];
+            }
             si[k] = hs.x == ~0u ? -1 : (int)hs.x;
             di[k] = hd.x == ~0u ? -1 : (int)hd.x;
             ts[k] = hs.y;
@@ -286,9 +308,22 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
             ei[k] = (size_t)(oi < 0 ? 0 : oi) * A + (size_t)(oj < 0 ? 0 : oj);
         }
         ShdEntry e[kB];
+        uint2 q[kB];
+        if (ptab) { // (uniform) the 8-B packet-path table
 #pragma unroll
-        for (int k = 0; k < kB; k++)
-            if (si[k] >= 0 && di[k] >= 0) e[k] = tab[ei[k]];
+            for (int k = 0; k < kB; k++) {
+                q[k] = make_uint2(kPtabFallback, 0u);
+                if (si[k] >= 0 && di[k] >= 0) q[k] = kProbe == 1 ? ptab[(ei[k] & 1023u) + (size_t)c.row_lo * A]
+                                                                  : ptab[ei[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < kB; k++) // entries that do not fit the 8-B form (none on the bench graphs)
+                if (si[k] >= 0 && di[k] >= 0 && q[k].x == kPtabFallback) e[k] = tab[ei[k]];
+        } else {
+#pragma unroll
+            for (int k = 0; k < kB; k++)
+                if (si[k] >= 0 && di[k] >= 0) e[k] = kProbe == 1 ? tab[(ei[k] & 1023u) + (size_t)c.row_lo * A] : tab[ei[k]];
+        }
         uint8_t st[kB];
         uint64_t tt[kB];
 #pragma unroll
@@ -297,10 +332,20 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
             tt[k] = 0;
             if (live[k] && si[k] >= 0 && di[k] >= 0) {
                 uint32_t rs = p[k].rng_state;
-                const double chance = (double)glibc_rand_r(&rs) / 2147483647.0; // random_nextDouble
+                const uint32_t r = (uint32_t)glibc_rand_r(&rs);
+                bool keep;
+                uint64_t delay;
+                if (ptab && q[k].x != kPtabFallback) {
+                    keep = r <= q[k].y; // == (chance <= rel), see kPtabFallback
+                    delay = q[k].x;
+                } else {
+                    const double chance = (double)r / 2147483647.0; // random_nextDouble
+                    keep = chance <= e[k].rel;
+                    delay = (uint64_t)ceil(e[k].lat * 1000000.0);
+                }
                 st[k] = SHD_DROPPED_LOSS;
-                if (p[k].now < boot_end || chance <= e[k].rel || p[k].payload_len == 0) { // worker.c:545
-                    uint64_t t = p[k].now + (uint64_t)ceil(e[k].lat * 1000000.0);     // worker.c:548-549
+                if (p[k].now < boot_end || keep || p[k].payload_len == 0) { // worker.c:545
+                    uint64_t t = p[k].now + delay;                          // worker.c:548-549
                     if (t >= end_time) {                                              // scheduler.c:236-239
                         st[k] = SHD_DROPPED_END;
                     } else {
@@ -315,13 +360,15 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
         for (int k = 0; k < kB; k++) {
             const bool dl = st[k] == SHD_DELIVERED;
             uint32_t rank = 0;
-            if (kRank) rank = dest_slot(dl, p[k].dst_host, cnt1, agg, lane); // (every lane: wave-level groups)
+            if (kProbe == 4) rank = dl ? (uint32_t)(idx[k] & 127u) : 0u;
+            else if (kRank) rank = dest_slot(dl, p[k].dst_host, cnt1, agg, lane); // (every lane: wave-level groups)
             const uint32_t oslot = kMode == 2 ? wave_alloc(dl && rank >= kSlab, novf, lane) : 0u;
             if (dl) {
                 const uint64_t t = tt[k];
                 if (!kRank) rank = atomicAdd(&hist[(p[k].dst_host - bk.host_lo) >> bk.shift], 1u); // LDS
                 const ShdDeliv ev{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)idx[k] + c.idx_base, rank};
-                if (kMode < 2) st_ev(&tmp[idx[k]], ev);
+                if (kProbe == 3) {
+                } else if (kMode < 2) st_ev(&tmp[idx[k]], ev);
                 else if (rank < kSlab)
                     st_ev(&tmp[bk.slab_rm ? (size_t)rank * bk.H + p[k].dst_host
                                           : (size_t)p[k].dst_host * kSlab + rank], ev);
@@ -433,6 +480,66 @@ __global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, si
     if (i == 0) {
         out[len] = bsum[nb];
         if (counters) counters[0] = bsum[nb];
+    }
+}
+
+// The same scan in ONE launch of one 1,024-thread workgroup (len <=
+// kScanOneMax, the per-destination counts of a round): each wave owns a
+// contiguous stretch of whole 256-element chunks; pass 1 sums it with 16-B
+// loads, the 16 wave sums are combined through LDS, pass 2 re-reads the
+// stretch (L2-warm) and writes the prefixes with a wave scan and a running
+// carry.  Replaces three launches whose boundaries cost more than the
+// 0.4 MB they move.  out[len] = total (and counters[0]).
+constexpr size_t kScanOneMax = 1u << 19;
+__global__ __launch_bounds__(1024) void k_scan_one(const uint32_t* __restrict__ in, size_t len,
+                                                   uint32_t* __restrict__ out, unsigned long long* counters) {
+    __shared__ uint32_t wsum[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const size_t S = (len + 16 * 256 - 1) / (16 * 256) * 256;
+    const size_t b0 = (size_t)w * S;
+    auto ld4 = [&](size_t i) {
+        uint4 v;
+        if (i + 3 < len) {
+            v = *reinterpret_cast<const uint4*>(in + i);
+        } else {
+            v.x = i < len ? in[i] : 0u;
+            v.y = i + 1 < len ? in[i + 1] : 0u;
+            v.z = i + 2 < len ? in[i + 2] : 0u;
+            v.w = i + 3 < len ? in[i + 3] : 0u;
+        }
+        return v;
+    };
+    uint32_t sum = 0;
+    for (size_t c = 0; c < S; c += 256) {
+        const uint4 v = ld4(b0 + c + 4 * lane);
+        sum += v.x + v.y + v.z + v.w;
+    }
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (lane == 0) wsum[w] = sum;
+    __syncthreads();
+    uint32_t carry = 0, total = 0;
+    for (int k = 0; k < 16; k++) {
+        if (k < w) carry += wsum[k];
+        total += wsum[k];
+    }
+    for (size_t c = 0; c < S && b0 + c < len; c += 256) {
+        const size_t i = b0 + c + 4 * lane;
+        const uint4 v = ld4(i);
+        const uint32_t t = v.x + v.y + v.z + v.w;
+        const uint32_t inc = wave_incl_scan(t, lane);
+        uint32_t e = carry + inc - t;
+        if (i < len) out[i] = e;
+        e += v.x;
+        if (i + 1 < len) out[i + 1] = e;
+        e += v.y;
+        if (i + 2 < len) out[i + 2] = e;
+        e += v.z;
+        if (i + 3 < len) out[i + 3] = e;
+        carry += (uint32_t)__shfl(inc, 63);
+    }
+    if (threadIdx.x == 0) {
+        out[len] = total;
+        if (counters) counters[0] = total;
     }
 }
 
@@ -1014,6 +1121,7 @@ struct MergeMeta {
     uint32_t* tpre;  // cap + 1
     uint32_t* done;  // cap * kMaxPasses
     uint32_t cap;
+    uint32_t cap_big; // entries of the big-segment list (nbig[0] never exceeds it)
 };
 constexpr uint32_t kMetaHdr = 64;
 
@@ -1095,7 +1203,10 @@ __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* uns
     __shared__ uint32_t sb[kMidThreads], sn[kMidThreads], sst[kMidThreads + 1];
     __shared__ uint32_t ws[kMidThreads / 64];
     __shared__ uint32_t hp[kMaxPasses + 1], cur[kMaxPasses + 1], s_part[kMaxPasses], s_ns;
-    const uint32_t nb = *nbig, tid = threadIdx.x, grid = gridDim.x;
+    // the list holds at most one entry per destination (cap_big): a count
+    // above it is a fault of an earlier stage, reported, never followed
+    const uint32_t nb_raw = nbig[0], tid = threadIdx.x, grid = gridDim.x;
+    const uint32_t nb = nb_raw <= mm.cap_big ? nb_raw : 0u;
     uint32_t base = 0;
     for (uint32_t qb = 0; qb < nb; qb += kMidThreads) {
         const uint32_t q = qb + tid;
@@ -1150,7 +1261,7 @@ __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* uns
         // this round's fault word: spin-limit hits of the merge (counted by
         // k_segsort_merge) and the metadata overflow bit (cannot happen: cap
         // covers n / (kChunk + 1)); read back by the host (ws_faults)
-        mm.hdr[3] = acc > mm.cap ? 0x80000000u : 0u;
+        mm.hdr[3] = (acc > mm.cap ? 0x80000000u : 0u) | ((nbig[2] | (nb_raw > mm.cap_big ? kFaultBigCap : 0u)) << 24);
         // segments taking part in pass p: those with more than p passes
         uint32_t part = 0;
         for (int p = (int)kMaxPasses - 1; p >= 0; p--) {
@@ -1432,15 +1543,41 @@ __global__ __launch_bounds__(256) void k_hist_slab(const ShdDeliv* __restrict__ 
 // to the bitonic-in-HBM list.  With a slab (the "slab" pipeline) segment d's
 // events are read from slab[d * kSlab ...]; a larger segment first copies its
 // kSlab slab slots to the front of its staging range scr[off[d] ...].
+//
+// Slab pipeline, fused form (ovf != nullptr): the overflow events (slots >=
+// kSlab of the listed segments, disjoint from the slab slots copied here) are
+// placed by the same launch, as k_place_ovf would.  Guards (cheap, always on):
+// an overflow event whose destination or slot falls outside its segment, or
+// an overflow count above the list's capacity, is not stored and sets a bit
+// of the round's fault word (nbig[2]), which the host reads back (-EIO).
 __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr, const uint32_t* __restrict__ off,
                                                      uint32_t H, uint32_t host_lo, ShdDeliv* __restrict__ out,
                                                      uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
                                                      uint32_t rsort, uint32_t flo, uint32_t fhi,
                                                      const ShdDeliv* __restrict__ slab, uint32_t slab_rm,
-                                                     uint32_t lds_keys) {
+                                                     uint32_t lds_keys, const ShdDeliv* __restrict__ ovf,
+                                                     uint32_t ovf_cap, uint32_t scr_cap) {
     const int lane = threadIdx.x & 63;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    if (ovf) {
+        // overflow events first: the listed segments' k_segsort_mid runs
+        // after this launch, so the order inside the launch is free
+        const uint32_t m = nbig[1];
+        const uint32_t top = off[H];
+        uint32_t flag = m > ovf_cap ? kFaultOvfCap : 0u;
+        if (top > scr_cap) flag |= kFaultOff;
+        for (uint32_t i = wave * 64 + lane; !flag && i < m; i += nwaves * 64) {
+            const ShdDeliv r = ld_ev(&ovf[i]);
+            const uint32_t d = r.dst_host - host_lo;
+            if (d >= H || r.pad < kSlab || r.pad >= off[d + 1] - off[d]) {
+                flag |= kFaultOvfRange;
+                break;
+            }
+            st_ev(&scr[off[d] + r.pad], r);
+        }
+        if (flag) atomicOr(nbig + 2, flag);
+    }
     // per-wave pass-1 key array of the rank sort (SHD_SEGSORT_LDS=0: readlanes)
     __shared__ unsigned long long keys[4][64 * 4 + 8];
     unsigned long long* lk = lds_keys ? keys[threadIdx.x >> 6] : nullptr;
@@ -1454,13 +1591,101 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
                 sort_segment(rsort, slab, base, nullptr, n, dh, out, b, lane, stride, lk);
             } else {
                 for (uint32_t i = lane; i < kSlab; i += 64) st_ev(&scr[b + i], ld_ev(&slab[base + (size_t)i * stride]));
-                if (lane == 0) big[atomicAdd(nbig, 1u)] = d;
+                if (lane == 0) {
+                    const uint32_t k = atomicAdd(nbig, 1u);
+                    if (k < H) big[k] = d;
+                    else atomicOr(nbig + 2, kFaultBigCap);
+                }
             }
         } else if (n <= (uint32_t)kSmallSeg) {
             sort_segment(rsort, scr, b, nullptr, n, dh, out, b, lane, 1u, lk);
         } else if (lane == 0) {
-            big[atomicAdd(nbig, 1u)] = d;
+            const uint32_t k = atomicAdd(nbig, 1u);
+            if (k < H) big[k] = d;
+            else atomicOr(nbig + 2, kFaultBigCap);
         }
+    }
+}
+
+// ---- multi-GPU regroup from destination-sorted runs ----
+// After the destination-owner exchange, the W blocks a rank receives are
+// each already grouped by destination and in event_compare order inside
+// every destination (the senders' rounds sorted them).  rofs[k * (Hr + 1) +
+// d] is destination d's start inside block k (relative to the block, which
+// starts at bbase[k] in `in`).  The regroup reads the runs in place: no
+// scatter into destination slabs, only the per-destination union of W runs.
+constexpr uint32_t kMaxRuns = 64; // = xchg.hip kMaxWorld
+
+__global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__ rofs, uint32_t W, uint32_t Hr,
+                                                    uint32_t* __restrict__ cnt) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < Hr; d += gridDim.x * blockDim.x) {
+        uint32_t c = 0;
+        for (uint32_t k = 0; k < W; k++) c += rofs[(size_t)k * (Hr + 1) + d + 1] - rofs[(size_t)k * (Hr + 1) + d];
+        cnt[d] = c;
+    }
+}
+
+// One wave per destination: its W runs (a run table in LDS: segment-local
+// start and source index of each run) are read as one segment and ranked
+// like a slab segment; segments above kSmallSeg events are copied to their
+// final range of the staging array and listed for k_segsort_mid / _merge.
+__global__ __launch_bounds__(256) void k_runs_sort(const ShdDeliv* __restrict__ in, const uint32_t* __restrict__ rofs,
+                                                   const uint32_t* __restrict__ bbase, uint32_t W, uint32_t Hr,
+                                                   const uint32_t* __restrict__ off, uint32_t host_lo,
+                                                   ShdDeliv* __restrict__ out, ShdDeliv* __restrict__ scr,
+                                                   uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
+                                                   uint32_t lds_keys) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    __shared__ unsigned long long keys[4][64 * 4 + 8];
+    __shared__ uint32_t rs_all[4][kMaxRuns + 1], rb_all[4][kMaxRuns];
+    uint32_t* rs = rs_all[wv];
+    uint32_t* rb = rb_all[wv];
+    unsigned long long* lk = lds_keys ? keys[wv] : nullptr;
+    for (uint32_t d = wave; d < Hr; d += nwaves) {
+        const uint32_t o = off[d], n = off[d + 1] - o;
+        if (n == 0) continue;
+        uint32_t len = 0, src = 0;
+        if ((uint32_t)lane < W) {
+            const uint32_t a = rofs[(size_t)lane * (Hr + 1) + d];
+            len = rofs[(size_t)lane * (Hr + 1) + d + 1] - a;
+            src = bbase[lane] + a;
+        }
+        const uint32_t inc = wave_incl_scan(len, lane);
+        if ((uint32_t)lane < W) {
+            rs[lane] = inc - len;
+            rb[lane] = src;
+        }
+        if (lane == 0) rs[W] = n;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        auto at = [&](uint32_t i) { // source index of segment element i (i < n)
+            uint32_t k = 0;
+            while (rs[k + 1] <= i) k++;
+            return rb[k] + (i - rs[k]);
+        };
+        if (n <= (uint32_t)kSmallSeg) {
+            auto load = [&](uint32_t i) {
+                const ShdDeliv r = ld_ev(&in[at(i)]);
+                return Ev{r.time, r.seq, r.src_host, r.pkt_index};
+            };
+            if (n <= 64) wave_rank_segment<1>(load, n, d + host_lo, out, o, lane, lk);
+            else if (n <= 128) wave_rank_segment<2>(load, n, d + host_lo, out, o, lane, lk);
+            else wave_rank_segment<4>(load, n, d + host_lo, out, o, lane, lk);
+        } else {
+            for (uint32_t i = lane; i < n; i += 64) st_ev(&scr[o + i], ld_ev(&in[at(i)]));
+            if (lane == 0) {
+                const uint32_t k = atomicAdd(nbig, 1u);
+                if (k < Hr) big[k] = d;
+                else atomicOr(nbig + 2, kFaultBigCap);
+            }
+        }
+        // the run table is rewritten for the next destination
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 }
 
@@ -1583,6 +1808,7 @@ int slab_reserve(Ws& w, uint32_t H) {
 
 MergeMeta merge_meta(const Ws& w) {
     MergeMeta m;
+    m.cap_big = w.cap_h;
     m.hdr = w.meta;
     m.seg = reinterpret_cast<uint4*>(w.meta + kMetaHdr);
     m.tpre = w.meta + kMetaHdr + 4ull * w.cap_meta;
@@ -1632,8 +1858,13 @@ int ws_faults(Ws& w, bool completed) {
     const uint32_t f = __atomic_load_n(w.fault, __ATOMIC_ACQUIRE);
     if (!f) return 0;
     *w.fault = 0;
-    return shd_fail(-EIO, "segment merge fault word %#x in a previous round (%u spin-limit hits%s)", f,
-                    f & 0x7fffffffu, (f & 0x80000000u) ? ", metadata overflow" : "");
+    const uint32_t g = (f >> 24) & 0x7fu;
+    return shd_fail(-EIO, "round fault word %#x in a previous round (%u merge spin-limit hits%s%s%s%s%s)", f,
+                    f & 0xffffffu, (f & 0x80000000u) ? ", merge metadata overflow" : "",
+                    (g & kFaultOvfRange) ? ", overflow event outside its segment" : "",
+                    (g & kFaultOvfCap) ? ", overflow count above its list" : "",
+                    (g & kFaultBigCap) ? ", big-segment list full" : "",
+                    (g & kFaultOff) ? ", offsets above the staging area" : "");
 }
 
 unsigned grid_for(size_t n, unsigned block, unsigned cap) {
@@ -1702,6 +1933,67 @@ int make_bucketing(uint32_t host_lo, uint32_t H, size_t n, Bucketing* out) {
     return 0;
 }
 
+// SHD_DEBUG_SYNC=1: synchronise after each stage of a round and name the
+// stage whose kernels failed; print the workspace and argument ranges once
+// per round and fail on an overlap (diagnostics; asynchronous otherwise)
+bool debug_sync() {
+    static const bool on = [] {
+        const char* v = getenv("SHD_DEBUG_SYNC");
+        return v && strcmp(v, "1") == 0;
+    }();
+    return on;
+}
+int dbg_sync(hipStream_t s, const char* stage) {
+    if (!debug_sync()) return 0;
+    const hipError_t e = hipStreamSynchronize(s);
+    return e == hipSuccess ? 0 : shd_fail(-EIO, "stage %s: %s", stage, hipGetErrorString(e));
+}
+int dbg_ranges(const Ws& w, const void* status, size_t n, const void* out, const void* offsets, uint32_t H) {
+    if (!debug_sync()) return 0;
+    struct R {
+        const char* name;
+        uintptr_t lo, hi;
+    } r[] = {{"ws.tmp", (uintptr_t)w.tmp, (uintptr_t)(w.tmp + w.cap_n)},
+             {"ws.st1", (uintptr_t)w.st1, (uintptr_t)(w.st1 + w.cap_n)},
+             {"ws.st2", (uintptr_t)w.st2, (uintptr_t)(w.st2 + w.cap_n)},
+             {"ws.cnt1", (uintptr_t)w.cnt1, (uintptr_t)(w.cnt1 + w.cap_m)},
+             {"ws.big", (uintptr_t)w.big, (uintptr_t)(w.big + w.cap_h)},
+             {"ws.nbig", (uintptr_t)w.nbig, (uintptr_t)(w.nbig + 4)},
+             {"ws.slab", (uintptr_t)w.slab, (uintptr_t)(w.slab + w.cap_slab)},
+             {"status", (uintptr_t)status, (uintptr_t)status + n},
+             {"out", (uintptr_t)out, (uintptr_t)out + n * sizeof(ShdDeliv)},
+             {"offsets", (uintptr_t)offsets, (uintptr_t)offsets + 4ull * (H + 1)}};
+    const int k = (int)(sizeof r / sizeof r[0]);
+    for (int i = 0; i < k; i++) fprintf(stderr, "[shd debug] %-8s %#lx..%#lx\n", r[i].name, (unsigned long)r[i].lo,
+                                        (unsigned long)r[i].hi);
+    for (int i = 0; i < k; i++)
+        for (int j = i + 1; j < k; j++)
+            if (r[i].lo && r[j].lo && r[i].lo < r[j].hi && r[j].lo < r[i].hi && r[i].hi > r[i].lo && r[j].hi > r[j].lo)
+                return shd_fail(-EIO, "debug: %s overlaps %s", r[i].name, r[j].name);
+    return 0;
+}
+
+// SHD_ROUND_FUSE=0: the three-launch scan and a separate overflow placement
+// launch (the launch count before the fused forms; parity-tested)
+bool round_fuse() {
+    const char* v = getenv("SHD_ROUND_FUSE");
+    return !(v && strcmp(v, "0") == 0);
+}
+
+// exclusive scan of len counts into out (out[len] = total; counters[0] = total)
+void scan_counts(const uint32_t* in, size_t len, uint32_t* out, uint32_t* bsum, unsigned long long* counters,
+                 hipStream_t s) {
+    if (len <= kScanOneMax && round_fuse()) {
+        hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(1024), 0, s, in, len, out, counters);
+        return;
+    }
+    const uint32_t nb = (uint32_t)((len + kScanTile - 1) / kScanTile);
+    hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, in, len, out, bsum);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, bsum, nb);
+    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(len + 1, 256, 1u << 30)), dim3(256), 0, s, out, len, bsum, nb,
+                       counters);
+}
+
 // ---- optional per-stage timing with HIP events on the launch stream ----
 constexpr int kStages = 4; // 0 packet-scatter, 1 scan, 2 placement, 3 per-bucket / per-destination sort
 constexpr int kMaxTimed = 1024;
@@ -1722,11 +2014,7 @@ void mark(int stage, hipStream_t s) {
 int group_and_sort(Ws& w, const ShdDeliv* in, const uint8_t* status, const uint32_t* rank, size_t n, const Bucketing& bk,
                    ShdDeliv* out, uint32_t* offsets, unsigned long long* counters, hipStream_t s) {
     const size_t m = (size_t)bk.nb * bk.ntiles;
-    const uint32_t nb = (uint32_t)((m + kScanTile - 1) / kScanTile);
-    hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, w.cnt1, m, w.off1, w.bsum);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, w.bsum, nb);
-    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m + 1, 256, 1u << 30)), dim3(256), 0, s, w.off1, m, w.bsum,
-                       nb, counters);
+    scan_counts(w.cnt1, m, w.off1, w.bsum, counters, s);
     mark(2, s);
     if (staged_partition()) {
         // parts of 2^pshift buckets, at most kPartsTarget of them
@@ -1761,22 +2049,24 @@ int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const 
                         uint32_t host_lo, uint32_t H, ShdDeliv* out, uint32_t* offsets,
                         unsigned long long* counters, hipStream_t s, const ShdDeliv* slab = nullptr,
                         uint32_t slab_rm = 0) {
-    const uint32_t nb = (uint32_t)((H + kScanTile - 1) / kScanTile);
-    hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, w.cnt1, (size_t)H, offsets, w.bsum);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, w.bsum, nb);
-    hipLaunchKernelGGL(k_scan_add, dim3(grid_for((size_t)H + 1, 256, 1u << 30)), dim3(256), 0, s, offsets, (size_t)H,
-                       w.bsum, nb, counters);
+    scan_counts(w.cnt1, (size_t)H, offsets, w.bsum, counters, s);
+    if (int rc = dbg_sync(s, "scan")) return rc;
     mark(2, s);
-    if (slab)
+    const bool fuse = slab && round_fuse();
+    if (slab && !fuse)
         hipLaunchKernelGGL(k_place_ovf, dim3(512), dim3(256), 0, s, w.st2, w.nbig + 1, offsets, host_lo,
                            w.st1);
-    else if (n)
+    else if (!slab && n)
         hipLaunchKernelGGL(k_place_rank, dim3(grid_for(n, 256 * kBatch, 1u << 20)), dim3(256), 0, s, in, status, rank,
                            n, host_lo, H, offsets, w.st1, 0u, H);
+    if (int rc = dbg_sync(s, "place")) return rc;
     mark(3, s);
     hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, w.st1, offsets, H, host_lo, out,
-                       w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm, lds_keys());
+                       w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm, lds_keys(), fuse ? w.st2 : nullptr,
+                       (uint32_t)w.cap_n, (uint32_t)w.cap_n);
+    if (int rc = dbg_sync(s, "k_segsort_dst")) return rc;
     if (int rc = sort_listed(w, w.st1, offsets, out, s)) return rc;
+    if (int rc = dbg_sync(s, "k_segsort_mid + k_segsort_merge")) return rc;
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort_rank launch");
@@ -1847,6 +2137,37 @@ extern "C" void shd_dev_ws_free(void* p) {
     delete w;
 }
 
+// ---- packet-path table (see kPtabFallback) ----
+namespace {
+__device__ __forceinline__ uint2 ptab_entry(const ShdEntry e) {
+    const double d = ceil(e.lat * 1000000.0);
+    if (!(e.lat >= 0.0) || !(d < 4294967295.0) || !(e.rel >= 0.0)) return make_uint2(kPtabFallback, 0u);
+    // the largest r in [0, 2^31 - 1] with (double)r / 2147483647.0 <= rel: the
+    // quotient is monotone in r, so start at floor(rel * (2^31 - 1)) and step
+    // to the boundary with the exact test
+    double g = floor(e.rel * 2147483647.0);
+    int64_t r = g < 0.0 ? 0 : (g > 2147483647.0 ? 2147483647 : (int64_t)g);
+    while (r < 2147483647 && (double)(r + 1) / 2147483647.0 <= e.rel) r++;
+    while (r >= 0 && (double)r / 2147483647.0 > e.rel) r--;
+    if (r < 0) return make_uint2(kPtabFallback, 0u);
+    return make_uint2((uint32_t)d, (uint32_t)r);
+}
+__global__ __launch_bounds__(256) void k_ptab_build(const ShdEntry* __restrict__ tab, size_t n, uint2* __restrict__ out) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = ptab_entry(tab[i]);
+}
+
+} // namespace
+
+extern "C" int shd_dev_ptab_build(const ShdEntry* tab, size_t nent, void* d_out, void* stream) {
+    if (!nent) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_ptab_build, dim3(grid_for(nent, 256, 32768)), dim3(256), 0, s, tab, nent,
+                       static_cast<uint2*>(d_out));
+    int rc = hip_status(hipGetLastError(), "k_ptab_build launch");
+    return rc ? rc : hip_status(hipStreamSynchronize(s), "k_ptab_build");
+}
+
 // Grow-only scratch of the multi-GPU exchange (device + pinned host), so a
 // round allocates nothing: hipFree / hipHostFree synchronise the device.
 // Callers run on one stream and synchronise it before returning, so a grow
@@ -1896,7 +2217,8 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     if ((rc = ws_reserve(w, n, m, H))) return rc;
     if (pipe == kSlabPipe && (rc = slab_reserve(w, H))) return rc;
     unsigned long long* counters = (unsigned long long*)d_counters;
-    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 8, s), "memset nbig")) ||
+    if ((rc = dbg_ranges(w, d_status, n, d_out, d_dst_offsets, H))) return rc;
+    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 12, s), "memset nbig")) ||
         (rc = hip_status(hipMemsetAsync(counters, 0xff, 16, s), "memset counters")))
         return rc;
     // rank: per-destination counters start at zero; bucket: every tile writes
@@ -1905,7 +2227,17 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     mark(0, s);
     if (n) {
         const char* sb = getenv("SHD_SCATTER_BATCH");
-        if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
+        const char* pr = getenv("SHD_SCATTER_PROBE");
+        const int probe = pr ? atoi(pr) : 0;
+#define SHD_PROBE_LAUNCH(P)                                                                                        \
+    hipLaunchKernelGGL((k_pkt_scatter<2, kBatch, P>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier, \
+                       end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2, w.nbig + 1)
+        if (pipe == kSlabPipe && probe == 1) SHD_PROBE_LAUNCH(1);
+        else if (pipe == kSlabPipe && probe == 2) SHD_PROBE_LAUNCH(2);
+        else if (pipe == kSlabPipe && probe == 3) SHD_PROBE_LAUNCH(3);
+        else if (pipe == kSlabPipe && probe == 4) SHD_PROBE_LAUNCH(4);
+#undef SHD_PROBE_LAUNCH
+        else if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
             hipLaunchKernelGGL((k_pkt_scatter<2, 8>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
                                end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2,
                                w.nbig + 1);
@@ -1928,6 +2260,7 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     }
     mark(1, s);
     if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
+    if ((rc = dbg_sync(s, "memsets + k_pkt_scatter"))) return rc;
     rc = pipe == kSlabPipe
              ? group_and_sort_rank(w, w.tmp, d_status, nullptr, n, 0, H, d_out, d_dst_offsets, counters, s, w.slab,
                                    bk.slab_rm)
@@ -1983,7 +2316,8 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
     if ((rc = ws_begin(w, s))) return rc;
     if ((rc = ws_reserve(w, n, m, H))) return rc;
     if (pipe == kSlabPipe && (rc = slab_reserve(w, H))) return rc;
-    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 8, s), "memset nbig"))) return rc;
+    if ((rc = dbg_ranges(w, nullptr, 0, d_out, d_dst_offsets, H))) return rc;
+    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 12, s), "memset nbig"))) return rc;
     if ((rk || !n) && (rc = hip_status(hipMemsetAsync(w.cnt1, 0, 4 * m, s), "memset cnt1"))) return rc;
     mark(0, s);
     if (n) {
@@ -2006,5 +2340,41 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
     if (rc) return rc;
     if (stream) return 0;
     if ((rc = hip_status(hipStreamSynchronize(s), "deliv sort"))) return rc;
+    return ws_faults(w, true);
+}
+
+// Regroup of the exchange's W received blocks (see k_runs_count): d_in holds
+// the n events of the blocks back to back (block k from d_bbase[k], a device
+// array of W + 1 prefix counts), d_rofs the W per-block offset arrays over
+// the host range [host_lo, host_hi).  Output as shd_dev_deliv_sort.
+extern "C" int shd_dev_deliv_merge_runs(void* ws, const ShdDeliv* d_in, size_t n, const uint32_t* d_rofs,
+                                        const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi,
+                                        ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (!ws) return shd_fail(-ENOMEM, "no round workspace");
+    if (W < 1 || W > kMaxRuns) return shd_fail(-EINVAL, "%u runs outside 1..%u", W, kMaxRuns);
+    Ws& w = *static_cast<Ws*>(ws);
+    const uint32_t H = host_hi - host_lo;
+    int rc;
+    if ((rc = ws_begin(w, s))) return rc;
+    if ((rc = ws_reserve(w, n, H, H))) return rc; // (st1: staging of the listed segments)
+    if ((rc = dbg_ranges(w, nullptr, 0, d_out, d_dst_offsets, H))) return rc;
+    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 12, s), "memset nbig"))) return rc;
+    mark(0, s);
+    hipLaunchKernelGGL(k_runs_count, dim3(grid_for(H, 256, 4096)), dim3(256), 0, s, d_rofs, W, H, w.cnt1);
+    mark(1, s);
+    scan_counts(w.cnt1, (size_t)H, d_dst_offsets, w.bsum, nullptr, s);
+    mark(2, s);
+    mark(3, s);
+    hipLaunchKernelGGL(k_runs_sort, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_rofs, d_bbase, W, H,
+                       d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
+    if ((rc = hip_status(hipGetLastError(), "k_runs_sort launch"))) return rc;
+    if ((rc = dbg_sync(s, "k_runs_sort"))) return rc;
+    if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s))) return rc;
+    mark(4, s);
+    if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
+    if ((rc = ws_end(w, s))) return rc;
+    if (stream) return 0;
+    if ((rc = hip_status(hipStreamSynchronize(s), "merge runs"))) return rc;
     return ws_faults(w, true);
 }

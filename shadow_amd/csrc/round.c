@@ -162,7 +162,7 @@ static int collect_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_o
         (rc = shd_dev_malloc((void**)&d_status, nn)) || (rc = shd_dev_malloc((void**)&d_cnt, 16)))
         goto done;
     if (n && (rc = shd_dev_h2d(d_recs, t->staged, sizeof(ShdPkt) * n))) goto done;
-    if ((rc = shd_sync_touch(t))) goto done;
+    if ((rc = shd_sync_touch(t)) || (rc = shd_ensure_ptab(t))) goto done;
     ShdPktCtx c;
     shd_pkt_ctx(t, &c);
     rc = shd_dev_packet_round(&c, d_recs, n, t->barrier, t->end_time, t->bootstrap_end, d_out, d_off, d_status,
@@ -313,6 +313,7 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
         c.row_lo = s->lo;
         c.row_hi = s->hi;
         c.idx_base = (uint32_t)pbeg[k];
+        c.ptab = NULL; /* shards decide from their f64 rows */
         rc = shd_dev_packet_round(&c, s->d_recs, nk, t->barrier, t->end_time, t->bootstrap_end, s->d_out, s->d_off,
                                   s->d_status, s->d_cnt, s->stream);
     }
@@ -345,8 +346,29 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
             if (b) rc = shd_dev_d2d(sm->d_recv + at, t->shards[k].d_out + o[lo], sizeof(ShdDeliv) * b);
             at += b;
         }
+        /* the S received blocks are each grouped by destination in
+         * event_compare order: merged as runs (their offsets are on the host) */
+        const size_t nro = (size_t)S * (hi - lo + 1) + (size_t)S + 1;
         if (!rc) rc = shd_dev_init(sm->device);
-        if (!rc) rc = shd_dev_deliv_sort(sm->ws, sm->d_recv, tot, lo, hi, sm->d_fin, sm->d_fin_off, sm->stream);
+        GROW(sm->d_rofs, sm->cap_rofs, nro, sizeof(uint32_t));
+        if (nro > sm->cap_rofs) sm->cap_rofs = nro + nro / 4 + 64;
+        if (!rc) {
+            uint32_t* h = (uint32_t*)malloc(sizeof(uint32_t) * nro);
+            if (!h) rc = -ENOMEM;
+            uint32_t base = 0;
+            for (int k = 0; k < S && !rc; k++) {
+                const uint32_t* o = offk + ((size_t)H + 1) * (size_t)k;
+                for (uint32_t j = 0; j <= hi - lo; j++) h[(size_t)k * (hi - lo + 1) + j] = o[lo + j] - o[lo];
+                h[(size_t)S * (hi - lo + 1) + k] = base;
+                base += o[hi] - o[lo];
+            }
+            if (!rc) h[(size_t)S * (hi - lo + 1) + S] = base;
+            if (!rc) rc = shd_dev_h2d(sm->d_rofs, h, sizeof(uint32_t) * nro);
+            free(h);
+        }
+        if (!rc)
+            rc = shd_dev_deliv_merge_runs(sm->ws, sm->d_recv, tot, sm->d_rofs, sm->d_rofs + (size_t)S * (hi - lo + 1),
+                                          (uint32_t)S, lo, hi, sm->d_fin, sm->d_fin_off, sm->stream);
         if (!rc) rc = shd_dev_stream_sync(sm->stream);
         if (!rc && out && tot) rc = shd_dev_d2h(out + obase, sm->d_fin, sizeof(ShdDeliv) * tot);
         if (!rc && dst_offsets) {
@@ -404,7 +426,7 @@ int shd_round_process_device(ShdTopology* t, const ShdPkt* d_recs, size_t n, uin
     if (!__atomic_load_n(&t->lookups_started, __ATOMIC_RELAXED)) __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
     if (t->nshards > 1) return shd_fail(-ENOTSUP, "a multi-shard table runs its rounds with shd_round_process_shards");
     pthread_mutex_lock(&t->round_mu);
-    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t))) {
+    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t)) && !(rc = shd_ensure_ptab(t))) {
         ShdPktCtx c;
         shd_pkt_ctx(t, &c);
         rc = shd_dev_packet_round(&c, d_recs, n, barrier, end_time, bootstrap_end, d_out, d_dst_offsets, d_status,
@@ -436,6 +458,16 @@ int shd_round_exchange(ShdTopology* t, const ShdTransport* x, const ShdDeliv* d_
         return shd_fail(-EINVAL, "host bounds must cover [0, %u)", t->nhosts);
     int rc = shd_dev_init(t->device);
     if (rc) return rc;
+    const char* runs = getenv("SHD_XCHG_RUNS"); /* 0: regroup by re-scattering (the round-2 form) */
+    if (!(runs && strcmp(runs, "0") == 0)) {
+        pthread_mutex_lock(&t->round_mu);
+        if (!t->ws) rc = shd_dev_ws_new(&t->ws);
+        if (!rc)
+            rc = shd_dev_exchange_runs(t->ws, x, d_events, d_dst_offsets, host_bounds, d_recv, recv_cap, d_out,
+                                       d_out_offsets, n_out, stream);
+        pthread_mutex_unlock(&t->round_mu);
+        return rc;
+    }
     uint64_t* send = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)x->world);
     if (!send) return -ENOMEM;
     size_t nrecv = 0;

@@ -190,6 +190,7 @@ static int adopt(ShdTopology* t, ShdEntry* d_tab, int owned) {
     int rc = shd_dev_d2h(t->h_tab, d_tab, sizeof(ShdEntry) * n);
     if (rc) return rc;
     if (t->d_tab && t->d_tab_owned && t->d_tab != d_tab) shd_dev_free(t->d_tab);
+    shd_ptab_drop(t);
     t->d_tab = d_tab;
     t->d_tab_owned = owned;
     t->tab_row_lo = 0;
@@ -365,6 +366,41 @@ int shd_sync_touch(ShdTopology* t) {
     return rc;
 }
 
+/* SHD_PTAB=0 keeps the rounds on the 16-B f64 entries (A/B measurements). */
+static int ptab_enabled(void) {
+    const char* v = getenv("SHD_PTAB");
+    return !(v && strcmp(v, "0") == 0);
+}
+
+void shd_ptab_drop(ShdTopology* t) {
+    shd_dev_free(t->d_ptab_alloc);
+    t->d_ptab_alloc = t->d_ptab = NULL;
+    t->ptab_unavailable = 0;
+}
+
+/* The rounds' 8-byte form of the resident rows (packet.hip kPtabFallback):
+ * {delay_ns, keep threshold} per entry, converted once per adopted table.
+ * Half the bytes of the random gather's footprint; the f64 table stays for
+ * the lookups.  If the allocation fails, the rounds read the f64 entries. */
+int shd_ensure_ptab(ShdTopology* t) {
+    if (t->d_ptab || t->ptab_unavailable || !t->d_tab || !ptab_enabled()) return 0;
+    const size_t rows = (size_t)(t->tab_row_hi - t->tab_row_lo), A = (size_t)t->A;
+    if (!rows) return 0;
+    void* d = NULL;
+    if (shd_dev_malloc(&d, rows * A * 8)) {
+        t->ptab_unavailable = 1;
+        return 0;
+    }
+    int rc = shd_dev_ptab_build(t->d_tab + (size_t)t->tab_row_lo * A, rows * A, d, NULL);
+    if (rc) {
+        shd_dev_free(d);
+        return rc;
+    }
+    t->d_ptab_alloc = d;
+    t->d_ptab = (char*)d - (ptrdiff_t)((size_t)t->tab_row_lo * A * 8);
+    return 0;
+}
+
 void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->tab = t->d_tab;
     c->A = t->A;
@@ -376,6 +412,7 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->row_lo = t->tab_row_lo;
     c->row_hi = t->tab_row_hi;
     c->idx_base = 0;
+    c->ptab = ptab_enabled() ? t->d_ptab : NULL;
     if (!t->ws) shd_dev_ws_new(&t->ws); /* (a failure leaves ws NULL: the launch reports -ENOMEM) */
     c->ws = t->ws;
 }

@@ -123,7 +123,13 @@ typedef struct {
     void* ws;                  /* the topology's device workspace (shd_dev_ws_new) */
     int row_lo, row_hi;        /* rows of tab present (a shard: others are never read) */
     uint32_t idx_base;         /* added to the record index an event carries (pkt_index) */
+    const void* ptab;          /* NULL or the 8-B packet-path table {delay_ns, keep threshold} indexed as tab */
 } ShdPktCtx;
+
+/* The 8-B packet-path table of nent entries of tab ({u32 delay_ns =
+ * ceil(lat * 1e6), u32 keep threshold over the 31-bit rand_r output}, or a
+ * fallback mark where the f64 entry must decide) into d_out; synchronous. */
+int shd_dev_ptab_build(const ShdEntry* tab, size_t nent, void* d_out, void* stream);
 
 /* Round-pipeline workspace (grow-only device buffers + the event that marks
  * the end of its last use), one per topology; callers serialise its use. */
@@ -137,6 +143,14 @@ int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uin
                          uint8_t* d_status, uint64_t* d_counters, void* stream);
 int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                        uint32_t* d_dst_offsets, void* stream);
+/* The same regroup from W received blocks that are each grouped by
+ * destination in event_compare order (the exchange's output): block k starts
+ * at event d_bbase[k] of d_in (W + 1 prefix counts, device), d_rofs holds
+ * per block the (host_hi - host_lo + 1) destination offsets relative to the
+ * block.  No scatter: the runs are read in place. */
+int shd_dev_deliv_merge_runs(void* ws, const ShdDeliv* d_in, size_t n, const uint32_t* d_rofs, const uint32_t* d_bbase,
+                             uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out, uint32_t* d_dst_offsets,
+                             void* stream);
 
 /* out[i] = tab[idx[i]] for n entries (device pointers; synchronous; on the
  * calling thread's device) */
@@ -148,6 +162,11 @@ int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPk
                           size_t* n_recv, void* stream);
 int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const uint32_t* host_bounds, int world,
                        uint64_t* send_elems, void* stream);
+/* shd_round_exchange's default form: events + per-destination run offsets to
+ * every owner, regrouped there by shd_dev_deliv_merge_runs; synchronous */
+int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdDeliv* d_events, const uint32_t* d_dst_offsets,
+                          const uint32_t* host_bounds, ShdDeliv* d_recv, size_t recv_cap, ShdDeliv* d_out,
+                          uint32_t* d_out_offsets, size_t* n_out, void* stream);
 int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
                             void* d_recv, size_t recv_cap, size_t* n_recv, void* stream);
 

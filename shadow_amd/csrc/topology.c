@@ -1325,6 +1325,7 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
 /* ------------------------------------------------------------------ */
 
 void shd_shards_clear(ShdTopology* t) {
+    shd_ptab_drop(t); /* (every re-adoption and the teardown pass here) */
     for (int k = 0; k < t->nshards; k++) {
         ShdShard* s = &t->shards[k];
         shd_dev_init(s->device);
@@ -1341,6 +1342,7 @@ void shd_shards_clear(ShdTopology* t) {
         shd_dev_free(s->d_off);
         shd_dev_free(s->d_fin_off);
         shd_dev_free(s->d_cnt);
+        shd_dev_free(s->d_rofs);
         shd_dev_stream_free(s->stream);
         pthread_mutex_destroy(&s->mu);
         memset(s, 0, sizeof *s);

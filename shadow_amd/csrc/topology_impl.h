@@ -66,7 +66,8 @@ typedef struct {
     uint8_t* d_status;
     uint32_t *d_off, *d_fin_off;
     uint64_t* d_cnt;
-    size_t cap_n, cap_r;
+    uint32_t* d_rofs; /* regroup: per source shard the rebased destination offsets + block bases */
+    size_t cap_n, cap_r, cap_rofs;
     uint32_t cap_h;
 } ShdShard;
 
@@ -116,6 +117,11 @@ struct ShdTopology {
 
     /* device state */
     ShdEntry* d_tab;
+    /* 8-B packet-path form of the resident rows of d_tab (shd_ensure_ptab),
+     * indexed like d_tab (d_ptab = allocation - tab_row_lo * A entries) */
+    void* d_ptab;
+    void* d_ptab_alloc;
+    int ptab_unavailable; /* the allocation failed: rounds read d_tab */
     int32_t *d_inc_off, *d_inc_nbr, *d_slot_vertex, *d_vertex_slot;
     uint32_t* d_host_info; /* nhosts x {slot, touch[slot]} for the packet kernel */
     uint32_t* h_host_info;
@@ -175,6 +181,10 @@ int shd_count_packet_locked(ShdTopology* t, int oi, int oj, uint64_t inc);
 int shd_count_reserve_locked(ShdTopology* t, uint64_t more);
 int shd_sync_touch(ShdTopology* t);
 void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c);
+/* builds the packet-path table of the resident rows if there is none
+ * (caller holds round_mu); a failed allocation leaves the f64 path */
+int shd_ensure_ptab(ShdTopology* t);
+void shd_ptab_drop(ShdTopology* t);
 int shd_ensure_routes(ShdTopology* t);
 
 #endif

@@ -138,7 +138,7 @@ int make_args(const uint32_t* bounds, int world, RouteArgs* ra) {
 
 // all-to-all of per-peer element counts, then of the blocks themselves
 int exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
-                    void* d_recv, size_t recv_cap, size_t* n_recv, hipStream_t s) {
+                    void* d_recv, size_t recv_cap, size_t* n_recv, hipStream_t s, uint64_t* recv_out = nullptr) {
     const int W = x->world;
     std::vector<uint64_t> recv_elems(W), sb(W), rb(W);
     int rc = x->alltoall_u64(x->user, send_elems, recv_elems.data());
@@ -163,7 +163,23 @@ int exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* s
     rc = x->alltoallv(x->user, d_send, sb.data(), d_recv, rb.data(), (void*)s);
     if (rc) return rc < 0 ? rc : -EIO;
     *n_recv = (size_t)total;
+    if (recv_out)
+        for (int r = 0; r < W; r++) recv_out[r] = recv_elems[r];
     return 0;
+}
+
+// Peer r's slice of this rank's destination offsets, rebased to its block:
+// out[lo_r + r + j] = off[lo_r + j] - off[lo_r], j = 0 .. H_r (the slices of
+// all peers back to back: sum of (H_r + 1) = H + W entries).
+__global__ __launch_bounds__(256) void k_offset_slices(const uint32_t* __restrict__ off, RouteArgs ra,
+                                                       uint32_t* __restrict__ out) {
+    const uint32_t total = ra.bounds[ra.world] + (uint32_t)ra.world;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
+        int r = 0;
+        while (r + 1 < ra.world && p >= ra.bounds[r + 1] + (uint32_t)(r + 1)) r++;
+        const uint32_t lo = ra.bounds[r], j = p - lo - (uint32_t)r;
+        out[p] = off[lo + j] - off[lo];
+    }
 }
 
 // ---- RCCL transport ----
@@ -306,6 +322,67 @@ extern "C" int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const
     if (!rc)
         for (int r = 0; r < world; r++) send_elems[r] = cuts[r + 1] - cuts[r];
     return rc;
+}
+
+// Destination-owner exchange + regroup by runs (shd_round_exchange): the
+// events of each peer's destinations and, beside them, the rebased
+// per-destination offsets of that block; the owner then merges the W
+// destination-sorted runs in place (shd_dev_deliv_merge_runs) instead of
+// scattering every received event into destination slabs again.  One
+// device scratch: [H + W slices | W x (H_me + 1) received offsets | W + 1
+// block bases]; its pinned host side carries the cuts and the block bases.
+extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdDeliv* d_events,
+                                     const uint32_t* d_dst_offsets, const uint32_t* host_bounds, ShdDeliv* d_recv,
+                                     size_t recv_cap, ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out,
+                                     void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int W = x->world, me = x->rank;
+    RouteArgs ra;
+    int rc = make_args(host_bounds, W, &ra);
+    if (rc) return rc;
+    const uint32_t H = host_bounds[W], lo = host_bounds[me], hi = host_bounds[me + 1], Hm = hi - lo;
+    const size_t n_sl = (size_t)H + W, n_ro = (size_t)W * (Hm + 1);
+    const size_t dev_words = (kMaxWorld + 1) + n_sl + n_ro + (W + 1);
+    void *dscr = nullptr, *hscr = nullptr;
+    if ((rc = shd_dev_ws_scratch(ws, 4 * dev_words, 4 * (2 * kMaxWorld + 2), &dscr, &hscr))) return rc;
+    uint32_t* d_cuts = static_cast<uint32_t*>(dscr);
+    uint32_t* d_sl = d_cuts + (kMaxWorld + 1);
+    uint32_t* d_ro = d_sl + n_sl;
+    uint32_t* d_bb = d_ro + n_ro;
+    uint32_t* h_cuts = static_cast<uint32_t*>(hscr);
+    uint32_t* h_bb = h_cuts + (kMaxWorld + 1);
+    // cuts of the events at the owners' host bounds, and the offset slices
+    hipLaunchKernelGGL(k_cuts, dim3(1), dim3(kMaxWorld + 1), 0, s, d_dst_offsets, ra, d_cuts);
+    hipLaunchKernelGGL(k_offset_slices, dim3((unsigned)((n_sl + 255) / 256 < 4096 ? (n_sl + 255) / 256 : 4096)),
+                       dim3(256), 0, s, d_dst_offsets, ra, d_sl);
+    if ((rc = hip_status(hipGetLastError(), "exchange cuts launch"))) return rc;
+    if ((rc = hip_status(hipMemcpyAsync(h_cuts, d_cuts, 4 * (size_t)(W + 1), hipMemcpyDeviceToHost, s), "cuts D2H")) ||
+        (rc = hip_status(hipStreamSynchronize(s), "cuts sync")))
+        return rc;
+    std::vector<uint64_t> send(W), recv(W), sb(W), rb(W);
+    for (int r = 0; r < W; r++) send[r] = h_cuts[r + 1] - h_cuts[r];
+    size_t nrecv = 0;
+    // the events (the capacity verdict is collective inside)
+    if ((rc = exchange_blocks(x, d_events + h_cuts[0], send.data(), sizeof(ShdDeliv), d_recv, recv_cap, &nrecv, s,
+                              recv.data())))
+        return rc;
+    // the offset slices: H_r + 1 words to peer r, H_me + 1 from each peer
+    for (int r = 0; r < W; r++) {
+        sb[r] = 4ull * (host_bounds[r + 1] - host_bounds[r] + 1);
+        rb[r] = 4ull * (Hm + 1);
+    }
+    rc = x->alltoallv(x->user, d_sl, sb.data(), d_ro, rb.data(), (void*)s);
+    if (rc) return rc < 0 ? rc : -EIO;
+    h_bb[0] = 0;
+    for (int r = 0; r < W; r++) h_bb[r + 1] = h_bb[r] + (uint32_t)recv[r];
+    if ((rc = hip_status(hipMemcpyAsync(d_bb, h_bb, 4 * (size_t)(W + 1), hipMemcpyHostToDevice, s), "bases H2D")))
+        return rc;
+    if ((rc = shd_dev_deliv_merge_runs(ws, d_recv, nrecv, d_ro, d_bb, (uint32_t)W, lo, hi, d_out, d_out_offsets,
+                                       stream)))
+        return rc;
+    if ((rc = hip_status(hipStreamSynchronize(s), "exchange runs"))) return rc;
+    *n_out = nrecv;
+    return 0;
 }
 
 extern "C" int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems,

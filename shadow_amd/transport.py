@@ -7,8 +7,10 @@ caller.  Shadow's C host plugs in RCCL
 Python transports wrap ``torch.distributed`` for tests and the benchmark:
 ``TorchTransport`` runs the all-to-all(v) on device tensors with the
 "nccl" backend (RCCL) or bounces the blocks through host memory with "gloo".
-Device buffers handed to the C calls must be registered (``register``) so
-that the callbacks can find the tensors behind the raw pointers.
+Device buffers handed to the C calls are found among the registered tensors
+(``register``) by address; anything else (the library's own scratch, e.g. the
+per-destination run offsets of the exchange) is staged through a temporary
+tensor with ``shd_memcpy``.
 """
 from __future__ import annotations
 
@@ -55,6 +57,23 @@ class TorchTransport:
             raise KeyError(f"device buffer {ptr:#x} was not registered with the transport")
         return self._bufs[ptr]
 
+    def _find(self, ptr: int, nbytes: int):
+        """The registered tensor bytes [ptr, ptr + nbytes) live in, or None
+        (a library-owned scratch buffer, staged through a tensor)."""
+        for base, t in self._bufs.items():
+            if base <= ptr and ptr + nbytes <= base + t.numel():
+                return t[ptr - base:ptr - base + nbytes]
+        return None
+
+    def _stage_in(self, ptr: int, nbytes: int) -> torch.Tensor:
+        v = self._find(ptr, nbytes)
+        if v is not None:
+            return v
+        t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)[:nbytes]
+        if nbytes:
+            check(lib().shd_memcpy(C.c_void_p(t.data_ptr()), C.c_void_p(ptr), nbytes))
+        return t
+
     def _alltoall_u64(self, _user, send, recv):
         try:
             s = torch.tensor([send[r] for r in range(self.world)], dtype=torch.int64, device=self.cdev)
@@ -71,8 +90,13 @@ class TorchTransport:
         try:
             sb = [int(send_bytes[r]) for r in range(self.world)]
             rb = [int(recv_bytes[r]) for r in range(self.world)]
-            src = self._buf(d_send)[:sum(sb)]
-            dst = self._buf(d_recv)[:sum(rb)]
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)  # the library's stream wrote the send side
+            src = self._stage_in(d_send, sum(sb))
+            dst = self._find(d_recv, sum(rb))
+            staged = dst is None
+            if staged:
+                dst = torch.empty(max(sum(rb), 1), dtype=torch.uint8, device=self.device)[:sum(rb)]
             if self.backend == "nccl":
                 dist.all_to_all_single(dst, src, rb, sb, group=self.group)
             else:
@@ -81,6 +105,8 @@ class TorchTransport:
                 dst.copy_(out.to(dst.device))
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
+            if staged and sum(rb):
+                check(lib().shd_memcpy(C.c_void_p(d_recv), C.c_void_p(dst.data_ptr()), sum(rb)))
             return 0
         except BaseException as e:
             self.error = e

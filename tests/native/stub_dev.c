@@ -113,6 +113,12 @@ int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_l
     return shd_fail(-ENOSYS, "stub device: no packet kernels");
 }
 
+int shd_dev_deliv_merge_runs(void* ws, const ShdDeliv* d_in, size_t n, const uint32_t* d_rofs, const uint32_t* d_bbase,
+                             uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out, uint32_t* d_dst_offsets,
+                             void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no packet kernels");
+}
+
 int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
                           const uint32_t* row_bounds, ShdPkt* d_scratch, ShdPkt* d_recv, size_t recv_cap,
                           size_t* n_recv, void* stream) {
@@ -122,9 +128,18 @@ int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const uint32_t* 
                        uint64_t* send_elems, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no exchange");
 }
+int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdDeliv* d_events, const uint32_t* d_dst_offsets,
+                          const uint32_t* host_bounds, ShdDeliv* d_recv, size_t recv_cap, ShdDeliv* d_out,
+                          uint32_t* d_out_offsets, size_t* n_out, void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no exchange");
+}
 int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
                             void* d_recv, size_t recv_cap, size_t* n_recv, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no exchange");
+}
+
+int shd_dev_ptab_build(const ShdEntry* tab, size_t nent, void* d_out, void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no packet table");
 }
 
 int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n, ShdEntry* d_out) {

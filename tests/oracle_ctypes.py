@@ -25,6 +25,8 @@ lib = C.CDLL(LIB_PATH)
 u32p = C.POINTER(C.c_uint32)
 u64p = C.POINTER(C.c_uint64)
 
+lib.orc_nic_tie_count.restype = C.c_uint64
+lib.orc_nic_tie_count.argtypes = []
 lib.orc_parse_time_ns.restype = C.c_int64
 lib.orc_parse_time_ns.argtypes = [C.c_char_p]
 lib.orc_parse_bandwidth_bits.restype = C.c_int64

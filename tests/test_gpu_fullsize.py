@@ -3,11 +3,14 @@
 C1: the whole 1,000-vertex complete-graph table (996 x 996 attached slots,
 H = 5,000), ms and ns edge variants, every row bitwise against the oracle's
 igraph-0.8 Dijkstra restatement (topology.c:1578-1814), rows on a thread pool.
+C2: the V = 20k sparse graph with H = 50k hosts (18,339 attached slots), ms
+and ns edge variants: every row of the table bitwise against the oracle.
 C3: 10M packets with uniform, unrestricted senders and destinations over all
 100k hosts on the V = 20k table; the oracle holds the whole 19,870^2 table.
-C4: the V = 100k / H = 200k table built device-resident (120 GB), 66 sampled
-full-length rows bitwise, and a device-resident round whose packets span all
-200k hosts, decided against rows the oracle holds (worker.c:536-576).
+C4: the V = 100k / H = 200k table built device-resident (120 GB), 1,027
+sampled full-length rows bitwise, and a device-resident round whose packets
+span all 200k hosts, decided against rows the oracle holds
+(worker.c:536-576).
 """
 import numpy as np
 import pytest
@@ -58,6 +61,42 @@ def test_c1_full_table_bit_exact(ns):
     olat, orel = orc.rows_parallel(sv, sv)
     bad = np.flatnonzero((bits(lat) != bits(olat)).any(1) | (bits(rel) != bits(orel)).any(1))
     assert len(bad) == 0, f"{len(bad)} rows differ, first {bad[:5]}"
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("ns", [False, True], ids=["ms", "ns"])
+def test_c2_full_table_bit_exact(ns):
+    """configs[2]: the V = 20k sparse graph with 50k hosts; every one of the
+    18,339 rows of the slab-kernel table against the oracle's Dijkstra
+    (compared in blocks of 2,048 rows, oracle rows on 16 threads)."""
+    import time
+
+    import torch
+    H, V = 50_000, 20_000
+    gml = synth.sparse_graph_gml(V, 0x5EED0002, ns_variant=ns)
+    top = Topology(gml)
+    ips, st, verts = scenario.register_hosts(top, H, seed=1)
+    A = top.slot_count()
+    sv = np.unique(verts).astype(np.int32)
+    assert len(sv) == A and A > 18_000
+    full = torch.empty(A * A * 2, dtype=torch.float64, device="cuda")
+    top.build_rows_device(0, A, full.data_ptr())
+    torch.cuda.synchronize()
+    orc = O.OracleTopology(gml)
+    _, st2, verts2 = scenario.register_hosts(orc, H, seed=1)
+    assert (verts == verts2).all() and (st == st2).all()
+    t0 = time.perf_counter()
+    bad = []
+    for b in range(0, A, 2048):
+        rows = np.arange(b, min(A, b + 2048))
+        got = full.view(A, A, 2)[b:b + len(rows)].cpu().numpy()
+        olat, orel = orc.rows_parallel(sv[rows], sv, 16)
+        diff = (bits(got[:, :, 0]) != bits(olat)).any(1) | (bits(got[:, :, 1]) != bits(orel)).any(1)
+        bad += [int(x) for x in rows[diff]]
+        print(f"[c2] rows {b}..{b + len(rows)} of {A} compared ({time.perf_counter() - t0:.1f}s)", flush=True)
+    assert not bad, f"{len(bad)} rows differ, first {bad[:8]}"
+    del full
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.timeout(500)
@@ -116,7 +155,7 @@ def c4():
     orc = O.OracleTopology(gml)
     ips_o, _, verts_o = scenario.register_hosts(orc, H, seed=1)
     assert (verts == verts_o).all()
-    rows = np.unique(np.r_[np.linspace(0, A - 1, 64).astype(np.int64), 0, 1, A - 1])
+    rows = np.unique(np.r_[np.linspace(0, A - 1, 1024).astype(np.int64), 0, 1, A - 1])
     got = full.view(A, A, 2)[torch.from_numpy(rows).cuda()].cpu().numpy()
     yield dict(top=top, orc=orc, ips=ips_o, st=st, verts=verts, sv=sv, A=A, H=H, rows=rows, got=got, full=full)
     del full
@@ -125,10 +164,10 @@ def c4():
 
 @pytest.mark.timeout(400)
 def test_c4_sampled_rows_bit_exact(c4):
-    """66 full-length rows (first, last and 64 evenly spaced) of the 86k x 86k
-    slab-kernel table against the oracle's Dijkstra."""
+    """1,027 full-length rows (first, second, last and 1,024 evenly spaced) of
+    the 86k x 86k slab-kernel table against the oracle's Dijkstra."""
     sv, rows, got = c4["sv"], c4["rows"], c4["got"]
-    olat, orel = c4["orc"].rows_parallel(sv[rows], sv)
+    olat, orel = c4["orc"].rows_parallel(sv[rows], sv, 16)
     bad = [int(rows[i]) for i in range(len(rows))
            if not (np.array_equal(bits(got[i, :, 0]), bits(olat[i])) and np.array_equal(bits(got[i, :, 1]),
                                                                                      bits(orel[i])))]

@@ -141,16 +141,19 @@ def test_unattached_address():
     assert top.is_routable(int(ips[0]), 0x01020304) is False
 
 
-@pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor", "slab_readlane", "slab_noagg", "rank_noagg"])
+@pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor", "slab_readlane", "slab_noagg", "rank_noagg",
+                        "slab_unfused"])
 def pipeline(request, monkeypatch):
     """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, the slab
     layout SHD_SLAB_LAYOUT, the segment sort's pass-1 key broadcast
-    SHD_SEGSORT_LDS and the wave-aggregated destination slots SHD_DEST_AGG,
-    read per launch)."""
+    SHD_SEGSORT_LDS, the wave-aggregated destination slots SHD_DEST_AGG and
+    the one-launch scan + folded overflow placement SHD_ROUND_FUSE, read per
+    launch)."""
     monkeypatch.setenv("SHD_PACKET_PIPELINE", request.param.split("_")[0])
     monkeypatch.setenv("SHD_SLAB_LAYOUT", "rank" if request.param.endswith("rankmajor") else "host")
     monkeypatch.setenv("SHD_SEGSORT_LDS", "0" if request.param.endswith("readlane") else "1")
     monkeypatch.setenv("SHD_DEST_AGG", "0" if request.param.endswith("noagg") else "1")
+    monkeypatch.setenv("SHD_ROUND_FUSE", "0" if request.param.endswith("unfused") else "1")
     return request.param
 
 

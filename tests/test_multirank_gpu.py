@@ -48,8 +48,8 @@ def _packets(rank, world, st):
     return synth.packet_batch(4000, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, hosts_lo=lo, hosts_hi=hi)
 
 
-def _worker(rank, world, port, mode, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, world, port, mode, q, runs="1"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SHD_XCHG_RUNS=runs)
     import torch
     import torch.distributed as dist
 
@@ -128,9 +128,12 @@ def _worker(rank, world, port, mode, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("mode", ["replicated", "sharded"])
-@pytest.mark.parametrize("world", [2, 3])
-def test_multirank_round_through_c_abi(world, mode):
+@pytest.mark.parametrize("mode,world,runs", [("replicated", 2, "1"), ("replicated", 3, "1"), ("sharded", 2, "1"),
+                                             ("sharded", 3, "1"), ("replicated", 3, "0"), ("sharded", 2, "0")])
+def test_multirank_round_through_c_abi(world, mode, runs):
+    """runs "1": the owner merges the W received destination-sorted runs in
+    place (default); "0": it re-scatters them into destination slabs (the
+    round-2 regroup, SHD_XCHG_RUNS=0)."""
     import torch.multiprocessing as mp
 
     import oracle_ctypes as O
@@ -138,7 +141,7 @@ def test_multirank_round_through_c_abi(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q, runs)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in range(world))
