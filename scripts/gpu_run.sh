@@ -3,6 +3,8 @@
 #   scripts/gpu_run.sh TAG STEP [STEP ...]
 # STEP: test[:EXPR]  pytest -m gpu (optionally -k EXPR), full output in gpurun_out/TAG/
 #       probe:ARGS   scripts/agg_probe.py ARGS (commas for spaces): in-process A/B of a knob
+#       ubench:NAME  scripts/NAME (a microbenchmark binary built here)
+#       pmc          scripts/pmc_r03.sh: PMC passes over C3 rounds, C2 and C4 builds -> traffic.json
 #       smoke        __graft_entry__.smoke()
 #       bench[:ARGS] bench.py (ARGS: extra arguments, commas for spaces)
 #       prof[:ARGS]  rocprofv3 --kernel-trace --stats of bench.py
@@ -43,6 +45,13 @@ for step in "$@"; do
         # scripts/agg_probe.py ENV V1 V2 ... (commas for spaces)
         timeout -k 10 600 python -u $R/scripts/agg_probe.py ${arg//,/ } > $D/probe$i.log 2>&1 || { tail -30 $D/probe$i.log; exit 1; }
         cat $D/probe$i.log ;;
+    ubench)
+        # a prebuilt scripts/ubench_* binary (built on the CPU side with hipcc)
+        timeout -k 10 300 $R/scripts/$arg > $D/$arg.log 2>&1 || { tail -20 $D/$arg.log; exit 1; }
+        cat $D/$arg.log ;;
+    pmc)
+        timeout -k 10 1000 bash $R/scripts/pmc_r03.sh $T/pmc > $D/pmc.log 2>&1 || { tail -20 $D/pmc.log; exit 1; }
+        tail -3 $D/pmc.log ;;
     prof)
         (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $D/prof -o prof -- \
             python3 $R/bench.py ${arg//,/ } > $D/prof_bench.json 2> $D/prof_bench.err) || { tail -30 $D/prof_bench.err; exit 1; }
