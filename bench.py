@@ -94,6 +94,30 @@ def gpu_state(dev_index):
     return st
 
 
+# Random-request ceilings measured on the box by scripts/ubench_mixed.hip
+# (independent random 16-B requests, by footprint and write share), the
+# bound the scatter and the slab SSSP kernels are compared against beside
+# their byte fraction.
+CEILING_JSON = os.path.join(ROOT, "profiles", "r03_request_ceiling.json")
+
+
+def request_ceiling(key):
+    try:
+        with open(CEILING_JSON) as f:
+            j = json.load(f)
+    except OSError:
+        return None, None
+    return j.get(key), j.get("_source")
+
+
+def request_roofline(requests, seconds, key, what):
+    ceiling, src = request_ceiling(key)
+    ach = requests / seconds / 1e9
+    return {"bound": "random requests", "requests_per_launch": requests, "requests": what, "achieved": ach,
+            "unit": "G requests/s", "peak": ceiling, "peak_case": key, "peak_source": src,
+            "frac": ach / ceiling if ceiling else None}
+
+
 # The C1 kernel (k_sssp_lds) keeps a row's whole state in LDS; its SQ
 # counters (profiles/r02i_sq_c1.log) put it on the per-pop LDS/VALU
 # instruction chain (1,375 instructions per pop, one wave per SIMD), not on
@@ -116,6 +140,10 @@ def routing_roofline(A, build_s, csr_bytes, rows, pops_per_row, traffic=None, bo
         out.update({"traffic": traffic["bytes"], "traffic_GBps": traffic["bytes"] / build_s / 1e9,
                     "requests": rq, "requests_per_pop": rq / (rows * pops_per_row) if rq else None,
                     "requests_per_s": rq / build_s if rq else None})
+        if rq and bound.startswith("hbm"):
+            ceil, src = request_ceiling("30720MB_37.5pct_writes")
+            out["request_ceiling"] = {"peak": ceil, "unit": "G requests/s", "source": src,
+                                      "frac": rq / build_s / 1e9 / ceil if ceil else None}
     return out
 
 
@@ -303,6 +331,11 @@ def main():
             "per_stage_GBps": dict(zip(STAGES, achieved)),
             "alg_bytes_per_launch": dict(zip(STAGES, alg_bytes)),
             "timing": "HIP events on the launch stream, averaged over the timed steps",
+            # the scatter's HBM-side random requests: the table gather per
+            # packet, the destination-slot atomic and the slab write per event
+            "request_roofline": request_roofline(P + 2.0 * delivered, per_launch_ms[0] * 1e-3, "6144MB_62.5pct_writes",
+                                                 "table gather per packet + slot atomic + slab write per event")
+            if per_launch_ms[0] > 0 else None,
             "pipeline": os.environ.get("SHD_PACKET_PIPELINE") or "slab",
         },
         "gpu_state": {"before_timed": state_before, "after_timed": gpu_state(local) if rank == 0 else None},

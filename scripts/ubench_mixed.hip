@@ -69,7 +69,7 @@ int main(int argc, char** argv) {
     const int grid = prop.multiProcessorCount * 32, steps = 64;
     const double reqs = (double)grid * 256 * steps * kB;
     const size_t foot_mb[] = {64, 1024, 6u << 10, 30u << 10};
-    const int wr[] = {0, 112, 128, 256}; // 0 %, 43.75 %, 50 %, 100 % writes (kB = 8: whole eighths)
+    const int wr[] = {0, 96, 128, 160, 256}; // 0, 37.5, 50, 62.5, 100 % writes (kB = 8: whole eighths)
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));

@@ -484,13 +484,15 @@ __global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, si
 }
 
 // The same scan in ONE launch of one 1,024-thread workgroup (len <=
-// kScanOneMax, the per-destination counts of a round): each wave owns a
-// contiguous stretch of whole 256-element chunks; pass 1 sums it with 16-B
-// loads, the 16 wave sums are combined through LDS, pass 2 re-reads the
-// stretch (L2-warm) and writes the prefixes with a wave scan and a running
-// carry.  Replaces three launches whose boundaries cost more than the
-// 0.4 MB they move.  out[len] = total (and counters[0]).
-constexpr size_t kScanOneMax = 1u << 19;
+// kScanOneMax): each wave owns a contiguous stretch of whole 256-element
+// chunks; pass 1 sums it with 16-B loads, the 16 wave sums are combined
+// through LDS, pass 2 re-reads the stretch (L2-warm) and writes the prefixes
+// with a wave scan and a running carry.  out[len] = total (and counters[0]).
+// Measured at H = 100k it is slower than the three launches (one CU walks
+// 0.4 MB twice: round 0.996 vs 0.969 ms, profiles/r03e_scatter_probes.log),
+// so it only takes small ranges, where a launch boundary costs more than
+// the walk.
+constexpr size_t kScanOneMax = 16384;
 __global__ __launch_bounds__(1024) void k_scan_one(const uint32_t* __restrict__ in, size_t len,
                                                    uint32_t* __restrict__ out, unsigned long long* counters) {
     __shared__ uint32_t wsum[16];
