@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r02z_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03f_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
@@ -244,13 +244,26 @@ def main():
     my_lo, my_hi = own_lo[rank], own_lo[rank + 1]
     sptr = stream.cuda_stream
     last = {}
+    # N>1: one call per round decides, groups by destination (unsorted),
+    # ships 24-B wire records to the destinations' owners over xGMI and merges
+    # them there (shd_round_process_exchange); SHD_BENCH_SPLIT=1 runs the
+    # sorted round + shd_round_exchange instead
+    split = os.environ.get("SHD_BENCH_SPLIT") == "1"
     if world > 1:
-        d_recv = torch.empty(2 * P * 32, dtype=torch.uint8, device=dev)
+        wire = 32 if split else 24
+        d_send = torch.empty(P * wire, dtype=torch.uint8, device=dev) if not split else d_out
+        d_recv = torch.empty(2 * P * wire, dtype=torch.uint8, device=dev)
         d_final = torch.empty(2 * P * 32, dtype=torch.uint8, device=dev)
         d_final_off = torch.empty(my_hi - my_lo + 1, dtype=torch.int32, device=dev)
-        xport.register(d_out, d_recv)
+        xport.register(d_out, d_recv, d_send)
 
     def step():
+        if world > 1 and not split:
+            last["nrecv"] = top.process_exchange(xport, d_recs.data_ptr(), P, barrier_t, end_t, 0, own_lo,
+                                                 d_send.data_ptr(), d_status.data_ptr(), d_cnt.data_ptr(),
+                                                 d_recv.data_ptr(), 2 * P, d_final.data_ptr(),
+                                                 d_final_off.data_ptr(), sptr)
+            return
         top.process_device(d_recs.data_ptr(), P, barrier_t, end_t, 0, d_out.data_ptr(), d_off.data_ptr(),
                            d_status.data_ptr(), d_cnt.data_ptr(), sptr)
         if world == 1:
@@ -279,8 +292,10 @@ def main():
     _lib.check(lib.shd_round_timing_enable(0))
     cnt = d_cnt.cpu().numpy().view(np.uint64)
     delivered = int(cnt[0])
-    seg = np.diff(d_off.cpu().numpy().astype(np.int64))
-    overflow = int(np.maximum(seg - 256, 0).sum())  # events past their destination's 256 slab slots
+    overflow = 0
+    if world == 1 or split:  # (the exchanged round keeps its offsets inside the library)
+        seg = np.diff(d_off.cpu().numpy().astype(np.int64))
+        overflow = int(np.maximum(seg - 256, 0).sum())  # events past their destination's 256 slab slots
     launches = max(nl.value, 1)
     per_launch_ms = [stage_ms[k] / launches for k in range(4)]
     # each rank's stage times; the roofline uses rank 0's live numbers
@@ -372,7 +387,7 @@ def main():
             "value": 5000.0 ** 2 / tr, "unit": "routed host-pairs/s", "vertex_pairs_per_s": A1 * A1 / tr,
             "ms_per_table": tr * 1e3, "kernel": "k_sssp_lds (igraph-exact Dijkstra, 1 wave/source)",
             "roofline": routing_roofline(A1, tr, 20.0 * 2 * info1["edges"] + 4 * 1001, max(h1 - l1, 0), 1000,
-                                         tj.get("routing_lds") if world == 1 else None, bound=C1_BOUND),
+                                         tj.get("routing_lds_c1") if world == 1 else None, bound=C1_BOUND),
             "c3_table": {"config": "the C3 rounds' table: V=%d sparse graph, H=%d hosts, A=%d" % (V, H, A),
                          "rows_s": t_c3, "allgather_s": max_over_ranks(t_ag_c3) if world > 1 else 0.0,
                          "host_pairs_per_s": float(H) * H / t_c3,

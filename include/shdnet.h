@@ -335,6 +335,22 @@ int shd_topology_allgather_rows(ShdTopology* top, const ShdTransport* xport, voi
 int shd_round_exchange(ShdTopology* top, const ShdTransport* xport, const ShdDeliv* d_events,
                        const uint32_t* d_dst_offsets, const uint32_t* host_bounds, ShdDeliv* d_recv, size_t recv_cap,
                        ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, void* stream);
+/* One round decided and exchanged in one call (the multi-GPU form of
+ * shd_round_process_device + shd_round_exchange): this rank's records are
+ * decided, grouped by destination WITHOUT the per-destination sort (the
+ * owner sorts the union of what it receives anyway) and shipped as 24-byte
+ * wire records {time, srcHostEventID, src host, pkt_index} -- a quarter
+ * fewer bytes over xGMI than ShdDeliv -- to the destinations' owners, which
+ * merge them into event_compare order: d_out / d_out_offsets / *n_out as
+ * shd_round_exchange's.  d_send: >= 24 * n bytes; d_recv: recv_cap wire
+ * records (24 * recv_cap bytes); d_status / d_counters as
+ * shd_round_process_device (counters[0]: events this rank decided,
+ * counters[1]: its min delivered time).  Needs the slab pipeline (default).
+ * Synchronous. */
+int shd_round_process_exchange(ShdTopology* top, const ShdTransport* xport, const ShdPkt* d_recs, size_t n,
+                               uint64_t barrier, uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds,
+                               void* d_send, uint8_t* d_status, uint64_t* d_counters, void* d_recv, size_t recv_cap,
+                               ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, void* stream);
 /* Row-sharded tables (C4 at N > 1, no full matrix anywhere): rank r holds
  * rows [row_bounds[r], row_bounds[r+1]) (slot ids, host memory).  Each
  * record is sent to the rank holding the row that answers it -- the row of

@@ -4,6 +4,7 @@
 # STEP: test[:EXPR]  pytest -m gpu (optionally -k EXPR), full output in gpurun_out/TAG/
 #       probe:ARGS   scripts/agg_probe.py ARGS (commas for spaces): in-process A/B of a knob
 #       ubench:NAME  scripts/NAME (a microbenchmark binary built here)
+#       rehearse[:ARGS]  bench.py at N=2 on one GPU over gloo (torch.distributed.run)
 #       pmc          scripts/pmc_r03.sh: PMC passes over C3 rounds, C2 and C4 builds -> traffic.json
 #       smoke        __graft_entry__.smoke()
 #       bench[:ARGS] bench.py (ARGS: extra arguments, commas for spaces)
@@ -45,6 +46,13 @@ for step in "$@"; do
         # scripts/agg_probe.py ENV V1 V2 ... (commas for spaces)
         timeout -k 10 600 python -u $R/scripts/agg_probe.py ${arg//,/ } > $D/probe$i.log 2>&1 || { tail -30 $D/probe$i.log; exit 1; }
         cat $D/probe$i.log ;;
+    rehearse)
+        # N=2 bench rehearsal on one GPU: both ranks on GPU 0, gloo collectives
+        # (the driver's N>1 runs use RCCL over xGMI); ARGS: extra bench args
+        SHD_BENCH_SHARE_GPU=1 SHD_BENCH_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 \
+            --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29555 $R/bench.py --gpus 2 ${arg//,/ } \
+            > $D/rehearse.json 2> $D/rehearse.err || { tail -30 $D/rehearse.err; exit 1; }
+        cat $D/rehearse.json ;;
     ubench)
         # a prebuilt scripts/ubench_* binary (built on the CPU side with hipcc)
         timeout -k 10 300 $R/scripts/$arg > $D/$arg.log 2>&1 || { tail -20 $D/$arg.log; exit 1; }

@@ -2,7 +2,7 @@
 # PMC passes (one rocprofv3 --pmc pass per counter group of pmc_groups.txt,
 # each under its own time limit) over: the C3 rounds (bench.py, routing and
 # CPU legs off), the C2 build (V=20k, H=50k) and the C4 build; folded into
-# gpurun_out/TAG/traffic.json by traffic.py.  Usage: scripts/pmc_r03.sh TAG
+# gpurun_out/TAG/traffic.json by traffic.py; plus the C1 build (x5).  Usage: scripts/pmc_r03.sh TAG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 T=${1:-r03pmc}
@@ -22,9 +22,12 @@ run_passes() { # NAME LIMIT CMD...
     done < $R/scripts/pmc_groups.txt
 }
 run_passes c3 150 python3 $R/bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline --no-nic &&
+run_passes c1 100 python3 $R/scripts/build_c4.py complete 1000 5000 0x5EED0001 &&
 run_passes c2 150 python3 $R/scripts/build_c4.py 20000 50000 0x5EED0002 &&
 run_passes c4 200 python3 $R/scripts/build_c4.py || exit 1
 python3 $R/scripts/traffic.py $O/traffic.json $(find $O/c3 -name "*counter_collection.csv") > /dev/null &&
+python3 $R/scripts/traffic.py $O/traffic.json --suffix _c1 --source "C1 build x5 (scripts/build_c4.py complete 1000 5000)" \
+    $(find $O/c1 -name "*counter_collection.csv") > /dev/null &&
 python3 $R/scripts/traffic.py $O/traffic.json --suffix _c2 --source "C2 build (scripts/build_c4.py 20000 50000)" \
     $(find $O/c2 -name "*counter_collection.csv") > /dev/null &&
 python3 $R/scripts/traffic.py $O/traffic.json --suffix _c4 --source "C4 build (scripts/build_c4.py)" \

@@ -1618,6 +1618,34 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
 // scatter into destination slabs, only the per-destination union of W runs.
 constexpr uint32_t kMaxRuns = 64; // = xchg.hip kMaxWorld
 
+// The exchange's wire record (24 B): a delivered event without its
+// destination (the block and offsets say it) and without the slot word.
+// 25 % fewer bytes over xGMI than the 32-B ShdDeliv.
+struct Wire {
+    unsigned long long t, q;
+    uint32_t s, ix;
+};
+static_assert(sizeof(Wire) == 24, "wire record");
+__device__ __forceinline__ Ev ld_wire(const Wire* p) {
+    const uint2* w = reinterpret_cast<const uint2*>(p); // 8-B aligned
+    const uint2 a = w[0], b = w[1], c = w[2];
+    return Ev{((unsigned long long)a.y << 32) | a.x, ((unsigned long long)b.y << 32) | b.x, c.x, c.y};
+}
+__device__ __forceinline__ void st_wire(Wire* p, unsigned long long t, unsigned long long q, uint32_t src,
+                                        uint32_t ix) {
+    uint2* w = reinterpret_cast<uint2*>(p);
+    w[0] = make_uint2((uint32_t)t, (uint32_t)(t >> 32));
+    w[1] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+    w[2] = make_uint2(src, ix);
+}
+// element i of a run-merge input: a ShdDeliv (kFmt 0) or a Wire (kFmt 1)
+template <int kFmt>
+__device__ __forceinline__ Ev ld_run(const void* in, uint32_t i) {
+    if (kFmt == 1) return ld_wire(static_cast<const Wire*>(in) + i);
+    const ShdDeliv r = ld_ev(static_cast<const ShdDeliv*>(in) + i);
+    return Ev{r.time, r.seq, r.src_host, r.pkt_index};
+}
+
 __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__ rofs, uint32_t W, uint32_t Hr,
                                                     uint32_t* __restrict__ cnt) {
     for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < Hr; d += gridDim.x * blockDim.x) {
@@ -1631,7 +1659,8 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
 // start and source index of each run) are read as one segment and ranked
 // like a slab segment; segments above kSmallSeg events are copied to their
 // final range of the staging array and listed for k_segsort_mid / _merge.
-__global__ __launch_bounds__(256) void k_runs_sort(const ShdDeliv* __restrict__ in, const uint32_t* __restrict__ rofs,
+template <int kFmt>
+__global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, const uint32_t* __restrict__ rofs,
                                                    const uint32_t* __restrict__ bbase, uint32_t W, uint32_t Hr,
                                                    const uint32_t* __restrict__ off, uint32_t host_lo,
                                                    ShdDeliv* __restrict__ out, ShdDeliv* __restrict__ scr,
@@ -1669,15 +1698,15 @@ __global__ __launch_bounds__(256) void k_runs_sort(const ShdDeliv* __restrict__ 
             return rb[k] + (i - rs[k]);
         };
         if (n <= (uint32_t)kSmallSeg) {
-            auto load = [&](uint32_t i) {
-                const ShdDeliv r = ld_ev(&in[at(i)]);
-                return Ev{r.time, r.seq, r.src_host, r.pkt_index};
-            };
+            auto load = [&](uint32_t i) { return ld_run<kFmt>(in, at(i)); };
             if (n <= 64) wave_rank_segment<1>(load, n, d + host_lo, out, o, lane, lk);
             else if (n <= 128) wave_rank_segment<2>(load, n, d + host_lo, out, o, lane, lk);
             else wave_rank_segment<4>(load, n, d + host_lo, out, o, lane, lk);
         } else {
-            for (uint32_t i = lane; i < n; i += 64) st_ev(&scr[o + i], ld_ev(&in[at(i)]));
+            for (uint32_t i = lane; i < n; i += 64) {
+                const Ev e = ld_run<kFmt>(in, at(i));
+                st_ev(&scr[o + i], ShdDeliv{e.t, e.q, e.s, d + host_lo, e.ix, 0u});
+            }
             if (lane == 0) {
                 const uint32_t k = atomicAdd(nbig, 1u);
                 if (k < Hr) big[k] = d;
@@ -1689,6 +1718,47 @@ __global__ __launch_bounds__(256) void k_runs_sort(const ShdDeliv* __restrict__ 
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
+}
+
+// The sender's side of a round that is exchanged next
+// (shd_round_process_exchange): the decided events grouped by destination
+// -- slab slots, then the overflow events at their ranks -- copied to the
+// wire array at off[d], unsorted: the owner sorts the union of the runs it
+// receives anyway (k_runs_sort), so the sender's segment sort is skipped.
+__global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__ slab, uint32_t slab_rm, uint32_t H,
+                                                    const uint32_t* __restrict__ off, const ShdDeliv* __restrict__ ovf,
+                                                    const uint32_t* __restrict__ nbig, uint32_t* __restrict__ fault,
+                                                    uint32_t ovf_cap, Wire* __restrict__ wire) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t m = nbig[1];
+    if (m > ovf_cap) {
+        if (wave == 0 && lane == 0) atomicOr(fault, kFaultOvfCap);
+    } else {
+        for (uint32_t i = wave * 64 + lane; i < m; i += nwaves * 64) {
+            const ShdDeliv r = ld_ev(&ovf[i]);
+            if (r.dst_host >= H || r.pad < kSlab || r.pad >= off[r.dst_host + 1] - off[r.dst_host]) {
+                atomicOr(fault, kFaultOvfRange);
+                continue;
+            }
+            st_wire(&wire[off[r.dst_host] + r.pad], r.time, r.seq, r.src_host, r.pkt_index);
+        }
+    }
+    for (uint32_t d = wave; d < H; d += nwaves) {
+        const uint32_t b = off[d], n = off[d + 1] - b;
+        const uint32_t k = n < kSlab ? n : kSlab;
+        const size_t base = slab_rm ? d : (size_t)d * kSlab, stride = slab_rm ? H : 1u;
+        for (uint32_t i = lane; i < k; i += 64) {
+            const ShdDeliv r = ld_ev(&slab[base + (size_t)i * stride]);
+            st_wire(&wire[b + i], r.time, r.seq, r.src_host, r.pkt_index);
+        }
+    }
+}
+
+// the round's fault word when no merge kernel runs: the stage guards only
+__global__ void k_fault_word(const uint32_t* __restrict__ nbig, MergeMeta mm) {
+    if (threadIdx.x == 0) mm.hdr[3] = nbig[2] << 24;
 }
 
 // ---- workspace (grow-only, one per topology; see shd_dev_ws_new) ----
@@ -2349,7 +2419,7 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
 // the n events of the blocks back to back (block k from d_bbase[k], a device
 // array of W + 1 prefix counts), d_rofs the W per-block offset arrays over
 // the host range [host_lo, host_hi).  Output as shd_dev_deliv_sort.
-extern "C" int shd_dev_deliv_merge_runs(void* ws, const ShdDeliv* d_in, size_t n, const uint32_t* d_rofs,
+extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, size_t n, const uint32_t* d_rofs,
                                         const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi,
                                         ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -2362,21 +2432,66 @@ extern "C" int shd_dev_deliv_merge_runs(void* ws, const ShdDeliv* d_in, size_t n
     if ((rc = ws_reserve(w, n, H, H))) return rc; // (st1: staging of the listed segments)
     if ((rc = dbg_ranges(w, nullptr, 0, d_out, d_dst_offsets, H))) return rc;
     if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 12, s), "memset nbig"))) return rc;
-    mark(0, s);
     hipLaunchKernelGGL(k_runs_count, dim3(grid_for(H, 256, 4096)), dim3(256), 0, s, d_rofs, W, H, w.cnt1);
-    mark(1, s);
     scan_counts(w.cnt1, (size_t)H, d_dst_offsets, w.bsum, nullptr, s);
-    mark(2, s);
-    mark(3, s);
-    hipLaunchKernelGGL(k_runs_sort, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_rofs, d_bbase, W, H,
-                       d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
+    if (wire)
+        hipLaunchKernelGGL(k_runs_sort<1>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_rofs, d_bbase, W, H,
+                           d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
+    else
+        hipLaunchKernelGGL(k_runs_sort<0>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_rofs, d_bbase, W, H,
+                           d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
     if ((rc = hip_status(hipGetLastError(), "k_runs_sort launch"))) return rc;
     if ((rc = dbg_sync(s, "k_runs_sort"))) return rc;
     if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s))) return rc;
-    mark(4, s);
-    if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
-    if ((rc = ws_end(w, s))) return rc;
+    if ((rc = ws_end(w, s))) return rc; // (not a timed round stage: shd_round_timing_* time the decide side)
     if (stream) return 0;
     if ((rc = hip_status(hipStreamSynchronize(s), "merge runs"))) return rc;
     return ws_faults(w, true);
+}
+
+// The sender's side of shd_round_process_exchange: the slab round up to the
+// per-destination offsets (d_off, H + 1), then the grouped, unsorted wire
+// records (k_group_wire) instead of the segment sort.  Slab pipeline only.
+extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                                            uint64_t end_time, uint64_t bootstrap_end, void* d_wire, uint32_t* d_off,
+                                            uint8_t* d_status, uint64_t* d_counters, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
+    Ws& w = *static_cast<Ws*>(c->ws);
+    const uint32_t H = c->nhosts;
+    if (pipeline_for(H, true) != kSlabPipe) return shd_fail(-ENOTSUP, "the exchanged round needs the slab pipeline");
+    Bucketing bk;
+    int rc = make_bucketing(0, H, n, &bk);
+    if (rc) return rc;
+    if ((rc = ws_begin(w, s))) return rc;
+    if ((rc = ws_reserve(w, n, H, H)) || (rc = slab_reserve(w, H))) return rc;
+    unsigned long long* counters = (unsigned long long*)d_counters;
+    if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 12, s), "memset nbig")) ||
+        (rc = hip_status(hipMemsetAsync(counters, 0xff, 16, s), "memset counters")) ||
+        (rc = hip_status(hipMemsetAsync(w.cnt1, 0, 4 * (size_t)H, s), "memset cnt1")))
+        return rc;
+    mark(0, s);
+    if (n)
+        hipLaunchKernelGGL(k_pkt_scatter<2>, dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier, end_time,
+                           bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2, w.nbig + 1);
+    mark(1, s);
+    if ((rc = hip_status(hipGetLastError(), "k_pkt_scatter launch"))) return rc;
+    scan_counts(w.cnt1, (size_t)H, d_off, w.bsum, counters, s);
+    mark(2, s);
+    mark(3, s);
+    hipLaunchKernelGGL(k_group_wire, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, w.slab, bk.slab_rm, H, d_off, w.st2,
+                       w.nbig, w.nbig + 2, (uint32_t)w.cap_n, static_cast<Wire*>(d_wire));
+    if ((rc = hip_status(hipGetLastError(), "k_group_wire launch"))) return rc;
+    mark(4, s);
+    if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
+    if ((rc = dbg_sync(s, "grouped round"))) return rc;
+    // the guard bits of this round (nbig[2]) go to the fault word the host
+    // reads back (no merge kernel runs on the sender's side)
+    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
+        w.fault = nullptr;
+        return shd_fail(-ENOMEM, "hipHostMalloc fault word");
+    }
+    hipLaunchKernelGGL(k_fault_word, dim3(1), dim3(64), 0, s, w.nbig, merge_meta(w));
+    if ((rc = hip_status(hipMemcpyAsync(w.fault, w.meta + 3, 4, hipMemcpyDeviceToHost, s), "fault word D2H"))) return rc;
+    return ws_end(w, s);
 }

@@ -367,7 +367,7 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
             free(h);
         }
         if (!rc)
-            rc = shd_dev_deliv_merge_runs(sm->ws, sm->d_recv, tot, sm->d_rofs, sm->d_rofs + (size_t)S * (hi - lo + 1),
+            rc = shd_dev_deliv_merge_runs(sm->ws, sm->d_recv, 0, tot, sm->d_rofs, sm->d_rofs + (size_t)S * (hi - lo + 1),
                                           (uint32_t)S, lo, hi, sm->d_fin, sm->d_fin_off, sm->stream);
         if (!rc) rc = shd_dev_stream_sync(sm->stream);
         if (!rc && out && tot) rc = shd_dev_d2h(out + obase, sm->d_fin, sizeof(ShdDeliv) * tot);
@@ -525,5 +525,28 @@ int shd_topology_allgather_rows(ShdTopology* t, const ShdTransport* x, void* d_t
     }
     if (!rc) rc = stream ? shd_dev_stream_sync(stream) : shd_dev_sync();
     free(off);
+    return rc;
+}
+
+int shd_round_process_exchange(ShdTopology* t, const ShdTransport* x, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                               uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds, void* d_send,
+                               uint8_t* d_status, uint64_t* d_counters, void* d_recv, size_t recv_cap,
+                               ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, void* stream) {
+    if (!t || !x || !host_bounds || !n_out || !d_send || !d_recv || x->world < 1 || x->rank < 0 ||
+        x->rank >= x->world)
+        return shd_fail(-EINVAL, "bad exchange arguments");
+    int rc = shd_ensure_routes(t);
+    if (rc) return rc;
+    if (t->nshards > 1) return shd_fail(-ENOTSUP, "a multi-shard table runs its rounds with shd_round_collect");
+    if (!__atomic_load_n(&t->lookups_started, __ATOMIC_RELAXED)) __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
+    pthread_mutex_lock(&t->round_mu);
+    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t)) && !(rc = shd_ensure_ptab(t))) {
+        ShdPktCtx c;
+        shd_pkt_ctx(t, &c);
+        rc = c.ws ? shd_dev_round_exchange(&c, x, d_recs, n, barrier, end_time, bootstrap_end, host_bounds, d_send,
+                                           d_status, d_counters, d_recv, recv_cap, d_out, d_out_offsets, n_out, stream)
+                  : -ENOMEM;
+    }
+    pthread_mutex_unlock(&t->round_mu);
     return rc;
 }

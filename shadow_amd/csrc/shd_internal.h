@@ -148,9 +148,20 @@ int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_l
  * at event d_bbase[k] of d_in (W + 1 prefix counts, device), d_rofs holds
  * per block the (host_hi - host_lo + 1) destination offsets relative to the
  * block.  No scatter: the runs are read in place. */
-int shd_dev_deliv_merge_runs(void* ws, const ShdDeliv* d_in, size_t n, const uint32_t* d_rofs, const uint32_t* d_bbase,
-                             uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out, uint32_t* d_dst_offsets,
-                             void* stream);
+int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, size_t n, const uint32_t* d_rofs,
+                             const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
+                             uint32_t* d_dst_offsets, void* stream);
+/* The sender's side of an exchanged round: decided events grouped by
+ * destination, unsorted, as 24-B wire records {time, seq, src, pkt_index}
+ * into d_wire, destination offsets (H + 1) into d_off; slab pipeline only. */
+int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                                 uint64_t end_time, uint64_t bootstrap_end, void* d_wire, uint32_t* d_off,
+                                 uint8_t* d_status, uint64_t* d_counters, void* stream);
+/* decide + group + exchange + merge in one call (shd_round_process_exchange) */
+int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                           uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds, void* d_wire_send,
+                           uint8_t* d_status, uint64_t* d_counters, void* d_wire_recv, size_t recv_cap,
+                           ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, void* stream);
 
 /* out[i] = tab[idx[i]] for n entries (device pointers; synchronous; on the
  * calling thread's device) */

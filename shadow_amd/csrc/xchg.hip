@@ -324,32 +324,33 @@ extern "C" int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const
     return rc;
 }
 
-// Destination-owner exchange + regroup by runs (shd_round_exchange): the
-// events of each peer's destinations and, beside them, the rebased
-// per-destination offsets of that block; the owner then merges the W
-// destination-sorted runs in place (shd_dev_deliv_merge_runs) instead of
-// scattering every received event into destination slabs again.  One
-// device scratch: [H + W slices | W x (H_me + 1) received offsets | W + 1
-// block bases]; its pinned host side carries the cuts and the block bases.
-extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdDeliv* d_events,
-                                     const uint32_t* d_dst_offsets, const uint32_t* host_bounds, ShdDeliv* d_recv,
-                                     size_t recv_cap, ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out,
-                                     void* stream) {
-    hipStream_t s = (hipStream_t)stream;
+// Destination-owner exchange + regroup by runs: the events of each peer's
+// destinations (elem_bytes each: 32-B ShdDeliv or the 24-B wire record) and,
+// beside them, the rebased per-destination offsets of that block; the owner
+// then merges the W destination-grouped runs in place
+// (shd_dev_deliv_merge_runs) instead of scattering every received event into
+// destination slabs again.  Scratch (device, caller-sized, see
+// xchg_scratch_words): [cuts | H + W slices | W x (H_me + 1) received offsets
+// | W + 1 block bases]; host (pinned): [cuts | block bases].
+namespace {
+size_t xchg_scratch_words(uint32_t H, int W, uint32_t Hm) {
+    return (kMaxWorld + 1) + ((size_t)H + W) + (size_t)W * (Hm + 1) + (W + 1);
+}
+int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, size_t elem_bytes, int wire,
+                       const uint32_t* d_dst_offsets, const uint32_t* host_bounds, void* d_recv, size_t recv_cap,
+                       ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, hipStream_t s, uint32_t* dscr,
+                       uint32_t* hscr) {
     const int W = x->world, me = x->rank;
     RouteArgs ra;
     int rc = make_args(host_bounds, W, &ra);
     if (rc) return rc;
     const uint32_t H = host_bounds[W], lo = host_bounds[me], hi = host_bounds[me + 1], Hm = hi - lo;
     const size_t n_sl = (size_t)H + W, n_ro = (size_t)W * (Hm + 1);
-    const size_t dev_words = (kMaxWorld + 1) + n_sl + n_ro + (W + 1);
-    void *dscr = nullptr, *hscr = nullptr;
-    if ((rc = shd_dev_ws_scratch(ws, 4 * dev_words, 4 * (2 * kMaxWorld + 2), &dscr, &hscr))) return rc;
-    uint32_t* d_cuts = static_cast<uint32_t*>(dscr);
+    uint32_t* d_cuts = dscr;
     uint32_t* d_sl = d_cuts + (kMaxWorld + 1);
     uint32_t* d_ro = d_sl + n_sl;
     uint32_t* d_bb = d_ro + n_ro;
-    uint32_t* h_cuts = static_cast<uint32_t*>(hscr);
+    uint32_t* h_cuts = hscr;
     uint32_t* h_bb = h_cuts + (kMaxWorld + 1);
     // cuts of the events at the owners' host bounds, and the offset slices
     hipLaunchKernelGGL(k_cuts, dim3(1), dim3(kMaxWorld + 1), 0, s, d_dst_offsets, ra, d_cuts);
@@ -363,8 +364,8 @@ extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdD
     for (int r = 0; r < W; r++) send[r] = h_cuts[r + 1] - h_cuts[r];
     size_t nrecv = 0;
     // the events (the capacity verdict is collective inside)
-    if ((rc = exchange_blocks(x, d_events + h_cuts[0], send.data(), sizeof(ShdDeliv), d_recv, recv_cap, &nrecv, s,
-                              recv.data())))
+    if ((rc = exchange_blocks(x, static_cast<const char*>(d_events) + (size_t)h_cuts[0] * elem_bytes, send.data(),
+                              elem_bytes, d_recv, recv_cap, &nrecv, s, recv.data())))
         return rc;
     // the offset slices: H_r + 1 words to peer r, H_me + 1 from each peer
     for (int r = 0; r < W; r++) {
@@ -377,12 +378,54 @@ extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdD
     for (int r = 0; r < W; r++) h_bb[r + 1] = h_bb[r] + (uint32_t)recv[r];
     if ((rc = hip_status(hipMemcpyAsync(d_bb, h_bb, 4 * (size_t)(W + 1), hipMemcpyHostToDevice, s), "bases H2D")))
         return rc;
-    if ((rc = shd_dev_deliv_merge_runs(ws, d_recv, nrecv, d_ro, d_bb, (uint32_t)W, lo, hi, d_out, d_out_offsets,
-                                       stream)))
+    if ((rc = shd_dev_deliv_merge_runs(ws, d_recv, wire, nrecv, d_ro, d_bb, (uint32_t)W, lo, hi, d_out, d_out_offsets,
+                                       s)))
         return rc;
     if ((rc = hip_status(hipStreamSynchronize(s), "exchange runs"))) return rc;
     *n_out = nrecv;
     return 0;
+}
+
+} // namespace
+
+extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdDeliv* d_events,
+                                     const uint32_t* d_dst_offsets, const uint32_t* host_bounds, ShdDeliv* d_recv,
+                                     size_t recv_cap, ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out,
+                                     void* stream) {
+    const int W = x->world;
+    if (W < 1 || W > kMaxWorld || x->rank < 0 || x->rank >= W) return shd_fail(-EINVAL, "bad world");
+    const uint32_t Hm = host_bounds[x->rank + 1] - host_bounds[x->rank];
+    void *dscr = nullptr, *hscr = nullptr;
+    int rc = shd_dev_ws_scratch(ws, 4 * xchg_scratch_words(host_bounds[W], W, Hm), 4 * (2 * kMaxWorld + 2), &dscr,
+                                &hscr);
+    if (rc) return rc;
+    return exchange_runs_core(ws, x, d_events, sizeof(ShdDeliv), 0, d_dst_offsets, host_bounds, d_recv, recv_cap,
+                              d_out, d_out_offsets, n_out, (hipStream_t)stream, static_cast<uint32_t*>(dscr),
+                              static_cast<uint32_t*>(hscr));
+}
+
+// A round decided and exchanged in one call (shd_round_process_exchange):
+// the sender groups its decided events by destination without sorting them
+// and ships 24-B wire records; the owners sort the union of what they get.
+extern "C" int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,
+                                      uint64_t barrier, uint64_t end_time, uint64_t bootstrap_end,
+                                      const uint32_t* host_bounds, void* d_wire_send, uint8_t* d_status,
+                                      uint64_t* d_counters, void* d_wire_recv, size_t recv_cap, ShdDeliv* d_out,
+                                      uint32_t* d_out_offsets, size_t* n_out, void* stream) {
+    const int W = x->world;
+    if (W < 1 || W > kMaxWorld || x->rank < 0 || x->rank >= W) return shd_fail(-EINVAL, "bad world");
+    const uint32_t H = c->nhosts, Hm = host_bounds[x->rank + 1] - host_bounds[x->rank];
+    if (host_bounds[0] != 0 || host_bounds[W] != H) return shd_fail(-EINVAL, "host bounds must cover [0, %u)", H);
+    const size_t words = ((size_t)H + 1) + xchg_scratch_words(H, W, Hm);
+    void *dscr = nullptr, *hscr = nullptr;
+    int rc = shd_dev_ws_scratch(c->ws, 4 * words, 4 * (2 * kMaxWorld + 2), &dscr, &hscr);
+    if (rc) return rc;
+    uint32_t* d_off = static_cast<uint32_t*>(dscr); // the sender's destination offsets (H + 1)
+    if ((rc = shd_dev_packet_round_grouped(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire_send, d_off, d_status,
+                                           d_counters, stream)))
+        return rc;
+    return exchange_runs_core(c->ws, x, d_wire_send, 24, 1, d_off, host_bounds, d_wire_recv, recv_cap, d_out,
+                              d_out_offsets, n_out, (hipStream_t)stream, d_off + (H + 1), static_cast<uint32_t*>(hscr));
 }
 
 extern "C" int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems,

@@ -255,6 +255,23 @@ class Topology:
         check(rc)
         return n.value
 
+    def process_exchange(self, xport, d_recs: int, n: int, barrier: int, end_time: int, bootstrap_end: int,
+                         host_bounds, d_send: int, d_status: int, d_counters: int, d_recv: int, recv_cap: int,
+                         d_out: int, d_out_offsets: int, stream: int = 0) -> int:
+        """shd_round_process_exchange: decide this rank's records, group them
+        unsorted as 24-B wire records, exchange them to the destinations'
+        owners and merge there; returns the events this rank received."""
+        hb = (C.c_uint32 * len(host_bounds))(*[int(x) for x in host_bounds])
+        nout = C.c_size_t()
+        rc = lib().shd_round_process_exchange(self._h, xport.handle, C.c_void_p(d_recs), n, barrier, end_time,
+                                              bootstrap_end, hb, C.c_void_p(d_send), C.c_void_p(d_status),
+                                              C.c_void_p(d_counters), C.c_void_p(d_recv), recv_cap, C.c_void_p(d_out),
+                                              C.c_void_p(d_out_offsets), C.byref(nout), C.c_void_p(stream))
+        if getattr(xport, "error", None) is not None:
+            raise xport.error
+        check(rc)
+        return nout.value
+
     def route_records(self, xport, d_recs: int, n: int, row_bounds, d_scratch: int, d_recv: int, recv_cap: int,
                       stream: int = 0) -> int:
         """shd_round_route_records: each record to the rank holding its answering row."""

@@ -113,10 +113,16 @@ int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_l
     return shd_fail(-ENOSYS, "stub device: no packet kernels");
 }
 
-int shd_dev_deliv_merge_runs(void* ws, const ShdDeliv* d_in, size_t n, const uint32_t* d_rofs, const uint32_t* d_bbase,
-                             uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out, uint32_t* d_dst_offsets,
-                             void* stream) {
+int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, size_t n, const uint32_t* d_rofs,
+                             const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
+                             uint32_t* d_dst_offsets, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no packet kernels");
+}
+int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                           uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds, void* d_wire_send,
+                           uint8_t* d_status, uint64_t* d_counters, void* d_wire_recv, size_t recv_cap,
+                           ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, void* stream) {
+    return shd_fail(-ENOSYS, "stub device: no exchange");
 }
 
 int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n,

@@ -9,6 +9,8 @@ replicated: rank r builds rows [row_bounds[r], row_bounds[r+1]) of the
   shd_round_exchange sends each event to its destination's owner rank, which
   regroups it with shd_deliv_sort_device.  The gathered table is checked
   bitwise against the oracle's rows.
+fused: the same table, then shd_round_process_exchange: decide, group by
+  destination without sorting, ship 24-B wire records, merge at the owner.
 sharded: rank r builds and holds only rows [row_bounds[r], row_bounds[r+1])
   (shd_topology_adopt_table_shard_device_resident); shd_round_route_records
   first moves every record to the rank holding the row that answers it,
@@ -66,7 +68,7 @@ def _worker(rank, world, port, mode, q, runs="1"):
         pk = _packets(rank, world, st)
         xp = TorchTransport(device=torch.device("cuda", 0))
         table = b""
-        if mode == "replicated":
+        if mode in ("replicated", "fused"):
             lo, hi = row_bounds[rank], row_bounds[rank + 1]
             tab = torch.zeros(A * A * 2, dtype=torch.float64, device="cuda")
             if hi > lo:
@@ -95,6 +97,29 @@ def _worker(rank, world, port, mode, q, runs="1"):
             recs = torch.empty(cap * 32, dtype=torch.uint8, device="cuda")
             xp.register(scratch, recs)
             n = top.route_records(xp, src.data_ptr(), len(pk), row_bounds, scratch.data_ptr(), recs.data_ptr(), cap)
+        if mode == "fused":  # decide + group + exchange + merge in one call (24-B wire records)
+            cap = 4000 * world
+            d_send = torch.empty(max(n, 1) * 24, dtype=torch.uint8, device="cuda")
+            d_wrecv = torch.empty(cap * 24, dtype=torch.uint8, device="cuda")
+            d_final = torch.empty(cap * 32, dtype=torch.uint8, device="cuda")
+            d_status = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
+            d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+            mine = host_bounds[rank + 1] - host_bounds[rank]
+            d_final_off = torch.empty(mine + 1, dtype=torch.int32, device="cuda")
+            xp.register(d_send, d_wrecv)
+            nrecv = top.process_exchange(xp, recs.data_ptr(), n, BARRIER, END, 0, host_bounds, d_send.data_ptr(),
+                                         d_status.data_ptr(), d_cnt.data_ptr(), d_wrecv.data_ptr(), cap,
+                                         d_final.data_ptr(), d_final_off.data_ptr())
+            status = d_status.cpu().numpy()[:n]
+            got = d_final.cpu().numpy().view(synth.DELIV_DTYPE)[:nrecv].copy()
+            offs = d_final_off.cpu().numpy()
+            assert offs[-1] == nrecv
+            assert np.array_equal(np.diff(offs), np.bincount(got["dst_host"] - host_bounds[rank], minlength=mine))
+            mt = torch.tensor([int(d_cnt.cpu().numpy().view(np.uint64)[1])], dtype=torch.float64)
+            dist.all_reduce(mt, op=dist.ReduceOp.MIN)
+            q.put((rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), table, None))
+            dist.destroy_process_group()
+            return
         cap = max(n, 1) * world
         d_out = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device="cuda")
         d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
@@ -129,7 +154,8 @@ def _worker(rank, world, port, mode, q, runs="1"):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("mode,world,runs", [("replicated", 2, "1"), ("replicated", 3, "1"), ("sharded", 2, "1"),
-                                             ("sharded", 3, "1"), ("replicated", 3, "0"), ("sharded", 2, "0")])
+                                             ("sharded", 3, "1"), ("replicated", 3, "0"), ("sharded", 2, "0"),
+                                             ("fused", 2, "1"), ("fused", 3, "1")])
 def test_multirank_round_through_c_abi(world, mode, runs):
     """runs "1": the owner merges the W received destination-sorted runs in
     place (default); "0": it re-scatters them into destination slabs (the
@@ -155,7 +181,7 @@ def test_multirank_round_through_c_abi(world, mode, runs):
     ips, st, verts = scenario.register_hosts(orc, H, 1)
     sv = np.unique(verts).astype(np.int32)
     lat, rel = orc.rows_parallel(sv, sv, 8)
-    if mode == "replicated":  # every rank's all-gathered table == the oracle's rows
+    if mode in ("replicated", "fused"):  # every rank's all-gathered table == the oracle's rows
         want = np.stack([lat, rel], axis=-1).tobytes()
         assert all(r[4] == want for r in res)
     orc.preload(sv, lat, rel)  # every row released in slot order, as touch_all / the shard adoption
