@@ -142,18 +142,19 @@ def test_unattached_address():
 
 
 @pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor", "slab_readlane", "slab_noagg", "rank_noagg",
-                        "slab_unfused"])
+                        "slab_unfused", "slab_wide"])
 def pipeline(request, monkeypatch):
     """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, the slab
     layout SHD_SLAB_LAYOUT, the segment sort's pass-1 key broadcast
     SHD_SEGSORT_LDS, the wave-aggregated destination slots SHD_DEST_AGG and
-    the one-launch scan + folded overflow placement SHD_ROUND_FUSE, read per
-    launch)."""
+    the folded overflow placement SHD_ROUND_FUSE and the compact 16-B slab
+    records SHD_SLAB_COMPACT, read per launch)."""
     monkeypatch.setenv("SHD_PACKET_PIPELINE", request.param.split("_")[0])
     monkeypatch.setenv("SHD_SLAB_LAYOUT", "rank" if request.param.endswith("rankmajor") else "host")
     monkeypatch.setenv("SHD_SEGSORT_LDS", "0" if request.param.endswith("readlane") else "1")
     monkeypatch.setenv("SHD_DEST_AGG", "0" if request.param.endswith("noagg") else "1")
     monkeypatch.setenv("SHD_ROUND_FUSE", "0" if request.param.endswith("unfused") else "1")
+    monkeypatch.setenv("SHD_SLAB_COMPACT", "0" if request.param.endswith("wide") else "1")
     return request.param
 
 
@@ -425,6 +426,27 @@ def test_every_packet_dropped(pipeline):
     oout, ostatus, omt = orc2.round(ips2, pk2, 110_000_000, 100_000_000)
     assert np.array_equal(status, ostatus) and mt == omt == 2**64 - 1 and len(out) == len(oout) == 0
     assert offs[-1] == 0
+
+
+def test_compact_slab_fallbacks(pipeline):
+    """Events the 16-B compact slab record cannot hold go whole to the 32-B
+    slab (packet.hip CSlab): srcHostEventIDs of 2^32 and more, and self
+    deliveries more than 2^31 ns before the barrier; mixed with compact ones
+    in the same destination segments, and rounds far from time 0."""
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    barrier = 10_000_000_000
+    pk = synth.packet_batch(40000, H, 0x5EED0420, barrier - 10_000_000, 10_000_000, st)
+    rng = np.random.default_rng(0x5EED0421)
+    big = rng.random(len(pk)) < 0.1
+    pk["seq"][big] += np.uint64(1 << 32)  # (src, seq) stays unique: a total order
+    early = np.flatnonzero(rng.random(len(pk)) < 0.05)
+    pk["dst_host"][early] = pk["src_host"][early]
+    pk["now"][early] = barrier - 3_000_000_000  # self delivery ~3 s before the barrier: no clamp
+    out, offs, status, mt = top.round(pk, barrier, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, barrier, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert (out["seq"] >= 1 << 32).sum() > 1000 and (out["time"] < barrier - 2**31).sum() > 100
 
 
 def test_device_api_unknown_hosts_not_delivered(pipeline):
