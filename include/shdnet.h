@@ -383,6 +383,19 @@ int shd_topology_shard_min_latency(ShdTopology* top, const void* d_rows, int row
 int shd_transport_rccl_unique_id(void* id128);
 int shd_transport_rccl_new(int rank, int world, const void* id128, int device, ShdTransport** out);
 void shd_transport_rccl_free(ShdTransport* xport);
+/* One process, several GPUs (Shadow's process model, core/manager.c:543-577),
+ * as ranks that are threads: one topology and one thread per device.
+ * rccl_new_all: ndev RCCL transports from ncclCommInitAll (out[k] drives
+ * devices[k]); free each with shd_transport_rccl_free.  local_new: world
+ * transports with no RCCL -- a collective is a thread barrier plus
+ * device-to-device copies each receiver pulls from the senders' buffers
+ * (peer access between GPUs; a plain copy on one GPU, e.g. to rehearse the
+ * multi-rank rounds with threads on one device); free each with
+ * shd_transport_local_free.  Every rank's thread must take part in every
+ * collective, as with RCCL. */
+int shd_transport_rccl_new_all(int ndev, const int* devices, ShdTransport** out);
+int shd_transport_local_new(int world, ShdTransport** out);
+void shd_transport_local_free(ShdTransport* xport);
 
 /* ---------------------------------------------------------------------- */
 /* Destination routers: router_enqueue + CoDel           */

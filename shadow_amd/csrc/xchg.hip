@@ -14,6 +14,8 @@
 #include <new>
 #include <vector>
 
+#include <pthread.h>
+
 #include "shd_internal.h"
 
 namespace {
@@ -483,6 +485,176 @@ extern "C" void shd_transport_rccl_free(ShdTransport* x) {
     if (t->h_u64) (void)hipHostFree(t->h_u64);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
+}
+
+// ---- in-process transports: one process, one thread and one topology per GPU ----
+// (Shadow is one process with one manager, core/manager.c:543-577.)
+//
+// shd_transport_rccl_new_all: one RCCL communicator per device from
+// ncclCommInitAll; the thread driving device k uses transport k.
+//
+// shd_transport_local_new: no RCCL at all -- the ranks are threads of this
+// process, so a collective is a barrier plus device-to-device copies that
+// each receiver pulls from the senders' published buffers (peer access over
+// xGMI between GPUs, a plain copy on one GPU).  Used to rehearse the
+// multi-rank rounds with threads on one GPU.
+namespace {
+
+struct LocalHub {
+    int world;
+    pthread_barrier_t bar;
+    std::vector<uint64_t> u64;        // world x world count exchange
+    std::vector<const char*> src;     // each rank's published send buffer
+    std::vector<std::vector<uint64_t>> boff; // each rank's block offsets (alltoallv: per peer; allgatherv: per rank)
+    int refs;
+    pthread_mutex_t mu;
+};
+
+struct Local {
+    ShdTransport x;
+    LocalHub* hub;
+    int device;
+};
+
+void hub_wait(LocalHub* h) { pthread_barrier_wait(&h->bar); }
+
+int local_alltoall_u64(void* user, const uint64_t* send, uint64_t* recv) {
+    Local* t = static_cast<Local*>(user);
+    LocalHub* h = t->hub;
+    const int W = h->world, me = t->x.rank;
+    for (int r = 0; r < W; r++) h->u64[(size_t)me * W + r] = send[r];
+    hub_wait(h);
+    for (int r = 0; r < W; r++) recv[r] = h->u64[(size_t)r * W + me];
+    hub_wait(h); // (the slots are reused by the next exchange)
+    return 0;
+}
+
+// every rank publishes its send buffer and per-peer block offsets; each
+// receiver copies its blocks out of the senders' buffers, in rank order
+int local_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
+                    const uint64_t* recv_bytes, void* stream) {
+    Local* t = static_cast<Local*>(user);
+    LocalHub* h = t->hub;
+    const int W = h->world, me = t->x.rank;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = hip_status(hipStreamSynchronize(s), "local alltoallv (send side ready)");
+    h->src[me] = static_cast<const char*>(d_send);
+    std::vector<uint64_t>& o = h->boff[me];
+    o.assign(W + 1, 0);
+    for (int r = 0; r < W; r++) o[r + 1] = o[r] + send_bytes[r];
+    hub_wait(h);
+    uint64_t at = 0;
+    for (int r = 0; r < W && !rc; r++) {
+        if (recv_bytes[r] != h->boff[r][me + 1] - h->boff[r][me]) rc = shd_fail(-EIO, "local alltoallv: block sizes disagree");
+        else if (recv_bytes[r])
+            rc = hip_status(hipMemcpyAsync(static_cast<char*>(d_recv) + at, h->src[r] + h->boff[r][me], recv_bytes[r],
+                                           hipMemcpyDefault, s),
+                            "local alltoallv copy");
+        at += recv_bytes[r];
+    }
+    if (!rc) rc = hip_status(hipStreamSynchronize(s), "local alltoallv");
+    hub_wait(h); // (senders keep their buffers until every receiver copied)
+    return rc;
+}
+
+int local_allgatherv(void* user, void* d_buf, const uint64_t* off, void* stream) {
+    Local* t = static_cast<Local*>(user);
+    LocalHub* h = t->hub;
+    const int W = h->world, me = t->x.rank;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = hip_status(hipStreamSynchronize(s), "local allgatherv (block ready)");
+    h->src[me] = static_cast<const char*>(d_buf);
+    hub_wait(h);
+    for (int r = 0; r < W && !rc; r++)
+        if (r != me && off[r + 1] > off[r])
+            rc = hip_status(hipMemcpyAsync(static_cast<char*>(d_buf) + off[r], h->src[r] + off[r], off[r + 1] - off[r],
+                                           hipMemcpyDefault, s),
+                            "local allgatherv copy");
+    if (!rc) rc = hip_status(hipStreamSynchronize(s), "local allgatherv");
+    hub_wait(h);
+    return rc;
+}
+
+} // namespace
+
+extern "C" int shd_transport_local_new(int world, ShdTransport** out) {
+    if (!out || world < 1 || world > kMaxWorld) return shd_fail(-EINVAL, "bad local transport args");
+    LocalHub* h = new (std::nothrow) LocalHub();
+    if (!h) return -ENOMEM;
+    h->world = world;
+    h->u64.assign((size_t)world * world, 0);
+    h->src.assign(world, nullptr);
+    h->boff.assign(world, std::vector<uint64_t>(world + 1, 0));
+    h->refs = world;
+    if (pthread_barrier_init(&h->bar, nullptr, (unsigned)world) != 0) {
+        delete h;
+        return shd_fail(-EAGAIN, "pthread_barrier_init");
+    }
+    pthread_mutex_init(&h->mu, nullptr);
+    for (int r = 0; r < world; r++) {
+        Local* t = new (std::nothrow) Local();
+        if (!t) return -ENOMEM; // (the transports made so far stay valid; the caller frees them)
+        t->hub = h;
+        t->device = -1;
+        t->x.rank = r;
+        t->x.world = world;
+        t->x.user = t;
+        t->x.alltoall_u64 = local_alltoall_u64;
+        t->x.alltoallv = local_alltoallv;
+        t->x.allgatherv = local_allgatherv;
+        out[r] = &t->x;
+    }
+    return 0;
+}
+
+extern "C" void shd_transport_local_free(ShdTransport* x) {
+    if (!x) return;
+    Local* t = static_cast<Local*>(x->user);
+    LocalHub* h = t->hub;
+    pthread_mutex_lock(&h->mu);
+    const int left = --h->refs;
+    pthread_mutex_unlock(&h->mu);
+    delete t;
+    if (left == 0) {
+        pthread_barrier_destroy(&h->bar);
+        pthread_mutex_destroy(&h->mu);
+        delete h;
+    }
+}
+
+// One communicator per device of this process (ncclCommInitAll); transport
+// k drives devices[k] and is used by the thread driving that device.
+extern "C" int shd_transport_rccl_new_all(int ndev, const int* devices, ShdTransport** out) {
+    if (!out || !devices || ndev < 1 || ndev > kMaxWorld) return shd_fail(-EINVAL, "bad RCCL transport args");
+    std::vector<ncclComm_t> comms(ndev);
+    int rc = nccl_status(ncclCommInitAll(comms.data(), ndev, devices), "ncclCommInitAll");
+    if (rc) return rc;
+    for (int k = 0; k < ndev && !rc; k++) {
+        out[k] = nullptr;
+        if ((rc = shd_dev_init(devices[k]))) break;
+        Rccl* t = new (std::nothrow) Rccl();
+        if (!t) {
+            rc = -ENOMEM;
+            break;
+        }
+        t->device = devices[k];
+        t->comm = comms[k];
+        if ((rc = hip_status(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking), "hipStreamCreate transport")) ||
+            (rc = hip_status(hipMalloc((void**)&t->d_u64, 16 * (size_t)ndev), "hipMalloc transport")) ||
+            (rc = hip_status(hipHostMalloc((void**)&t->h_u64, 16 * (size_t)ndev, hipHostMallocDefault),
+                             "hipHostMalloc transport"))) {
+            delete t;
+            break;
+        }
+        t->x.rank = k;
+        t->x.world = ndev;
+        t->x.user = t;
+        t->x.alltoall_u64 = rccl_alltoall_u64;
+        t->x.alltoallv = rccl_alltoallv;
+        t->x.allgatherv = rccl_allgatherv;
+        out[k] = &t->x;
+    }
+    return rc;
 }
 
 namespace {

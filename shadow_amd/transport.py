@@ -169,3 +169,43 @@ class RcclTransport:
         if self._p:
             lib().shd_transport_rccl_free(self._p)
             self._p = C.c_void_p()
+
+
+class _Rank:
+    """One in-process transport (a rank that is a thread of this process)."""
+
+    def __init__(self, handle, rank, world):
+        self.handle, self.rank, self.world = handle, rank, world
+        self.error = None
+
+    def register(self, *tensors):  # (takes raw device pointers)
+        pass
+
+
+class InProcessTransports:
+    """Transports for ranks that are threads of one process, one topology
+    and one thread per device (include/shdnet.h): ``kind="local"`` --
+    barrier + device-to-device copies, no RCCL (rehearsals with threads on
+    one GPU); ``kind="rccl"`` -- one RCCL communicator per device from
+    ncclCommInitAll (``devices`` lists them).  ``ranks[k]`` goes to the
+    thread driving rank k; every rank's thread takes part in every
+    collective."""
+
+    def __init__(self, world: int, kind: str = "local", devices=None):
+        arr = (C.c_void_p * world)()
+        if kind == "local":
+            check(lib().shd_transport_local_new(world, arr))
+        else:
+            devs = (C.c_int * world)(*(devices if devices is not None else range(world)))
+            check(lib().shd_transport_rccl_new_all(world, devs, arr))
+        self.kind = kind
+        self.ranks = [_Rank(C.c_void_p(arr[k]), k, world) for k in range(world)]
+
+    def close(self):
+        for r in self.ranks:
+            if r.handle and r.handle.value:
+                if self.kind == "local":
+                    lib().shd_transport_local_free(r.handle)
+                else:
+                    lib().shd_transport_rccl_free(r.handle)
+                r.handle = C.c_void_p()
