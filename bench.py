@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03f_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03g_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
@@ -510,15 +510,23 @@ def main():
                 xport.register(r_scr, r_in, r_out, r_recv)
 
             def round4():
-                n4 = P4
-                if world > 1:
-                    n4 = t4.route_records(xport, r_recs.data_ptr(), P4, row_bounds, r_scr.data_ptr(),
-                                          r_in.data_ptr(), cap4, sptr)
-                t4.process_device(r_in.data_ptr(), n4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
-                                  r_status.data_ptr(), r_cnt.data_ptr(), sptr)
-                if world > 1:
+                if world == 1:
+                    t4.process_device(r_in.data_ptr(), P4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
+                                      r_status.data_ptr(), r_cnt.data_ptr(), sptr)
+                    return
+                # records to their answering row's rank, decided there, events to
+                # their destination's owner as grouped 24-B wire records
+                n4 = t4.route_records(xport, r_recs.data_ptr(), P4, row_bounds, r_scr.data_ptr(),
+                                      r_in.data_ptr(), cap4, sptr)
+                if split:
+                    t4.process_device(r_in.data_ptr(), n4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
+                                      r_status.data_ptr(), r_cnt.data_ptr(), sptr)
                     t4.exchange(xport, r_out.data_ptr(), r_off.data_ptr(), host_bounds4, r_recv.data_ptr(), cap4,
                                 r_fin.data_ptr(), r_fin_off.data_ptr(), sptr)
+                else:
+                    t4.process_exchange(xport, r_in.data_ptr(), n4, barrier_t, end_t, 0, host_bounds4, r_out.data_ptr(),
+                                        r_status.data_ptr(), r_cnt.data_ptr(), r_recv.data_ptr(), cap4,
+                                        r_fin.data_ptr(), r_fin_off.data_ptr(), sptr)
 
             for _ in range(3):
                 round4()
