@@ -9,6 +9,8 @@
 #       smoke        __graft_entry__.smoke()
 #       bench[:ARGS] bench.py (ARGS: extra arguments, commas for spaces)
 #       prof[:ARGS]  rocprofv3 --kernel-trace --stats of bench.py
+#       run:CMD      any command (commas for spaces; may start with VAR=value
+#                    assignments), output to run$i.log
 # Every GPU step runs under its own time limit and the first failure ends
 # the call (no further GPU work after a fault, abort or timeout).
 set -o pipefail
@@ -64,6 +66,9 @@ for step in "$@"; do
         (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $D/prof -o prof -- \
             python3 $R/bench.py ${arg//,/ } > $D/prof_bench.json 2> $D/prof_bench.err) || { tail -30 $D/prof_bench.err; exit 1; }
         find $D/prof -name "*kernel_stats.csv" | head -1 ;;
+    run)
+        timeout -k 10 900 env ${arg//,/ } > $D/run$i.log 2>&1 || { tail -30 $D/run$i.log; exit 1; }
+        cat $D/run$i.log ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done

@@ -3,7 +3,8 @@
 algorithm: SHD_SSSP_TOP = LDS heap positions per wave, SHD_SSSP_WAVES) on
 the C2 (and optionally C4) build and checks every variant's table is bitwise
 equal to the first one's.  Usage: routing_variants.py [--c4] VARIANT...
-VARIANT = "kern=blk|slab[,top=256|512][,wpe=7|8][,waves=N]"."""
+VARIANT = "kern=islab|blk|slab[,top=256|512][,wpe=7|8][,waves=N]" (islab: the
+integer-key blocked heap, whole-ms graphs)."""
 import argparse
 import os
 import sys
@@ -36,7 +37,7 @@ def main():
         for v in a.variants:
             kv = dict(x.split("=") for x in v.split(","))
             os.environ["SHD_SSSP_TOP"] = kv.get("top", "256")
-            os.environ["SHD_SSSP_KERNEL"] = kv.get("kern", "blk")
+            os.environ["SHD_SSSP_KERNEL"] = kv.get("kern", "islab")
             os.environ["SHD_SSSP_WPE"] = kv.get("wpe", "8")
             os.environ["SHD_SSSP_LDS_SEQ"] = kv.get("seq", "0")
             if "waves" in kv:

@@ -31,6 +31,8 @@ void shd_topology_release_device(ShdTopology* t) {
     shd_dev_free(t->d_snb);
     shd_dev_free(t->d_swr);
     shd_dev_free(t->d_soff);
+    shd_dev_free(t->d_sl);
+    t->d_sl = NULL;
     t->d_snb = t->d_swr = NULL;
     t->d_soff = NULL;
     t->d_tab = NULL;
@@ -122,7 +124,38 @@ static int prepare(ShdTopology* t) {
             snb[2 * o] = t->v_attached[v] ? -2 : -1;
         }
         for (size_t o = M + (size_t)t->V; o < SM; o++) snb[2 * o] = -1;
-        rc = shd_dev_malloc(&t->d_snb, sizeof(int32_t) * 2 * SM);
+        /* integer-latency copy for k_sssp_islab: every latency a whole
+         * number of ms and every path sum below 2^32 - 1 (a simple path has
+         * < V edges) -- then u32 sums equal the f64 sums bit for bit */
+        int int_ok = 1;
+        double max_w = 0.0;
+        for (size_t k = 0; k < M && int_ok; k++) {
+            if (!(w[k] >= 0.0) || w[k] != (double)(uint32_t)w[k]) int_ok = 0;
+            else if (w[k] > max_w) max_w = w[k];
+        }
+        if (int_ok && (double)t->V * max_w >= 4294967295.0) int_ok = 0;
+        if (int_ok) {
+            /* {int32 nbr, uint32 w, double rel} */
+            unsigned char* sl = (unsigned char*)calloc(SM, 16);
+            if (!sl) {
+                free(snb);
+                free(swr);
+                free(soff);
+                rc = -ENOMEM;
+                goto fail;
+            }
+            for (size_t o = 0; o < SM; o++) {
+                const int32_t nbr = snb[2 * o];
+                const uint32_t wi = nbr >= 0 ? (uint32_t)swr[2 * o] : 0u;
+                memcpy(sl + 16 * o, &nbr, 4);
+                memcpy(sl + 16 * o + 4, &wi, 4);
+                memcpy(sl + 16 * o + 8, &swr[2 * o + 1], 8);
+            }
+            rc = shd_dev_malloc(&t->d_sl, 16 * SM);
+            if (!rc) rc = shd_dev_h2d(t->d_sl, sl, 16 * SM);
+            free(sl);
+        }
+        if (!rc) rc = shd_dev_malloc(&t->d_snb, sizeof(int32_t) * 2 * SM);
         if (!rc) rc = shd_dev_h2d(t->d_snb, snb, sizeof(int32_t) * 2 * SM);
         if (!rc) rc = shd_dev_malloc(&t->d_swr, sizeof(double) * 2 * SM);
         if (!rc) rc = shd_dev_h2d(t->d_swr, swr, sizeof(double) * 2 * SM);
@@ -178,6 +211,7 @@ static ShdGraphDev graph_dev(const ShdTopology* t) {
     g.snb = t->d_snb;
     g.swr = t->d_swr;
     g.soff = t->d_soff;
+    g.sl = t->d_sl;
     return g;
 }
 
@@ -252,12 +286,14 @@ int shd_topology_build_rows_device(ShdTopology* t, int row_lo, int row_hi, void*
 /* ---- single-process multi-GPU build (shd_topology_build_shards) ---- */
 
 /* The device graph arrays of prepare(), with their sizes (bytes). */
-static void graph_arrays(ShdTopology* t, const void* src[9], size_t bytes[9]) {
+#define NGRAPH_ARRAYS 10
+static void graph_arrays(ShdTopology* t, const void* src[NGRAPH_ARRAYS], size_t bytes[NGRAPH_ARRAYS]) {
     const size_t M = (size_t)t->M, V = (size_t)t->V, SM = M + V + 64 * 16;
-    const void* s[9] = {t->d_inc_off, t->d_inc_nbr, t->d_inc_w, t->d_inc_r, t->d_slot_vertex,
-                        t->d_vertex_slot, t->d_snb, t->d_swr, t->d_soff};
-    const size_t b[9] = {4 * (V + 1), 4 * M, 8 * M, 8 * M, 4 * (size_t)t->A, 4 * V, 8 * SM, 16 * SM, 4 * V};
-    for (int k = 0; k < 9; k++) src[k] = s[k], bytes[k] = b[k];
+    const void* s[NGRAPH_ARRAYS] = {t->d_inc_off, t->d_inc_nbr, t->d_inc_w, t->d_inc_r, t->d_slot_vertex,
+                                    t->d_vertex_slot, t->d_snb, t->d_swr, t->d_soff, t->d_sl};
+    const size_t b[NGRAPH_ARRAYS] = {4 * (V + 1), 4 * M, 8 * M, 8 * M, 4 * (size_t)t->A, 4 * V, 8 * SM, 16 * SM, 4 * V,
+                                     t->d_sl ? 16 * SM : 0};
+    for (int k = 0; k < NGRAPH_ARRAYS; k++) src[k] = s[k], bytes[k] = b[k];
 }
 
 typedef struct {
@@ -271,15 +307,15 @@ typedef struct {
 static void* build_shard(void* arg) {
     ShardJob* j = (ShardJob*)arg;
     ShdTopology* t = j->t;
-    const void* src[9];
-    size_t bytes[9];
-    void* dst[9] = {0};
+    const void* src[NGRAPH_ARRAYS];
+    size_t bytes[NGRAPH_ARRAYS];
+    void* dst[NGRAPH_ARRAYS] = {0};
     graph_arrays(t, src, bytes);
     int rc = shd_dev_init(j->device);
     ShdGraphDev g = graph_dev(t);
     if (!rc && j->device != t->device) { /* the graph on this shard's device (peer copies) */
-        for (int k = 0; k < 9 && !rc; k++)
-            if (!(rc = shd_dev_malloc(&dst[k], bytes[k]))) rc = shd_dev_d2d(dst[k], src[k], bytes[k]);
+        for (int k = 0; k < NGRAPH_ARRAYS && !rc; k++)
+            if (bytes[k] && !(rc = shd_dev_malloc(&dst[k], bytes[k]))) rc = shd_dev_d2d(dst[k], src[k], bytes[k]);
         g.inc_off = (const int32_t*)dst[0];
         g.inc_nbr = (const int32_t*)dst[1];
         g.inc_w = (const double*)dst[2];
@@ -289,9 +325,10 @@ static void* build_shard(void* arg) {
         g.snb = dst[6];
         g.swr = dst[7];
         g.soff = (const int32_t*)dst[8];
+        g.sl = dst[9];
     }
     if (!rc) rc = shd_dev_build_rows(&g, t->use_sp, j->lo, j->hi, j->base);
-    for (int k = 0; k < 9; k++) shd_dev_free(dst[k]);
+    for (int k = 0; k < NGRAPH_ARRAYS; k++) shd_dev_free(dst[k]);
     j->rc = rc;
     if (rc) snprintf(j->err, sizeof j->err, "%s", shd_last_error());
     return NULL;

@@ -41,6 +41,7 @@
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
 
 #include "shd_internal.h"
 
@@ -986,6 +987,466 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
     }
 }
 
+// ---- integer-key slab kernel (k_sssp_islab): graphs whose latencies are whole ms ----
+// When every edge latency is a whole number of ms and V * max latency <
+// 2^32 - 1 (ShdGraphDev.sl present), every distance igraph forms -- f64 sums
+// of whole numbers below 2^53 -- is exact, so a u32 holds it bit for bit and
+// the heap compares u32 dist instead of f64 -dist (x.key < c.key <=> dc < dx;
+// ties compare equal in both).  That shrinks a heap node to 8 B {dist, v},
+// and the storage is laid out for few HBM requests per heap operation:
+//  * positions [0, 511) (levels 0..8) in LDS, 4 KiB per wave;
+//  * below, 4-level subtrees ("blocks", roots at levels 9, 13, 17, ...) of 15
+//    nodes in one 128-B line each, so a sink reads the two child blocks of
+//    its hole (the 4 levels under it) with two line requests, walks them
+//    data-parallel, and its moves inside a block all land in that block's line;
+//  * each vertex's 16-B record {dist u32, pos u32, rel f64}: pos is the block
+//    the vertex's node sits in (1: the LDS top, 0: never queued), so only moves
+//    that cross a block boundary write a pos (not every level a node moves),
+//    a decrease-key finds its node among the 15 slots of the line it loads
+//    anyway for the shift-up, and the neighbour gather of a pop brings the
+//    pos of every neighbour with its distance.
+// The list handle no longer rides in the node: the pop reads soff[u] (a 4-B
+// array shared by every wave, L2-resident).  Heap moves are igraph_2wheap's,
+// exactly as in Heap above.
+namespace ik {
+typedef unsigned long long u64;
+constexpr int kTop = 511; // LDS positions: levels 0..8
+constexpr int kTopLv = 9; // first HBM level
+constexpr uint32_t kInf = 0xffffffffu;
+
+struct __attribute__((aligned(16))) Rec {
+    uint32_t d;   // distance in ms (kInf: not reached)
+    uint32_t pos; // 0 never queued, 1 LDS top, block id + 2
+    double rel;
+};
+struct __attribute__((aligned(16))) Ent { // one incidence-list entry (ShdGraphDev.sl)
+    int nbr;
+    uint32_t w;
+    double rel;
+};
+
+__device__ __forceinline__ uint32_t kd(u64 x) { return (uint32_t)(x >> 32); }
+__device__ __forceinline__ int kv(u64 x) { return (int)(uint32_t)x; }
+__device__ __forceinline__ u64 mk(uint32_t d, int v) { return ((u64)d << 32) | (uint32_t)v; }
+__device__ __forceinline__ int lvl(int p) { return 31 - __builtin_clz((unsigned)p + 1); }
+// first block id of block level k: 512 * (16^k - 1) / 15 = 512 * 0x11..1 (k hex ones)
+__host__ __device__ __forceinline__ int bbase(int k) { return (int)((0x11111111u & ((1u << (4 * k)) - 1u)) << 9); }
+__device__ __forceinline__ u64 uni64(u64 x) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 lane64(u64 x, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+    return ((u64)hi << 32) | lo;
+}
+// HBM position p (>= kTop): its block id; *slot = its slot in the block
+__device__ __forceinline__ int bid_of(int p, int* slot) {
+    const int L = lvl(p);
+    const int k = (L - kTopLv) >> 2, Lr = kTopLv + 4 * k, d = L - Lr;
+    *slot = (1 << d) - 1 + ((p + 1) & ((1 << d) - 1));
+    return bbase(k) + ((p + 1) >> d) - (1 << Lr);
+}
+__device__ __forceinline__ uint32_t tag_of(int p) {
+    if (p < kTop) return 1u;
+    int s;
+    return (uint32_t)bid_of(p, &s) + 2u;
+}
+__device__ __forceinline__ int root_of(int bid) {
+    int k = 0;
+    while (bbase(k + 1) <= bid) k++;
+    return bid - bbase(k) + (1 << (kTopLv + 4 * k)) - 1;
+}
+
+// kStats: event counters (SHD_SSSP_STATS=1, measurement only)
+enum { kStPops, kStSinkHbm, kStPush, kStRaiseHbm, kStRaiseLds, kStUpRounds, kStUpClimb, kStLogOvf, kStBatches,
+       kStHeapSum, kStUpHbmRounds, kStN };
+constexpr u64 kSent = ~0ull; // an empty heap slot: dist kInf, vertex -1
+
+// A heap place: b < 0: LDS position s; else slot s of HBM block b.
+// Block navigation (no positions needed):
+//  * children of LDS position s at level 8: the roots of blocks 2s - 510, 2s - 509;
+//  * children of bottom slot s (7..14) of block b: the roots of blocks
+//    16b + 2s + 498 and the next one (independent of the block level);
+//  * parent of the root of block b: LDS position (b + 510) / 2 when b < 512,
+//    else slot 7 + ((b - 512) & 15) / 2 of block (b - 512) / 16.
+// Every slot at or past the heap's end holds kSent, so the sink and the
+// decrease-key search need no size tests: an empty child is never the
+// larger one and never larger than the sinking node.
+template <bool kStats>
+struct Heap {
+    unsigned long long st[kStats ? kStN : 1];
+    __device__ __forceinline__ void stat(int i, unsigned long long x = 1) {
+        if (kStats) st[i] += x;
+    }
+    u64* top;    // LDS: position p at top[p + 1] (a sibling pair is one aligned 16-B read); top[0] scratch
+    u64* blk;    // 16 u64 per block (slot 15 unused)
+    Rec* rec;
+    int n;
+    int lane;
+    int nblk;
+    // pos stores made since the current batch's gather (which read the
+    // neighbours' pos): lane i holds entry i; nlog > 64 = overflowed
+    int log_v;
+    uint32_t log_t;
+    int nlog;
+
+    __device__ __forceinline__ void set_pos(int v, uint32_t t) {
+        rec[v].pos = t;
+        __asm__ volatile("; ipos store" ::: "memory");
+        if (lane == nlog) log_v = v, log_t = t;
+        nlog++;
+    }
+    // v's pos: the last logged store, else the gathered value g (or a fresh
+    // load when the log overflowed)
+    __device__ __forceinline__ uint32_t pos_of(int v, uint32_t g) {
+        if (nlog > 64) {
+            stat(kStLogOvf);
+            return (uint32_t)__builtin_amdgcn_readfirstlane((int)rec[v].pos);
+        }
+        const unsigned long long m = __ballot(lane < nlog && log_v == v);
+        if (!m) return g;
+        return (uint32_t)__builtin_amdgcn_readlane((int)log_t, 63 - __builtin_clzll(m));
+    }
+    // the place of position p
+    __device__ __forceinline__ static void loc_of(int p, int& b, int& s) {
+        if (p < kTop) {
+            b = -1, s = p;
+        } else {
+            b = bid_of(p, &s);
+        }
+    }
+    __device__ __forceinline__ static uint32_t tag(int b) { return b < 0 ? 1u : (uint32_t)b + 2u; }
+    // node x into place (b, s) by lane l (l < 0: every lane, same value)
+    __device__ __forceinline__ void put(int b, int s, u64 x, int l = -1) {
+        if (b < 0) {
+            if (l < 0 || lane == l) top[s + 1] = x;
+            __asm__ volatile("; iput lds" ::: "memory");
+        } else {
+            if (l < 0 || lane == l) blk[(size_t)b * 16 + s] = x;
+            __asm__ volatile("; iput hbm" ::: "memory");
+        }
+    }
+
+    // Shift-up of x from place (b, s); returns x's new pos tag.  One round
+    // per storage unit: the ancestors from the parent up to the top of the
+    // parent's block (or every LDS ancestor) are compared at once, one per
+    // lane, a ballot says which x is not smaller than (the nearest cnt, heap
+    // order), and those move one level down the path.  se >= 0: (b, s) is in
+    // a block whose line the caller holds (lane s = slot s), so a first round
+    // inside that block needs no load.
+    __device__ __forceinline__ uint32_t up(int b, int s, u64 x, u64 line = 0, bool held = false) {
+        const uint32_t dx = kd(x);
+        for (;;) {
+            if (b < 0 && s == 0) break; // the root
+            // the round's unit: ub < 0: LDS, ancestors from position ps up;
+            // else block ub, ancestors from slot ps up
+            int ub, ps;
+            if (b < 0) {
+                ub = -1, ps = (s - 1) >> 1;
+            } else if (s > 0) {
+                ub = b, ps = (s - 1) >> 1;
+            } else if (b < 512) {
+                ub = -1, ps = (b + 510) >> 1;
+            } else {
+                ub = (b - 512) >> 4, ps = 7 + (((b - 512) & 15) >> 1);
+            }
+            const int K = lvl(ps) + 1;
+            const int sa = ((ps + 1) >> lane) - 1; // lane j: j-th ancestor in the unit
+            u64 c = 0;
+            stat(kStUpRounds);
+            if (ub < 0) {
+                if (lane < K) c = top[sa + 1];
+                __asm__ volatile("; iup lds" ::: "memory");
+            } else {
+                stat(kStUpHbmRounds);
+                if (held && ub == b) {
+                    const int src = lane < K ? sa : 0;
+                    const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(4 * src, (int)(uint32_t)line);
+                    const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(4 * src, (int)(uint32_t)(line >> 32));
+                    c = ((u64)hi << 32) | lo;
+                } else if (lane < K) {
+                    c = blk[(size_t)ub * 16 + sa];
+                }
+                __asm__ volatile("; iup hbm" ::: "memory");
+            }
+            held = false;
+            const unsigned long long m = __ballot(lane < K && dx <= kd(c)); // x climbs past these
+            const int cnt = (int)__builtin_ctzll(~m);
+            if (cnt == 0) break;
+            stat(kStUpClimb);
+            // ancestor 0 into x's place, ancestor j >= 1 into ancestor j-1's
+            put(b, s, c, 0);
+            if (lane >= 1 && lane < cnt) {
+                const int q = ((ps + 1) >> (lane - 1)) - 1;
+                if (ub < 0) {
+                    top[q + 1] = c;
+                    __asm__ volatile("; iup mv lds" ::: "memory");
+                } else {
+                    blk[(size_t)ub * 16 + q] = c;
+                    __asm__ volatile("; iup mv hbm" ::: "memory");
+                }
+            }
+            if (b >= 0 && s == 0) set_pos(kv(lane64(c, 0)), tag(b)); // crossed into x's old block
+            b = ub, s = ((ps + 1) >> (cnt - 1)) - 1;
+            if (cnt < K) break;
+        }
+        put(b, s, x);
+        return tag(b);
+    }
+    __device__ __forceinline__ uint32_t push(int v, uint32_t d) {
+        stat(kStPush);
+        int b, s;
+        loc_of(n++, b, s);
+        return up(b, s, mk(d, v));
+    }
+    // igraph_2wheap_modify with a smaller distance: a shift-up at v's node.
+    // A pos that names no node holding v (never expected) is counted in *err
+    // and the update skipped: the launch then fails instead of reading
+    // outside the slab.
+    __device__ __forceinline__ uint32_t raise(int v, uint32_t d, uint32_t t, unsigned* err) {
+        stat(t == 1u ? kStRaiseLds : kStRaiseHbm);
+        if (t == 1u) {
+            int found = -1;
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                if (q * 64 + lane < kTop && kv(top[q * 64 + lane + 1]) == v) found = q * 64 + lane;
+            const unsigned long long bm = __ballot(found >= 0);
+            if (!bm) {
+                if (lane == 0) atomicOr(err, 1u);
+                return t;
+            }
+            const int e = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(found, __builtin_ctzll(bm)));
+            return up(-1, e, mk(d, v));
+        }
+        if (t < 2u || (int)(t - 2u) >= nblk) {
+            if (lane == 0) atomicOr(err, 2u);
+            return t;
+        }
+        const int b = (int)t - 2;
+        u64 c = kSent;
+        if (lane < 15) c = blk[(size_t)b * 16 + lane];
+        __asm__ volatile("; iraise find" ::: "memory");
+        const unsigned long long bm = __ballot(lane < 15 && kv(c) == v);
+        if (!bm) {
+            if (lane == 0) atomicOr(err, 4u);
+            return t;
+        }
+        return up(b, __builtin_ctzll(bm), mk(d, v), c, true);
+    }
+
+    // delete_max's sink of x (the old last node, whose place had tag tfrom)
+    // from the root: the LDS levels one per step, branch-free on the vector
+    // unit (every lane computes the same walk), then the HBM levels four at a
+    // time -- the two child blocks of the hole, one node per lane, walked
+    // data-parallel (ballots: which sibling is larger, which nodes x is
+    // larger than), each moved node stored one level up by its own lane
+    __device__ __forceinline__ void sink(u64 x, uint32_t tfrom) {
+        const uint32_t dx = kd(x);
+        int ev = 0;
+        bool alive = true;
+#pragma unroll 1
+        for (int it = 0; it < kTopLv - 1; it++) {
+            if (__ballot(alive) == 0ull) break;
+            const int l = 2 * ev + 1;
+            const uint4 pr = *reinterpret_cast<const uint4*>(top + l + 1);
+            __asm__ volatile("; isink lds" ::: "memory");
+            const bool right = pr.w < pr.y;
+            const uint32_t dc = right ? pr.w : pr.y;
+            const uint32_t vc = right ? pr.z : pr.x;
+            const bool mv = alive && dc < dx;
+            top[mv ? ev + 1 : 0] = ((u64)dc << 32) | vc;
+            __asm__ volatile("; isink mv lds" ::: "memory");
+            ev = mv ? l + (right ? 1 : 0) : ev;
+            alive = mv;
+        }
+        int hb = -1, hs = __builtin_amdgcn_readfirstlane(ev);
+        if (__ballot(alive) != 0ull) { // the hole reached level 8: HBM blocks
+            const int j = 31 - __builtin_clz((unsigned)lane + 2); // lane's level under the hole
+            const int bi = lane + 2 - (1 << j);                    // ... and index in that level
+            const int sb = bi >> (j - 1);                          // child block 0 / 1
+            const int bslot = (1 << (j - 1)) - 1 + (bi & ((1 << (j - 1)) - 1)); // slot in it
+            for (;;) {
+                const int b0 = hb < 0 ? 2 * hs - 510 : 16 * hb + 2 * hs + 498;
+                if (b0 + 1 >= nblk) break; // (no block there: past every possible heap position)
+                stat(kStSinkHbm);
+                u64 c = kSent;
+                if (j <= 4) c = blk[(size_t)(b0 + sb) * 16 + bslot];
+                __asm__ volatile("; isink hbm" ::: "memory");
+                const uint32_t dc = kd(c);
+                const uint32_t dsib = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)dc, 0xB1, 0xF, 0xF, false);
+                // rm bit at a left child: the right sibling is larger (smaller
+                // dist; an empty right sibling never is)
+                const unsigned long long rm = __ballot((lane & 1) == 0 && dsib < dc);
+                const bool larger = (int)((rm >> (lane & ~1)) & 1ull) == (lane & 1);
+                const unsigned long long g = __ballot(j <= 4 && larger && dc < dx);
+                bool mvl = (g >> lane) & 1ull;
+#pragma unroll
+                for (int i = 1; i < 4; i++)
+                    if (i < j) mvl = mvl && ((g >> ((2 << (i - 1)) - 2 + (bi >> (j - i)))) & 1ull);
+                const unsigned long long mv = __ballot(mvl);
+                if (mv == 0ull) break;
+                const int lv = __builtin_popcountll(mv);
+                const int l1 = __builtin_ctzll(mv);
+                // the level-1 mover into the hole (the LDS or the parent block: a crossing)
+                put(hb, hs, c, l1);
+                set_pos(kv(lane64(c, l1)), tag(hb));
+                if (mvl && j > 1) { // the others one level up inside their block
+                    blk[(size_t)(b0 + sb) * 16 + ((bslot - 1) >> 1)] = c;
+                    __asm__ volatile("; isink mv blk" ::: "memory");
+                }
+                const int hl = 63 - __builtin_clzll(mv); // the new hole: the deepest mover's place
+                hb = b0 + __builtin_amdgcn_readlane(sb, hl);
+                hs = __builtin_amdgcn_readlane(bslot, hl);
+                if (lv < 4) break;
+            }
+        }
+        put(hb, hs, x);
+        if (tag(hb) != tfrom) set_pos(kv(x), tag(hb));
+    }
+};
+
+// blocks a wave's heap needs for positions < V (+1: a hole's child pair):
+// those of the deepest block level in use hold every root of its top level
+// up to position V - 1
+__host__ __device__ __forceinline__ int blk_count(long V) {
+    if (V <= kTop) return 0;
+    const long p = V - 1;
+    int L = 0;
+    while ((2L << L) <= p + 1) L++;
+    const int k = (L - kTopLv) >> 2, Lr = kTopLv + 4 * k;
+    long roots = p - (1L << Lr) + 2; // roots at level Lr with position <= p
+    if (roots > (1L << Lr)) roots = 1L << Lr;
+    return (int)(bbase(k) + roots) + 1;
+}
+} // namespace ik
+
+// Slab per wave: nblk 128-B heap blocks, then V 16-B records.
+template <bool kStats>
+__global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_sssp_islab(
+    ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab, char* __restrict__ slab, size_t slab_stride,
+    size_t nblk, unsigned* __restrict__ err, unsigned long long* __restrict__ stats) {
+    using namespace ik;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
+    const int gw = (int)blockIdx.x * wpb + w, nw = (int)gridDim.x * wpb;
+    const int V = g.V, A = g.A;
+    u64* top = reinterpret_cast<u64*>(smem) + w * (kTop + 1);
+    u64* blk = reinterpret_cast<u64*>(slab + (size_t)gw * slab_stride);
+    Rec* rec = reinterpret_cast<Rec*>(blk + nblk * 16);
+    const Ent* __restrict__ sl = static_cast<const Ent*>(g.sl);
+    const int* __restrict__ soff = g.soff;
+    // every heap slot starts empty (and is emptied again at the end of a row)
+    for (int q = lane; q <= kTop; q += 64) top[q] = kSent;
+    for (size_t q = lane; q < nblk * 16; q += 64) blk[q] = kSent;
+
+    for (int row = row_lo + gw; row < row_hi; row += nw) {
+        const int src = g.slot_vertex[row];
+        for (int v = lane; v < V; v += 64) rec[v] = Rec{kInf, 0u, 0.0};
+        wave_fence();
+        ik::Heap<kStats> h;
+        h.top = top, h.blk = blk, h.rec = rec, h.n = 0, h.lane = lane, h.nblk = (int)nblk;
+        h.log_v = 0, h.log_t = 0u, h.nlog = 0;
+        if (kStats)
+            for (int i = 0; i < kStN; i++) h.st[i] = 0;
+        rec[src] = Rec{0u, 1u, 1.0};
+        top[1] = mk(0u, src);
+        h.n = 1;
+        int to_reach = A;
+        // the next root's list handle, loaded right after the sink (the
+        // updates that follow rarely replace the root): pv = its vertex
+        int pv = -1, pso = 0;
+        while (h.n > 0 && to_reach > 0) {
+            h.stat(kStPops);
+            h.stat(kStHeapSum, (unsigned long long)h.n);
+            const u64 t = uni64(top[1]); // LDS (the root)
+            const int u = kv(t);
+            const uint32_t du = kd(t);
+            const int so = u == pv ? uni(pso) : uni(soff[u]);
+            int b = so >> 8;
+            // issued together: u's entries (lanes past the sentinel re-read
+            // it), the last heap node (the removal sinks it) and rel[u]
+            const int li = lane < (so & 255) ? lane : (so & 255) - 1;
+            Ent en = sl[b + li];
+            // the last node (the removal sinks it); its place becomes empty
+            const int last = --h.n;
+            int lb, ls;
+            h.loc_of(last, lb, ls);
+            u64 xl;
+            if (lb < 0) {
+                xl = top[ls + 1];
+                top[ls + 1] = kSent;
+                __asm__ volatile("; ilast lds" ::: "memory");
+            } else {
+                xl = blk[(size_t)lb * 16 + ls];
+                blk[(size_t)lb * 16 + ls] = kSent;
+                __asm__ volatile("; ilast hbm" ::: "memory");
+            }
+            const double ru_l = rec[u].rel;
+            bool first = true;
+            double ru = 0.0;
+            for (;;) {
+                h.stat(kStBatches);
+                const unsigned long long sm = __ballot(en.nbr < 0);
+                const int fs = sm ? __builtin_ctzll(sm) : 64;
+                const bool ok = lane < fs && en.nbr != u;
+                // neighbour {dist, pos} gathers
+                u64 cur = ok ? *reinterpret_cast<const u64*>(&rec[en.nbr]) : 0ull;
+                h.nlog = 0;
+                if (first) {
+                    if (last > 0) h.sink(uni64(xl), h.tag(lb));
+                    // (the wait for rel[u] covers every load issued so far:
+                    // the prefetch goes after it, not into it)
+                    ru = uni_d(ru_l);
+                    pv = h.n > 0 ? kv(uni64(top[1])) : -1;
+                    if (pv >= 0) pso = soff[pv];
+                    first = false;
+                }
+                __asm__ volatile("" : "+v"(cur));
+                if (fs < 64 && __builtin_amdgcn_readlane(en.nbr, fs) == -2) --to_reach;
+                const uint32_t alt = du + en.w;
+                const double rv = ru * en.rel;
+                const uint32_t cd = (uint32_t)cur;
+                unsigned long long m = __ballot(ok && alt < cd);
+                const unsigned long long fm = __ballot(ok && cd == kInf);
+                while (m) { // igraph's order: incidence order, one edge at a time
+                    const int l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const int vv = __builtin_amdgcn_readlane(en.nbr, l);
+                    const uint32_t aa = (uint32_t)__builtin_amdgcn_readlane((int)alt, l);
+                    uint32_t tg;
+                    if ((fm >> l) & 1ull) {
+                        tg = h.push(vv, aa);
+                    } else {
+                        const uint32_t gp = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cur >> 32), l);
+                        tg = h.raise(vv, aa, h.pos_of(vv, gp), err);
+                    }
+                    rec[vv] = Rec{aa, tg, readlane_d(rv, l)};
+                    __asm__ volatile("; irec store" ::: "memory");
+                    if (lane == h.nlog) h.log_v = vv, h.log_t = tg;
+                    h.nlog++;
+                }
+                if (fs < 64) break;
+                b += 64; // lists longer than 64 entries: next batch
+                en = sl[b + lane];
+            }
+        }
+        // empty the heap for the next row (slots past n are empty already)
+        for (int q = lane; q <= kTop; q += 64) top[q] = kSent;
+        for (int q = lane, e = blk_count(h.n) * 16; q < e; q += 64) blk[q] = kSent;
+        wave_fence();
+        write_row(g, row, src, tab, lane, [&](int v, double& l, double& r) {
+            const Rec x = rec[v];
+            l = x.d == kInf ? -1.0 : (double)x.d;
+            r = x.rel;
+        });
+        wave_fence();
+        if (kStats && lane == 0)
+            for (int i = 0; i < kStN; i++) atomicAdd(&stats[i], h.st[i]);
+    }
+}
+
 // _topology_lookupDirectPath (topology.c:1816-1858): the (s,d) edge itself.
 __global__ __launch_bounds__(256) void k_direct_rows(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab) {
     const int A = g.A;
@@ -1094,6 +1555,66 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
                                slab, bstride, nblk);
         rc = hip_status(hipGetLastError(), "k_sssp_blk launch");
         if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_blk");
+        (void)hipFree(slab);
+        return rc;
+    }
+    // whole-ms latencies: the integer-key blocked heap (SHD_SSSP_KERNEL=slab:
+    // the f64 slab kernel for every graph)
+    if (g.sl && !(kern && strcmp(kern, "slab") == 0)) {
+        const size_t nblk = (size_t)ik::blk_count(g.V) + 1; // (+1: a right sibling block past the last)
+        const size_t stride = (nblk * 128 + sizeof(ik::Rec) * (size_t)g.V + 255) & ~(size_t)255;
+        int dev = 0, cus = 0;
+        if ((rc = hip_status(hipGetDevice(&dev), "hipGetDevice")) ||
+            (rc = hip_status(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
+                             "hipDeviceGetAttribute")))
+            return rc;
+        long waves = (long)cus * kWavesPerCU;
+        if (const char* e = getenv("SHD_SSSP_WAVES")) {
+            const long x = atol(e);
+            if (x > 0) waves = x;
+        }
+        if (waves > rows) waves = rows;
+        int grid = (int)((waves + kSlabWaves - 1) / kSlabWaves);
+        char* slab = nullptr;
+        while (hipMalloc((void**)&slab, stride * kSlabWaves * (size_t)grid) != hipSuccess) {
+            (void)hipGetLastError();
+            if (grid <= 16) return shd_fail(-ENOMEM, "cannot allocate SSSP workspace");
+            grid /= 2;
+        }
+        const size_t lds = sizeof(unsigned long long) * (ik::kTop + 1) * kSlabWaves;
+        unsigned* err = nullptr; // heap-consistency fault bits (raise)
+        if ((rc = hip_status(hipMalloc((void**)&err, sizeof *err), "hipMalloc")) ||
+            (rc = hip_status(hipMemset(err, 0, sizeof *err), "hipMemset"))) {
+            (void)hipFree(slab);
+            return rc;
+        }
+        // SHD_SSSP_STATS=1: the counting build of the kernel, totals to stderr
+        const char* st_env = getenv("SHD_SSSP_STATS");
+        unsigned long long* stats = nullptr;
+        if (st_env && atoi(st_env) == 1 && hipMalloc((void**)&stats, 8 * ik::kStN) == hipSuccess) {
+            (void)hipMemset(stats, 0, 8 * ik::kStN);
+            hipLaunchKernelGGL(k_sssp_islab<true>, dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo, row_hi,
+                               tab, slab, stride, nblk, err, stats);
+        } else {
+            hipLaunchKernelGGL(k_sssp_islab<false>, dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo, row_hi,
+                               tab, slab, stride, nblk, err, nullptr);
+        }
+        rc = hip_status(hipGetLastError(), "k_sssp_islab launch");
+        if (!rc) rc = hip_status(hipDeviceSynchronize(), "k_sssp_islab");
+        if (stats) {
+            unsigned long long h[ik::kStN] = {0};
+            if (!rc && hipMemcpy(h, stats, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
+                static const char* nm[ik::kStN] = {"pops",      "sink_hbm_iters", "push",      "raise_hbm",
+                                                   "raise_lds", "up_rounds",      "up_climbs", "log_overflow",
+                                                   "batches",   "heap_size_sum",  "up_hbm_rounds"};
+                for (int i = 0; i < ik::kStN; i++) fprintf(stderr, "islab_stat %s %llu\n", nm[i], h[i]);
+            }
+            (void)hipFree(stats);
+        }
+        unsigned herr = 0;
+        if (!rc) rc = hip_status(hipMemcpy(&herr, err, sizeof herr, hipMemcpyDeviceToHost), "hipMemcpy");
+        if (!rc && herr) rc = shd_fail(-EIO, "k_sssp_islab: heap position fault %#x", herr);
+        (void)hipFree(err);
         (void)hipFree(slab);
         return rc;
     }

@@ -71,6 +71,11 @@ typedef struct {
     const void* snb;
     const void* swr;
     const int32_t* soff; /* V */
+    /* integer-latency lists (same offsets and sentinels as snb): 16-B entries
+     * {nbr, (uint32) w_ms, 1 - loss}; present only when every edge latency is
+     * a whole number of ms and V * max latency < 2^32 - 1, so that every path
+     * sum the f64 kernel would form is an exact u32 (k_sssp_islab) */
+    const void* sl;
 } ShdGraphDev;
 
 typedef struct {

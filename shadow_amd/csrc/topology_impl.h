@@ -127,6 +127,7 @@ struct ShdTopology {
     uint32_t* h_host_info;
     double *d_inc_w, *d_inc_r;
     void *d_snb, *d_swr; /* sentinel-terminated incidence lists (slab kernel) */
+    void* d_sl;          /* integer-latency form of the same lists (NULL: not eligible) */
     int32_t* d_soff;
     uint32_t *d_touch, *d_pair_bits;
 

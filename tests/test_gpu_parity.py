@@ -62,8 +62,10 @@ def test_routing_table_bit_exact(name):
 
 @pytest.mark.parametrize("name", ["sparse5000_hbm", "sparse4500_dir_ns_hbm", "dense4400_hbm"])
 def test_flat_slab_kernel_bit_exact(name, monkeypatch):
-    """The flat-slab heap (SHD_SSSP_KERNEL=slab, heap position p at rest[p + 1])
-    kept beside the default blocked-slab heap: same rows, bit for bit."""
+    """The f64 flat-slab heap (SHD_SSSP_KERNEL=slab, heap position p at
+    rest[p + 1]; the default for graphs with fractional-ms latencies) forced on
+    whole-ms graphs too, where the integer-key blocked heap is the default:
+    same rows, bit for bit."""
     monkeypatch.setenv("SHD_SSSP_KERNEL", "slab")
     gml, H = GRAPHS[name]
     top, orc, _, _ = make_pair(gml, H)
@@ -72,6 +74,30 @@ def test_flat_slab_kernel_bit_exact(name, monkeypatch):
         ol, orl = orc.row(int(s), sv)
         assert np.array_equal(bits(lat[i]), bits(ol)), (name, i)
         assert np.array_equal(bits(rel[i]), bits(orl)), (name, i)
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_int_blocked_heap_deep_levels(directed):
+    """Heaps of more than 8,191 nodes: the integer-key kernel's second level of
+    HBM blocks (roots at level 13) and the crossings between block levels, on
+    a dense whole-ms graph (V = 12,000, average degree 40), sampled rows
+    against the oracle and every row against the f64 slab kernel."""
+    import os
+    gml = synth.sparse_graph_gml(12000, 0x5EED0072, avg_degree=40.0, directed=directed)
+    top, orc, _, _ = make_pair(gml, 60)
+    lat, rel, sv = top.table()
+    for i in range(0, len(sv), max(1, len(sv) // 12)):
+        ol, orl = orc.row(int(sv[i]), sv)
+        assert np.array_equal(bits(lat[i]), bits(ol)), i
+        assert np.array_equal(bits(rel[i]), bits(orl)), i
+    os.environ["SHD_SSSP_KERNEL"] = "slab"
+    try:
+        top2, _, _, _ = make_pair(gml, 60)
+        lat2, rel2, _ = top2.table()
+    finally:
+        del os.environ["SHD_SSSP_KERNEL"]
+    assert np.array_equal(bits(lat), bits(lat2))
+    assert np.array_equal(bits(rel), bits(rel2))
 
 
 @pytest.mark.parametrize("waves", [1, 6])
