@@ -1195,11 +1195,100 @@ struct Heap {
         put(b, s, x);
         return tag(b);
     }
+    // Shift-up of x from HBM place (b, s) (b >= 0) with the first round
+    // fused: the ancestors inside b (from the held line when `held`, lane q
+    // = slot q) and those of b's parent unit (b's parent's block, or every
+    // LDS ancestor) are compared in one round, so a climb that leaves its
+    // block still costs one memory round trip.  Returns x's new pos tag.
+    __device__ __forceinline__ uint32_t up2(int b, int s, u64 x, u64 line, bool held) {
+        const uint32_t dx = kd(x);
+        const int ds = lvl(s); // ancestors inside b: slots ((s + 1) >> j) - 1, j = 1..ds
+        // b's parent unit: pb < 0: the LDS, ancestors from position pp up; else block pb from slot pp up
+        int pb, pp;
+        if (b < 512) {
+            pb = -1, pp = (b + 510) >> 1;
+        } else {
+            pb = (b - 512) >> 4, pp = 7 + (((b - 512) & 15) >> 1);
+        }
+        const int pK = lvl(pp) + 1;
+        const int K = ds + pK;
+        // lane j < ds: in-block ancestor j + 1; ds <= j < K: parent-unit ancestor i = j - ds
+        const bool inb = lane < ds;
+        const int i = lane - ds;
+        const int qa = ((s + 1) >> (lane + 1)) - 1; // in-block ancestor slot (lane < ds)
+        const int qp = ((pp + 1) >> (i < 0 ? 0 : i)) - 1; // parent-unit place (lane >= ds)
+        u64 c = 0;
+        if (held) {
+            const int src = inb ? qa : 0;
+            const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(4 * src, (int)(uint32_t)line);
+            const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(4 * src, (int)(uint32_t)(line >> 32));
+            c = ((u64)hi << 32) | lo;
+        } else if (inb) {
+            c = blk[(size_t)b * 16 + qa];
+        }
+        if (!inb && lane < K) {
+            if (pb < 0) {
+                c = top[qp + 1];
+                __asm__ volatile("; iup2 lds" ::: "memory");
+            } else {
+                c = blk[(size_t)pb * 16 + qp];
+                __asm__ volatile("; iup2 hbm" ::: "memory");
+            }
+        }
+        stat(kStUpRounds);
+        stat(kStUpHbmRounds);
+        const unsigned long long m = __ballot(lane < K && dx <= kd(c)); // x climbs past these
+        const int cnt = (int)__builtin_ctzll(~m);
+        if (cnt == 0) {
+            put(b, s, x);
+            return tag(b);
+        }
+        stat(kStUpClimb);
+        // ancestor j moves into ancestor j-1's place (j = 0: x's place):
+        // in b for j <= ds (j = ds: b's root, a crossing), else in the parent unit
+        if (lane < cnt) {
+            if (lane <= ds) {
+                const int q = lane == 0 ? s : ((s + 1) >> lane) - 1;
+                blk[(size_t)b * 16 + q] = c;
+                __asm__ volatile("; iup2 mv blk" ::: "memory");
+            } else {
+                const int q = ((pp + 1) >> (i - 1)) - 1;
+                if (pb < 0) {
+                    top[q + 1] = c;
+                    __asm__ volatile("; iup2 mv lds" ::: "memory");
+                } else {
+                    blk[(size_t)pb * 16 + q] = c;
+                    __asm__ volatile("; iup2 mv pblk" ::: "memory");
+                }
+            }
+        }
+        if (cnt > ds) set_pos(kv(lane64(c, ds)), tag(b)); // parent-unit ancestor 0 crossed into b
+        if (cnt <= ds) { // x stays in b
+            const int q = ((s + 1) >> cnt) - 1;
+            put(b, q, x);
+            return tag(b);
+        }
+        const int q = ((pp + 1) >> (cnt - 1 - ds)) - 1; // x's place in the parent unit
+        if (cnt < K || pb < 0) {
+            put(pb, q, x);
+            return tag(pb);
+        }
+        return up(pb, q, x); // climbed past the whole parent block (q = its root)
+    }
+    // the place of position n, when the caller knows it (the pop's emptied
+    // place is where the first push of the pop goes)
+    int cb_p = -1, cb_b = 0, cb_s = 0;
     __device__ __forceinline__ uint32_t push(int v, uint32_t d) {
         stat(kStPush);
         int b, s;
-        loc_of(n++, b, s);
-        return up(b, s, mk(d, v));
+        if (n == cb_p) {
+            b = cb_b, s = cb_s;
+        } else {
+            loc_of(n, b, s);
+        }
+        n++;
+        if (b < 0) return up(b, s, mk(d, v));
+        return up2(b, s, mk(d, v), 0, false);
     }
     // igraph_2wheap_modify with a smaller distance: a shift-up at v's node.
     // A pos that names no node holding v (never expected) is counted in *err
@@ -1233,7 +1322,7 @@ struct Heap {
             if (lane == 0) atomicOr(err, 4u);
             return t;
         }
-        return up(b, __builtin_ctzll(bm), mk(d, v), c, true);
+        return up2(b, __builtin_ctzll(bm), mk(d, v), c, true);
     }
 
     // delete_max's sink of x (the old last node, whose place had tag tfrom)
@@ -1267,6 +1356,10 @@ struct Heap {
             const int bi = lane + 2 - (1 << j);                    // ... and index in that level
             const int sb = bi >> (j - 1);                          // child block 0 / 1
             const int bslot = (1 << (j - 1)) - 1 + (bi & ((1 << (j - 1)) - 1)); // slot in it
+            // the lane's ancestors at levels 1..3 under the hole (itself where it has none)
+            const int an1 = j > 1 ? (bi >> (j - 1)) : lane;
+            const int an2 = j > 2 ? 2 + (bi >> (j - 2)) : lane;
+            const int an3 = j > 3 ? 6 + (bi >> (j - 3)) : lane;
             for (;;) {
                 const int b0 = hb < 0 ? 2 * hs - 510 : 16 * hb + 2 * hs + 498;
                 if (b0 + 1 >= nblk) break; // (no block there: past every possible heap position)
@@ -1279,12 +1372,12 @@ struct Heap {
                 // rm bit at a left child: the right sibling is larger (smaller
                 // dist; an empty right sibling never is)
                 const unsigned long long rm = __ballot((lane & 1) == 0 && dsib < dc);
-                const bool larger = (int)((rm >> (lane & ~1)) & 1ull) == (lane & 1);
+                const uint32_t larger = (uint32_t)((rm >> (lane & ~1)) ^ (unsigned long long)lane ^ 1ull) & 1u;
                 const unsigned long long g = __ballot(j <= 4 && larger && dc < dx);
-                bool mvl = (g >> lane) & 1ull;
-#pragma unroll
-                for (int i = 1; i < 4; i++)
-                    if (i < j) mvl = mvl && ((g >> ((2 << (i - 1)) - 2 + (bi >> (j - i)))) & 1ull);
+                // a lane moves iff it and its ancestors in the block pair are all g
+                const uint32_t mvb = (uint32_t)(g >> lane) & (uint32_t)(g >> an1) & (uint32_t)(g >> an2) &
+                                     (uint32_t)(g >> an3) & 1u;
+                const bool mvl = mvb != 0u;
                 const unsigned long long mv = __ballot(mvl);
                 if (mv == 0ull) break;
                 const int lv = __builtin_popcountll(mv);
@@ -1373,6 +1466,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
             const int last = --h.n;
             int lb, ls;
             h.loc_of(last, lb, ls);
+            h.cb_p = last, h.cb_b = lb, h.cb_s = ls;
             u64 xl;
             if (lb < 0) {
                 xl = top[ls + 1];
