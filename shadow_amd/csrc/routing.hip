@@ -1043,10 +1043,13 @@ __device__ __forceinline__ u64 lane64(u64 x, int l) {
 }
 // HBM position p (>= kTop): its block id; *slot = its slot in the block
 __device__ __forceinline__ int bid_of(int p, int* slot) {
-    const int L = lvl(p);
-    const int k = (L - kTopLv) >> 2, Lr = kTopLv + 4 * k, d = L - Lr;
-    *slot = (1 << d) - 1 + ((p + 1) & ((1 << d) - 1));
-    return bbase(k) + ((p + 1) >> d) - (1 << Lr);
+    const int t = lvl(p) - kTopLv;
+    const int d = t & 3, k = t >> 2;
+    const int m = (1 << d) - 1;
+    *slot = m + ((p + 1) & m);
+    // bbase(k) - 2^(9 + 4k) for the block levels a heap of < 2^21 nodes uses
+    const int c = k == 0 ? -512 : k == 1 ? 512 - 8192 : k == 2 ? 8704 - 131072 : 139776 - 2097152;
+    return ((p + 1) >> d) + c;
 }
 __device__ __forceinline__ uint32_t tag_of(int p) {
     if (p < kTop) return 1u;
@@ -1335,9 +1338,10 @@ struct Heap {
         const uint32_t dx = kd(x);
         int ev = 0;
         bool alive = true;
-#pragma unroll 1
+        // (no early exit: x is a bottom node and nearly always sinks past
+        // all eight levels; a stopped walk just rewrites the scratch slot)
+#pragma unroll
         for (int it = 0; it < kTopLv - 1; it++) {
-            if (__ballot(alive) == 0ull) break;
             const int l = 2 * ev + 1;
             const uint4 pr = *reinterpret_cast<const uint4*>(top + l + 1);
             __asm__ volatile("; isink lds" ::: "memory");
@@ -1516,10 +1520,10 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
                         const uint32_t gp = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cur >> 32), l);
                         tg = h.raise(vv, aa, h.pos_of(vv, gp), err);
                     }
+                    // (not logged: vv occurs once in the list, so no later
+                    // update of this batch asks for its pos)
                     rec[vv] = Rec{aa, tg, readlane_d(rv, l)};
                     __asm__ volatile("; irec store" ::: "memory");
-                    if (lane == h.nlog) h.log_v = vv, h.log_t = tg;
-                    h.nlog++;
                 }
                 if (fs < 64) break;
                 b += 64; // lists longer than 64 entries: next batch
