@@ -125,6 +125,19 @@ def request_roofline(requests, seconds, key, what):
 C1_BOUND = "lds/valu instruction chain (SQ counters: 1,375 instr/pop)"
 
 
+# The sparse configs' latencies are whole ms, so their rows are built by the
+# integer-key blocked-heap kernel; graphs with fractional-ms
+# latencies use k_sssp_slab.
+SLAB_KERNEL = ("k_sssp_islab (igraph-exact Dijkstra, 1 wave/source, persistent; u32 keys, 8-B heap nodes, "
+               "4-level 128-B HBM blocks)")
+
+
+def routing_traffic(tj, suffix):
+    """PMC record of the sparse routing build (the integer-key kernel's; a
+    traffic file measured on the f64 kernel has none)."""
+    return tj.get("routing_islab" + suffix)
+
+
 def routing_roofline(A, build_s, csr_bytes, rows, pops_per_row, traffic=None, bound="hbm (random-request rate)"):
     """Routing build roofline: compulsory bytes = the 16-B {lat, rel} table
     entries written (16 A x rows) + the CSR read once; the slab kernel is
@@ -393,7 +406,7 @@ def main():
                          "host_pairs_per_s": float(H) * H / t_c3,
                          "roofline": routing_roofline(A, t_c3, 20.0 * 2 * info2["edges"] + 4 * (V + 1),
                                                       max(hi - lo, 0), V,
-                                                      tj.get("routing_slab") if world == 1 else None)},
+                                                      routing_traffic(tj, "") if world == 1 else None)},
         }
         del tab1, t1
 
@@ -431,9 +444,9 @@ def main():
             "value": float(H2) ** 2 / tr2, "unit": "routed host-pairs/s", "vertex_pairs_per_s": float(A2) * A2 / tr2,
             "build_s": tr2, "allgather_s": tag2,
             "value_incl_allgather": float(H2) ** 2 / (tr2 + tag2),
-            "kernel": "k_sssp_slab (igraph-exact Dijkstra, 1 wave/source, persistent)",
+            "kernel": SLAB_KERNEL,
             "roofline": routing_roofline(A2, tr2, 20.0 * 2 * info2["edges"] + 4 * (V + 1), max(h2 - l2, 0), V,
-                                         tj.get("routing_slab_c2") if world == 1 else None),
+                                         routing_traffic(tj, "_c2") if world == 1 else None),
         }
         del tab2, t2
         torch.cuda.empty_cache()
@@ -467,10 +480,10 @@ def main():
                       % (args.c4_vertices, args.c4_hosts, A4, world),
             "value": float(args.c4_hosts) ** 2 / tr4, "unit": "routed host-pairs/s",
             "vertex_pairs_per_s": float(A4) * A4 / tr4, "build_s": tr4,
-            "kernel": "k_sssp_slab (igraph-exact Dijkstra, 1 wave/source, persistent)",
+            "kernel": SLAB_KERNEL,
             "roofline": routing_roofline(A4, tr4, 20.0 * 2 * t4.info()["edges"] + 4 * (args.c4_vertices + 1),
                                          max(h4 - l4, 0), args.c4_vertices,
-                                         tj.get("routing_slab_c4") if world == 1 else None),
+                                         routing_traffic(tj, "_c4") if world == 1 else None),
         }
         # C4 packet delivery: 1,000 rounds on the 100k-vertex table.  N=1: the
         # whole table is resident (A4^2 x 16 B = 120 GB of the 288 GB).  N>1:
