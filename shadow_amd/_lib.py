@@ -11,7 +11,8 @@ import errno
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libshdnet.so")
+# SHD_LIB: another in-tree build of the same library (A/B measurements)
+LIB_PATH = os.environ.get("SHD_LIB") or os.path.join(HERE, "libshdnet.so")
 
 
 class ShdError(RuntimeError):

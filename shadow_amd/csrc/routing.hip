@@ -1205,6 +1205,25 @@ struct Heap {
     // block still costs one memory round trip.  Returns x's new pos tag.
     __device__ __forceinline__ uint32_t up2(int b, int s, u64 x, u64 line, bool held) {
         const uint32_t dx = kd(x);
+        if (held && s > 0) { // the ancestors inside the held line first: no load
+            const int ds = lvl(s);
+            const int qa = ((s + 1) >> (lane + 1)) - 1;
+            const int src = lane < ds ? qa : 0;
+            const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(4 * src, (int)(uint32_t)line);
+            const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(4 * src, (int)(uint32_t)(line >> 32));
+            const u64 c = ((u64)hi << 32) | lo;
+            const unsigned long long m = __ballot(lane < ds && dx <= kd(c));
+            const int cnt = (int)__builtin_ctzll(~m);
+            if (cnt < ds) { // x stays below the block's root
+                if (lane < cnt) {
+                    const int q = lane == 0 ? s : ((s + 1) >> lane) - 1;
+                    blk[(size_t)b * 16 + q] = c;
+                    __asm__ volatile("; iup2h mv blk" ::: "memory");
+                }
+                put(b, ((s + 1) >> cnt) - 1, x);
+                return tag(b);
+            }
+        }
         const int ds = lvl(s); // ancestors inside b: slots ((s + 1) >> j) - 1, j = 1..ds
         // b's parent unit: pb < 0: the LDS, ancestors from position pp up; else block pb from slot pp up
         int pb, pp;
