@@ -1564,6 +1564,158 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
     }
 }
 
+// ---- integer-key LDS kernel (k_sssp_ilds): dense graphs with whole-ms latencies (C1) ----
+// k_sssp_lds's structure (one wave per row, the whole row in LDS, kRelax
+// batches of 64 list entries in flight per pop) with the integer keys of
+// k_sssp_islab: 8-B heap nodes {dist u32, v}, u32 compares, 16-B list
+// entries {nbr, w, 1 - loss} (the list handles copied into LDS once per
+// wave), the removal's sink as a branch-free walk on the vector unit, and a
+// shift-up as one data-parallel round (every ancestor is in LDS).  pos is
+// exact (position + 1) -- in LDS every move may as well record it.  LDS: 28 B
+// per vertex (k_sssp_lds: 36).
+__global__ __launch_bounds__(64) void k_sssp_ilds(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab) {
+    using namespace ik;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int kRelax = 16;
+    const int lane = threadIdx.x & 63;
+    const int V = g.V, A = g.A;
+    u64* top = reinterpret_cast<u64*>(smem);                      // V + 2: position p at top[p + 1]; top[0] scratch
+    uint32_t* dp = reinterpret_cast<uint32_t*>(top + V + 2);      // 2V: {dist, pos + 1} per vertex, + 2 scratch
+    double* rel = reinterpret_cast<double*>(dp + 2 * V + 2);       // V
+    int* so_l = reinterpret_cast<int*>(rel + V);                  // V: list handles
+    const Ent* __restrict__ sl = static_cast<const Ent*>(g.sl);
+    uint32_t* const pscr = dp + 2 * V; // scratch for masked-off pos stores
+    for (int v = lane; v < V; v += 64) so_l[v] = g.soff[v];
+    for (int row = row_lo + (int)blockIdx.x; row < row_hi; row += (int)gridDim.x) {
+        const int src = g.slot_vertex[row];
+        for (int v = lane; v < V; v += 64) reinterpret_cast<u64*>(dp)[v] = (u64)kInf; // dist kInf, pos 0
+        wave_fence();
+        top[1] = mk(0u, src);
+        reinterpret_cast<u64*>(dp)[src] = 1ull << 32; // dist 0 at position 0
+        rel[src] = 1.0;
+        int n = 1;
+        // shift-up of x from position e (one round: all ancestors in LDS);
+        // returns x's final position
+        auto up = [&](int e, u64 x) -> int {
+            const uint32_t dx = kd(x);
+            if (e > 0) {
+                const int K = lvl(e);
+                const int a = ((e + 1) >> (lane + 1)) - 1;
+                u64 c = 0;
+                if (lane < K) c = top[a + 1];
+                const unsigned long long m = __ballot(lane < K && dx <= kd(c));
+                const int cnt = (int)__builtin_ctzll(~m);
+                if (lane < cnt) {
+                    const int d = ((e + 1) >> lane) - 1;
+                    top[d + 1] = c;
+                    dp[2 * kv(c) + 1] = (uint32_t)d + 1u;
+                }
+                e = ((e + 1) >> cnt) - 1;
+            }
+            top[e + 1] = x;
+            return e;
+        };
+        int to_reach = A;
+        while (n > 0 && to_reach > 0) {
+            const u64 t = uni64(top[1]);
+            const int u = kv(t);
+            const uint32_t du = kd(t);
+            const int so = uni(so_l[u]);
+            int b = so >> 8;
+            const int lim = (so & 255) == 255 ? 64 * kRelax : (so & 255); // entries worth reading
+            Ent en[kRelax];
+#pragma unroll
+            for (int q = 0; q < kRelax; q++) { // (entries past the sentinel re-read it)
+                const int k = q * 64 + lane < lim ? q * 64 + lane : lim - 1;
+                en[q] = sl[b + k];
+            }
+            const double ru = rel[u];
+            // delete_max: the last node sinks from the root (branch-free walk)
+            const int last = --n;
+            if (last > 0) {
+                const u64 x = uni64(top[last + 1]);
+                const uint32_t dx = kd(x);
+                int ev = 0;
+                bool alive = true;
+                for (;;) {
+                    const int l = 2 * ev + 1;
+                    const bool has = alive && l < n;
+                    if (__ballot(has) == 0ull) break;
+                    const uint4 pr = *reinterpret_cast<const uint4*>(top + l + 1);
+                    const bool right = l + 1 < n && pr.w < pr.y;
+                    const uint32_t dc = right ? pr.w : pr.y;
+                    const uint32_t vc = right ? pr.z : pr.x;
+                    const bool mv = has && dc < dx;
+                    top[mv ? ev + 1 : 0] = ((u64)dc << 32) | vc;
+                    *(mv ? &dp[2 * vc + 1] : pscr) = (uint32_t)ev + 1u;
+                    ev = mv ? l + (right ? 1 : 0) : ev;
+                    alive = mv;
+                }
+                const int e = __builtin_amdgcn_readfirstlane(ev);
+                top[e + 1] = x;
+                dp[2 * kv(x) + 1] = (uint32_t)e + 1u;
+            }
+            // kRelax batches are relaxed together (LDS gathers, then the
+            // updates in incidence order): an update writes only its own
+            // neighbour's dist, and a neighbour occurs once per list
+            for (;;) {
+                int end = 64 * kRelax;
+#pragma unroll
+                for (int q = kRelax - 1; q >= 0; q--) {
+                    const unsigned long long m = __ballot(en[q].nbr < 0);
+                    if (m) end = q * 64 + __builtin_ctzll(m);
+                }
+                bool imp[kRelax], fresh[kRelax];
+                uint32_t alt[kRelax];
+                double rv[kRelax];
+#pragma unroll
+                for (int q = 0; q < kRelax; q++) {
+                    const bool ok = q * 64 + lane < end && en[q].nbr != u;
+                    const uint32_t cd = ok ? dp[2 * en[q].nbr] : 0u;
+                    alt[q] = du + en[q].w;
+                    rv[q] = ru * en[q].rel;
+                    fresh[q] = ok && cd == kInf;
+                    imp[q] = ok && alt[q] < cd;
+                }
+#pragma unroll
+                for (int q = 0; q < kRelax; q++) {
+                    unsigned long long m = __ballot(imp[q]);
+                    const unsigned long long fm = __ballot(fresh[q]);
+                    while (m) { // igraph's order: incidence order, one edge at a time
+                        const int l = __builtin_ctzll(m);
+                        m &= m - 1;
+                        const int vv = __builtin_amdgcn_readlane(en[q].nbr, l);
+                        const uint32_t aa = (uint32_t)__builtin_amdgcn_readlane((int)alt[q], l);
+                        const int e0 = (fm >> l) & 1ull ? n++ : (int)uni((int)dp[2 * vv + 1]) - 1;
+                        const int e = up(e0, mk(aa, vv));
+                        reinterpret_cast<u64*>(dp)[vv] = ((u64)(e + 1) << 32) | aa;
+                        rel[vv] = readlane_d(rv[q], l);
+                    }
+                }
+                if (end < 64 * kRelax) {
+                    // the sentinel: -2 when u is an attached vertex
+                    int sv = 0;
+#pragma unroll
+                    for (int q = 0; q < kRelax; q++)
+                        if (end >= q * 64 && end < q * 64 + 64) sv = __builtin_amdgcn_readlane(en[q].nbr, end - q * 64);
+                    if (sv == -2) --to_reach;
+                    break;
+                }
+                b += 64 * kRelax; // lists longer than kRelax * 64 entries
+#pragma unroll
+                for (int q = 0; q < kRelax; q++) en[q] = sl[b + q * 64 + lane];
+            }
+        }
+        wave_fence();
+        write_row(g, row, src, tab, lane, [&](int v, double& l, double& r) {
+            const uint32_t d = dp[2 * v];
+            l = d == kInf ? -1.0 : (double)d;
+            r = rel[v];
+        });
+        wave_fence();
+    }
+}
+
 // _topology_lookupDirectPath (topology.c:1816-1858): the (s,d) edge itself.
 __global__ __launch_bounds__(256) void k_direct_rows(ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab) {
     const int A = g.A;
@@ -1622,6 +1774,18 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         if ((rc = hip_status(hipGetLastError(), "k_direct_rows launch"))) return rc;
         return hip_status(hipDeviceSynchronize(), "k_direct_rows");
     }
+    const char* kern = getenv("SHD_SSSP_KERNEL");
+    // whole-ms latencies: the integer-key LDS kernel (SHD_SSSP_KERNEL=lds: the f64 one)
+    if (g.V <= kLdsMaxV && g.sl && !(kern && strcmp(kern, "lds") == 0)) {
+        const size_t lds = 8 * ((size_t)g.V + 2) + 8 * (size_t)g.V + 8 + 8 * (size_t)g.V + 4 * (size_t)g.V;
+        if (lds > 65536 && (rc = hip_status(hipFuncSetAttribute((const void*)k_sssp_ilds,
+                                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                                            "hipFuncSetAttribute")))
+            return rc;
+        hipLaunchKernelGGL(k_sssp_ilds, dim3(rows), dim3(64), lds, nullptr, g, row_lo, row_hi, tab);
+        if ((rc = hip_status(hipGetLastError(), "k_sssp_ilds launch"))) return rc;
+        return hip_status(hipDeviceSynchronize(), "k_sssp_ilds");
+    }
     if (g.V <= kLdsMaxV) {
         const size_t lds = sizeof(HNode) * ((size_t)g.V + 1) + 20 * (size_t)g.V;
         // SHD_SSSP_LDS_SEQ=1: level-by-level sink and shift-up
@@ -1638,7 +1802,6 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
         return hip_status(hipDeviceSynchronize(), "k_sssp_lds");
     }
     if (!g.snb || !g.swr || !g.soff) return shd_fail(-EINVAL, "slab kernel needs the sentinel incidence arrays");
-    const char* kern = getenv("SHD_SSSP_KERNEL");
     if (kern && strcmp(kern, "blk") == 0) { // SHD_SSSP_KERNEL=blk: the blocked slab heap
         const size_t nblk = blk_count((long)g.V + 1);
         const size_t bstride = (nblk * 128 + 20 * (size_t)g.V + 255) & ~(size_t)255;

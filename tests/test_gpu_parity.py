@@ -76,6 +76,21 @@ def test_flat_slab_kernel_bit_exact(name, monkeypatch):
         assert np.array_equal(bits(rel[i]), bits(orl)), (name, i)
 
 
+@pytest.mark.parametrize("name", ["complete30_ms", "complete25_dir", "sparse300_ms"])
+def test_f64_lds_kernel_bit_exact(name, monkeypatch):
+    """The f64 LDS kernel (SHD_SSSP_KERNEL=lds; the default for graphs of at
+    most 4,096 vertices with fractional-ms latencies) forced on whole-ms
+    graphs, where the integer-key LDS kernel is the default."""
+    monkeypatch.setenv("SHD_SSSP_KERNEL", "lds")
+    gml, H = GRAPHS[name]
+    top, orc, _, _ = make_pair(gml, H)
+    lat, rel, sv = top.table()
+    for i, s in enumerate(sv):
+        ol, orl = orc.row(int(s), sv)
+        assert np.array_equal(bits(lat[i]), bits(ol)), (name, i)
+        assert np.array_equal(bits(rel[i]), bits(orl)), (name, i)
+
+
 @pytest.mark.parametrize("directed", [False, True])
 def test_int_blocked_heap_deep_levels(directed):
     """Heaps of more than 8,191 nodes: the integer-key kernel's second level of
