@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03g_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03h_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
@@ -118,11 +118,11 @@ def request_roofline(requests, seconds, key, what):
             "frac": ach / ceiling if ceiling else None}
 
 
-# The C1 kernel (k_sssp_lds) keeps a row's whole state in LDS; its SQ
-# counters (profiles/r02i_sq_c1.log) put it on the per-pop LDS/VALU
-# instruction chain (1,375 instructions per pop, one wave per SIMD), not on
-# memory requests.
-C1_BOUND = "lds/valu instruction chain (SQ counters: 1,375 instr/pop)"
+# The C1 kernel (k_sssp_ilds) keeps a row's whole state in LDS; its SQ
+# counters (profiles/r03h_sq_c1: 640 SALU + 492 VALU + 71 LDS instructions
+# per pop, one wave per SIMD, 44 % of wave cycles waiting) put it on the
+# per-pop instruction chain, not on memory requests.
+C1_BOUND = "salu/valu/lds instruction chain (SQ counters, profiles/r03h_sq_c1: 1,132 instr/pop, one wave per SIMD)"
 
 
 # The sparse configs' latencies are whole ms, so their rows are built by the
@@ -398,9 +398,9 @@ def main():
         result["routing"] = {
             "config": "C1 complete graph V=1000 (E=500,500 incl. self-loops), H=5000 hosts, A=%d attached" % A1,
             "value": 5000.0 ** 2 / tr, "unit": "routed host-pairs/s", "vertex_pairs_per_s": A1 * A1 / tr,
-            "ms_per_table": tr * 1e3, "kernel": "k_sssp_lds (igraph-exact Dijkstra, 1 wave/source)",
+            "ms_per_table": tr * 1e3, "kernel": "k_sssp_ilds (igraph-exact Dijkstra, 1 wave/source, row in LDS, u32 keys)",
             "roofline": routing_roofline(A1, tr, 20.0 * 2 * info1["edges"] + 4 * 1001, max(h1 - l1, 0), 1000,
-                                         tj.get("routing_lds_c1") if world == 1 else None, bound=C1_BOUND),
+                                         tj.get("routing_ilds_c1") if world == 1 else None, bound=C1_BOUND),
             "c3_table": {"config": "the C3 rounds' table: V=%d sparse graph, H=%d hosts, A=%d" % (V, H, A),
                          "rows_s": t_c3, "allgather_s": max_over_ranks(t_ag_c3) if world > 1 else 0.0,
                          "host_pairs_per_s": float(H) * H / t_c3,

@@ -14,7 +14,7 @@ import sys
 
 STAGE = {"k_pkt_scatter": "packet_scatter", "k_place_rank": "place", "k_place_bucket": "place",
          "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_slab<256>": "routing_slab",
-         "k_sssp_islab<false>": "routing_islab",
+         "k_sssp_islab<false>": "routing_islab", "k_sssp_ilds": "routing_ilds",
          "k_sssp_lds<true>": "routing_lds", "k_scan_one": "scan"}
 
 
