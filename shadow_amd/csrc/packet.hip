@@ -51,7 +51,7 @@ constexpr int kChunks = 1536;      // scatter workgroups per launch (columns of 
 constexpr int kMaxBuckets = 4096;  // destination buckets (LDS histogram size)
 constexpr int kScanTile = 4096;    // 256 threads x 16
 constexpr int kSmallSeg = 256;     // wave register sort up to 4 events per lane
-constexpr uint32_t kSlab = kSmallSeg; // "slab" pipeline: event slots reserved per destination
+constexpr uint32_t kSlab = 128; // "slab" pipeline: event slots reserved per destination
 constexpr int kSortBlock = 1024;   // k_bucket_sort workgroup (16 waves)
 constexpr int kMaxPerBucket = 2 * kSortBlock; // destinations per bucket (LDS scan width)
 constexpr int kBucketCap = 4096;   // events per bucket staged in LDS by k_bucket_sort (30 B each)
