@@ -392,6 +392,18 @@ def main():
         torch.cuda.synchronize(dev)
         barrier()
         tr = max_over_ranks((time.perf_counter() - s0) / reps)
+        # north_star's dense-graph kernel, latencies only (blocked min-plus
+        # Floyd-Warshall; the table's reliabilities need igraph's heap order)
+        fw1 = torch.empty(A1 * A1, dtype=torch.float64, device=dev)
+        t1.latency_table_fw(fw1.data_ptr())  # warm
+        torch.cuda.synchronize(dev)
+        s0 = time.perf_counter()
+        for _ in range(reps):
+            t1.latency_table_fw(fw1.data_ptr())
+        torch.cuda.synchronize(dev)
+        t_fw1 = max_over_ranks((time.perf_counter() - s0) / reps)
+        fw_same = bool(torch.equal(fw1.view(A1, A1), tab1.view(A1, A1, 2)[:, :, 0])) if world == 1 else None
+        del fw1
         info1 = t1.info()
         info2 = top.info()
         t_c3 = max(max_over_ranks(t_rows_c3), 1e-9)
@@ -399,6 +411,8 @@ def main():
             "config": "C1 complete graph V=1000 (E=500,500 incl. self-loops), H=5000 hosts, A=%d attached" % A1,
             "value": 5000.0 ** 2 / tr, "unit": "routed host-pairs/s", "vertex_pairs_per_s": A1 * A1 / tr,
             "ms_per_table": tr * 1e3, "kernel": "k_sssp_ilds (igraph-exact Dijkstra, 1 wave/source, row in LDS, u32 keys)",
+            "latency_only_minplus": {"ms": t_fw1 * 1e3, "kernel": "blocked min-plus Floyd-Warshall, 64x64 LDS tiles "
+                                     "(shd_topology_latency_table_fw)", "equals_table_latencies": fw_same},
             "roofline": routing_roofline(A1, tr, 20.0 * 2 * info1["edges"] + 4 * 1001, max(h1 - l1, 0), 1000,
                                          tj.get("routing_ilds_c1") if world == 1 else None, bound=C1_BOUND),
             "c3_table": {"config": "the C3 rounds' table: V=%d sparse graph, H=%d hosts, A=%d" % (V, H, A),

@@ -165,6 +165,15 @@ int shd_device_free(int device, void* d_ptr);
  * shd_device_alloc_table); synchronous. */
 int shd_device_copy(int device, void* d_dst, const void* d_src, size_t bytes);
 int shd_topology_build_rows_device(ShdTopology* top, int row_lo, int row_hi, void* d_table);
+/* Latencies only: the A x A lat_ms column of the table (row-major doubles,
+ * slots as above) into device memory d_lat, by blocked min-plus
+ * Floyd-Warshall over 64 x 64 LDS tiles -- the shortest-path latencies do
+ * not depend on igraph's tie order (the reliabilities do, which is why the
+ * table itself is built by the Dijkstra kernels).  Bit-identical to the
+ * table's latencies; graphs whose edge latencies are all whole ms and with at
+ * most 16,384 vertices (-ENOTSUP otherwise).  Releases nothing (no lookup
+ * side effects).  Synchronous. */
+int shd_topology_latency_table_fw(ShdTopology* top, void* d_lat);
 int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
 /* Adopts a device table WITHOUT a host mirror (tables larger than host RAM
  * wants: A = 86k slots is 120 GB).  Nothing is released at adoption: as in

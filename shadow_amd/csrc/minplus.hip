@@ -1,0 +1,228 @@
+// minplus.hip -- the latency half of the routing table by blocked min-plus
+// Floyd-Warshall (north_star's dense-graph kernel), for whole-ms graphs.
+//
+// The routing table's latencies are shortest-path distances; they do not
+// depend on which of several equal-latency paths igraph's heap picks (only
+// the reliabilities do), so any exact all-pairs algorithm
+// reproduces them.  With every edge latency a whole number of ms (the
+// condition of ShdGraphDev.sl, the integer-key SSSP kernels' condition)
+// every path sum is an exact integer below 2^32 - 1, so u32 min-plus gives
+// the f64 values bit for bit.  Entries are then formed as
+// _topology_computeSourcePaths stores them (topology.c:1744-1791): the self
+// path by _topology_computeShortestPathToSelf's rule (loops at L, other
+// edges at 2L, topology.c:1431-1576), latency 0 -> 1 ms, unreachable -1.
+//
+// Layout: a Vp x Vp u32 distance matrix (Vp = V rounded up to 64), 64 x 64
+// tiles.  Round kb: the diagonal tile closes over its own 64 vertices (one
+// workgroup, 64 dependent steps in LDS), the tiles of row and column kb
+// relax through it (64 steps each), then every other tile takes one min-plus
+// product of its row-kb and column-kb tiles, both staged in LDS (16 KB
+// each; 256 threads, a 4 x 4 register block per thread, two 16-B LDS reads
+// and 32 VALU per k).  The products are the O(V^3) part.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdint>
+
+#include "shd_internal.h"
+
+namespace {
+
+constexpr int kT = 64;                  // tile edge
+constexpr uint32_t kInfD = 0x3FFFFFFFu; // unreachable; two of them still fit a u32
+constexpr int kMaxV = 16384;            // Vp^2 x 4 B = 1 GiB
+
+__global__ __launch_bounds__(256) void k_fw_init(uint32_t* __restrict__ D, int Vp) {
+    const size_t n = (size_t)Vp * Vp;
+    for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (size_t)gridDim.x * 256)
+        D[q] = (q / Vp == q % Vp) ? 0u : kInfD;
+}
+
+// direct edges (igraph_incident mode OUT: an undirected edge is in both lists)
+__global__ __launch_bounds__(256) void k_fw_edges(ShdGraphDev g, uint32_t* __restrict__ D, int Vp) {
+    for (int u = blockIdx.x; u < g.V; u += gridDim.x)
+        for (int k = g.inc_off[u] + threadIdx.x; k < g.inc_off[u + 1]; k += 256) {
+            const int v = g.inc_nbr[k];
+            if (v != u) atomicMin(&D[(size_t)u * Vp + v], (uint32_t)g.inc_w[k]);
+        }
+}
+
+// The dependent phases (the diagonal tile closing over itself, the row and
+// column tiles relaxing through it) keep each thread's 4 x 4 block in
+// registers; step k needs the tile's current row k and/or column k, which
+// the 16 threads owning them publish to a double-buffered LDS line before
+// the step's single barrier.
+__device__ __forceinline__ void ld_block(uint32_t (&d)[4][4], const uint32_t* D, int Vp, int ti, int tj, int ty, int tx) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&D[(size_t)(ti * kT + ty * 4 + r) * Vp + tj * kT + tx * 4]);
+        d[r][0] = v.x, d[r][1] = v.y, d[r][2] = v.z, d[r][3] = v.w;
+    }
+}
+__device__ __forceinline__ void st_block(const uint32_t (&d)[4][4], uint32_t* D, int Vp, int ti, int tj, int ty, int tx) {
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        *reinterpret_cast<uint4*>(&D[(size_t)(ti * kT + ty * 4 + r) * Vp + tj * kT + tx * 4]) =
+            make_uint4(d[r][0], d[r][1], d[r][2], d[r][3]);
+}
+// row k%4 of the block (its owner publishes it) / column k%4
+__device__ __forceinline__ uint4 blk_row(const uint32_t (&d)[4][4], int r) {
+    uint4 o = make_uint4(d[0][0], d[0][1], d[0][2], d[0][3]);
+#pragma unroll
+    for (int q = 1; q < 4; q++)
+        if (r == q) o = make_uint4(d[q][0], d[q][1], d[q][2], d[q][3]);
+    return o;
+}
+__device__ __forceinline__ uint4 blk_col(const uint32_t (&d)[4][4], int c) {
+    uint4 o = make_uint4(d[0][0], d[1][0], d[2][0], d[3][0]);
+#pragma unroll
+    for (int q = 1; q < 4; q++)
+        if (c == q) o = make_uint4(d[0][q], d[1][q], d[2][q], d[3][q]);
+    return o;
+}
+__device__ __forceinline__ void relax(uint32_t (&d)[4][4], const uint4 cv, const uint4 rv) {
+    const uint32_t a[4] = {cv.x, cv.y, cv.z, cv.w}, b[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t x = a[r] + b[c];
+            d[r][c] = x < d[r][c] ? x : d[r][c];
+        }
+}
+
+// round kb, phase 1 (one workgroup): Floyd-Warshall inside the diagonal tile
+__global__ __launch_bounds__(256) void k_fw_diag(uint32_t* __restrict__ D, int Vp, int kb) {
+    __shared__ __attribute__((aligned(16))) uint32_t rowb[2][kT], colb[2][kT];
+    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    uint32_t d[4][4];
+    ld_block(d, D, Vp, kb, kb, ty, tx);
+    for (int k = 0; k < kT; k++) {
+        const int p = k & 1;
+        if (ty == (k >> 2)) *reinterpret_cast<uint4*>(&rowb[p][tx * 4]) = blk_row(d, k & 3);
+        if (tx == (k >> 2)) *reinterpret_cast<uint4*>(&colb[p][ty * 4]) = blk_col(d, k & 3);
+        __syncthreads();
+        relax(d, *reinterpret_cast<const uint4*>(&colb[p][ty * 4]), *reinterpret_cast<const uint4*>(&rowb[p][tx * 4]));
+    }
+    st_block(d, D, Vp, kb, kb, ty, tx);
+}
+
+// round kb, phase 2: tile (kb, j) and tile (j, kb) for every j != kb
+// (blockIdx.x < nb - 1: row tiles, relaxed through the diagonal tile's
+// columns; else column tiles, through its rows)
+__global__ __launch_bounds__(256) void k_fw_cross(uint32_t* __restrict__ D, int Vp, int kb, int nb) {
+    __shared__ __attribute__((aligned(16))) uint32_t dg[kT][kT]; // row tiles: transposed (dg[k][a] = diag[a][k])
+    __shared__ __attribute__((aligned(16))) uint32_t lb[2][kT];
+    const bool row = (int)blockIdx.x < nb - 1;
+    int j = row ? (int)blockIdx.x : (int)blockIdx.x - (nb - 1);
+    if (j >= kb) j++;
+    for (int q = threadIdx.x; q < kT * kT; q += 256) {
+        const int r = q / kT, c = q % kT;
+        const uint32_t v = D[(size_t)(kb * kT + r) * Vp + kb * kT + c];
+        if (row) dg[c][r] = v;
+        else dg[r][c] = v;
+    }
+    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    uint32_t d[4][4];
+    if (row) ld_block(d, D, Vp, kb, j, ty, tx);
+    else ld_block(d, D, Vp, j, kb, ty, tx);
+    __syncthreads();
+    for (int k = 0; k < kT; k++) {
+        const int p = k & 1;
+        if (row) { // d[a][b] = min(d[a][b], diag[a][k] + d[k][b]): row k of this tile
+            if (ty == (k >> 2)) *reinterpret_cast<uint4*>(&lb[p][tx * 4]) = blk_row(d, k & 3);
+            __syncthreads();
+            relax(d, *reinterpret_cast<const uint4*>(&dg[k][ty * 4]), *reinterpret_cast<const uint4*>(&lb[p][tx * 4]));
+        } else { // d[a][b] = min(d[a][b], d[a][k] + diag[k][b]): column k of this tile
+            if (tx == (k >> 2)) *reinterpret_cast<uint4*>(&lb[p][ty * 4]) = blk_col(d, k & 3);
+            __syncthreads();
+            relax(d, *reinterpret_cast<const uint4*>(&lb[p][ty * 4]), *reinterpret_cast<const uint4*>(&dg[k][tx * 4]));
+        }
+    }
+    if (row) st_block(d, D, Vp, kb, j, ty, tx);
+    else st_block(d, D, Vp, j, kb, ty, tx);
+}
+
+// round kb, phase 3: every tile (i, j), i, j != kb: d = min(d, rowtile (+) coltile)
+__global__ __launch_bounds__(256) void k_fw_prod(uint32_t* __restrict__ D, int Vp, int kb) {
+    __shared__ __attribute__((aligned(16))) uint32_t at[kT][kT]; // D[i][kb] transposed: at[k][i]
+    __shared__ __attribute__((aligned(16))) uint32_t bt[kT][kT]; // D[kb][j]: bt[k][j]
+    int ti = blockIdx.y, tj = blockIdx.x;
+    if (ti >= kb) ti++;
+    if (tj >= kb) tj++;
+    for (int q = threadIdx.x; q < kT * kT; q += 256) {
+        const int r = q / kT, c = q % kT;
+        at[c][r] = D[(size_t)(ti * kT + r) * Vp + kb * kT + c];
+        bt[r][c] = D[(size_t)(kb * kT + r) * Vp + tj * kT + c];
+    }
+    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    uint32_t d[4][4];
+    ld_block(d, D, Vp, ti, tj, ty, tx);
+    __syncthreads();
+#pragma unroll 8
+    for (int k = 0; k < kT; k++)
+        relax(d, *reinterpret_cast<const uint4*>(&at[k][ty * 4]), *reinterpret_cast<const uint4*>(&bt[k][tx * 4]));
+    st_block(d, D, Vp, ti, tj, ty, tx);
+}
+
+// the A x A latency table from the distances (one block per row)
+__global__ __launch_bounds__(256) void k_fw_rows(ShdGraphDev g, const uint32_t* __restrict__ D, int Vp,
+                                                 double* __restrict__ lat) {
+    const int A = g.A;
+    for (int i = blockIdx.x; i < A; i += gridDim.x) {
+        const int u = g.slot_vertex[i];
+        double* out = lat + (size_t)i * A;
+        for (int j = threadIdx.x; j < A; j += 256) {
+            if (j == i) continue;
+            const uint32_t d = D[(size_t)u * Vp + g.slot_vertex[j]];
+            out[j] = d >= kInfD ? -1.0 : (d == 0 ? 1.0 : (double)d); // topology.c:1787-1791
+        }
+        if (threadIdx.x < 64) { // the self path, topology.c:1431-1576 (first strict minimum)
+            const int lane = threadIdx.x;
+            double best = 0.0;
+            int bk = 0x7fffffff;
+            for (int k = g.inc_off[u] + lane; k < g.inc_off[u + 1]; k += 64) {
+                double l = g.inc_w[k];
+                if (g.inc_nbr[k] != u) l *= 2.0;
+                if (bk == 0x7fffffff || l < best) best = l, bk = k;
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                const double ob = __shfl_xor(best, o);
+                const int ok = __shfl_xor(bk, o);
+                if (ok != 0x7fffffff && (bk == 0x7fffffff || ob < best || (ob == best && ok < bk))) best = ob, bk = ok;
+            }
+            if (lane == 0) out[i] = bk == 0x7fffffff ? 0.0 : best;
+        }
+    }
+}
+
+int hip_rc(hipError_t e, const char* what) {
+    if (e == hipSuccess) return 0;
+    return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
+}
+
+} // namespace
+
+extern "C" int shd_dev_fw_latency(const ShdGraphDev* gp, double* d_lat) {
+    const ShdGraphDev g = *gp;
+    if (!g.sl) return shd_fail(-ENOTSUP, "min-plus latencies need whole-ms edge latencies");
+    if (g.V > kMaxV) return shd_fail(-ENOTSUP, "min-plus latencies: %d vertices > %d", g.V, kMaxV);
+    const int Vp = (g.V + kT - 1) / kT * kT, nb = Vp / kT;
+    uint32_t* D = nullptr;
+    int rc = hip_rc(hipMalloc((void**)&D, (size_t)Vp * Vp * 4), "hipMalloc distances");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_fw_init, dim3(1024), dim3(256), 0, nullptr, D, Vp);
+    hipLaunchKernelGGL(k_fw_edges, dim3(g.V < 4096 ? g.V : 4096), dim3(256), 0, nullptr, g, D, Vp);
+    for (int kb = 0; kb < nb; kb++) {
+        hipLaunchKernelGGL(k_fw_diag, dim3(1), dim3(256), 0, nullptr, D, Vp, kb);
+        if (nb > 1) {
+            hipLaunchKernelGGL(k_fw_cross, dim3(2 * (nb - 1)), dim3(256), 0, nullptr, D, Vp, kb, nb);
+            hipLaunchKernelGGL(k_fw_prod, dim3(nb - 1, nb - 1), dim3(256), 0, nullptr, D, Vp, kb);
+        }
+    }
+    hipLaunchKernelGGL(k_fw_rows, dim3(g.A < 4096 ? g.A : 4096), dim3(256), 0, nullptr, g, D, Vp, d_lat);
+    rc = hip_rc(hipGetLastError(), "min-plus launch");
+    if (!rc) rc = hip_rc(hipDeviceSynchronize(), "min-plus");
+    (void)hipFree(D);
+    return rc;
+}

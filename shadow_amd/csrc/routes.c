@@ -283,6 +283,16 @@ int shd_topology_build_rows_device(ShdTopology* t, int row_lo, int row_hi, void*
     return rc;
 }
 
+int shd_topology_latency_table_fw(ShdTopology* t, void* d_lat) {
+    if (!t || !d_lat) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
+    int rc = prepare(t);
+    ShdGraphDev g = graph_dev(t);
+    if (!rc) rc = shd_dev_fw_latency(&g, (double*)d_lat);
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
+}
+
 /* ---- single-process multi-GPU build (shd_topology_build_shards) ---- */
 
 /* The device graph arrays of prepare(), with their sizes (bytes). */

@@ -1051,16 +1051,6 @@ __device__ __forceinline__ int bid_of(int p, int* slot) {
     const int c = k == 0 ? -512 : k == 1 ? 512 - 8192 : k == 2 ? 8704 - 131072 : 139776 - 2097152;
     return ((p + 1) >> d) + c;
 }
-__device__ __forceinline__ uint32_t tag_of(int p) {
-    if (p < kTop) return 1u;
-    int s;
-    return (uint32_t)bid_of(p, &s) + 2u;
-}
-__device__ __forceinline__ int root_of(int bid) {
-    int k = 0;
-    while (bbase(k + 1) <= bid) k++;
-    return bid - bbase(k) + (1 << (kTopLv + 4 * k)) - 1;
-}
 
 // kStats: event counters (SHD_SSSP_STATS=1, measurement only)
 enum { kStPops, kStSinkHbm, kStPush, kStRaiseHbm, kStRaiseLds, kStUpRounds, kStUpClimb, kStLogOvf, kStBatches,

@@ -103,6 +103,10 @@ void shd_dev_stream_free(void* s);
  * use_sp = 1: igraph-exact Dijkstra per source slot + self path (R-7, R-9);
  * use_sp = 0: direct edge per pair (R-10).  Synchronous. */
 int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab);
+/* The A x A latency half of the table (lat_ms doubles, row-major) by blocked
+ * min-plus Floyd-Warshall (minplus.hip); whole-ms graphs only (-ENOTSUP
+ * otherwise), V <= 16384.  Synchronous. */
+int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat);
 /* min latency over the entries (i, j), i < j, lat >= 0, of rows [row_lo,
  * row_hi) of an A-column table (rows: row i at rows + (i - row_lo) * A); -1 if none */
 int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out);

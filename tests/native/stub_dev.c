@@ -63,6 +63,12 @@ void stub_entry(int i, int j, double* lat, double* rel) {
     *rel = 0.5 + (double)((i * 29 + j * 53) % 41) / 100.0;
 }
 
+int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat) {
+    (void)g;
+    (void)d_lat;
+    return -ENOTSUP;
+}
+
 int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab) {
     (void)use_sp;
     for (int i = row_lo; i < row_hi; i++)

@@ -61,6 +61,11 @@ def test_c1_full_table_bit_exact(ns):
     olat, orel = orc.rows_parallel(sv, sv)
     bad = np.flatnonzero((bits(lat) != bits(olat)).any(1) | (bits(rel) != bits(orel)).any(1))
     assert len(bad) == 0, f"{len(bad)} rows differ, first {bad[:5]}"
+    if not ns:  # whole-ms latencies: the min-plus Floyd-Warshall latencies too
+        import torch
+        d = torch.empty(996 * 996, dtype=torch.float64, device="cuda")
+        top.latency_table_fw(d.data_ptr())
+        assert np.array_equal(bits(d.cpu().numpy().reshape(996, 996)), bits(olat))
 
 
 @pytest.mark.timeout(600)

@@ -721,3 +721,32 @@ def test_teardown_path_log_matches_reference(name, use_sp):
     got = top.cached_paths_log()
     assert got == orc.cached_paths_log()
     assert len(got) > 0
+
+
+@pytest.mark.parametrize("name", ["complete30_ms", "complete25_dir", "sparse300_ms", "sparse5000_hbm", "dense4400_hbm"])
+def test_minplus_latencies_equal_table(name):
+    """shd_topology_latency_table_fw (blocked min-plus Floyd-Warshall, 64 x 64
+    LDS tiles): the latency half of the table, bit for bit, self paths and
+    directed graphs included; no lookup side effects."""
+    import torch
+    gml, H = GRAPHS[name]
+    top, orc, _, _ = make_pair(gml, H)
+    lat, rel, sv = top.table()
+    A = len(sv)
+    d = torch.empty(A * A, dtype=torch.float64, device="cuda")
+    top.latency_table_fw(d.data_ptr())
+    fw = d.cpu().numpy().reshape(A, A)
+    assert np.array_equal(bits(fw), bits(lat)), name
+
+
+def test_minplus_needs_whole_ms():
+    """Fractional-ms latencies: the min-plus entry declines (-ENOTSUP)."""
+    import torch
+    gml, H = GRAPHS["complete40_ns"]
+    top, _, _, _ = make_pair(gml, H)
+    A = top.slot_count()
+    d = torch.empty(A * A, dtype=torch.float64, device="cuda")
+    from shadow_amd._lib import ShdError
+    with pytest.raises(ShdError) as ei:
+        top.latency_table_fw(d.data_ptr())
+    assert ei.value.code == -95  # ENOTSUP
