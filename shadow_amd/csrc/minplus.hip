@@ -13,9 +13,10 @@
 // edges at 2L, topology.c:1431-1576), latency 0 -> 1 ms, unreachable -1.
 //
 // Layout: a Vp x Vp u32 distance matrix (Vp = V rounded up to 64), 64 x 64
-// tiles.  Round kb: the diagonal tile closes over its own 64 vertices (one
-// workgroup, 64 dependent steps in LDS), the tiles of row and column kb
-// relax through it (64 steps each), then every other tile takes one min-plus
+// tiles.  Round kb: the diagonal tile closes over its own 64 vertices (64
+// dependent steps, redone by each workgroup of the next phase rather than
+// launched alone), the tiles of row and column kb relax through it (64 steps
+// each), then every other tile takes one min-plus
 // product of its row-kb and column-kb tiles, both staged in LDS (16 KB
 // each; 256 threads, a 4 x 4 register block per thread, two 16-B LDS reads
 // and 32 VALU per k).  The products are the O(V^3) part.
@@ -91,11 +92,9 @@ __device__ __forceinline__ void relax(uint32_t (&d)[4][4], const uint4 cv, const
         }
 }
 
-// round kb, phase 1 (one workgroup): Floyd-Warshall inside the diagonal tile
-__global__ __launch_bounds__(256) void k_fw_diag(uint32_t* __restrict__ D, int Vp, int kb) {
-    __shared__ __attribute__((aligned(16))) uint32_t rowb[2][kT], colb[2][kT];
-    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
-    uint32_t d[4][4];
+// the diagonal tile's closure (phase 1) in registers, from D
+__device__ __forceinline__ void close_diag(uint32_t (&d)[4][4], uint32_t (*rowb)[kT], uint32_t (*colb)[kT],
+                                           const uint32_t* D, int Vp, int kb, int ty, int tx) {
     ld_block(d, D, Vp, kb, kb, ty, tx);
     for (int k = 0; k < kT; k++) {
         const int p = k & 1;
@@ -104,26 +103,31 @@ __global__ __launch_bounds__(256) void k_fw_diag(uint32_t* __restrict__ D, int V
         __syncthreads();
         relax(d, *reinterpret_cast<const uint4*>(&colb[p][ty * 4]), *reinterpret_cast<const uint4*>(&rowb[p][tx * 4]));
     }
-    st_block(d, D, Vp, kb, kb, ty, tx);
 }
 
-// round kb, phase 2: tile (kb, j) and tile (j, kb) for every j != kb
-// (blockIdx.x < nb - 1: row tiles, relaxed through the diagonal tile's
-// columns; else column tiles, through its rows)
+// round kb, phases 1 + 2: every workgroup closes the diagonal tile itself
+// (the same 64 steps in each, in parallel: one launch less per round; block
+// 0 stores it), then relaxes its tile of row or column kb through it
+// (blockIdx.x < nb - 1: row tiles, through the diagonal tile's columns;
+// else column tiles, through its rows)
 __global__ __launch_bounds__(256) void k_fw_cross(uint32_t* __restrict__ D, int Vp, int kb, int nb) {
     __shared__ __attribute__((aligned(16))) uint32_t dg[kT][kT]; // row tiles: transposed (dg[k][a] = diag[a][k])
-    __shared__ __attribute__((aligned(16))) uint32_t lb[2][kT];
+    __shared__ __attribute__((aligned(16))) uint32_t lb[2][kT], rowb[2][kT], colb[2][kT];
+    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    uint32_t d[4][4];
+    close_diag(d, rowb, colb, D, Vp, kb, ty, tx);
+    if (nb == 1 || blockIdx.x == 0) st_block(d, D, Vp, kb, kb, ty, tx);
+    if (nb == 1) return;
     const bool row = (int)blockIdx.x < nb - 1;
     int j = row ? (int)blockIdx.x : (int)blockIdx.x - (nb - 1);
     if (j >= kb) j++;
-    for (int q = threadIdx.x; q < kT * kT; q += 256) {
-        const int r = q / kT, c = q % kT;
-        const uint32_t v = D[(size_t)(kb * kT + r) * Vp + kb * kT + c];
-        if (row) dg[c][r] = v;
-        else dg[r][c] = v;
-    }
-    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
-    uint32_t d[4][4];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            if (row) dg[tx * 4 + c][ty * 4 + r] = d[r][c];
+            else dg[ty * 4 + r][tx * 4 + c] = d[r][c];
+        }
     if (row) ld_block(d, D, Vp, kb, j, ty, tx);
     else ld_block(d, D, Vp, j, kb, ty, tx);
     __syncthreads();
@@ -214,11 +218,8 @@ extern "C" int shd_dev_fw_latency(const ShdGraphDev* gp, double* d_lat) {
     hipLaunchKernelGGL(k_fw_init, dim3(1024), dim3(256), 0, nullptr, D, Vp);
     hipLaunchKernelGGL(k_fw_edges, dim3(g.V < 4096 ? g.V : 4096), dim3(256), 0, nullptr, g, D, Vp);
     for (int kb = 0; kb < nb; kb++) {
-        hipLaunchKernelGGL(k_fw_diag, dim3(1), dim3(256), 0, nullptr, D, Vp, kb);
-        if (nb > 1) {
-            hipLaunchKernelGGL(k_fw_cross, dim3(2 * (nb - 1)), dim3(256), 0, nullptr, D, Vp, kb, nb);
-            hipLaunchKernelGGL(k_fw_prod, dim3(nb - 1, nb - 1), dim3(256), 0, nullptr, D, Vp, kb);
-        }
+        hipLaunchKernelGGL(k_fw_cross, dim3(nb > 1 ? 2 * (nb - 1) : 1), dim3(256), 0, nullptr, D, Vp, kb, nb);
+        if (nb > 1) hipLaunchKernelGGL(k_fw_prod, dim3(nb - 1, nb - 1), dim3(256), 0, nullptr, D, Vp, kb);
     }
     hipLaunchKernelGGL(k_fw_rows, dim3(g.A < 4096 ? g.A : 4096), dim3(256), 0, nullptr, g, D, Vp, d_lat);
     rc = hip_rc(hipGetLastError(), "min-plus launch");

@@ -111,10 +111,10 @@ static int prepare(ShdTopology* t) {
         }
         for (int v = 0; v < t->V; v++) {
             const int32_t cnt = t->inc_off[v + 1] - t->inc_off[v] + 1;
-            soff[v] = ((t->inc_off[v] + v) << 8) | (cnt < 255 ? cnt : 255);
+            soff[v] = (int32_t)(((uint32_t)(t->inc_off[v] + v) << 8) | (uint32_t)(cnt < 255 ? cnt : 255));
         }
         for (int v = 0; v < t->V; v++) {
-            size_t o = (size_t)(soff[v] >> 8);
+            size_t o = (size_t)((uint32_t)soff[v] >> 8);
             for (int32_t k = t->inc_off[v]; k < t->inc_off[v + 1]; k++, o++) {
                 snb[2 * o] = t->inc_nbr[k];
                 snb[2 * o + 1] = soff[t->inc_nbr[k]];

@@ -727,7 +727,7 @@ __global__ __launch_bounds__(64) void k_sssp_lds(ShdGraphDev g, int row_lo, int 
             const double ru = rel[u];
             // the list's first kRelax batches are loaded before the root is
             // removed: their latency overlaps the (LDS) sink
-            int b = t.so >> 8;
+            int b = (int)((unsigned)t.so >> 8); // (unsigned: starts up to 2^24)
             const int lim = (t.so & 255) == 255 ? 64 * kRelax : (t.so & 255); // entries worth reading
             int2 nb[kRelax];
             double2 wr[kRelax];
@@ -837,7 +837,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
             const HNode t = h.top_node(); // LDS
             const int u = t.v;
             const double mindist = -t.key;
-            int b = t.so >> 8;
+            int b = (int)((unsigned)t.so >> 8); // (unsigned: starts up to 2^24)
             // issued together: u's incidence entries (only as many lanes as
             // the list has entries, sentinel included), the last heap node
             // (the removal sinks it) and rel[u]
@@ -935,7 +935,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
             const HNode t = h.top_node(); // LDS
             const int u = t.v;
             const double mindist = -t.key;
-            int b = t.so >> 8;
+            int b = (int)((unsigned)t.so >> 8); // (unsigned: starts up to 2^24)
             const int li = lane < (t.so & 255) ? lane : (t.so & 255) - 1;
             int2 nb = snb[b + li];
             double2 wr = swr[b + li];
@@ -1470,7 +1470,7 @@ __global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80)
             const int u = kv(t);
             const uint32_t du = kd(t);
             const int so = u == pv ? uni(pso) : uni(soff[u]);
-            int b = so >> 8;
+            int b = (int)((unsigned)so >> 8); // (unsigned: starts up to 2^24)
             // issued together: u's entries (lanes past the sentinel re-read
             // it), the last heap node (the removal sinks it) and rel[u]
             const int li = lane < (so & 255) ? lane : (so & 255) - 1;
@@ -1611,7 +1611,7 @@ __global__ __launch_bounds__(64) void k_sssp_ilds(ShdGraphDev g, int row_lo, int
             const int u = kv(t);
             const uint32_t du = kd(t);
             const int so = uni(so_l[u]);
-            int b = so >> 8;
+            int b = (int)((unsigned)so >> 8); // (unsigned: starts up to 2^24)
             const int lim = (so & 255) == 255 ? 64 * kRelax : (so & 255); // entries worth reading
             Ent en[kRelax];
 #pragma unroll

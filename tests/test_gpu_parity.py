@@ -750,3 +750,22 @@ def test_minplus_needs_whole_ms():
     with pytest.raises(ShdError) as ei:
         top.latency_table_fw(d.data_ptr())
     assert ei.value.code == -95  # ENOTSUP
+
+
+@pytest.mark.timeout(600)
+def test_large_complete_graph_list_handles():
+    """A complete graph with more than 2^23 incidence entries (V = 3,000: 9M):
+    list starts above 2^23 in the 24-bit handles (read unsigned); sampled
+    rows against the oracle, the min-plus latencies against the table."""
+    import torch
+    gml = synth.complete_graph_gml(3000, 0x5EED0081)
+    top, orc, _, _ = make_pair(gml, 6000)
+    lat, rel, sv = top.table()
+    for i in list(range(0, len(sv), 97)) + [len(sv) - 1]:
+        ol, orl = orc.row(int(sv[i]), sv)
+        assert np.array_equal(bits(lat[i]), bits(ol)), i
+        assert np.array_equal(bits(rel[i]), bits(orl)), i
+    A = len(sv)
+    d = torch.empty(A * A, dtype=torch.float64, device="cuda")
+    top.latency_table_fw(d.data_ptr())
+    assert np.array_equal(bits(d.cpu().numpy().reshape(A, A)), bits(lat))
