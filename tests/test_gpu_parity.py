@@ -769,3 +769,4 @@ def test_large_complete_graph_list_handles():
     d = torch.empty(A * A, dtype=torch.float64, device="cuda")
     top.latency_table_fw(d.data_ptr())
     assert np.array_equal(bits(d.cpu().numpy().reshape(A, A)), bits(lat))
+
