@@ -1303,11 +1303,22 @@ struct Heap {
         return up2(b, s, mk(d, v), 0, false);
     }
     // igraph_2wheap_modify with a smaller distance: a shift-up at v's node.
-    // A pos that names no node holding v (never expected) is counted in *err
-    // and the update skipped: the launch then fails instead of reading
-    // outside the slab.
+    // A node that moved up into the LDS top keeps the block its pos names
+    // (no pos store for that move: one write request less per pop), so a
+    // block that does not hold v sends the search to the LDS top.  A pos
+    // that names neither (never expected) is counted in *err and the update
+    // skipped: the launch then fails instead of reading outside the slab.
     __device__ __forceinline__ uint32_t raise(int v, uint32_t d, uint32_t t, unsigned* err) {
         stat(t == 1u ? kStRaiseLds : kStRaiseHbm);
+        if (t >= 2u && (int)(t - 2u) < nblk) {
+            const int b = (int)t - 2;
+            u64 c = kSent;
+            if (lane < 15) c = blk[(size_t)b * 16 + lane];
+            __asm__ volatile("; iraise find" ::: "memory");
+            const unsigned long long bm = __ballot(lane < 15 && kv(c) == v);
+            if (bm) return up2(b, __builtin_ctzll(bm), mk(d, v), c, true);
+            t = 1u; // moved up into the LDS top since
+        }
         if (t == 1u) {
             int found = -1;
 #pragma unroll
@@ -1321,20 +1332,8 @@ struct Heap {
             const int e = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(found, __builtin_ctzll(bm)));
             return up(-1, e, mk(d, v));
         }
-        if (t < 2u || (int)(t - 2u) >= nblk) {
-            if (lane == 0) atomicOr(err, 2u);
-            return t;
-        }
-        const int b = (int)t - 2;
-        u64 c = kSent;
-        if (lane < 15) c = blk[(size_t)b * 16 + lane];
-        __asm__ volatile("; iraise find" ::: "memory");
-        const unsigned long long bm = __ballot(lane < 15 && kv(c) == v);
-        if (!bm) {
-            if (lane == 0) atomicOr(err, 4u);
-            return t;
-        }
-        return up2(b, __builtin_ctzll(bm), mk(d, v), c, true);
+        if (lane == 0) atomicOr(err, 2u);
+        return t;
     }
 
     // delete_max's sink of x (the old last node, whose place had tag tfrom)
@@ -1397,7 +1396,7 @@ struct Heap {
                 const int l1 = __builtin_ctzll(mv);
                 // the level-1 mover into the hole (the LDS or the parent block: a crossing)
                 put(hb, hs, c, l1);
-                set_pos(kv(lane64(c, l1)), tag(hb));
+                if (hb >= 0) set_pos(kv(lane64(c, l1)), tag(hb)); // (into the LDS: pos left stale, see raise)
                 if (mvl && j > 1) { // the others one level up inside their block
                     blk[(size_t)(b0 + sb) * 16 + ((bslot - 1) >> 1)] = c;
                     __asm__ volatile("; isink mv blk" ::: "memory");
@@ -1409,7 +1408,7 @@ struct Heap {
             }
         }
         put(hb, hs, x);
-        if (tag(hb) != tfrom) set_pos(kv(x), tag(hb));
+        if (hb >= 0 && tag(hb) != tfrom) set_pos(kv(x), tag(hb)); // (into the LDS: pos left stale, see raise)
     }
 };
 
