@@ -1311,12 +1311,15 @@ struct Heap {
     __device__ __forceinline__ uint32_t raise(int v, uint32_t d, uint32_t t, unsigned* err) {
         stat(t == 1u ? kStRaiseLds : kStRaiseHbm);
         if (t >= 2u && (int)(t - 2u) < nblk) {
-            const int b = (int)t - 2;
-            u64 c = kSent;
-            if (lane < 15) c = blk[(size_t)b * 16 + lane];
-            __asm__ volatile("; iraise find" ::: "memory");
-            const unsigned long long bm = __ballot(lane < 15 && kv(c) == v);
-            if (bm) return up2(b, __builtin_ctzll(bm), mk(d, v), c, true);
+            // the named block, then its ancestors' blocks (a node the sink
+            // moved up across a block boundary keeps its old pos)
+            for (int b = (int)t - 2; b >= 0; b = b >= 512 ? (b - 512) >> 4 : -1) {
+                u64 c = kSent;
+                if (lane < 15) c = blk[(size_t)b * 16 + lane];
+                __asm__ volatile("; iraise find" ::: "memory");
+                const unsigned long long bm = __ballot(lane < 15 && kv(c) == v);
+                if (bm) return up2(b, __builtin_ctzll(bm), mk(d, v), c, true);
+            }
             t = 1u; // moved up into the LDS top since
         }
         if (t == 1u) {
@@ -1396,7 +1399,8 @@ struct Heap {
                 const int l1 = __builtin_ctzll(mv);
                 // the level-1 mover into the hole (the LDS or the parent block: a crossing)
                 put(hb, hs, c, l1);
-                if (hb >= 0) set_pos(kv(lane64(c, l1)), tag(hb)); // (into the LDS: pos left stale, see raise)
+                // (the level-1 mover goes up into the hole's block or the LDS:
+                // its pos is left naming a block below, see raise)
                 if (mvl && j > 1) { // the others one level up inside their block
                     blk[(size_t)(b0 + sb) * 16 + ((bslot - 1) >> 1)] = c;
                     __asm__ volatile("; isink mv blk" ::: "memory");
