@@ -249,7 +249,15 @@ constexpr uint32_t kPtabFallback = 0xFFFFFFFFu;
 // kProbe (measurement only, SHD_SCATTER_PROBE; outputs are NOT the round's):
 // 1 skips the table gather, 2 the host->slot gathers, 3 the event store,
 // 4 the destination-slot atomic -- each stage's share of the kernel time.
-template <int kMode, int kB = kBatch, int kProbe = 0>
+// kNT: the table gather with the non-temporal (streaming) cache policy
+// (default: the gathered lines are not re-read, and streaming them keeps the
+// slab lines and the counters in the L2: scatter 0.597 vs 0.617 ms,
+// profiles/r03nt_scatter_nt.log).  Measured and not kept there: streaming
+// slab stores (0.80 ms: each 16-B store leaves the L2 as its own partial
+// write), status stores (no change), record loads (+0.005 ms).
+// SHD_SCATTER_NT=0 is the plain form.
+typedef unsigned int shd_v4u __attribute__((ext_vector_type(4)));
+template <int kMode, int kB = kBatch, int kProbe = 0, bool kNT = true>
 __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
                                                         uint64_t barrier, uint64_t end_time, uint64_t boot_end,
                                                         Bucketing bk, ShdDeliv* __restrict__ tmp,
@@ -327,8 +335,14 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
 #pragma unroll
             for (int k = 0; k < kB; k++) {
                 q[k] = make_uint2(kPtabFallback, 0u);
-                if (si[k] >= 0 && di[k] >= 0) q[k] = kProbe == 1 ? ptab[(ei[k] & 1023u) + (size_t)c.row_lo * A]
-                                                                  : ptab[ei[k]];
+                if (si[k] >= 0 && di[k] >= 0) {
+                    if (kProbe == 1) q[k] = ptab[(ei[k] & 1023u) + (size_t)c.row_lo * A];
+                    else if (kNT) {
+                        const unsigned long long v =
+                            __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ptab) + ei[k]);
+                        q[k] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+                    } else q[k] = ptab[ei[k]];
+                }
             }
 #pragma unroll
             for (int k = 0; k < kB; k++) // entries that do not fit the 8-B form (none on the bench graphs)
@@ -770,9 +784,14 @@ struct Ev {
 };
 
 // a compact slab slot (CSlab) as an event; the marker sends it to the 32-B slab
+template <bool kNT = false>
 __device__ __forceinline__ Ev c_load(const uint4* __restrict__ cslab, const ShdDeliv* __restrict__ slab, size_t i,
                                      unsigned long long tbase) {
-    const uint4 c = cslab[i];
+    uint4 c;
+    if (kNT) {
+        const shd_v4u v = __builtin_nontemporal_load(reinterpret_cast<const shd_v4u*>(cslab) + i);
+        c = make_uint4(v.x, v.y, v.z, v.w);
+    } else c = cslab[i];
     if (c.x != kCMark) return Ev{tbase + c.x, (unsigned long long)c.w, c.y, c.z};
     const ShdDeliv r = ld_ev(&slab[i]);
     return Ev{r.time, r.seq, r.src_host, r.pkt_index};
@@ -816,7 +835,7 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return v;
 }
 
-template <int E, typename Load>
+template <int E, int kNT = 0, typename Load>
 __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* __restrict__ out, uint32_t o,
                                   int lane, unsigned long long* lk = nullptr) {
     Ev v[E];
@@ -908,7 +927,14 @@ __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* _
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)(e * 64 + lane);
-        if (i < n) st_ev(&out[o + rank[e]], ShdDeliv{v[e].t, v[e].q, v[e].s, d, v[e].ix, 0u});
+        if (i >= n) continue;
+        if (kNT) {
+            shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[o + rank[e]]);
+            const shd_v4u a = {(uint32_t)v[e].t, (uint32_t)(v[e].t >> 32), (uint32_t)v[e].q, (uint32_t)(v[e].q >> 32)};
+            const shd_v4u b = {v[e].s, d, v[e].ix, 0u};
+            __builtin_nontemporal_store(a, q);
+            __builtin_nontemporal_store(b, q + 1);
+        } else st_ev(&out[o + rank[e]], ShdDeliv{v[e].t, v[e].q, v[e].s, d, v[e].ix, 0u});
     }
 }
 
@@ -1583,6 +1609,7 @@ __global__ __launch_bounds__(256) void k_hist_slab(const ShdDeliv* __restrict__ 
 // an overflow event whose destination or slot falls outside its segment, or
 // an overflow count above the list's capacity, is not stored and sets a bit
 // of the round's fault word (nbig[2]), which the host reads back (-EIO).
+template <int kNT = 0>
 __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr, const uint32_t* __restrict__ off,
                                                      uint32_t H, uint32_t host_lo, ShdDeliv* __restrict__ out,
                                                      uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
@@ -1622,10 +1649,12 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
         if (slab && cslab) { // compact records (rank sort)
             const size_t base = slab_rm ? d : (size_t)d * kSlab, stride = slab_rm ? H : 1u;
             if (n <= kSlab) {
-                auto load = [&](uint32_t i) { return c_load(cslab, slab, base + (size_t)i * stride, tbase); };
-                if (n <= 64) wave_rank_segment<1>(load, n, dh, out, b, lane, lk);
-                else if (n <= 128) wave_rank_segment<2>(load, n, dh, out, b, lane, lk);
-                else wave_rank_segment<4>(load, n, dh, out, b, lane, lk);
+                auto load = [&](uint32_t i) {
+                    return c_load<(kNT & 1) != 0>(cslab, slab, base + (size_t)i * stride, tbase);
+                };
+                if (n <= 64) wave_rank_segment<1, kNT / 2>(load, n, dh, out, b, lane, lk);
+                else if (n <= 128) wave_rank_segment<2, kNT / 2>(load, n, dh, out, b, lane, lk);
+                else wave_rank_segment<4, kNT / 2>(load, n, dh, out, b, lane, lk);
             } else {
                 for (uint32_t i = lane; i < kSlab; i += 64) {
                     const Ev e = c_load(cslab, slab, base + (size_t)i * stride, tbase);
@@ -2210,9 +2239,21 @@ int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const 
                            n, host_lo, H, offsets, w.st1, 0u, H);
     if (int rc = dbg_sync(s, "place")) return rc;
     mark(3, s);
-    hipLaunchKernelGGL(k_segsort_dst, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, w.st1, offsets, H, host_lo, out,
-                       w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm, lds_keys(), fuse ? w.st2 : nullptr,
-                       (uint32_t)w.cap_n, (uint32_t)w.cap_n, cslab, tbase);
+    // streaming cache policy (SHD_SEGSORT_NT bits, default 3): 1 the compact
+    // slab loads (read once), 2 the output stores (not re-read by the round;
+    // streaming them also leaves the next scatter's lines cached): round 0.819
+    // -0.826 vs 0.855-0.880 ms in one process (profiles/r03nt_segsort_nt.log)
+    const char* ntv = getenv("SHD_SEGSORT_NT");
+    const int nt = ntv ? atoi(ntv) : 3;
+#define SHD_SEGSORT_LAUNCH(M)                                                                                      \
+    hipLaunchKernelGGL(k_segsort_dst<M>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, w.st1, offsets, H, host_lo, \
+                       out, w.big, w.nbig, rank_sort(), 0u, H, slab, slab_rm, lds_keys(), fuse ? w.st2 : nullptr,   \
+                       (uint32_t)w.cap_n, (uint32_t)w.cap_n, cslab, tbase)
+    if (nt == 1) SHD_SEGSORT_LAUNCH(1);
+    else if (nt == 2) SHD_SEGSORT_LAUNCH(2);
+    else if (nt == 3) SHD_SEGSORT_LAUNCH(3);
+    else SHD_SEGSORT_LAUNCH(0);
+#undef SHD_SEGSORT_LAUNCH
     if (int rc = dbg_sync(s, "k_segsort_dst")) return rc;
     if (int rc = sort_listed(w, w.st1, offsets, out, s)) return rc;
     if (int rc = dbg_sync(s, "k_segsort_mid + k_segsort_merge")) return rc;
@@ -2383,6 +2424,8 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
         const char* sb = getenv("SHD_SCATTER_BATCH");
         const char* pr = getenv("SHD_SCATTER_PROBE");
         const int probe = pr ? atoi(pr) : 0;
+        const char* ntv = getenv("SHD_SCATTER_NT");
+        const int nt = ntv ? atoi(ntv) : 1;
 #define SHD_PROBE_LAUNCH(P)                                                                                        \
     hipLaunchKernelGGL((k_pkt_scatter<2, kBatch, P>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier, \
                        end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2, w.nbig + 1, cs)
@@ -2391,7 +2434,11 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
         else if (pipe == kSlabPipe && probe == 3) SHD_PROBE_LAUNCH(3);
         else if (pipe == kSlabPipe && probe == 4) SHD_PROBE_LAUNCH(4);
 #undef SHD_PROBE_LAUNCH
-        else if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
+        else if (pipe == kSlabPipe && nt == 0)
+            hipLaunchKernelGGL((k_pkt_scatter<2, kBatch, 0, false>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n,
+                               barrier, end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2,
+                               w.nbig + 1, cs);
+else if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
             hipLaunchKernelGGL((k_pkt_scatter<2, 8>), dim3(bk.ntiles), dim3(kBlock), 0, s, *c, d_recs, n, barrier,
                                end_time, bootstrap_end, bk, w.slab, d_status, w.cnt1, counters, w.st2,
                                w.nbig + 1, cs);
