@@ -2,7 +2,7 @@
 """In-process A/B of a per-launch knob on the C3 round (no allocation / box
 variance between the arms): alternating blocks of 20 rounds, live per-stage
 timing, outputs compared.  Usage: agg_probe.py [ENV_NAME VALUE VALUE ...]
-(default: SHD_DEST_AGG 1 0)."""
+(default: SHD_DEST_AGG 1 0); VALUE "-" leaves the variable unset."""
 import ctypes as C
 import os
 import sys
@@ -36,7 +36,10 @@ def main():
     name, vals = (sys.argv[1], sys.argv[2:]) if len(sys.argv) > 2 else ("SHD_DEST_AGG", ["1", "0"])
     for rep in range(3):
         for agg in vals:
-            os.environ[name] = agg
+            if agg == "-":
+                os.environ.pop(name, None)
+            else:
+                os.environ[name] = agg
             for _ in range(2):
                 top.process_device(d_recs.data_ptr(), P, 110_000_000, 10**15, 0, d_out.data_ptr(),
                                    d_off.data_ptr(), d_status.data_ptr(), d_cnt.data_ptr(), 0)
