@@ -38,7 +38,7 @@ def main():
     for f in files:
         for r in csv.DictReader(open(f)):
             k = kname(r["Kernel_Name"])
-            k = "k_pkt_scatter" if k.startswith("k_pkt_scatter") else k
+            k = k.split("<", 1)[0]  # template instances (k_pkt_scatter<2, 4, 0, true>, k_segsort_dst<3>)
             agg.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
     res = {}
     for k, st in STAGE.items():
