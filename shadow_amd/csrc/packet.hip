@@ -1266,7 +1266,7 @@ __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* uns
                                                              const uint32_t* __restrict__ off,
                                                              const uint32_t* __restrict__ big,
                                                              const uint32_t* __restrict__ nbig, ShdDeliv* out,
-                                                             ShdDeliv* scratch, MergeMeta mm) {
+                                                             ShdDeliv* scratch, MergeMeta mm, uint32_t rank_small) {
     extern __shared__ __attribute__((aligned(16))) char mid_smem[];
     Ev* sv = reinterpret_cast<Ev*>(mid_smem);
     __shared__ uint32_t sb[kMidThreads], sn[kMidThreads], sst[kMidThreads + 1];
@@ -1305,7 +1305,26 @@ __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* uns
             const uint32_t c = loc - bu(sst[lo]), sbb = bu(sb[lo]), snn = bu(sn[lo]);
             const uint32_t cb = sbb + c * kChunk, cn = snn - c * kChunk < kChunk ? snn - c * kChunk : kChunk;
             ShdDeliv* dst = (snn <= kChunk || (merge_passes(snn) & 1u) == 0) ? out : scratch;
-            lds_sort_run(unsorted, dst, cb, cn, bu(unsorted[cb].dst_host), sv);
+            if (rank_small && snn <= (uint32_t)kSmallSeg) {
+                // a segment of at most 256 events (the slab pipeline lists
+                // every segment above its 128 slab slots): one wave's rank
+                // sort, as k_segsort_dst's, instead of the workgroup's
+                // 256-wide bitonic network (36 barrier stages)
+                if (threadIdx.x < 64) {
+                    const uint32_t dh = bu(unsorted[cb].dst_host);
+                    auto load = [&](uint32_t i) {
+                        const ShdDeliv r = ld_ev(&unsorted[cb + i]);
+                        return Ev{r.time, r.seq, r.src_host, r.pkt_index};
+                    };
+                    unsigned long long* lk = reinterpret_cast<unsigned long long*>(sv); // 64 * 4 + 8 keys
+                    if (snn <= 64) wave_rank_segment<1>(load, snn, dh, dst, cb, (int)threadIdx.x, lk);
+                    else if (snn <= 128) wave_rank_segment<2>(load, snn, dh, dst, cb, (int)threadIdx.x, lk);
+                    else wave_rank_segment<4>(load, snn, dh, dst, cb, (int)threadIdx.x, lk);
+                }
+                __syncthreads();
+            } else {
+                lds_sort_run(unsorted, dst, cb, cn, bu(unsorted[cb].dst_host), sv);
+            }
         }
         base += total;
         __syncthreads();
@@ -2017,8 +2036,9 @@ int mid_attr() {
 int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDeliv* out, hipStream_t s) {
     if (int rc = mid_attr()) return rc;
     const MergeMeta mm = merge_meta(w);
+    const char* mr = getenv("SHD_MID_RANK");
     hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(kMidThreads), kMidLds, s, unsorted, offsets, w.big, w.nbig,
-                       out, w.st1, mm);
+                       out, w.st1, mm, (uint32_t)!(mr && strcmp(mr, "0") == 0));
     if (int rc = hip_status(hipGetLastError(), "k_segsort_mid launch")) return rc;
     hipLaunchKernelGGL(k_segsort_merge, dim3(512), dim3(256), 0, s, out, w.st1, mm);
     if (int rc = hip_status(hipGetLastError(), "k_segsort_merge launch")) return rc;
