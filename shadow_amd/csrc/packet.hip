@@ -529,6 +529,29 @@ __global__ __launch_bounds__(256) void k_scan_add(uint32_t* __restrict__ out, si
     }
 }
 
+// k_scan_top and k_scan_add in one launch: every workgroup sums the tile
+// totals before its tile itself (bsum[0..t), at most a few hundred words,
+// L2-warm) instead of reading a prefix array a one-workgroup launch wrote.
+// A 256-element group lies in one kScanTile tile; out[len] (the group that
+// holds index len) = that sum + the tile's own total when len is inside it.
+__global__ __launch_bounds__(256) void k_scan_add_tiles(uint32_t* __restrict__ out, size_t len,
+                                                        const uint32_t* __restrict__ bsum, uint32_t nb,
+                                                        unsigned long long* counters) {
+    const size_t i0 = (size_t)blockIdx.x * blockDim.x;
+    const uint32_t t = (uint32_t)(i0 / kScanTile);
+    uint32_t v = 0;
+    for (uint32_t k = threadIdx.x; k < t && k < nb; k += blockDim.x) v += bsum[k];
+    uint32_t pre;
+    (void)block_excl_scan(v, &pre);
+    const size_t i = i0 + threadIdx.x;
+    if (i < len) out[i] += pre;
+    if (i == len) {
+        const uint32_t tot = pre + (t < nb ? bsum[t] : 0u);
+        out[len] = tot;
+        if (counters) counters[0] = tot;
+    }
+}
+
 // The same scan in ONE launch of one 1,024-thread workgroup (len <=
 // kScanOneMax): each wave owns a contiguous stretch of whole 256-element
 // chunks; pass 1 sums it with 16-B loads, the 16 wave sums are combined
@@ -2197,6 +2220,12 @@ void scan_counts(const uint32_t* in, size_t len, uint32_t* out, uint32_t* bsum, 
     }
     const uint32_t nb = (uint32_t)((len + kScanTile - 1) / kScanTile);
     hipLaunchKernelGGL(k_scan_local, dim3(nb ? nb : 1), dim3(256), 0, s, in, len, out, bsum);
+    const char* s3 = getenv("SHD_SCAN3");
+    if (!(s3 && strcmp(s3, "1") == 0)) {
+        hipLaunchKernelGGL(k_scan_add_tiles, dim3(grid_for(len + 1, 256, 1u << 30)), dim3(256), 0, s, out, len, bsum,
+                           nb, counters);
+        return;
+    }
     hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(256), 0, s, bsum, nb);
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(len + 1, 256, 1u << 30)), dim3(256), 0, s, out, len, bsum, nb,
                        counters);
