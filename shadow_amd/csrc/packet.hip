@@ -1455,6 +1455,9 @@ __global__ __launch_bounds__(256) void k_segsort_merge(ShdDeliv* out, ShdDeliv* 
     __shared__ uint32_t sh[8];
     const uint32_t tid = threadIdx.x;
     const uint32_t items = bu(mm.hdr[1]);
+    // no segment above kChunk (every uniform round): leave without touching
+    // the claim counter -- 512 same-address atomics cost more than the launch
+    if (items == 0) return;
     uint32_t done_slot = ~0u; // the previous tile's (segment, pass) counter, published at the next claim
     for (;;) {
         // one lane: publish the previous tile (its stores were drained before
