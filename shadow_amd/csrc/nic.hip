@@ -33,6 +33,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
+#include <cstdlib>
+#include <cstring>
 
 #include "codel_dev.h"
 #include "shd_internal.h"
@@ -159,12 +161,15 @@ struct Host {
         }
     }
     // _networkinterface_refillTokenBucketsCB (:166-186)
-    __device__ void refill(uint64_t now) {
+    __device__ void refill_tokens() {
         s.refill_pending = 0;
         s.recv_remaining += s.recv_refill; // _networkinterface_refillTokenBucket (:108-115)
         if (s.recv_remaining > s.recv_capacity) s.recv_remaining = s.recv_capacity;
         s.send_remaining += s.send_refill;
         if (s.send_remaining > s.send_capacity) s.send_remaining = s.send_capacity;
+    }
+    __device__ void refill(uint64_t now) {
+        refill_tokens();
         receive(now);
         send(now);
         schedule_if_needed(s, now);
@@ -193,6 +198,14 @@ __global__ __launch_bounds__(256) void k_nic_init(uint32_t n, const uint64_t* __
     st[h] = s;
 }
 
+// kMerged: the three event kinds share one call site each for receive, send
+// and the refill scheduling (a lane's calls and their order are unchanged:
+// arrival -> receive if the router queue was empty; send request -> send;
+// refill -> receive, send, schedule), so a wave whose lanes took different
+// kinds runs the CoDel dequeue and the send loop once per event, not once
+// per kind (SHD_NIC_MERGED=1; the per-kind calls stay the default until
+// measured).
+template <bool kMerged>
 __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, const ShdDeliv* __restrict__ ev,
                                                 const uint32_t* __restrict__ eoff, const uint32_t* __restrict__ elen,
                                                 const ShdNicSend* __restrict__ sends,
@@ -253,6 +266,8 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
         const bool own_is_send = have_s && (!have_r || ts <= tr);
         const uint64_t town = own_is_send ? ts : tr;
         const bool own_exists = have_s || have_r;
+        uint64_t now = 0;
+        bool do_recv = false, do_send = false, do_sched = false;
         if (have_a && (!own_exists || ta < town || (ta == town && a.src_host < self))) {
             if (a.dst_host != self) bad |= kErrHost;
             if (ta < last) bad |= kErrOrder;
@@ -272,16 +287,26 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
                 a_nxt = ev[i + 1];
                 l_nxt = elen[i + 1];
             }
-            if (!buffered) H.receive(ta);
+            if (kMerged) now = ta, do_recv = !buffered;
+            else if (!buffered) H.receive(ta);
         } else if (own_is_send) {
             if (ts >= window_end) {
                 bad |= kErrWindow;
                 break;
             }
             H.sk++; // networkinterface_wantsSend (:633-661)
-            H.send(ts);
+            if (kMerged) now = ts, do_send = true;
+            else H.send(ts);
+        } else if (kMerged) {
+            H.refill_tokens(); // _networkinterface_refillTokenBucketsCB (:166-186)
+            now = tr, do_recv = do_send = do_sched = true;
         } else {
             H.refill(tr);
+        }
+        if (kMerged) {
+            if (do_recv) H.receive(now);
+            if (do_send) H.send(now);
+            if (do_sched) schedule_if_needed(H.s, now);
         }
         if (H.q.bad) bad |= kErrAssert;
     }
@@ -374,10 +399,17 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
         rc = hip_status(hipMemsetAsync(d_send_time + srange[0], 0xff, sizeof(uint64_t) * (srange[1] - srange[0]), s),
                         "memset");
     if (!rc) {
-        hipLaunchKernelGGL(k_nic_run, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base, d_events,
-                           d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end, bootstrap_end,
-                           d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status, fate_cap, d_send_time,
-                           d_err);
+        const char* mv = getenv("SHD_NIC_MERGED");
+        if (!(mv && strcmp(mv, "1") == 0))
+            hipLaunchKernelGGL(k_nic_run<false>, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base,
+                               d_events, d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end,
+                               bootstrap_end, d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status,
+                               fate_cap, d_send_time, d_err);
+        else
+            hipLaunchKernelGGL(k_nic_run<true>, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base,
+                               d_events, d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end,
+                               bootstrap_end, d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status,
+                               fate_cap, d_send_time, d_err);
         rc = hip_status(hipGetLastError(), "k_nic_run launch");
     }
     if (!rc) rc = hip_status(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s), "D2H");
