@@ -203,8 +203,9 @@ __global__ __launch_bounds__(256) void k_nic_init(uint32_t n, const uint64_t* __
 // arrival -> receive if the router queue was empty; send request -> send;
 // refill -> receive, send, schedule), so a wave whose lanes took different
 // kinds runs the CoDel dequeue and the send loop once per event, not once
-// per kind (SHD_NIC_MERGED=1; the per-kind calls stay the default until
-// measured).
+// per kind: window 0.567 vs 0.654 ms on the C3 round output, identical
+// fates and states (profiles/r03nicm_merged.log; SHD_NIC_MERGED=0 keeps the
+// per-kind calls).
 template <bool kMerged>
 __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, const ShdDeliv* __restrict__ ev,
                                                 const uint32_t* __restrict__ eoff, const uint32_t* __restrict__ elen,
@@ -400,7 +401,7 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
                         "memset");
     if (!rc) {
         const char* mv = getenv("SHD_NIC_MERGED");
-        if (!(mv && strcmp(mv, "1") == 0))
+        if (mv && strcmp(mv, "0") == 0)
             hipLaunchKernelGGL(k_nic_run<false>, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base,
                                d_events, d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end,
                                bootstrap_end, d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status,
