@@ -278,7 +278,14 @@ int shd_round_collect(ShdTopology* top, ShdDeliv* out, size_t cap, size_t* n_out
  * hipStream_t (NULL = default stream).  Lookup side effects are NOT applied:
  * rows must have been touched (shd_round_append or shd_topology_touch_all).
  * out needs n entries, dst_offsets nhosts+1, status n; counters[0] =
- * delivered count, counters[1] = min delivered time (both written async). */
+ * delivered count, counters[1] = min delivered time (both written async).
+ * A round whose device-side guards fired (a merge tile that gave up waiting,
+ * a metadata overflow, an out-of-range overflow event) has SHD_ROUND_FAULT
+ * set in counters[0] -- in that same round, so an asynchronous caller sees
+ * it with the count -- and its outputs must not be used; the call returns
+ * -EIO itself when stream is NULL (synchronous), else the next call on the
+ * topology does (once). */
+#define SHD_ROUND_FAULT (1ull << 63)
 int shd_round_process_device(ShdTopology* top, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                              uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out,
                              uint32_t* d_dst_offsets, uint8_t* d_status, uint64_t* d_counters, void* stream);

@@ -31,6 +31,10 @@ extern "C" int shd_dev_init(int device) {
     return hip_err(hipSetDevice(device), "hipSetDevice");
 }
 
+extern "C" int shd_dev_mem_info(size_t* free_bytes, size_t* total_bytes) {
+    return hip_err(hipMemGetInfo(free_bytes, total_bytes), "hipMemGetInfo");
+}
+
 extern "C" int shd_dev_malloc(void** p, size_t bytes) {
     *p = nullptr;
     return hip_err(hipMalloc(p, bytes ? bytes : 4), "hipMalloc");

@@ -1207,15 +1207,29 @@ __device__ __forceinline__ uint32_t merge_passes(uint32_t n) {
 // the segments taking part in pass p are a prefix), their tile prefix, and
 // per (segment, pass) a count of finished tiles.
 struct MergeMeta {
-    uint32_t* hdr;   // [0] segments, [1] items, [2] work counter, [3] spin-limit hits,
-                     // [4 + p] first item of pass p (p <= kMaxPasses), [32 + p] segments in pass p
+    uint32_t* hdr;   // [0] segments, [1] items, [2] work counter, [3] this round's fault word,
+                     // [4 + p] first item of pass p (p <= kMaxPasses), [32 + p] segments in pass p,
+                     // [kStickyFault] OR of every round's fault word since the host last read it
     uint4* seg;      // cap
     uint32_t* tpre;  // cap + 1
     uint32_t* done;  // cap * kMaxPasses
     uint32_t cap;
     uint32_t cap_big; // entries of the big-segment list (nbig[0] never exceeds it)
+    unsigned long long* flag; // the caller's counters[0] (or null): SHD_ROUND_FAULT set in the faulting round
+    uint32_t spin_limit;      // merge waits before a tile gives up (SHD_DEBUG_MERGE_SPIN; 0: every wait faults)
 };
 constexpr uint32_t kMetaHdr = 64;
+constexpr uint32_t kStickyFault = 60;
+
+// A fault of this round: its word into the round's header slot, the sticky
+// word the host reads back, and the caller-visible bit of counters[0]
+// (include/shdnet.h SHD_ROUND_FAULT), so the call whose round faulted can see
+// it without waiting for a later call.
+__device__ __forceinline__ void note_fault(const MergeMeta& mm, uint32_t f) {
+    if (!f) return;
+    atomicOr(&mm.hdr[kStickyFault], f);
+    if (mm.flag) atomicOr(mm.flag, (unsigned long long)SHD_ROUND_FAULT);
+}
 
 // Block-uniform value read from LDS or memory, made wave-uniform for the
 // compiler (an SGPR): loops and branches around barriers must be uniform in
@@ -1372,7 +1386,10 @@ __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* uns
         // this round's fault word: spin-limit hits of the merge (counted by
         // k_segsort_merge) and the metadata overflow bit (cannot happen: cap
         // covers n / (kChunk + 1)); read back by the host (ws_faults)
-        mm.hdr[3] = (acc > mm.cap ? 0x80000000u : 0u) | ((nbig[2] | (nb_raw > mm.cap_big ? kFaultBigCap : 0u)) << 24);
+        const uint32_t fw =
+            (acc > mm.cap ? 0x80000000u : 0u) | ((nbig[2] | (nb_raw > mm.cap_big ? kFaultBigCap : 0u)) << 24);
+        mm.hdr[3] = fw;
+        note_fault(mm, fw);
         // segments taking part in pass p: those with more than p passes
         uint32_t part = 0;
         for (int p = (int)kMaxPasses - 1; p >= 0; p--) {
@@ -1493,13 +1510,15 @@ __global__ __launch_bounds__(256) void k_segsort_merge(ShdDeliv* out, ShdDeliv* 
         if (p > 0) { // the segment's previous pass must be complete (its tiles were claimed before this one)
             if (tid == 0) {
                 uint32_t spins = 0;
-                while (__hip_atomic_load(&mm.done[sgi * kMaxPasses + p - 1], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) < ntile) {
+                bool gave_up = mm.spin_limit == 0; // (debug knob: every wait gives up)
+                while (!gave_up && __hip_atomic_load(&mm.done[sgi * kMaxPasses + p - 1], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) < ntile) {
                     __builtin_amdgcn_s_sleep(2);
-                    if (++spins == (1u << 22)) { // every wave ends (inputs that never complete would be a bug)
-                        atomicAdd(&mm.hdr[3], 1u);
-                        break;
-                    }
+                    gave_up = ++spins >= mm.spin_limit; // every wave ends (inputs that never complete would be a bug)
+                }
+                if (gave_up) {
+                    atomicAdd(&mm.hdr[3], 1u);
+                    note_fault(mm, 1u);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // drops this CU's stale lines
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (holds the barrier for the invalidate)
@@ -1898,7 +1917,10 @@ __global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__
 
 // the round's fault word when no merge kernel runs: the stage guards only
 __global__ void k_fault_word(const uint32_t* __restrict__ nbig, MergeMeta mm) {
-    if (threadIdx.x == 0) mm.hdr[3] = nbig[2] << 24;
+    if (threadIdx.x == 0) {
+        mm.hdr[3] = nbig[2] << 24;
+        note_fault(mm, nbig[2] << 24);
+    }
 }
 
 // ---- workspace (grow-only, one per topology; see shd_dev_ws_new) ----
@@ -1946,6 +1968,8 @@ int ws_quiesce(Ws& w) {
     return hip_status(hipEventSynchronize(w.done), "hipEventSynchronize ws");
 }
 
+int ws_faults(Ws& w, bool completed, hipStream_t s);
+
 int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
     int rc = 0;
     if ((n > w.cap_n || m + 1 > w.cap_m || H + 1 > w.cap_h) && (rc = ws_quiesce(w))) return rc;
@@ -1968,7 +1992,8 @@ int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
     // merge metadata: segments above kChunk events are at most n / (kChunk + 1)
     const uint32_t cm = (uint32_t)((n + n / 8 + 1024) / (kChunk + 1) + 2);
     if (!w.meta || cm > w.cap_meta) {
-        if ((rc = ws_quiesce(w))) return rc;
+        // (an unread fault of the last round lives in the sticky word about to be freed)
+        if ((rc = ws_quiesce(w)) || (rc = ws_faults(w, true, nullptr))) return rc;
         (void)hipFree(w.meta);
         w.meta = nullptr;
         w.cap_meta = 0;
@@ -2032,7 +2057,14 @@ int slab_reserve(Ws& w, uint32_t H) {
     return rc;
 }
 
-MergeMeta merge_meta(const Ws& w) {
+// SHD_DEBUG_MERGE_SPIN=k: merge waits give up after k spins (0: at once, so
+// every multi-pass segment faults -- the test of the fault path); default 2^22
+uint32_t merge_spin_limit() {
+    const char* v = getenv("SHD_DEBUG_MERGE_SPIN");
+    return v ? (uint32_t)strtoul(v, nullptr, 10) : (1u << 22);
+}
+
+MergeMeta merge_meta(const Ws& w, unsigned long long* flag) {
     MergeMeta m;
     m.cap_big = w.cap_h;
     m.hdr = w.meta;
@@ -2040,6 +2072,8 @@ MergeMeta merge_meta(const Ws& w) {
     m.tpre = w.meta + kMetaHdr + 4ull * w.cap_meta;
     m.done = m.tpre + w.cap_meta + 1;
     m.cap = w.cap_meta;
+    m.flag = flag;
+    m.spin_limit = merge_spin_limit();
     return m;
 }
 
@@ -2055,39 +2089,56 @@ int mid_attr() {
     return rc;
 }
 
-// listed segments: LDS runs, then the merge passes of the larger ones.  The
-// round's merge fault word (hdr[3]: tiles that gave up waiting for their
-// segment's previous pass, or a metadata overflow) is copied to pinned host
-// memory behind the merge; ws_faults reports it.
-int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDeliv* out, hipStream_t s) {
+// The workspace's sticky fault word (meta hdr[kStickyFault]: the OR of every
+// round's fault word since the host last read it) copied to pinned host
+// memory at the end of a round, on its stream.  The device only ORs into the
+// sticky word, so a round that finishes before the host looked cannot hide
+// an earlier round's fault.
+int copy_faults(Ws& w, hipStream_t s) {
+    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
+        w.fault = nullptr;
+        return shd_fail(-ENOMEM, "hipHostMalloc fault word");
+    }
+    return hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 4, hipMemcpyDeviceToHost, s), "fault word D2H");
+}
+
+// listed segments: LDS runs, then the merge passes of the larger ones.  A
+// round's fault (tiles that gave up waiting for their segment's previous
+// pass, a metadata overflow, a stage guard) sets SHD_ROUND_FAULT in the
+// caller's counters[0] (flag) during the round and the sticky word, which
+// ws_faults reports.
+int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDeliv* out, hipStream_t s,
+                unsigned long long* flag) {
     if (int rc = mid_attr()) return rc;
-    const MergeMeta mm = merge_meta(w);
+    const MergeMeta mm = merge_meta(w, flag);
     const char* mr = getenv("SHD_MID_RANK");
     hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(kMidThreads), kMidLds, s, unsorted, offsets, w.big, w.nbig,
                        out, w.st1, mm, (uint32_t)!(mr && strcmp(mr, "0") == 0));
     if (int rc = hip_status(hipGetLastError(), "k_segsort_mid launch")) return rc;
     hipLaunchKernelGGL(k_segsort_merge, dim3(512), dim3(256), 0, s, out, w.st1, mm);
     if (int rc = hip_status(hipGetLastError(), "k_segsort_merge launch")) return rc;
-    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
-        w.fault = nullptr;
-        return shd_fail(-ENOMEM, "hipHostMalloc fault word");
-    }
-    return hip_status(hipMemcpyAsync(w.fault, mm.hdr + 3, 4, hipMemcpyDeviceToHost, s), "fault word D2H");
+    return copy_faults(w, s);
 }
 
-// The merge fault word of the workspace's last completed round (non-blocking:
-// a round still running is checked by a later call).  -EIO: a merge tile hit
-// its spin limit (its input may have been incomplete: the destination
-// segment may be mis-sorted) or the merge metadata overflowed.
-int ws_faults(Ws& w, bool completed) {
+// The sticky fault word as of the workspace's last completed use.  completed:
+// the caller has synchronised that use (the report is about the call's own
+// round); else non-blocking -- a round still running is checked by a later
+// call (an asynchronous caller sees its own round's fault in counters[0]).
+// A fault read here is cleared on the device too (s: a stream the next
+// launches follow; NULL = synchronously -- nothing is in flight).  -EIO: a
+// merge tile hit its spin limit (its input may have been incomplete: the
+// destination segment may be mis-sorted), the merge metadata overflowed or a
+// stage guard fired.
+int ws_faults(Ws& w, bool completed, hipStream_t s) {
     if (!w.used || !w.fault) return 0;
     if (!completed && hipEventQuery(w.done) != hipSuccess) return 0;
     const uint32_t f = __atomic_load_n(w.fault, __ATOMIC_ACQUIRE);
     if (!f) return 0;
     *w.fault = 0;
+    (void)(s ? hipMemsetAsync(w.meta + kStickyFault, 0, 4, s) : hipMemset(w.meta + kStickyFault, 0, 4));
     const uint32_t g = (f >> 24) & 0x7fu;
-    return shd_fail(-EIO, "round fault word %#x in a previous round (%u merge spin-limit hits%s%s%s%s%s)", f,
-                    f & 0xffffffu, (f & 0x80000000u) ? ", merge metadata overflow" : "",
+    return shd_fail(-EIO, "round fault word %#x (%s%s%s%s%s%s)", f,
+                    (f & 0xffffffu) ? "merge spin-limit hits" : "", (f & 0x80000000u) ? ", merge metadata overflow" : "",
                     (g & kFaultOvfRange) ? ", overflow event outside its segment" : "",
                     (g & kFaultOvfCap) ? ", overflow count above its list" : "",
                     (g & kFaultBigCap) ? ", big-segment list full" : "",
@@ -2275,7 +2326,7 @@ int group_and_sort(Ws& w, const ShdDeliv* in, const uint8_t* status, const uint3
     mark(3, s);
     hipLaunchKernelGGL(k_bucket_sort, dim3(bk.nb), dim3(kSortBlock), 0, s, w.st1, bk, w.off1, offsets, out,
                        w.big, w.nbig);
-    if (int rc = sort_listed(w, out, offsets, out, s)) return rc; // placed unsorted in out; st1 is free now
+    if (int rc = sort_listed(w, out, offsets, out, s, counters)) return rc; // placed unsorted in out; st1 is free now
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
     return hip_status(hipGetLastError(), "group_and_sort launch");
@@ -2317,7 +2368,7 @@ int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const 
     else SHD_SEGSORT_LAUNCH(0);
 #undef SHD_SEGSORT_LAUNCH
     if (int rc = dbg_sync(s, "k_segsort_dst")) return rc;
-    if (int rc = sort_listed(w, w.st1, offsets, out, s)) return rc;
+    if (int rc = sort_listed(w, w.st1, offsets, out, s, counters)) return rc;
     if (int rc = dbg_sync(s, "k_segsort_mid + k_segsort_merge")) return rc;
     mark(4, s);
     if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
@@ -2346,7 +2397,7 @@ int ws_begin(Ws& w, hipStream_t s) {
     if (rc) return rc;
     if (w.device >= 0 && w.device != dev) return shd_fail(-EINVAL, "workspace of device %d used on device %d", w.device, dev);
     w.device = dev;
-    if ((rc = ws_faults(w, false))) return rc;
+    if ((rc = ws_faults(w, false, s))) return rc;
     if (!w.done && (rc = hip_status(hipEventCreateWithFlags(&w.done, hipEventDisableTiming), "hipEventCreate ws")))
         return rc;
     if (w.used && w.last != s) return hip_status(hipStreamWaitEvent(s, w.done, 0), "hipStreamWaitEvent ws");
@@ -2359,6 +2410,16 @@ int ws_end(Ws& w, hipStream_t s) {
 }
 
 } // namespace
+
+// The workspace's faults after its last use, waited for: for callers that
+// synchronised their own streams (multi-shard collect, the exchange).
+extern "C" int shd_dev_ws_check_faults(void* ws) {
+    if (!ws) return 0;
+    Ws& w = *static_cast<Ws*>(ws);
+    if (!w.used) return 0;
+    if (int rc = hip_status(hipEventSynchronize(w.done), "hipEventSynchronize ws")) return rc;
+    return ws_faults(w, true, nullptr);
+}
 
 extern "C" int shd_dev_ws_new(void** ws) {
     *ws = new (std::nothrow) Ws();
@@ -2538,7 +2599,7 @@ else if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
     if (rc) return rc;
     if (stream) return 0;
     if ((rc = hip_status(hipStreamSynchronize(s), "packet round"))) return rc;
-    return ws_faults(w, true);
+    return ws_faults(w, true, s);
 }
 
 extern "C" int shd_round_timing_enable(int enable) {
@@ -2608,7 +2669,7 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
     if (rc) return rc;
     if (stream) return 0;
     if ((rc = hip_status(hipStreamSynchronize(s), "deliv sort"))) return rc;
-    return ws_faults(w, true);
+    return ws_faults(w, true, s);
 }
 
 // Regroup of the exchange's W received blocks (see k_runs_count): d_in holds
@@ -2638,11 +2699,11 @@ extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, si
                            d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
     if ((rc = hip_status(hipGetLastError(), "k_runs_sort launch"))) return rc;
     if ((rc = dbg_sync(s, "k_runs_sort"))) return rc;
-    if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s))) return rc;
+    if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s, nullptr))) return rc;
     if ((rc = ws_end(w, s))) return rc; // (not a timed round stage: shd_round_timing_* time the decide side)
     if (stream) return 0;
     if ((rc = hip_status(hipStreamSynchronize(s), "merge runs"))) return rc;
-    return ws_faults(w, true);
+    return ws_faults(w, true, s);
 }
 
 // The sender's side of shd_round_process_exchange: the slab round up to the
@@ -2687,11 +2748,7 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
     if ((rc = dbg_sync(s, "grouped round"))) return rc;
     // the guard bits of this round (nbig[2]) go to the fault word the host
     // reads back (no merge kernel runs on the sender's side)
-    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
-        w.fault = nullptr;
-        return shd_fail(-ENOMEM, "hipHostMalloc fault word");
-    }
-    hipLaunchKernelGGL(k_fault_word, dim3(1), dim3(64), 0, s, w.nbig, merge_meta(w));
-    if ((rc = hip_status(hipMemcpyAsync(w.fault, w.meta + 3, 4, hipMemcpyDeviceToHost, s), "fault word D2H"))) return rc;
+    hipLaunchKernelGGL(k_fault_word, dim3(1), dim3(64), 0, s, w.nbig, merge_meta(w, counters));
+    if ((rc = copy_faults(w, s))) return rc;
     return ws_end(w, s);
 }

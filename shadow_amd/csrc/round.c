@@ -167,6 +167,11 @@ static int collect_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_o
     shd_pkt_ctx(t, &c);
     rc = shd_dev_packet_round(&c, d_recs, n, t->barrier, t->end_time, t->bootstrap_end, d_out, d_off, d_status,
                               d_cnt, NULL);
+    if (shd_ptab_release_for_retry(t, rc)) {
+        shd_pkt_ctx(t, &c);
+        rc = shd_dev_packet_round(&c, d_recs, n, t->barrier, t->end_time, t->bootstrap_end, d_out, d_off, d_status,
+                                  d_cnt, NULL);
+    }
     if (rc) goto done;
     uint64_t cnt[2];
     if ((rc = shd_dev_d2h(cnt, d_cnt, 16))) goto done;
@@ -321,7 +326,7 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
         ShdShard* s = &t->shards[k];
         const size_t nk = pbeg[k + 1] - pbeg[k];
         if (!(rc = shd_dev_init(s->device)) && !(rc = shd_dev_stream_sync(s->stream)) &&
-            !(rc = shd_dev_d2h(cnt[k], s->d_cnt, 16)) &&
+            !(rc = shd_dev_ws_check_faults(s->ws)) && !(rc = shd_dev_d2h(cnt[k], s->d_cnt, 16)) &&
             !(rc = shd_dev_d2h(offk + ((size_t)H + 1) * (size_t)k, s->d_off, sizeof(uint32_t) * ((size_t)H + 1))))
             rc = shd_dev_d2h(pst + pbeg[k], s->d_status, nk);
     }
@@ -370,6 +375,7 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
             rc = shd_dev_deliv_merge_runs(sm->ws, sm->d_recv, 0, tot, sm->d_rofs, sm->d_rofs + (size_t)S * (hi - lo + 1),
                                           (uint32_t)S, lo, hi, sm->d_fin, sm->d_fin_off, sm->stream);
         if (!rc) rc = shd_dev_stream_sync(sm->stream);
+        if (!rc) rc = shd_dev_ws_check_faults(sm->ws);
         if (!rc && out && tot) rc = shd_dev_d2h(out + obase, sm->d_fin, sizeof(ShdDeliv) * tot);
         if (!rc && dst_offsets) {
             if ((rc = shd_dev_d2h(dst_offsets + lo, sm->d_fin_off, sizeof(uint32_t) * ((size_t)(hi - lo) + 1))))
@@ -431,6 +437,11 @@ int shd_round_process_device(ShdTopology* t, const ShdPkt* d_recs, size_t n, uin
         shd_pkt_ctx(t, &c);
         rc = shd_dev_packet_round(&c, d_recs, n, barrier, end_time, bootstrap_end, d_out, d_dst_offsets, d_status,
                                   d_counters, stream);
+        if (shd_ptab_release_for_retry(t, rc)) { /* the workspace did not fit beside the 8-B table */
+            shd_pkt_ctx(t, &c);
+            rc = shd_dev_packet_round(&c, d_recs, n, barrier, end_time, bootstrap_end, d_out, d_dst_offsets,
+                                      d_status, d_counters, stream);
+        }
     }
     pthread_mutex_unlock(&t->round_mu);
     return rc;

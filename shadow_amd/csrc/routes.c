@@ -130,7 +130,8 @@ static int prepare(ShdTopology* t) {
         int int_ok = 1;
         double max_w = 0.0;
         for (size_t k = 0; k < M && int_ok; k++) {
-            if (!(w[k] >= 0.0) || w[k] != (double)(uint32_t)w[k]) int_ok = 0;
+            /* (range first: the cast of a value >= 2^32 is undefined) */
+            if (!(w[k] >= 0.0 && w[k] < 4294967296.0) || w[k] != (double)(uint32_t)w[k]) int_ok = 0;
             else if (w[k] > max_w) max_w = w[k];
         }
         if (int_ok && (double)t->V * max_w >= 4294967295.0) int_ok = 0;
@@ -428,13 +429,27 @@ void shd_ptab_drop(ShdTopology* t) {
 /* The rounds' 8-byte form of the resident rows (packet.hip kPtabFallback):
  * {delay_ns, keep threshold} per entry, converted once per adopted table.
  * Half the bytes of the random gather's footprint; the f64 table stays for
- * the lookups.  If the allocation fails, the rounds read the f64 entries. */
+ * the lookups.  It is an optional copy (C4: 60 GB beside the 120 GB table),
+ * so it is built only when it takes at most half of the free device memory
+ * and leaves kPtabHeadroom for the round workspace and the caller's buffers;
+ * otherwise, or if the allocation fails, the rounds read the f64 entries
+ * (and shd_ptab_release_for_retry drops it when a later allocation fails).
+ * SHD_PTAB_MAX_BYTES caps it (tests of the f64 path). */
+#define SHD_PTAB_HEADROOM (8ull << 30)
 int shd_ensure_ptab(ShdTopology* t) {
     if (t->d_ptab || t->ptab_unavailable || !t->d_tab || !ptab_enabled()) return 0;
     const size_t rows = (size_t)(t->tab_row_hi - t->tab_row_lo), A = (size_t)t->A;
     if (!rows) return 0;
+    const size_t need = rows * A * 8;
+    size_t fr = 0, tot = 0;
+    const char* mx = getenv("SHD_PTAB_MAX_BYTES");
+    if ((mx && need > (size_t)strtoull(mx, NULL, 10)) || shd_dev_mem_info(&fr, &tot) || need > fr / 2 ||
+        fr - need < SHD_PTAB_HEADROOM) {
+        t->ptab_unavailable = 1;
+        return 0;
+    }
     void* d = NULL;
-    if (shd_dev_malloc(&d, rows * A * 8)) {
+    if (shd_dev_malloc(&d, need)) {
         t->ptab_unavailable = 1;
         return 0;
     }
@@ -446,6 +461,16 @@ int shd_ensure_ptab(ShdTopology* t) {
     t->d_ptab_alloc = d;
     t->d_ptab = (char*)d - (ptrdiff_t)((size_t)t->tab_row_lo * A * 8);
     return 0;
+}
+
+/* A round allocation failed (-ENOMEM) while the optional 8-B table holds
+ * device memory: drop it for good (the f64 entries decide) and say whether
+ * the caller should retry. */
+int shd_ptab_release_for_retry(ShdTopology* t, int rc) {
+    if (rc != -ENOMEM || !t->d_ptab_alloc) return 0;
+    shd_ptab_drop(t);
+    t->ptab_unavailable = 1;
+    return 1;
 }
 
 void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {

@@ -85,6 +85,8 @@ typedef struct {
 
 int shd_dev_init(int device);
 int shd_dev_malloc(void** p, size_t bytes);
+/* free and total device memory of the calling thread's device */
+int shd_dev_mem_info(size_t* free_bytes, size_t* total_bytes);
 int shd_dev_free(void* p);
 /* physically contiguous when granted, else hipMalloc; *contig says which */
 int shd_dev_malloc_table(void** p, size_t bytes, int* contig);
@@ -147,6 +149,9 @@ void shd_dev_ws_free(void* ws);
 /* grow-only exchange scratch of a workspace: dev_bytes of device memory and
  * host_bytes of pinned host memory (either pointer may be NULL) */
 int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, void** h);
+/* The workspace's round faults after its last use (waits for it): 0, or -EIO
+ * once per faulted round (merge spin-out, metadata overflow, stage guard). */
+int shd_dev_ws_check_faults(void* ws);
 int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                          uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets,
                          uint8_t* d_status, uint64_t* d_counters, void* stream);

@@ -186,6 +186,7 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c);
  * (caller holds round_mu); a failed allocation leaves the f64 path */
 int shd_ensure_ptab(ShdTopology* t);
 void shd_ptab_drop(ShdTopology* t);
+int shd_ptab_release_for_retry(ShdTopology* t, int rc);
 int shd_ensure_routes(ShdTopology* t);
 
 #endif

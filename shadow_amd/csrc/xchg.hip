@@ -138,13 +138,26 @@ int make_args(const uint32_t* bounds, int world, RouteArgs* ra) {
     return 0;
 }
 
-// all-to-all of per-peer element counts, then of the blocks themselves
+// A count that says "this rank failed before the exchange" (no real count
+// comes near it): a rank whose local stage failed still takes part in the
+// count all-to-all, so every rank learns it and all of them return together
+// instead of leaving the others waiting in the payload collective.
+constexpr uint64_t kPeerFailed = ~0ull;
+
+// all-to-all of per-peer element counts, then of the blocks themselves.
+// local_rc != 0: this rank failed before the exchange (send_elems unused);
+// it returns local_rc and every peer returns -EIO, after the same counts
+// all-to-all.
 int exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems, size_t elem_bytes,
-                    void* d_recv, size_t recv_cap, size_t* n_recv, hipStream_t s, uint64_t* recv_out = nullptr) {
+                    void* d_recv, size_t recv_cap, size_t* n_recv, hipStream_t s, uint64_t* recv_out = nullptr,
+                    int local_rc = 0) {
     const int W = x->world;
-    std::vector<uint64_t> recv_elems(W), sb(W), rb(W);
-    int rc = x->alltoall_u64(x->user, send_elems, recv_elems.data());
+    std::vector<uint64_t> recv_elems(W), sb(W), rb(W), fail(W, kPeerFailed);
+    int rc = x->alltoall_u64(x->user, local_rc ? fail.data() : send_elems, recv_elems.data());
     if (rc) return rc < 0 ? rc : -EIO;
+    if (local_rc) return local_rc;
+    for (int r = 0; r < W; r++)
+        if (recv_elems[r] == kPeerFailed) return shd_fail(-EIO, "rank %d failed before the exchange", r);
     uint64_t total = 0;
     for (int r = 0; r < W; r++) {
         total += recv_elems[r];
@@ -287,23 +300,25 @@ extern "C" int shd_dev_route_records(const ShdPktCtx* c, const ShdTransport* x, 
     // counts and offsets in the workspace's persistent scratch (no per-round
     // hipMalloc / hipFree), offsets read back into its pinned host side
     void *dscr = nullptr, *hscr = nullptr;
-    if ((rc = shd_dev_ws_scratch(c->ws, 4 * (2 * m + 1), 4 * (m + 1), &dscr, &hscr))) return rc;
-    uint32_t* d_cnt = static_cast<uint32_t*>(dscr);
-    uint32_t* d_off = d_cnt + m;
-    const uint32_t* off = static_cast<const uint32_t*>(hscr);
     std::vector<uint64_t> send(W);
-    const uint2* hi = reinterpret_cast<const uint2*>(c->host_info);
-    hipLaunchKernelGGL(k_route<0>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk, d_cnt,
-                       nullptr, nullptr);
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, d_cnt, (uint32_t)m, d_off);
-    hipLaunchKernelGGL(k_route<1>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
-                       nullptr, d_off, d_part);
-    if ((rc = hip_status(hipGetLastError(), "k_route launch"))) return rc;
-    if ((rc = hip_status(hipMemcpyAsync(hscr, d_off, 4 * (m + 1), hipMemcpyDeviceToHost, s), "route D2H")) ||
-        (rc = hip_status(hipStreamSynchronize(s), "route sync")))
-        return rc;
-    for (int r = 0; r < W; r++) send[r] = off[(size_t)(r + 1) * nblocks] - off[(size_t)r * nblocks];
-    rc = exchange_blocks(x, d_part, send.data(), sizeof(ShdPkt), d_recv, recv_cap, n_recv, s);
+    // (a failure from here on still goes through the count all-to-all)
+    if (!(rc = shd_dev_ws_scratch(c->ws, 4 * (2 * m + 1), 4 * (m + 1), &dscr, &hscr))) {
+        uint32_t* d_cnt = static_cast<uint32_t*>(dscr);
+        uint32_t* d_off = d_cnt + m;
+        const uint32_t* off = static_cast<const uint32_t*>(hscr);
+        const uint2* hi = reinterpret_cast<const uint2*>(c->host_info);
+        hipLaunchKernelGGL(k_route<0>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
+                           d_cnt, nullptr, nullptr);
+        hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(1024), 0, s, d_cnt, (uint32_t)m, d_off);
+        hipLaunchKernelGGL(k_route<1>, dim3(nblocks), dim3(kRouteBlock), 0, s, d_recs, n, hi, c->nhosts, ra, chunk,
+                           nullptr, d_off, d_part);
+        if (!(rc = hip_status(hipGetLastError(), "k_route launch")) &&
+            !(rc = hip_status(hipMemcpyAsync(hscr, d_off, 4 * (m + 1), hipMemcpyDeviceToHost, s), "route D2H")))
+            rc = hip_status(hipStreamSynchronize(s), "route sync");
+        if (!rc)
+            for (int r = 0; r < W; r++) send[r] = off[(size_t)(r + 1) * nblocks] - off[(size_t)r * nblocks];
+    }
+    rc = exchange_blocks(x, d_part, send.data(), sizeof(ShdPkt), d_recv, recv_cap, n_recv, s, nullptr, rc);
     if (!rc) rc = hip_status(hipStreamSynchronize(s), "route exchange");
     return rc;
 }
@@ -338,14 +353,25 @@ namespace {
 size_t xchg_scratch_words(uint32_t H, int W, uint32_t Hm) {
     return (kMaxWorld + 1) + ((size_t)H + W) + (size_t)W * (Hm + 1) + (W + 1);
 }
+// local_rc != 0: this rank's own round failed; it still joins the count
+// all-to-all (exchange_blocks) so that every rank fails together.
 int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, size_t elem_bytes, int wire,
                        const uint32_t* d_dst_offsets, const uint32_t* host_bounds, void* d_recv, size_t recv_cap,
                        ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, hipStream_t s, uint32_t* dscr,
-                       uint32_t* hscr) {
+                       uint32_t* hscr, int local_rc = 0) {
     const int W = x->world, me = x->rank;
     RouteArgs ra;
-    int rc = make_args(host_bounds, W, &ra);
+    int rc = make_args(host_bounds, W, &ra); // (checked by every rank alike: no collective yet)
     if (rc) return rc;
+    if (!local_rc) { // SHD_DEBUG_FAIL_RANK=r: rank r fails before the exchange (test of the agreement)
+        const char* f = getenv("SHD_DEBUG_FAIL_RANK");
+        if (f && atoi(f) == me) local_rc = shd_fail(-EIO, "debug: injected failure of rank %d", me);
+    }
+    if (local_rc) { // only the count all-to-all that tells the peers
+        std::vector<uint64_t> none(W, 0);
+        size_t nr = 0;
+        return exchange_blocks(x, nullptr, none.data(), elem_bytes, nullptr, 0, &nr, s, nullptr, local_rc);
+    }
     const uint32_t H = host_bounds[W], lo = host_bounds[me], hi = host_bounds[me + 1], Hm = hi - lo;
     const size_t n_sl = (size_t)H + W, n_ro = (size_t)W * (Hm + 1);
     uint32_t* d_cuts = dscr;
@@ -355,19 +381,23 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
     uint32_t* h_cuts = hscr;
     uint32_t* h_bb = h_cuts + (kMaxWorld + 1);
     // cuts of the events at the owners' host bounds, and the offset slices
-    hipLaunchKernelGGL(k_cuts, dim3(1), dim3(kMaxWorld + 1), 0, s, d_dst_offsets, ra, d_cuts);
-    hipLaunchKernelGGL(k_offset_slices, dim3((unsigned)((n_sl + 255) / 256 < 4096 ? (n_sl + 255) / 256 : 4096)),
-                       dim3(256), 0, s, d_dst_offsets, ra, d_sl);
-    if ((rc = hip_status(hipGetLastError(), "exchange cuts launch"))) return rc;
-    if ((rc = hip_status(hipMemcpyAsync(h_cuts, d_cuts, 4 * (size_t)(W + 1), hipMemcpyDeviceToHost, s), "cuts D2H")) ||
-        (rc = hip_status(hipStreamSynchronize(s), "cuts sync")))
-        return rc;
+    {
+        hipLaunchKernelGGL(k_cuts, dim3(1), dim3(kMaxWorld + 1), 0, s, d_dst_offsets, ra, d_cuts);
+        hipLaunchKernelGGL(k_offset_slices, dim3((unsigned)((n_sl + 255) / 256 < 4096 ? (n_sl + 255) / 256 : 4096)),
+                           dim3(256), 0, s, d_dst_offsets, ra, d_sl);
+        if (!(rc = hip_status(hipGetLastError(), "exchange cuts launch")) &&
+            !(rc = hip_status(hipMemcpyAsync(h_cuts, d_cuts, 4 * (size_t)(W + 1), hipMemcpyDeviceToHost, s),
+                              "cuts D2H")))
+            rc = hip_status(hipStreamSynchronize(s), "cuts sync");
+    }
     std::vector<uint64_t> send(W), recv(W), sb(W), rb(W);
-    for (int r = 0; r < W; r++) send[r] = h_cuts[r + 1] - h_cuts[r];
+    if (!rc)
+        for (int r = 0; r < W; r++) send[r] = h_cuts[r + 1] - h_cuts[r];
     size_t nrecv = 0;
-    // the events (the capacity verdict is collective inside)
-    if ((rc = exchange_blocks(x, static_cast<const char*>(d_events) + (size_t)h_cuts[0] * elem_bytes, send.data(),
-                              elem_bytes, d_recv, recv_cap, &nrecv, s, recv.data())))
+    // the events (the capacity verdict is collective inside, and so is a
+    // failure of this rank's stages above)
+    if ((rc = exchange_blocks(x, static_cast<const char*>(d_events) + (rc ? 0 : (size_t)h_cuts[0] * elem_bytes),
+                              send.data(), elem_bytes, d_recv, recv_cap, &nrecv, s, recv.data(), rc)))
         return rc;
     // the offset slices: H_r + 1 words to peer r, H_me + 1 from each peer
     for (int r = 0; r < W; r++) {
@@ -384,6 +414,9 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
                                        s)))
         return rc;
     if ((rc = hip_status(hipStreamSynchronize(s), "exchange runs"))) return rc;
+    // the sender's round and this merge ran on the workspace: their faults
+    // are this call's (synchronous) -- reported now, not by a later call
+    if ((rc = shd_dev_ws_check_faults(ws))) return rc;
     *n_out = nrecv;
     return 0;
 }
@@ -398,12 +431,11 @@ extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdD
     if (W < 1 || W > kMaxWorld || x->rank < 0 || x->rank >= W) return shd_fail(-EINVAL, "bad world");
     const uint32_t Hm = host_bounds[x->rank + 1] - host_bounds[x->rank];
     void *dscr = nullptr, *hscr = nullptr;
-    int rc = shd_dev_ws_scratch(ws, 4 * xchg_scratch_words(host_bounds[W], W, Hm), 4 * (2 * kMaxWorld + 2), &dscr,
-                                &hscr);
-    if (rc) return rc;
+    const int rc = shd_dev_ws_scratch(ws, 4 * xchg_scratch_words(host_bounds[W], W, Hm), 4 * (2 * kMaxWorld + 2),
+                                      &dscr, &hscr); // (a failure still joins the first collective)
     return exchange_runs_core(ws, x, d_events, sizeof(ShdDeliv), 0, d_dst_offsets, host_bounds, d_recv, recv_cap,
                               d_out, d_out_offsets, n_out, (hipStream_t)stream, static_cast<uint32_t*>(dscr),
-                              static_cast<uint32_t*>(hscr));
+                              static_cast<uint32_t*>(hscr), rc);
 }
 
 // A round decided and exchanged in one call (shd_round_process_exchange):
@@ -420,14 +452,15 @@ extern "C" int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x,
     if (host_bounds[0] != 0 || host_bounds[W] != H) return shd_fail(-EINVAL, "host bounds must cover [0, %u)", H);
     const size_t words = ((size_t)H + 1) + xchg_scratch_words(H, W, Hm);
     void *dscr = nullptr, *hscr = nullptr;
+    // (a failed local stage still joins the exchange's first collective)
     int rc = shd_dev_ws_scratch(c->ws, 4 * words, 4 * (2 * kMaxWorld + 2), &dscr, &hscr);
-    if (rc) return rc;
     uint32_t* d_off = static_cast<uint32_t*>(dscr); // the sender's destination offsets (H + 1)
-    if ((rc = shd_dev_packet_round_grouped(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire_send, d_off, d_status,
-                                           d_counters, stream)))
-        return rc;
+    if (!rc)
+        rc = shd_dev_packet_round_grouped(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire_send, d_off, d_status,
+                                          d_counters, stream);
     return exchange_runs_core(c->ws, x, d_wire_send, 24, 1, d_off, host_bounds, d_wire_recv, recv_cap, d_out,
-                              d_out_offsets, n_out, (hipStream_t)stream, d_off + (H + 1), static_cast<uint32_t*>(hscr));
+                              d_out_offsets, n_out, (hipStream_t)stream, rc ? nullptr : d_off + (H + 1),
+                              static_cast<uint32_t*>(hscr), rc);
 }
 
 extern "C" int shd_dev_exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* send_elems,
@@ -629,8 +662,9 @@ extern "C" int shd_transport_rccl_new_all(int ndev, const int* devices, ShdTrans
     std::vector<ncclComm_t> comms(ndev);
     int rc = nccl_status(ncclCommInitAll(comms.data(), ndev, devices), "ncclCommInitAll");
     if (rc) return rc;
+    for (int k = 0; k < ndev; k++) out[k] = nullptr;
+    int made = 0; // transports built so far (they own comms[0, made))
     for (int k = 0; k < ndev && !rc; k++) {
-        out[k] = nullptr;
         if ((rc = shd_dev_init(devices[k]))) break;
         Rccl* t = new (std::nothrow) Rccl();
         if (!t) {
@@ -643,6 +677,9 @@ extern "C" int shd_transport_rccl_new_all(int ndev, const int* devices, ShdTrans
             (rc = hip_status(hipMalloc((void**)&t->d_u64, 16 * (size_t)ndev), "hipMalloc transport")) ||
             (rc = hip_status(hipHostMalloc((void**)&t->h_u64, 16 * (size_t)ndev, hipHostMallocDefault),
                              "hipHostMalloc transport"))) {
+            (void)hipFree(t->d_u64);
+            if (t->h_u64) (void)hipHostFree(t->h_u64);
+            if (t->stream) (void)hipStreamDestroy(t->stream);
             delete t;
             break;
         }
@@ -653,6 +690,14 @@ extern "C" int shd_transport_rccl_new_all(int ndev, const int* devices, ShdTrans
         t->x.alltoallv = rccl_alltoallv;
         t->x.allgatherv = rccl_allgatherv;
         out[k] = &t->x;
+        made = k + 1;
+    }
+    if (rc) { // all or nothing: free what was built and the communicators no transport took
+        for (int k = 0; k < made; k++) {
+            shd_transport_rccl_free(out[k]);
+            out[k] = nullptr;
+        }
+        for (int k = made; k < ndev; k++) (void)ncclCommDestroy(comms[k]);
     }
     return rc;
 }

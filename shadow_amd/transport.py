@@ -16,6 +16,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
+
 import torch
 import torch.distributed as dist
 
@@ -76,10 +78,12 @@ class TorchTransport:
 
     def _alltoall_u64(self, _user, send, recv):
         try:
-            s = torch.tensor([send[r] for r in range(self.world)], dtype=torch.int64, device=self.cdev)
+            # u64 values (a failed rank sends UINT64_MAX) carried as int64 bits
+            u = np.array([send[r] for r in range(self.world)], dtype=np.uint64)
+            s = torch.from_numpy(u.view(np.int64)).to(self.cdev)
             out = torch.empty_like(s)
             dist.all_to_all_single(out, s, group=self.group)
-            for r, v in enumerate(out.cpu().tolist()):
+            for r, v in enumerate(out.cpu().numpy().view(np.uint64).tolist()):
                 recv[r] = v
             return 0
         except BaseException as e:  # never unwind through the C caller

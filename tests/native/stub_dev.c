@@ -107,6 +107,11 @@ void shd_dev_ws_free(void* ws) { free(ws); }
 int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, void** h) {
     return shd_fail(-ENOSYS, "stub device: no exchange scratch");
 }
+int shd_dev_ws_check_faults(void* ws) { return 0; }
+int shd_dev_mem_info(size_t* free_bytes, size_t* total_bytes) {
+    *free_bytes = *total_bytes = (size_t)1 << 40;
+    return 0;
+}
 
 int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
                          uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,

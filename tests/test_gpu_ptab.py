@@ -97,3 +97,37 @@ def test_round_with_and_without_the_table(name, monkeypatch):
         assert mt == omt, mode
         assert np.array_equal(out, oout), mode
     assert (ostatus == 0).sum() > 0, "some packets must be dropped for the threshold to matter"
+
+
+def test_table_refused_when_it_does_not_fit(monkeypatch):
+    """The 8-B table is optional: above its budget (here SHD_PTAB_MAX_BYTES=1;
+    in production half the free HBM with 8 GiB headroom, routes.c) it is not
+    built and the rounds decide from the f64 entries -- same results."""
+    import torch
+
+    from shadow_amd import Topology
+    from test_gpu_parity import GRAPHS
+    monkeypatch.setenv("SHD_PTAB_MAX_BYTES", "1")
+    gml, H = GRAPHS["sparse300_ns"]
+    top = Topology(gml)
+    ips, st, verts = scenario.register_hosts(top, H, 1)
+    orc = O.OracleTopology(gml)
+    ips2, _, _ = scenario.register_hosts(orc, H, 1)
+    top.touch_all()
+    lat, rel, sv = top.table()
+    orc.preload(sv, lat, rel)
+    pk = synth.packet_batch(30000, H, 0x5EED0A03, 100_000_000, 10_000_000, st)
+    n = len(pk)
+    d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                       d_status.data_ptr(), d_cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    cnt = d_cnt.cpu().numpy().view(np.uint64)
+    oout, ostatus, omt = orc.round(ips2, pk, 110_000_000, 10**15)
+    assert np.array_equal(d_status.cpu().numpy(), ostatus) and int(cnt[1]) == omt
+    assert np.array_equal(d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]], oout)

@@ -1,12 +1,21 @@
 """Multi-rank rounds with the ranks as threads of ONE process (Shadow runs
 one process with one manager, core/manager.c:543-577): one topology and one
-thread per rank, the in-process transport (shd_transport_local_new: a thread
-barrier plus device-to-device copies), all ranks on GPU 0 here.  Each rank
-builds its share of the rows, the C-ABI all-gather completes every rank's
-table, then each rank decides its senders' packets and the events go to
-their destinations' owners -- both with shd_round_process_exchange (grouped,
-24-B wire records) and with shd_round_process_device + shd_round_exchange.
-The union over ranks must equal the oracle's single round."""
+thread per rank, all ranks on GPU 0 here.  Transports:
+  * local -- shd_transport_local_new (a thread barrier plus device-to-device
+    copies), world 2 and 3;
+  * rccl_all -- shd_transport_rccl_new_all: the product's own RCCL
+    communicator from ncclCommInitAll (ncclGroupStart / ncclSend / ncclRecv
+    on the transport's streams), world 1 on the one GPU (RCCL puts one rank
+    per device; the sends and receives go to self);
+  * rccl_uid -- shd_transport_rccl_new, the one-process-per-GPU form (the
+    unique id handed over by torch.distributed, here a world-1 gloo group).
+Each rank builds its share of the rows, the C-ABI all-gather completes every
+rank's table, then each rank decides its senders' packets and the events go
+to their destinations' owners -- with shd_round_process_exchange (grouped,
+24-B wire records) and with shd_round_process_device + shd_round_exchange;
+the records also go through shd_round_route_records on a row-sharded table.
+The union over ranks must equal the oracle's single round.  A rank that
+fails before the exchange makes every rank fail together (no hang)."""
 import threading
 
 import numpy as np
@@ -18,6 +27,7 @@ pytestmark = pytest.mark.gpu
 
 H = 300
 BARRIER, END = 110_000_000, 10**15
+NPK = 4000
 
 
 def _gml():
@@ -28,86 +38,107 @@ def _gml():
 def _packets(rank, world, st):
     from shadow_amd import synth
     lo, hi = rank * H // world, (rank + 1) * H // world
-    return synth.packet_batch(4000, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, hosts_lo=lo, hosts_hi=hi)
+    return synth.packet_batch(NPK, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, hosts_lo=lo, hosts_hi=hi)
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("fused", [True, False], ids=["process_exchange", "device+exchange"])
-def test_threads_as_ranks(world, fused):
-    import torch
+class _UidTransport:
+    """shd_transport_rccl_new over a world-1 torch.distributed group."""
 
-    from shadow_amd import Topology, scenario, synth
+    def __init__(self):
+        import os
+        import socket
+
+        import torch.distributed as dist
+
+        from shadow_amd.transport import RcclTransport
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        self.x = RcclTransport(0)
+        self.ranks = [self.x]
+
+    def close(self):
+        import torch.distributed as dist
+        self.x.close()
+        dist.destroy_process_group()
+
+
+def _transports(kind, world):
     from shadow_amd.transport import InProcessTransports
-    xps = InProcessTransports(world, "local")
-    tops, res, errs = [], [None] * world, []
-    gml = _gml()
-    for r in range(world):
-        top = Topology(gml)
-        ips, st, verts = scenario.register_hosts(top, H, seed=1)
-        tops.append((top, st))
-    A = tops[0][0].slot_count()
-    row_bounds = [r * A // world for r in range(world + 1)]
-    host_bounds = [r * H // world for r in range(world + 1)]
-    bufs = []
-    for r in range(world):
-        n = 4000
-        cap = n * world
-        bufs.append(dict(
-            tab=torch.zeros(A * A * 2, dtype=torch.float64, device="cuda"),
-            recs=torch.from_numpy(_packets(r, world, tops[r][1]).view(np.uint8)).cuda(),
-            send=torch.empty(n * 32, dtype=torch.uint8, device="cuda"),
-            off=torch.empty(H + 1, dtype=torch.int32, device="cuda"),
-            status=torch.empty(n, dtype=torch.uint8, device="cuda"),
-            cnt=torch.empty(2, dtype=torch.int64, device="cuda"),
-            recv=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
-            fin=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
-            fin_off=torch.empty(host_bounds[r + 1] - host_bounds[r] + 1, dtype=torch.int32, device="cuda")))
-    torch.cuda.synchronize()
+    if kind == "local":
+        return InProcessTransports(world, "local")
+    if kind == "rccl_all":
+        return InProcessTransports(world, "rccl", devices=[0] * world)
+    return _UidTransport()
 
-    def rank_main(r):
+
+def _run_ranks(world, fn):
+    errs = [None] * world
+    res = [None] * world
+
+    def main(r):
         try:
-            top, _ = tops[r]
-            b, xp = bufs[r], xps.ranks[r]
-            lo, hi = row_bounds[r], row_bounds[r + 1]
-            if hi > lo:
-                top.build_rows_device(lo, hi, b["tab"].data_ptr())
-            top.allgather_rows(xp, b["tab"].data_ptr(), row_bounds)
-            top.adopt_table_device(b["tab"].data_ptr())
-            top.touch_all()
-            n = 4000
-            if fused:
-                nrecv = top.process_exchange(xp, b["recs"].data_ptr(), n, BARRIER, END, 0, host_bounds,
-                                             b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
-                                             b["recv"].data_ptr(), n * world, b["fin"].data_ptr(),
-                                             b["fin_off"].data_ptr())
-            else:
-                top.process_device(b["recs"].data_ptr(), n, BARRIER, END, 0, b["send"].data_ptr(),
-                                   b["off"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(), 0)
-                nrecv = top.exchange(xp, b["send"].data_ptr(), b["off"].data_ptr(), host_bounds, b["recv"].data_ptr(),
-                                     n * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
-            res[r] = nrecv
+            res[r] = fn(r)
         except BaseException as e:  # reported by the main thread
-            errs.append(e)
+            errs[r] = e
 
-    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    th = [threading.Thread(target=main, args=(r,)) for r in range(world)]
     for t in th:
         t.start()
     for t in th:
         t.join(timeout=240)
     assert not any(t.is_alive() for t in th), "a rank thread is stuck in a collective"
-    assert not errs, errs[0]
-    xps.close()
+    return res, errs
+
+
+def _setup(world):
+    import torch
+
+    from shadow_amd import Topology, scenario
+    gml = _gml()
+    tops = []
+    for r in range(world):
+        top = Topology(gml)
+        ips, st, verts = scenario.register_hosts(top, H, seed=1)
+        tops.append((top, st))
+    A = tops[0][0].slot_count()
+    host_bounds = [r * H // world for r in range(world + 1)]
+    bufs = []
+    for r in range(world):
+        cap = NPK * world
+        bufs.append(dict(
+            tab=torch.zeros(A * A * 2, dtype=torch.float64, device="cuda"),
+            recs=torch.from_numpy(_packets(r, world, tops[r][1]).view(np.uint8)).cuda(),
+            send=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
+            routed=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
+            off=torch.empty(H + 1, dtype=torch.int32, device="cuda"),
+            status=torch.empty(cap, dtype=torch.uint8, device="cuda"),
+            cnt=torch.empty(2, dtype=torch.int64, device="cuda"),
+            recv=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
+            fin=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
+            fin_off=torch.empty(host_bounds[r + 1] - host_bounds[r] + 1, dtype=torch.int32, device="cuda")))
+    torch.cuda.synchronize()
+    return gml, tops, A, host_bounds, bufs
+
+
+def _oracle_round(gml, world):
     orc = O.OracleTopology(gml)
+    from shadow_amd import scenario
     ips, st, verts = scenario.register_hosts(orc, H, 1)
     sv = np.unique(verts).astype(np.int32)
     lat, rel = orc.rows_parallel(sv, sv, 8)
-    want = np.stack([lat, rel], axis=-1).tobytes()
-    for b in bufs:  # every rank's all-gathered table
-        assert b["tab"].cpu().numpy().tobytes() == want
+    want_tab = np.stack([lat, rel], axis=-1).tobytes()
     orc.preload(sv, lat, rel)
     allpk = np.concatenate([_packets(r, world, st) for r in range(world)])
     ref, status, mt = orc.round(ips, allpk, BARRIER, END)
+    return want_tab, ref, mt
+
+
+def _check_union(bufs, res, world, host_bounds, ref, mt, nrec=None):
+    from shadow_amd import synth
     merged = np.concatenate([bufs[r]["fin"].cpu().numpy().view(synth.DELIV_DTYPE)[:res[r]] for r in range(world)])
     assert len(merged) == len(ref)
     for k in ("dst_host", "time", "src_host", "seq"):
@@ -119,3 +150,107 @@ def test_threads_as_ranks(world, fused):
         assert offs[-1] == res[r]
         assert np.array_equal(np.diff(offs), np.bincount(got["dst_host"] - host_bounds[r],
                                                          minlength=host_bounds[r + 1] - host_bounds[r]))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("kind,world", [("local", 2), ("local", 3), ("rccl_all", 1), ("rccl_uid", 1)])
+@pytest.mark.parametrize("fused", [True, False], ids=["process_exchange", "device+exchange"])
+def test_threads_as_ranks(kind, world, fused):
+    gml, tops, A, host_bounds, bufs = _setup(world)
+    row_bounds = [r * A // world for r in range(world + 1)]
+    xps = _transports(kind, world)
+
+    def rank_main(r):
+        top, _ = tops[r]
+        b, xp = bufs[r], xps.ranks[r]
+        lo, hi = row_bounds[r], row_bounds[r + 1]
+        if hi > lo:
+            top.build_rows_device(lo, hi, b["tab"].data_ptr())
+        top.allgather_rows(xp, b["tab"].data_ptr(), row_bounds)
+        top.adopt_table_device(b["tab"].data_ptr())
+        top.touch_all()
+        if fused:
+            return top.process_exchange(xp, b["recs"].data_ptr(), NPK, BARRIER, END, 0, host_bounds,
+                                        b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
+                                        b["recv"].data_ptr(), NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+        top.process_device(b["recs"].data_ptr(), NPK, BARRIER, END, 0, b["send"].data_ptr(), b["off"].data_ptr(),
+                           b["status"].data_ptr(), b["cnt"].data_ptr(), 0)
+        return top.exchange(xp, b["send"].data_ptr(), b["off"].data_ptr(), host_bounds, b["recv"].data_ptr(),
+                            NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+
+    try:
+        res, errs = _run_ranks(world, rank_main)
+        assert not any(errs), [e for e in errs if e]
+    finally:
+        xps.close()
+    want_tab, ref, mt = _oracle_round(gml, world)
+    for b in bufs:  # every rank's all-gathered table
+        assert b["tab"].cpu().numpy().tobytes() == want_tab
+    _check_union(bufs, res, world, host_bounds, ref, mt)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("kind,world", [("local", 2), ("rccl_all", 1)])
+def test_row_sharded_route_decide_exchange(kind, world):
+    """C4 at N>1: the rows stay sharded (no all-gather); every record goes to
+    the rank holding its answering row (shd_round_route_records), is decided
+    there on the shard, and its event to its destination's owner."""
+    import torch
+    gml, tops, A, host_bounds, bufs = _setup(world)
+    row_bounds = [r * A // world for r in range(world + 1)]
+    xps = _transports(kind, world)
+    for r in range(world):  # full tables built once, then each rank adopts only its shard
+        tops[r][0].build_rows_device(0, A, bufs[r]["tab"].data_ptr())
+    torch.cuda.synchronize()
+    shards = [bufs[r]["tab"].view(A, A * 2)[row_bounds[r]:row_bounds[r + 1]].clone() for r in range(world)]
+    gmin = min(tops[r][0].shard_min_latency(shards[r].data_ptr(), row_bounds[r], row_bounds[r + 1])
+               for r in range(world) if row_bounds[r + 1] > row_bounds[r])
+
+    def rank_main(r):
+        top, _ = tops[r]
+        b, xp = bufs[r], xps.ranks[r]
+        top.adopt_table_shard_device_resident(shards[r].data_ptr(), row_bounds[r], row_bounds[r + 1], gmin)
+        n = top.route_records(xp, b["recs"].data_ptr(), NPK, row_bounds, b["routed"].data_ptr(),
+                              b["send"].data_ptr(), NPK * world)
+        return top.process_exchange(xp, b["send"].data_ptr(), n, BARRIER, END, 0, host_bounds, b["recv"].data_ptr(),
+                                    b["status"].data_ptr(), b["cnt"].data_ptr(), b["routed"].data_ptr(),
+                                    NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+
+    try:
+        res, errs = _run_ranks(world, rank_main)
+        assert not any(errs), [e for e in errs if e]
+    finally:
+        xps.close()
+    _, ref, mt = _oracle_round(gml, world)
+    _check_union(bufs, res, world, host_bounds, ref, mt)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("kind,world", [("local", 2), ("local", 3)])
+def test_one_rank_failing_fails_every_rank(kind, world, monkeypatch):
+    """A rank whose own stage fails before the exchange (SHD_DEBUG_FAIL_RANK)
+    still joins the count all-to-all: it returns its error, every peer -EIO,
+    and nobody waits in the payload collective."""
+    import errno
+
+    from shadow_amd._lib import ShdError
+    gml, tops, A, host_bounds, bufs = _setup(world)
+    xps = _transports(kind, world)
+    monkeypatch.setenv("SHD_DEBUG_FAIL_RANK", "1")
+
+    def rank_main(r):
+        top, _ = tops[r]
+        b, xp = bufs[r], xps.ranks[r]
+        top.build_rows_device(0, A, b["tab"].data_ptr())
+        top.adopt_table_device(b["tab"].data_ptr())
+        top.touch_all()
+        return top.process_exchange(xp, b["recs"].data_ptr(), NPK, BARRIER, END, 0, host_bounds,
+                                    b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
+                                    b["recv"].data_ptr(), NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+
+    try:
+        res, errs = _run_ranks(world, rank_main)
+    finally:
+        xps.close()
+    assert all(isinstance(e, ShdError) and e.code == -errno.EIO for e in errs), errs
+    assert "injected" in str(errs[1]) and all("rank 1 failed" in str(errs[r]) for r in range(world) if r != 1)
