@@ -135,9 +135,22 @@ int shd_topology_log_cached_paths(ShdTopology* top, ShdPathLogFn fn, void* user,
 int shd_topology_lookup_batch(ShdTopology* top, const uint32_t* src_ips, const uint32_t* dst_ips, size_t n,
                               double* lat_ms, double* rel);
 
+/* The min-jump callback (worker_updateMinTimeJump, worker.h:89) gets every
+ * new running minimum, strictly decreasing, in the serial touch order.  On a
+ * device-resident table the rows first touched by lookups and sends are
+ * reduced on the GPU asynchronously, in batches, and the callback fires when
+ * their minima are folded: at the latest at the next round boundary
+ * (shd_round_collect), minimum query or teardown log, or at
+ * shd_topology_release_sync.  Shadow's controller reads the min jump only at
+ * the round boundary (controller.c:390-422), so it sees the same values. */
 int shd_topology_set_min_jump_callback(ShdTopology* top, ShdMinJumpFn fn, void* user);
-/* Running min of released latencies (topology.c:48, 1253-1264); 0 if none. */
+/* Running min of released latencies (topology.c:48, 1253-1264); 0 if none.
+ * Folds the queued releases first. */
 int shd_topology_get_min_path_latency(ShdTopology* top, double* min_ms);
+/* Waits for the queued releases of a device-resident table and folds their
+ * minima (callback included) in touch order; for callers of the device round
+ * API (shd_round_process_device) at their round boundary. */
+int shd_topology_release_sync(ShdTopology* top);
 
 /* Introspection for tests and tooling. */
 int shd_topology_info(ShdTopology* top, int* vertices, int* edges, int* directed, int* complete,

@@ -48,6 +48,7 @@ PROTOS = {
     "shd_topology_lookup_batch": (C.c_int, [_P, _P, _P, C.c_size_t, _P, _P]),
     "shd_topology_set_min_jump_callback": (C.c_int, [_P, MINJUMP_FN, _P]),
     "shd_topology_get_min_path_latency": (C.c_int, [_P, _dp]),
+    "shd_topology_release_sync": (C.c_int, [_P]),
     "shd_topology_info": (C.c_int, [_P, _ip, _ip, _ip, _ip, _ip]),
     "shd_topology_vertex_of_host": (C.c_int, [_P, C.c_uint32, _ip]),
     "shd_topology_copy_table": (C.c_int, [_P, _P, _P, _P, C.c_int]),

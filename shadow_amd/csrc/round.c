@@ -81,16 +81,15 @@ int shd_round_append_worker(ShdTopology* t, int worker, const ShdPkt* recs, size
         b->recs = s;
         b->cap = nc;
     }
-    ShdRelBatch rb = {0};
     for (size_t i = 0; i < n && !rc; i++) {
         rec_slots(t, &recs[i], &si, &di);
         int oi, oj;
-        rc = shd_resolve_b(t, si, di, &oi, &oj, &rb); /* topology_getReliability's lookup, at send time */
+        rc = shd_resolve(t, si, di, &oi, &oj); /* topology_getReliability's lookup, at send time */
         if (!rc) b->recs[b->n++] = recs[i];
     }
-    /* device-resident rows this batch touched, released in touch order */
-    const int rcf = shd_release_flush(t, &rb);
-    shd_relbatch_free(&rb);
+    /* device-resident rows first touched here are queued; launched in batches
+     * (never waited for at send time), folded in touch order at the boundary */
+    const int rcf = shd_release_kick(t);
     return rc ? rc : rcf;
 }
 
@@ -417,7 +416,12 @@ int shd_round_collect(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_out, 
                       uint8_t* status, uint64_t* min_time) {
     if (!t) return -EINVAL;
     pthread_mutex_lock(&t->round_mu);
-    int rc = t->nshards > 1 ? collect_shards_locked(t, out, cap, n_out, dst_offsets, status, min_time)
+    /* the round boundary: releases queued by this round's sends and lookups
+     * are folded into the running minimum (and the min-jump callback) first,
+     * in touch order -- what the controller reads next (controller.c:390-422) */
+    int rc = shd_release_sync(t, 1);
+    if (!rc)
+        rc = t->nshards > 1 ? collect_shards_locked(t, out, cap, n_out, dst_offsets, status, min_time)
                             : collect_locked(t, out, cap, n_out, dst_offsets, status, min_time);
     pthread_mutex_unlock(&t->round_mu);
     return rc;

@@ -112,14 +112,21 @@ int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat);
 /* min latency over the entries (i, j), i < j, lat >= 0, of rows [row_lo,
  * row_hi) of an A-column table (rows: row i at rows + (i - row_lo) * A); -1 if none */
 int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out);
-/* Lazy row release (release.hip): for each listed row rows[r] (absolute slot,
- * row r at base + rows[r] * A) with touch sequence seqs[r], the minimum
- * latency over columns j != rows[r] with touch[j] > seqs[r] and lat >= 0;
- * out[r] = -1 if none.  rows / seqs / touch / out are host arrays; runs on the
- * calling thread's device, synchronously.  *scratch: grow-only device buffers
- * of the caller (NULL the first time), freed with shd_dev_release_scratch_free. */
-int shd_dev_release_min(const ShdEntry* base, int A, const int32_t* rows, const uint32_t* seqs, int n,
-                        const uint32_t* touch, double* out, void** scratch);
+/* Lazy row release (release.hip), asynchronous: queues on the release
+ * scratch's own stream, for each listed row rows[r] (absolute slot, row r at
+ * base + rows[r] * A) with touch sequence seqs[r], the minimum latency over
+ * columns j != rows[r] with touch[j] > seqs[r] and lat >= 0 (touch: host
+ * array of A sequences taken after the listed rows drew theirs); returns
+ * without waiting.  Runs on the calling thread's device.  *scratch: grow-only
+ * buffers + stream of the caller (NULL the first time), freed with
+ * shd_dev_release_scratch_free. */
+int shd_dev_release_launch(const ShdEntry* base, int A, const int32_t* rows, const uint32_t* seqs, int n,
+                           const uint32_t* touch, void** scratch);
+/* Waits for the launches since the last collect; their minima in launch
+ * order into out (-1: none released), *n of them (at most cap). */
+int shd_dev_release_collect(void* scratch, double* out, size_t cap, size_t* n);
+/* rows launched and not yet collected */
+size_t shd_dev_release_pending(void* scratch);
 void shd_dev_release_scratch_free(void* scratch);
 
 /* Packet round on device arrays (see shd_round_process_device). */

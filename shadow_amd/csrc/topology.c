@@ -499,6 +499,7 @@ void shd_topology_free(ShdTopology* t) {
     pthread_mutex_destroy(&t->pkt_mu);
     pthread_mutex_destroy(&t->pair_mu);
     pthread_mutex_destroy(&t->round_mu);
+    pthread_mutex_destroy(&t->rel_mu);
     shd_gml_free(&t->doc);
     free(t->efrom);
     free(t->eto);
@@ -547,6 +548,7 @@ int shd_topology_new_from_text(const char* text, int use_shortest_path, int devi
     pthread_mutex_init(&t->pkt_mu, NULL);
     pthread_mutex_init(&t->pair_mu, NULL);
     pthread_mutex_init(&t->round_mu, NULL);
+    pthread_mutex_init(&t->rel_mu, NULL);
     t->nworkers = 1;
     t->wbuf = (ShdWorkerBuf*)calloc(1, sizeof(ShdWorkerBuf));
     if (!t->wbuf) {
@@ -764,8 +766,12 @@ int shd_topology_set_min_jump_callback(ShdTopology* t, ShdMinJumpFn fn, void* us
     return 0;
 }
 
+int shd_release_sync(ShdTopology* t, int fold);
+
 int shd_topology_get_min_path_latency(ShdTopology* t, double* m) {
     if (!t || !m) return -EINVAL;
+    int rc = shd_release_sync(t, 1); /* the queued releases first, in touch order */
+    if (rc) return rc;
     pthread_mutex_lock(&t->min_mu);
     *m = t->min_lat;
     pthread_mutex_unlock(&t->min_mu);
@@ -851,95 +857,169 @@ int shd_read_entries(ShdTopology* t, const uint64_t* idx, size_t n, ShdEntry* ou
     return rc;
 }
 
-/* ---- row releases ---- */
+/* ---- row releases ----
+ * A host-mirrored table releases a row right at its first touch.  On a
+ * device-resident table a first touch (and a first self lookup) only QUEUES
+ * the release: the minimum a row releases depends only on which rows were
+ * touched before it (touch order), so it can be reduced on the GPU any time
+ * later against any later snapshot of the touch sequence.  Queued rows are
+ * launched asynchronously in batches of kRelLaunchRows (release.hip, on each
+ * shard's own stream; the lookups and sends never wait for them), and every
+ * result is folded into the running minimum -- and the min-jump callback
+ * fired -- in touch order at the next point that reads the minimum: the
+ * minimum query, the round boundary (collect / process), the teardown log,
+ * shd_topology_release_sync.  Shadow's controller reads the min jump only at
+ * the round boundary (controller.c:390-422; manager.c:506-511 only records
+ * it), so the callback values and their order are the serial execution's. */
 
-static int relbatch_push(ShdRelBatch* b, int row, uint32_t seq) {
-    if (b->n == b->cap) {
-        int nc = b->cap ? 2 * b->cap : 64;
-        int32_t* r = (int32_t*)realloc(b->rows, sizeof(int32_t) * (size_t)nc);
-        if (r) b->rows = r;
-        uint32_t* s = r ? (uint32_t*)realloc(b->seqs, sizeof(uint32_t) * (size_t)nc) : NULL;
-        if (s) b->seqs = s;
-        if (!r || !s) return -ENOMEM;
-        b->cap = nc;
+#define REL_LAUNCH_ROWS 1024
+
+static int rel_push(ShdRelList* q, int32_t row, uint32_t seq, uint64_t key) {
+    if (q->n == q->cap) {
+        size_t nc = q->cap ? 2 * q->cap : 256;
+        ShdRelItem* v = (ShdRelItem*)realloc(q->v, sizeof(ShdRelItem) * nc);
+        if (!v) return -ENOMEM;
+        q->v = v;
+        q->cap = nc;
     }
-    b->rows[b->n] = row;
-    b->seqs[b->n++] = seq;
+    ShdRelItem* it = &q->v[q->n];
+    it->row = row;
+    it->seq = seq;
+    it->key = key;
+    it->ord = q->n;
+    __atomic_store_n(&q->n, q->n + 1, __ATOMIC_RELAXED); /* (shd_release_kick peeks at the length unlocked) */
     return 0;
 }
 
-void shd_relbatch_free(ShdRelBatch* b) {
-    free(b->rows);
-    free(b->seqs);
-    b->rows = NULL;
-    b->seqs = NULL;
-    b->n = b->cap = 0;
+void shd_rel_list_free(ShdRelList* q) {
+    free(q->v);
+    q->v = NULL;
+    q->n = q->cap = 0;
 }
 
-/* Releases the rows of b (device-resident table), in their order: one
- * reduction per shard over the rows it holds (release.hip), with a snapshot
- * of the touch sequences taken after every row of b drew its number -- a row
- * touched before row i has a smaller number and was published before i's was
- * drawn, every other row compares greater than i's either way, so the
- * snapshot selects exactly the columns the serial store loop would.  Self
- * entries (rows encoded -1 - slot, sequence unused) carry their value. */
-int shd_release_flush(ShdTopology* t, ShdRelBatch* b) {
-    if (!b || !b->n) return 0;
-    const int A = t->A, n = b->n;
+/* Launches every queued row on its shard (caller holds rel_mu): one snapshot
+ * of the touch sequence, taken now -- every queued row drew its number
+ * already, and every row touched before one of them has its number stored --
+ * and one asynchronous reduction per shard.  Self paths wait for the fold. */
+static int rel_launch_locked(ShdTopology* t) {
+    ShdRelList* q = &t->relq;
+    if (!q->n) return 0;
+    const int A = t->A;
     uint32_t* snap = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)A);
-    double* mn = (double*)malloc(sizeof(double) * (size_t)n);
-    int32_t* rk = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
-    uint32_t* sk = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
-    int* pos = (int*)malloc(sizeof(int) * (size_t)n);
-    double* ok = (double*)malloc(sizeof(double) * (size_t)n);
-    int rc = (snap && mn && rk && sk && pos && ok) ? 0 : -ENOMEM;
+    int32_t* rk = (int32_t*)malloc(sizeof(int32_t) * q->n);
+    uint32_t* sk = (uint32_t*)malloc(sizeof(uint32_t) * q->n);
+    int rc = (snap && rk && sk) ? 0 : -ENOMEM;
     if (!rc)
         for (int j = 0; j < A; j++) snap[j] = touch_of(t, j);
-    int covered = 0;
-    for (int r = 0; r < n && !rc; r++)
-        if (b->rows[r] < 0) { /* a self pair: its one entry */
-            ShdEntry e;
-            const size_t s = (size_t)(-1 - b->rows[r]);
-            rc = ent_read(t, s * (size_t)A + s, &e);
-            mn[r] = e.lat;
-            covered++;
-        }
+    for (size_t r = 0; r < q->n && !rc; r++)
+        if (q->v[r].row < 0) rc = rel_push(&t->relself, q->v[r].row, 0, q->v[r].key);
     for (int k = 0; k < t->nshards && !rc; k++) {
         ShdShard* s = &t->shards[k];
         int m = 0;
-        for (int r = 0; r < n; r++)
-            if (b->rows[r] >= s->lo && b->rows[r] < s->hi) rk[m] = b->rows[r], sk[m] = b->seqs[r], pos[m++] = r;
-        if (!m) continue;
+        for (size_t r = 0; r < q->n && !rc; r++)
+            if (q->v[r].row >= s->lo && q->v[r].row < s->hi) {
+                rk[m] = q->v[r].row, sk[m++] = q->v[r].seq;
+                rc = rel_push(&s->sent, q->v[r].row, q->v[r].seq, q->v[r].key);
+            }
+        if (!m || rc) continue;
         pthread_mutex_lock(&s->mu);
-        if (!(rc = shd_dev_init(s->device)))
-            rc = shd_dev_release_min(s->base, A, rk, sk, m, snap, ok, &s->rel_scratch);
+        if (!(rc = shd_dev_init(s->device))) rc = shd_dev_release_launch(s->base, A, rk, sk, m, snap, &s->rel_scratch);
         pthread_mutex_unlock(&s->mu);
-        if (!rc)
-            for (int x = 0; x < m; x++) mn[pos[x]] = ok[x];
-        covered += m;
     }
-    if (!rc && covered != n) rc = shd_fail(-EXDEV, "a touched row lives on another rank");
-    if (!rc)
-        for (int r = 0; r < n; r++)
-            if (mn[r] >= 0) note_released(t, mn[r]);
-    b->n = 0;
+    for (size_t r = 0; r < q->n && !rc; r++)
+        if (q->v[r].row >= 0 && !shd_shard_of(t, q->v[r].row)) rc = shd_fail(-EXDEV, "a touched row lives on another rank");
+    __atomic_store_n(&q->n, 0, __ATOMIC_RELAXED);
     free(snap);
-    free(mn);
     free(rk);
     free(sk);
-    free(pos);
-    free(ok);
+    shd_dev_init(t->device);
     return rc;
 }
+
+/* The caller's batch of lookups / sends is done: launch the queued rows once
+ * there are enough of them (never waits for the GPU). */
+int shd_release_kick(ShdTopology* t) {
+    if (__atomic_load_n(&t->relq.n, __ATOMIC_RELAXED) < REL_LAUNCH_ROWS) return 0;
+    pthread_mutex_lock(&t->rel_mu);
+    int rc = t->relq.n >= REL_LAUNCH_ROWS ? rel_launch_locked(t) : 0;
+    pthread_mutex_unlock(&t->rel_mu);
+    return rc;
+}
+
+static int rel_cmp(const void* a, const void* b) {
+    const ShdRelItem* x = (const ShdRelItem*)a;
+    const ShdRelItem* y = (const ShdRelItem*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return x->ord < y->ord ? -1 : (x->ord > y->ord ? 1 : 0);
+}
+
+/* Every queued and launched release, waited for; fold = 1: their minima go
+ * into the running minimum (and the callback) in touch order; fold = 0: they
+ * are discarded (teardown, re-adoption). */
+int shd_release_sync(ShdTopology* t, int fold) {
+    pthread_mutex_lock(&t->rel_mu);
+    int rc = rel_launch_locked(t);
+    size_t total = t->relself.n;
+    for (int k = 0; k < t->nshards; k++) total += t->shards[k].sent.n;
+    ShdRelItem* all = (ShdRelItem*)malloc(sizeof(ShdRelItem) * (total ? total : 1));
+    double* val = (double*)malloc(sizeof(double) * (total ? total : 1));
+    if (!all || !val) rc = rc ? rc : -ENOMEM;
+    size_t m = 0;
+    for (int k = 0; k < t->nshards; k++) { /* (collected even after an error: nothing stays in flight) */
+        ShdShard* s = &t->shards[k];
+        if (!s->sent.n) continue;
+        size_t n = 0;
+        int rc2 = 0;
+        pthread_mutex_lock(&s->mu);
+        if (!(rc2 = shd_dev_init(s->device)))
+            rc2 = shd_dev_release_collect(s->rel_scratch, val ? val + m : NULL, val ? s->sent.n : 0, &n);
+        pthread_mutex_unlock(&s->mu);
+        if (!rc2 && n != s->sent.n) rc2 = shd_fail(-EIO, "release results %zu of %zu", n, s->sent.n);
+        for (size_t r = 0; r < n && all; r++) all[m + r] = s->sent.v[r];
+        m += n;
+        s->sent.n = 0;
+        if (!rc) rc = rc2;
+    }
+    if (t->relself.n && !rc && fold) { /* self paths: one gather of their entries */
+        const size_t n = t->relself.n;
+        uint64_t* idx = (uint64_t*)malloc(sizeof(uint64_t) * n);
+        ShdEntry* e = (ShdEntry*)malloc(sizeof(ShdEntry) * n);
+        rc = (idx && e) ? 0 : -ENOMEM;
+        for (size_t r = 0; r < n && !rc; r++) {
+            const uint64_t sl = (uint64_t)(-1 - t->relself.v[r].row);
+            idx[r] = sl * (uint64_t)t->A + sl;
+        }
+        if (!rc) rc = shd_read_entries(t, idx, n, e);
+        for (size_t r = 0; r < n && !rc; r++) {
+            all[m] = t->relself.v[r];
+            val[m++] = e[r].lat;
+        }
+        free(idx);
+        free(e);
+    }
+    t->relself.n = 0;
+    if (!rc && fold && m) {
+        for (size_t r = 0; r < m; r++) all[r].seq = (uint32_t)r; /* (the value's index; keys order the fold) */
+        qsort(all, m, sizeof(ShdRelItem), rel_cmp);
+        for (size_t r = 0; r < m; r++)
+            if (val[all[r].seq] >= 0) note_released(t, val[all[r].seq]);
+    }
+    free(all);
+    free(val);
+    pthread_mutex_unlock(&t->rel_mu);
+    shd_dev_init(t->device);
+    return rc;
+}
+
+int shd_topology_release_sync(ShdTopology* t) { return t ? shd_release_sync(t, 1) : -EINVAL; }
 
 /* Releases row i (a touch).  The row's sequence number is drawn and
  * published under touch_mu; the entries it releases are then every (i, y)
  * whose y is untouched or was touched later (sequence > i's) -- exactly the
  * pairs the serial execution in sequence order stores from row i, whatever
  * the interleaving with other touches.  A host-mirrored row is reduced right
- * here; a device-resident one by shd_release_flush, now (b == NULL) or at the
- * end of the caller's batch. */
-static int touch_row(ShdTopology* t, int i, ShdRelBatch* b) {
+ * here; a device-resident one is queued (see above). */
+static int touch_row(ShdTopology* t, int i) {
     pthread_mutex_lock(&t->touch_mu);
     uint32_t seq = t->touch[i];
     const int mine = seq == SHD_UNTOUCHED;
@@ -952,11 +1032,9 @@ static int touch_row(ShdTopology* t, int i, ShdRelBatch* b) {
     pthread_mutex_unlock(&t->touch_mu);
     if (!mine) return 0;
     if (!t->h_tab) {
-        if (b) return relbatch_push(b, i, seq);
-        ShdRelBatch one = {0};
-        int rc = relbatch_push(&one, i, seq);
-        if (!rc) rc = shd_release_flush(t, &one);
-        shd_relbatch_free(&one);
+        pthread_mutex_lock(&t->rel_mu);
+        const int rc = rel_push(&t->relq, i, seq, 2 * (uint64_t)seq + 1);
+        pthread_mutex_unlock(&t->rel_mu);
         return rc;
     }
     const ShdEntry* row = t->h_tab + (size_t)i * (size_t)t->A;
@@ -971,10 +1049,19 @@ static int touch_row(ShdTopology* t, int i, ShdRelBatch* b) {
     return 0;
 }
 
-/* First (X, X) lookup: releases the self path (topology.c:1597-1599). */
-static int release_self(ShdTopology* t, int si, ShdRelBatch* b) {
+/* First (X, X) lookup: releases the self path (topology.c:1597-1599); on a
+ * device-resident table queued after the rows touched so far. */
+static int release_self(ShdTopology* t, int si) {
     if (__atomic_exchange_n(&t->self_released[si], 1, __ATOMIC_ACQ_REL)) return 0;
-    if (b && !t->h_tab) return relbatch_push(b, -1 - si, 0); /* after the rows the batch touched before it */
+    if (!t->h_tab) {
+        pthread_mutex_lock(&t->touch_mu);
+        const uint64_t key = 2 * (uint64_t)t->next_touch;
+        pthread_mutex_unlock(&t->touch_mu);
+        pthread_mutex_lock(&t->rel_mu);
+        const int rc = rel_push(&t->relq, -1 - si, 0, key);
+        pthread_mutex_unlock(&t->rel_mu);
+        return rc;
+    }
     ShdEntry e;
     int rc = ent_read(t, (size_t)si * (size_t)t->A + (size_t)si, &e);
     if (!rc && e.lat >= 0) note_released(t, e.lat);
@@ -996,19 +1083,17 @@ static void set_pair_bit(ShdTopology* t, int i, int j) {
 /* _topology_getPathEntry (topology.c:1900-1981) for slots (si, di): applies
  * the side effects and returns the slot pair whose entry answers.  Lock-free
  * on a hit; safe to call from any number of threads. */
-int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) { return shd_resolve_b(t, si, di, oi, oj, NULL); }
-
-int shd_resolve_b(ShdTopology* t, int si, int di, int* oi, int* oj, ShdRelBatch* b) {
+int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) {
     size_t A = (size_t)t->A;
     int rc = 0;
     if (t->use_sp) {
         if (si == di) {
-            if ((rc = release_self(t, si, b))) return rc;
+            if ((rc = release_self(t, si))) return rc;
             *oi = *oj = si;
         } else {
             uint32_t ts = touch_of(t, si), td = touch_of(t, di);
             int hit = t->directed ? (ts != SHD_UNTOUCHED && ts < td) : (ts != SHD_UNTOUCHED || td != SHD_UNTOUCHED);
-            if (!hit && ts == SHD_UNTOUCHED && (rc = touch_row(t, si, b))) return rc;
+            if (!hit && ts == SHD_UNTOUCHED && (rc = touch_row(t, si))) return rc;
             /* re-read both: a concurrent touch of di with a smaller sequence
              * was published before ours (touch_mu), so it is visible here */
             ts = touch_of(t, si);
@@ -1107,15 +1192,12 @@ int shd_topology_lookup_batch(ShdTopology* t, const uint32_t* sips, const uint32
     if (!idx) return -ENOMEM;
     int rc = 0;
     size_t done = 0;
-    ShdRelBatch b = {0};
     for (; done < n; done++) { /* the side effects, in call order */
         int si, di, oi, oj;
-        if ((rc = slots_of(t, sips[done], dips[done], &si, &di)) || (rc = shd_resolve_b(t, si, di, &oi, &oj, &b)))
-            break;
+        if ((rc = slots_of(t, sips[done], dips[done], &si, &di)) || (rc = shd_resolve(t, si, di, &oi, &oj))) break;
         idx[done] = (uint64_t)oi * (uint64_t)t->A + (uint64_t)oj;
     }
-    int rcf = shd_release_flush(t, &b); /* the rows this batch touched, in touch order */
-    shd_relbatch_free(&b);
+    int rcf = shd_release_kick(t); /* the rows this batch touched (launched once enough are queued) */
     if (!rc) rc = rcf;
     if (done && (lat || rel)) {
         ShdEntry* e = (ShdEntry*)malloc(sizeof(ShdEntry) * done);
@@ -1275,13 +1357,14 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
     uint64_t n = 0;
     if (nlines) *nlines = 0;
     if (!__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return 0;
+    int rc = shd_release_sync(t, 1); /* (topology_free's log follows every release) */
+    if (rc) return rc;
     const int A = t->A;
     ShdEntry* row = NULL;
     if (!t->h_tab) {
         row = (ShdEntry*)malloc(sizeof(ShdEntry) * (size_t)A);
         if (!row) return -ENOMEM;
     }
-    int rc = 0;
     pthread_mutex_lock(&t->pkt_mu);
     for (int i = 0; i < A && !rc; i++) {
         const uint32_t si = touch_of(t, i);
@@ -1326,10 +1409,14 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
 
 void shd_shards_clear(ShdTopology* t) {
     shd_ptab_drop(t); /* (every re-adoption and the teardown pass here) */
+    (void)shd_release_sync(t, 0); /* nothing of the old table stays queued or in flight */
+    shd_rel_list_free(&t->relq);
+    shd_rel_list_free(&t->relself);
     for (int k = 0; k < t->nshards; k++) {
         ShdShard* s = &t->shards[k];
         shd_dev_init(s->device);
         shd_dev_release_scratch_free(s->rel_scratch);
+        shd_rel_list_free(&s->sent);
         shd_dev_free(s->d_host_info);
         shd_dev_free(s->d_touch);
         shd_dev_free(s->d_pair_bits);
@@ -1462,11 +1549,9 @@ int shd_topology_touch_all(ShdTopology* t) {
     if (rc) return rc;
     __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
     if (t->use_sp) {
-        ShdRelBatch b = {0};
         for (int i = 0; i < t->A && !rc; i++)
-            if (touch_of(t, i) == SHD_UNTOUCHED) rc = touch_row(t, i, &b);
-        int rcf = shd_release_flush(t, &b);
-        shd_relbatch_free(&b);
+            if (touch_of(t, i) == SHD_UNTOUCHED) rc = touch_row(t, i);
+        int rcf = shd_release_sync(t, 1); /* (the steady state: every row released) */
         if (!rc) rc = rcf;
     } else {
         for (int i = 0; i < t->A; i++)

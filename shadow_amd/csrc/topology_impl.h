@@ -44,6 +44,23 @@ typedef struct {
     uint32_t cap, n, tomb;
 } IpMap;
 
+/* A queued release of a device-resident table (topology.c "row releases"):
+ * a row's first touch (row >= 0, its touch sequence) or a first self lookup
+ * (row = -1 - slot).  key orders the fold: 2 * seq + 1 for a row, 2 *
+ * next_touch for a self path released while next_touch rows were touched;
+ * ord keeps queue order among equal keys. */
+typedef struct {
+    int32_t row;
+    uint32_t seq;
+    uint64_t key;
+    uint64_t ord;
+} ShdRelItem;
+typedef struct {
+    ShdRelItem* v;
+    size_t n, cap;
+} ShdRelList;
+void shd_rel_list_free(ShdRelList* q);
+
 /* A device-resident piece of the routing table (no host mirror): rows [lo,
  * hi) on `device`, row r at base + r * A.  One shard for a single-GPU table,
  * several for a single-process multi-GPU table (shd_topology_adopt_table_shards);
@@ -54,7 +71,8 @@ typedef struct {
     int device;
     ShdEntry* base;
     int lo, hi;
-    void* rel_scratch; /* shd_dev_release_min buffers */
+    void* rel_scratch; /* shd_dev_release_launch buffers + stream */
+    ShdRelList sent;   /* rows launched on this shard, not yet collected (launch order) */
     pthread_mutex_t mu;
     /* per-shard packet-round state (multi-shard topologies, round.c) */
     uint32_t *d_host_info, *d_touch, *d_pair_bits;
@@ -71,17 +89,6 @@ typedef struct {
     uint32_t cap_h;
 } ShdShard;
 
-/* Rows a thread touched in one batch call (append / lookup batch), released
- * together after the batch: one device pass instead of one per row.  The
- * reference's min-jump side effect only matters at the next round boundary
- * (controller.c:141-153, 390-422), so releasing at the end of the call is
- * indistinguishable to Shadow; the rows are released in their sequence
- * order, so the callback sees the serial sequence of minima. */
-typedef struct {
-    int32_t* rows;
-    uint32_t* seqs;
-    int n, cap;
-} ShdRelBatch;
 
 struct ShdTopology {
     int device;
@@ -143,6 +150,8 @@ struct ShdTopology {
     int nshards;
     ShdShard shards[SHD_MAX_SHARDS];
     uint32_t* host_bounds; /* nshards + 1: destination hosts owned per shard (multi-shard rounds) */
+    ShdRelList relq;    /* queued releases, not launched (under rel_mu) */
+    ShdRelList relself; /* self paths of launched batches, read at the fold */
     double min_lat;
     ShdMinJumpFn cb;
     void* cb_user;
@@ -163,16 +172,17 @@ struct ShdTopology {
 
     /* synchronisation (see the header comment) */
     int ready; /* table built and adopted: lookups may proceed (atomic) */
-    pthread_mutex_t setup_mu, touch_mu, min_mu, pkt_mu, pair_mu, round_mu;
+    pthread_mutex_t setup_mu, touch_mu, min_mu, pkt_mu, pair_mu, round_mu, rel_mu;
 };
 
 void shd_topology_release_device(ShdTopology* t);
 void shd_shards_clear(ShdTopology* t);
 int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj);
-/* shd_resolve with the row releases deferred into b (flush with shd_release_flush) */
-int shd_resolve_b(ShdTopology* t, int si, int di, int* oi, int* oj, ShdRelBatch* b);
-int shd_release_flush(ShdTopology* t, ShdRelBatch* b);
-void shd_relbatch_free(ShdRelBatch* b);
+/* device-resident releases (topology.c): launch the queue once it is long
+ * enough (never waits); wait for everything and fold it in touch order (fold
+ * = 1) or drop it (0) */
+int shd_release_kick(ShdTopology* t);
+int shd_release_sync(ShdTopology* t, int fold);
 /* the shard holding row `row` of a device-resident table (NULL: another rank's) */
 ShdShard* shd_shard_of(ShdTopology* t, int row);
 /* n table entries by flat index (host mirror or the owning shards' devices) */

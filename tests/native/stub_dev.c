@@ -86,18 +86,47 @@ int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, doubl
     return 0;
 }
 
-int shd_dev_release_min(const ShdEntry* base, int A, const int32_t* rows, const uint32_t* seqs, int n,
-                        const uint32_t* touch, double* out, void** scratch) {
+/* release: computed at launch on the host, kept until collect */
+typedef struct {
+    double* v;
+    size_t n, cap;
+} StubRel;
+int shd_dev_release_launch(const ShdEntry* base, int A, const int32_t* rows, const uint32_t* seqs, int n,
+                           const uint32_t* touch, void** scratch) {
+    StubRel* s = (StubRel*)*scratch;
+    if (!s && !(s = (StubRel*)calloc(1, sizeof *s))) return -ENOMEM;
+    *scratch = s;
+    if (s->n + (size_t)n > s->cap) {
+        size_t nc = 2 * (s->n + (size_t)n) + 16;
+        double* v = (double*)realloc(s->v, sizeof(double) * nc);
+        if (!v) return -ENOMEM;
+        s->v = v;
+        s->cap = nc;
+    }
     for (int r = 0; r < n; r++) {
         const ShdEntry* row = base + (size_t)rows[r] * (size_t)A;
-        out[r] = -1.0;
+        double m = -1.0;
         for (int j = 0; j < A; j++)
-            if (j != rows[r] && touch[j] > seqs[r] && row[j].lat >= 0 && (out[r] < 0 || row[j].lat < out[r]))
-                out[r] = row[j].lat;
+            if (j != rows[r] && touch[j] > seqs[r] && row[j].lat >= 0 && (m < 0 || row[j].lat < m)) m = row[j].lat;
+        s->v[s->n++] = m;
     }
     return 0;
 }
-void shd_dev_release_scratch_free(void* scratch) { (void)scratch; }
+int shd_dev_release_collect(void* scratch, double* out, size_t cap, size_t* n) {
+    StubRel* s = (StubRel*)scratch;
+    *n = 0;
+    if (!s || !s->n) return 0;
+    if (s->n > cap) return -ENOSPC;
+    memcpy(out, s->v, sizeof(double) * s->n);
+    *n = s->n;
+    s->n = 0;
+    return 0;
+}
+size_t shd_dev_release_pending(void* scratch) { return scratch ? ((StubRel*)scratch)->n : 0; }
+void shd_dev_release_scratch_free(void* scratch) {
+    if (scratch) free(((StubRel*)scratch)->v);
+    free(scratch);
+}
 
 int shd_dev_ws_new(void** ws) {
     *ws = malloc(1);
