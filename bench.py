@@ -209,11 +209,15 @@ def main():
     xport = None
     if world > 1:
         # the exchange and the all-gather run inside libshdnet
-        # (shd_round_exchange, shd_topology_allgather_rows); the collectives
-        # come from RCCL: torch's communicator by default, the library's own
-        # with SHD_XPORT=rccl (gloo only in CPU rehearsals)
+        # (shd_round_exchange, shd_topology_allgather_rows) over the library's
+        # own RCCL communicator (shd_transport_rccl_new: ncclSend/ncclRecv
+        # groups stream-ordered on the round's stream, the counts on the
+        # transport's stream; the rank-0 unique id travels through
+        # torch.distributed once).  torch.distributed's collectives
+        # (TorchTransport) only for gloo rehearsals on one GPU, or SHD_XPORT=torch.
         from shadow_amd.transport import RcclTransport, TorchTransport
-        xport = RcclTransport(local) if os.environ.get("SHD_XPORT") == "rccl" else TorchTransport(device=dev)
+        use_torch = backend != "nccl" or os.environ.get("SHD_XPORT") == "torch"
+        xport = TorchTransport(device=dev) if use_torch else RcclTransport(local)
 
     # routing rows sharded by source slot (§8e); at N>1 the full matrix the
     # replicated C3 rounds read is completed by the C-ABI all-gather
@@ -350,6 +354,9 @@ def main():
             "packets_per_round_per_gpu": P, "hosts": H, "vertices": V, "attached_vertices": A,
             "delivered_per_round_rank0": delivered, "slab_overflow_events_rank0": overflow,
             "parallelism": f"dst-shard x{world}",
+            "transport": None if xport is None else type(xport).__name__ + (
+                " (libshdnet RCCL: ncclSend/ncclRecv)" if type(xport).__name__ == "RcclTransport"
+                else f" (torch.distributed {backend})"),
         },
         "roofline": {
             "kernel": STAGES[dom], "bound": "hbm", "achieved": achieved[dom], "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -499,30 +506,92 @@ def main():
                                          max(h4 - l4, 0), args.c4_vertices,
                                          routing_traffic(tj, "_c4") if world == 1 else None),
         }
-        # C4 packet delivery: 1,000 rounds on the 100k-vertex table.  N=1: the
-        # whole table is resident (A4^2 x 16 B = 120 GB of the 288 GB).  N>1:
-        # the rows stay sharded (no full matrix anywhere): each record first
-        # goes to the rank holding its answering row (shd_round_route_records),
-        # is decided there, and its event goes to its destination's owner
-        # (shd_round_exchange).  Weak scaling: c4_packets per rank per round.
+        # C4 packet delivery on the 100k-vertex table as a simulation.  N=1: the
+        # whole table is resident (A4^2 x 16 B = 120 GB of the 288 GB) with NO
+        # row released at adoption; the first round goes through the host API
+        # (shd_round_append_worker at send time: every first touch queues its
+        # row's release, reduced asynchronously on the GPU; shd_round_collect
+        # folds them at the boundary) -- the time to the steady state is
+        # reported beside the build.  Then `c4_rounds` simulated rounds on the
+        # device: the load generator (shd_synth_sends_device) has every sender
+        # of the rank send m packets with its rand_r state and event counter
+        # carried from round to round, new destinations every round, the
+        # barrier advancing by the window.  N>1: the rows stay sharded (no full
+        # matrix anywhere): each record first goes to the rank holding its
+        # answering row (shd_round_route_records), is decided there, and its
+        # event goes to its destination's owner (shd_round_process_exchange).
+        # Weak scaling: c4_packets per rank per round.
         if args.c4_rounds > 0:
+            lib4 = _lib.lib()
+            P4, H4 = args.c4_packets, args.c4_hosts
+            s_lo, s_hi = rank * H4 // world, (rank + 1) * H4 // world
+            pool4 = np.arange(s_lo, s_hi, dtype=np.uint32)  # this rank's senders
+            m4 = max(1, P4 // max(len(pool4), 1))
+            n4 = len(pool4) * m4
+            W4, T04, SEED4 = 10_000_000, 100_000_000, 0x5EED0008
+            st4 = states4[pool4].astype(np.uint32)
+            sq4 = np.zeros(len(pool4), dtype=np.uint64)
+            first = None
             if world == 1:
-                t4.adopt_table_device_resident(shard4.ptr)  # no 120 GB host mirror
+                t4.adopt_table_device_resident(shard4.ptr)  # no 120 GB host mirror, nothing released yet
+                rec0, st4, sq4 = synth.synth_sends(pool4, m4, 0, SEED4, T04, W4, st4, sq4, ndst=H4)
+                nw = 8  # worker threads of the host (their buffers); appended here in worker order
+                _lib.check(lib4.shd_round_set_workers(t4.handle, nw))
+                _lib.check(lib4.shd_round_begin(t4.handle, T04 + W4, end_t, 0))
+                bounds = [k * len(rec0) // nw for k in range(nw + 1)]
+                s0 = time.perf_counter()
+                for w in range(nw):
+                    chunk = np.ascontiguousarray(rec0[bounds[w]:bounds[w + 1]])
+                    _lib.check(lib4.shd_round_append_worker(t4.handle, w, chunk.ctypes.data, len(chunk)))
+                t_app = time.perf_counter() - s0
+                s0 = time.perf_counter()
+                _lib.check(lib4.shd_topology_release_sync(t4.handle))
+                t_rel = time.perf_counter() - s0
+                seq = np.empty(A4, dtype=np.uint32)
+                _lib.check(lib4.shd_topology_touch_order(t4.handle, seq.ctypes.data, None, A4))
+                touched = int((seq != 0xFFFFFFFF).sum())
+                out0 = np.zeros(len(rec0), dtype=synth.DELIV_DTYPE)
+                offs0 = np.zeros(H4 + 1, dtype=np.uint32)
+                stat0 = np.zeros(len(rec0), dtype=np.uint8)
+                nout0, mt0 = C.c_size_t(), C.c_uint64()
+                s0 = time.perf_counter()
+                _lib.check(lib4.shd_round_collect(t4.handle, out0.ctypes.data, len(out0), C.byref(nout0),
+                                                  offs0.ctypes.data, stat0.ctypes.data, C.byref(mt0)))
+                t_col = time.perf_counter() - s0
+                s0 = time.perf_counter()
+                t4.touch_all()  # rows no host's send touched first: the steady state of the later rounds
+                t_rest = time.perf_counter() - s0
+                min_ms = t4.min_path_latency()
+                del out0, stat0
+                first = {
+                    "packets": len(rec0), "senders": len(pool4), "workers": nw, "rows": A4,
+                    "rows_first_touched": touched, "append_s": t_app, "release_wait_s": t_rel,
+                    "collect_s": t_col, "delivered": int(nout0.value), "touch_rest_s": t_rest,
+                    "steady_state_s": t_app + t_rel + t_col + t_rest,
+                    "steady_state_vs_build": (t_app + t_rel + t_col + t_rest) / tr4, "min_path_latency_ms": min_ms,
+                    "what": "round 0 through the host API: every host sends (shd_round_append_worker, 8 worker "
+                            "buffers: the send-time lookups, first touches queue their rows' releases, launched "
+                            "asynchronously in batches of 1,024); release_wait = the residual wait of the fold "
+                            "(shd_topology_release_sync); collect = the round boundary incl. PCIe both ways; "
+                            "touch_rest = the rows no send touched first, released in slot order",
+                }
+                log(f"C4 first round: {touched} of {A4} rows first-touched by the sends; append {t_app:.2f}s, "
+                    f"release wait {t_rel:.3f}s, collect {t_col:.2f}s, rest {t_rest:.2f}s")
             else:
                 mn = torch.tensor([t4.shard_min_latency(shard4.ptr, l4, h4) if h4 > l4 else -1.0],
                                   dtype=torch.float64, device=cdev)
                 mn[mn < 0] = float("inf")
                 dist.all_reduce(mn, op=dist.ReduceOp.MIN)
                 t4.adopt_table_shard_device_resident(shard4.ptr, l4, h4, float(mn.item()))
-            P4 = args.c4_packets
-            H4 = args.c4_hosts
-            s_lo, s_hi = rank * H4 // world, (rank + 1) * H4 // world
-            pk4 = synth.packet_batch(P4, H4, 0x5EED0008 + rank, 100_000_000, 10_000_000, states4,
-                                     hosts_lo=s_lo, hosts_hi=s_hi)
-            cap4 = 2 * P4
-            r_recs = torch.from_numpy(pk4.view(np.uint8)).to(dev)
+            cap4 = 2 * n4
+            d_pool4 = torch.from_numpy(pool4.view(np.int32)).to(dev)
+            d_st4 = [torch.from_numpy(st4.view(np.int32)).to(dev), torch.empty(len(pool4), dtype=torch.int32,
+                                                                               device=dev)]
+            d_sq4 = [torch.from_numpy(sq4.view(np.int64)).to(dev), torch.empty(len(pool4), dtype=torch.int64,
+                                                                               device=dev)]
+            r_recs = torch.empty(n4 * 32, dtype=torch.uint8, device=dev)
             r_in = torch.empty(cap4 * 32, dtype=torch.uint8, device=dev) if world > 1 else r_recs
-            r_scr = torch.empty(P4 * 32, dtype=torch.uint8, device=dev) if world > 1 else None
+            r_scr = torch.empty(n4 * 32, dtype=torch.uint8, device=dev) if world > 1 else None
             r_out = torch.empty(cap4 * 32, dtype=torch.uint8, device=dev)
             r_off = torch.empty(H4 + 1, dtype=torch.int32, device=dev)
             r_status = torch.empty(cap4, dtype=torch.uint8, device=dev)
@@ -535,59 +604,75 @@ def main():
                 r_fin_off = torch.empty(host_bounds4[rank + 1] - host_bounds4[rank] + 1, dtype=torch.int32,
                                         device=dev)
                 xport.register(r_scr, r_in, r_out, r_recv)
+            rnd = [1]  # next round index (round 0 was the host-API round at N=1)
 
             def round4():
+                r = rnd[0]
+                rnd[0] += 1
+                a, b = r % 2, (r + 1) % 2
+                t0r = T04 + r * W4
+                _lib.check(lib4.shd_synth_sends_device(
+                    C.c_void_p(d_pool4.data_ptr()), len(pool4), m4, r, SEED4, t0r, W4, None, H4,
+                    C.c_void_p(d_st4[a].data_ptr()), C.c_void_p(d_st4[b].data_ptr()), C.c_void_p(d_sq4[a].data_ptr()),
+                    C.c_void_p(d_sq4[b].data_ptr()), C.c_void_p(r_recs.data_ptr()), C.c_void_p(sptr)))
                 if world == 1:
-                    t4.process_device(r_in.data_ptr(), P4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
+                    t4.process_device(r_recs.data_ptr(), n4, t0r + W4, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
                                       r_status.data_ptr(), r_cnt.data_ptr(), sptr)
                     return
                 # records to their answering row's rank, decided there, events to
                 # their destination's owner as grouped 24-B wire records
-                n4 = t4.route_records(xport, r_recs.data_ptr(), P4, row_bounds, r_scr.data_ptr(),
+                nr = t4.route_records(xport, r_recs.data_ptr(), n4, row_bounds, r_scr.data_ptr(),
                                       r_in.data_ptr(), cap4, sptr)
-                if split:
-                    t4.process_device(r_in.data_ptr(), n4, barrier_t, end_t, 0, r_out.data_ptr(), r_off.data_ptr(),
-                                      r_status.data_ptr(), r_cnt.data_ptr(), sptr)
-                    t4.exchange(xport, r_out.data_ptr(), r_off.data_ptr(), host_bounds4, r_recv.data_ptr(), cap4,
-                                r_fin.data_ptr(), r_fin_off.data_ptr(), sptr)
-                else:
-                    t4.process_exchange(xport, r_in.data_ptr(), n4, barrier_t, end_t, 0, host_bounds4, r_out.data_ptr(),
-                                        r_status.data_ptr(), r_cnt.data_ptr(), r_recv.data_ptr(), cap4,
-                                        r_fin.data_ptr(), r_fin_off.data_ptr(), sptr)
+                t4.process_exchange(xport, r_in.data_ptr(), nr, t0r + W4, end_t, 0, host_bounds4, r_out.data_ptr(),
+                                    r_status.data_ptr(), r_cnt.data_ptr(), r_recv.data_ptr(), cap4,
+                                    r_fin.data_ptr(), r_fin_off.data_ptr(), sptr)
 
             for _ in range(3):
                 round4()
             torch.cuda.synchronize(dev)
             barrier()
+            _lib.check(lib4.shd_round_timing_enable(1))
             s0 = time.perf_counter()
             for _ in range(args.c4_rounds):
                 round4()
             torch.cuda.synchronize(dev)
             barrier()
             tp4 = max_over_ranks(time.perf_counter() - s0)
+            st4ms = (C.c_double * 4)()
+            nl4 = C.c_int()
+            _lib.check(lib4.shd_round_timing_read(st4ms, 4, C.byref(nl4)))
+            _lib.check(lib4.shd_round_timing_enable(0))
             c4 = result["routing"]["c4"]
+            if first:
+                c4["first_round"] = first
             c4["rounds"] = {
-                "rounds": args.c4_rounds, "packets_per_round": P4 * world, "seconds": tp4,
-                "packets_per_s": P4 * world * args.c4_rounds / tp4, "ms_per_round": tp4 / args.c4_rounds * 1e3,
-                "delivered_per_round_rank0": int(r_cnt.cpu().numpy().view(np.uint64)[0]),
-                "input": "one synthetic batch per rank (senders = the rank's host shard, uniform destinations over "
-                         "the 200k hosts, reserved rand_r pre-states) replayed every round, resident in HBM; "
-                         + ("full 120 GB table resident" if world == 1 else
-                            "rows sharded by source slot; records routed to their answering row's rank, events "
-                            "exchanged to their destination's owner"),
+                "rounds": args.c4_rounds, "packets_per_round": n4 * world, "seconds": tp4,
+                "packets_per_s": n4 * world * args.c4_rounds / tp4, "ms_per_round": tp4 / args.c4_rounds * 1e3,
+                "handoff_ms_per_round_rank0": sum(st4ms[k] for k in range(4)) / max(nl4.value, 1),
+                "delivered_last_round_rank0": int(r_cnt.cpu().numpy().view(np.uint64)[0]),
+                "per_round_advance": "barrier += 10 ms; every sender's rand_r state and event counter carried on the "
+                                     "device; new destinations each round (shd_synth_sends_device, in the timed "
+                                     "loop; handoff_ms = the decide/group/sort stages alone)",
+                "input": f"each rank's {len(pool4)} senders x {m4} packets per round, destinations uniform over the "
+                         f"{H4} hosts; " + ("full 120 GB table resident, rows released by round 0's sends, the "
+                                            "rest in slot order" if world == 1 else
+                                            "rows sharded by source slot; records routed to their answering row's "
+                                            "rank, events exchanged to their destination's owner"),
             }
-            log(f"C4 {args.c4_rounds} rounds x {P4} packets/rank in {tp4:.2f}s")
+            log(f"C4 {args.c4_rounds} simulated rounds x {n4} packets/rank in {tp4:.2f}s")
             del r_recs, r_out, r_status
         del shard4, t4
         torch.cuda.empty_cache()
 
     # ------------------------------------------------------- CPU baseline (N=1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(gml, H, states, top, result, c4_ctx, pk)
+        result["cpu_baseline"] = cpu_baseline(gml, H, states, top, result, c4_ctx, pk, args.c2_hosts)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        if hasattr(xport, "close"):
+            xport.close()
         dist.destroy_process_group()
 
 
@@ -650,7 +735,24 @@ def cpu_rows_parallel(orc, sources, targets, threads):
     return (time.perf_counter() - t0) / len(sources)
 
 
-def cpu_baseline(gml, H, states, top, result, c4_ctx=None, pk=None):
+def host_cpu():
+    """The box's CPU as the CPU baseline ran on it (model and
+    core count stated): /proc/cpuinfo's model, the machine's CPUs and the
+    ones this process may run on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "threads_used": int(os.environ.get("SHD_CPU_THREADS", "16"))}
+
+
+def cpu_baseline(gml, H, states, top, result, c4_ctx=None, pk=None, c2_hosts=50_000):
     """The oracle (C restatement of worker_sendPacket + per-destination binary
     heaps) timed on this host: the headline figure is the bench's own C3
     batch over the full table on one core; beside it the same batch on the
@@ -662,6 +764,7 @@ def cpu_baseline(gml, H, states, top, result, c4_ctx=None, pk=None):
     threads = int(os.environ.get("SHD_CPU_THREADS", "16"))
     lat, rel, sv = top.table()
     base = {}
+    hostinfo = host_cpu()
     if pk is not None:
         # the real C3 workload: every attached row preloaded (the GPU timed
         # region's steady state), the bench's own 10M-packet batch
@@ -728,6 +831,18 @@ def cpu_baseline(gml, H, states, top, result, c4_ctx=None, pk=None):
                           "cores": threads, "kind": "port",
                           "sample": f"all {len(targets)} C1 source rows, {threads} threads: "
                                     f"{per_mt * len(targets):.2f}s"}
+    # C2 itself (configs[2]: the V=20k graph with 50k hosts): every source
+    # row on the box's CPU share, rows independent (no global graphLock)
+    o2 = O.OracleTopology(gml)
+    _, _, v2 = scenario.register_hosts(o2, c2_hosts, seed=1)
+    sv2 = np.unique(v2).astype(np.int32)
+    per2 = cpu_rows_parallel(o2, sv2, sv2, threads)
+    full2 = per2 * len(sv2)
+    base["routing_c2_mt"] = {"value": float(c2_hosts) ** 2 / full2, "unit": "routed host-pairs/s", "cores": threads,
+                             "kind": "port",
+                             "sample": f"all {len(sv2)} C2 source rows (V=20k, H={c2_hosts}), {threads} threads: "
+                                       f"{full2:.2f}s", "build_s": full2}
+    del o2
     if c4_ctx is not None:
         g4, sv4 = c4_ctx
         o4 = O.OracleTopology(g4)
@@ -742,6 +857,7 @@ def cpu_baseline(gml, H, states, top, result, c4_ctx=None, pk=None):
         c4 = result.get("routing", {}).get("c4")
         if c4:
             base["routing_c4_mt"]["value"] = c4["value"] * c4["build_s"] / full4
+    base["host"] = hostinfo
     return base
 
 

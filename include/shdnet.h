@@ -539,6 +539,22 @@ int shd_round_timing_read(double* stage_ms, int nstages, int* launches);
 int shd_parse_time_ns(const char* s, uint64_t* ns);
 int shd_parse_bandwidth_bits(const char* s, uint64_t* bits_per_s);
 
+/* Synthetic load for simulated rounds (benchmarks and tests: it stands in
+ * for the hosts' applications; not part of the hand-off).  Every sender
+ * d_pool[k] (k < npool) sends m packets into d_recs (npool * m records,
+ * sender-major): packet j reserves the sender's j-th rand_r draw of the round
+ * (worker.c:540-541; the record carries that draw's pre-state), goes to
+ * d_dst_pool[x % ndst] (or host x % ndst when d_dst_pool is NULL; the next
+ * one if that is the sender) at a time in the j-th of m slices of [t0, t0 +
+ * window_ns), x a splitmix64 hash of (seed, round, k, j).  The senders'
+ * rand_r states and event counters are carried: d_state_in / d_seq_in (per
+ * pool position) -> d_state_out / d_seq_out after the round.  Device
+ * pointers; stream: hipStream_t or NULL. */
+int shd_synth_sends_device(const uint32_t* d_pool, uint32_t npool, uint32_t m, uint32_t round, uint64_t seed,
+                           uint64_t t0, uint64_t window_ns, const uint32_t* d_dst_pool, uint32_t ndst,
+                           const uint32_t* d_state_in, uint32_t* d_state_out, const uint64_t* d_seq_in,
+                           uint64_t* d_seq_out, ShdPkt* d_recs, void* stream);
+
 /* Last error message for this thread (static storage). */
 const char* shd_last_error(void);
 

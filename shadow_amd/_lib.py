@@ -92,6 +92,8 @@ PROTOS = {
     "shd_transport_local_new": (C.c_int, [C.c_int, _P]),
     "shd_transport_local_free": (None, [_P]),
     "shd_memcpy": (C.c_int, [_P, _P, C.c_size_t]),
+    "shd_synth_sends_device": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64,
+                                         _P, C.c_uint32, _P, _P, _P, _P, _P, _P]),
     "shd_topology_log_cached_paths": (C.c_int, [_P, PATH_LOG_FN, _P, _u64p]),
     "shd_nic_init": (C.c_int, [C.c_uint32, _P, _P, C.c_uint64, _P, _P]),
     "shd_event_lengths": (C.c_int, [_P, C.c_size_t, _P, C.c_uint32, _P, _P]),

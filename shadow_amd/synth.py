@@ -232,3 +232,57 @@ def packet_batch(n: int, nhosts: int, seed: int, window_start: int, window_ns: i
     rec["rng_state"] = pre
     rec["payload_len"] = payload
     return rec
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    """splitmix64's finaliser on a uint64 array (csrc/synth.hip mix64)."""
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def synth_sends(pool: np.ndarray, m: int, rnd: int, seed: int, t0: int, window_ns: int, states: np.ndarray,
+                seqs: np.ndarray, dst_pool: np.ndarray | None = None, ndst: int | None = None):
+    """numpy restatement of shd_synth_sends_device (csrc/synth.hip), the
+    simulated rounds' load generator: sender k = pool[k] sends m packets;
+    packet j reserves the sender's j-th rand_r draw of the round (its record
+    carries the pre-state; the state m draws on is carried out), goes to a
+    hashed destination (dst_pool[x % ndst], or host x % ndst; the next one if
+    that is the sender itself) at a time in the j-th of m slices of [t0, t0 +
+    window).  Returns (records, states after the round, seqs after)."""
+    pool = np.asarray(pool, dtype=np.uint32)
+    npool = len(pool)
+    n = npool * m
+    ndst = len(dst_pool) if dst_pool is not None else int(ndst)
+    with np.errstate(over="ignore"):
+        key = np.uint64(seed) * np.uint64(0xD1B54A32D192ED03) + np.uint64(rnd) * np.uint64(0x8CB92BA72F3D8DD7)
+        x = _mix64(key + np.arange(n, dtype=np.uint64))
+    k = np.repeat(np.arange(npool), m)
+    j = np.tile(np.arange(m, dtype=np.uint64), npool)
+    h = pool[k]
+    s = np.asarray(states, dtype=np.uint32)[k]
+    st = s.copy()
+    for step in range(1, m):  # packet j's pre-state: j draws into the round
+        s = glibc_rand_r_advance(s)
+        st = np.where(j >= np.uint64(step), s, st)
+    di = (x % np.uint64(ndst)).astype(np.int64)
+    dmap = (lambda i: np.asarray(dst_pool, dtype=np.uint32)[i]) if dst_pool is not None else \
+        (lambda i: i.astype(np.uint32))
+    d = dmap(di)
+    clash = (d == h) & (ndst > 1)
+    di = np.where(clash, np.where(di + 1 == ndst, 0, di + 1), di)
+    d = dmap(di)
+    sl = np.uint64(window_ns // m)
+    rec = np.empty(n, dtype=PKT_DTYPE)
+    rec["now"] = np.uint64(t0) + j * sl + ((x >> np.uint64(32)) % sl if int(sl) else np.uint64(0))
+    rec["seq"] = np.asarray(seqs, dtype=np.uint64)[k] + j
+    rec["src_host"] = h
+    rec["dst_host"] = d
+    rec["rng_state"] = st
+    rec["payload_len"] = np.where(((x >> np.uint64(16)) & np.uint64(1023)) < np.uint64(922), 1448, 0).astype(np.uint32)
+    out_states = np.asarray(states, dtype=np.uint32).copy()
+    for _ in range(m):
+        out_states = glibc_rand_r_advance(out_states)
+    return rec, out_states, np.asarray(seqs, dtype=np.uint64) + np.uint64(m)
