@@ -98,7 +98,7 @@ def gpu_state(dev_index):
 # (independent random 16-B requests, by footprint and write share), the
 # bound the scatter and the slab SSSP kernels are compared against beside
 # their byte fraction.
-CEILING_JSON = os.path.join(ROOT, "profiles", "r03_request_ceiling.json")
+CEILING_JSON = os.path.join(ROOT, "profiles", "r04_request_ceiling.json")
 
 
 def request_ceiling(key):
@@ -317,11 +317,23 @@ def main():
     per_launch_ms = [stage_ms[k] / launches for k in range(4)]
     # each rank's stage times; the roofline uses rank 0's live numbers
     dom = int(np.argmax(per_launch_ms))
-    # scan: counts in, offsets out; place: only the overflow events move
-    # (k_place_ovf; 0 B when no segment outgrew its slab); sort: every
-    # delivered event in and out
-    alg_bytes = [BYTES_SCATTER_PER_PKT * P, 4.0 * 2 * H, BYTES_MOVE_PER_EVENT * overflow,
-                 BYTES_MOVE_PER_EVENT * delivered]
+    pid = C.c_int()
+    _lib.check(lib.shd_round_pipeline_of(H, P, C.byref(pid)))
+    pipe_name = ["bucket", "rank", "slab", "part"][pid.value]
+    if pipe_name == "part":
+        # k_part_scatter: record 32 B + 2 x 4 B slots + the 16 B entry (§8d) +
+        # 1 B status in, the 16-B staged event out per delivered packet;
+        # k_part_sort (+ listed segments): the staged event in, the 32-B event
+        # and the offsets out
+        kernels = ["k_part_scatter", "-", "-", "k_part_sort (+ k_segsort_mid/merge for listed segments)"]
+        alg_bytes = [(32 + 2 * 4 + 16 + 1) * P + 16.0 * delivered, 0.0, 0.0, (16 + 32) * delivered + 4.0 * (H + 1)]
+    else:
+        # scan: counts in, offsets out; place: only the overflow events move
+        # (k_place_ovf; 0 B when no segment outgrew its slab); sort: every
+        # delivered event in and out
+        kernels = ["k_pkt_scatter", "k_scan_*", "k_place_ovf", "k_segsort_dst (+ mid/merge)"]
+        alg_bytes = [BYTES_SCATTER_PER_PKT * P, 4.0 * 2 * H, BYTES_MOVE_PER_EVENT * overflow,
+                     BYTES_MOVE_PER_EVENT * delivered]
     achieved = [alg_bytes[k] / (per_launch_ms[k] * 1e-3) / 1e9 if per_launch_ms[k] > 0 else 0.0 for k in range(4)]
     total_pkts = P * world * args.steps
     value = total_pkts / dt
@@ -359,19 +371,29 @@ def main():
                 else f" (torch.distributed {backend})"),
         },
         "roofline": {
-            "kernel": STAGES[dom], "bound": "hbm", "achieved": achieved[dom], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "kernel": kernels[dom], "stage": STAGES[dom], "bound": "hbm", "achieved": achieved[dom],
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved[dom] / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
             "traffic_GBps": (traffic / (per_launch_ms[dom] * 1e-3) / 1e9) if traffic else None,
             "per_stage_ms": dict(zip(STAGES, per_launch_ms)),
+            "per_stage_kernels": dict(zip(STAGES, kernels)),
             "per_stage_GBps": dict(zip(STAGES, achieved)),
             "alg_bytes_per_launch": dict(zip(STAGES, alg_bytes)),
             "timing": "HIP events on the launch stream, averaged over the timed steps",
-            # the scatter's HBM-side random requests: the table gather per
-            # packet, the destination-slot atomic and the slab write per event
-            "request_roofline": request_roofline(P + 2.0 * delivered, per_launch_ms[0] * 1e-3, "6144MB_62.5pct_writes",
-                                                 "table gather per packet + slot atomic + slab write per event")
+            # the scatter's irreducible random requests: one table gather per
+            # packet (3.16 GB table), against the measured rate of independent
+            # 8-B gathers from a table of that size (scripts/ubench_fetch.hip)
+            "request_roofline": request_roofline(float(P), per_launch_ms[0] * 1e-3, "gath8_3160MB",
+                                                 "one 8-B table gather per packet (the scatter's other accesses: "
+                                                 + ("streamed records, LDS staging, bucket-ordered runs"
+                                                    if pipe_name == "part" else
+                                                    "plus one slot atomic and one 16-B slab store per event") + ")")
             if per_launch_ms[0] > 0 else None,
-            "pipeline": os.environ.get("SHD_PACKET_PIPELINE") or "slab",
+            # the whole hand-off at SURVEY.md §8d's 88 B per packet over every stage
+            "handoff": {"alg_bytes_per_packet": BYTES_SCATTER_PER_PKT, "ms": sum(per_launch_ms),
+                        "achieved": BYTES_SCATTER_PER_PKT * P / (sum(per_launch_ms) * 1e-3) / 1e9,
+                        "frac": BYTES_SCATTER_PER_PKT * P / (sum(per_launch_ms) * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "pipeline": pipe_name,
         },
         "gpu_state": {"before_timed": state_before, "after_timed": gpu_state(local) if rank == 0 else None},
     }

@@ -530,6 +530,9 @@ int shd_memcpy(void* dst, const void* src, size_t bytes);
  * per-destination count), 1 scan, 2 place, 3 segment sort.  enable resets
  * the record; read sums the elapsed ms per stage over recorded launches. */
 int shd_round_timing_enable(int enable);
+/* The grouping pipeline a round of n records over nhosts destinations runs
+ * (SHD_PACKET_PIPELINE or the default): 0 bucket, 1 rank, 2 slab, 3 part. */
+int shd_round_pipeline_of(uint32_t nhosts, size_t n, int* pipe);
 int shd_round_timing_read(double* stage_ms, int nstages, int* launches);
 
 /* Unit strings as the GML loader reads them (replace parse_time_nanosec /

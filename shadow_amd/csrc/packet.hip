@@ -1915,6 +1915,380 @@ __global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__
     }
 }
 
+// ---- "part" pipeline: LDS-staged bucket partition, then one LDS sort per bucket ----
+// The slab pipeline's scatter pays two random HBM requests per delivered
+// event beyond the table gather: the destination counter's atomic and a 16-B
+// partial-line store into a 147 MB slab (profiles/r04a_ubench_part.log: the
+// gather floor 0.318 ms, with the slab form 0.573 ms).  Here:
+//   k_part_scatter  a workgroup decides kPartCH records (the scatter's decision,
+//                   unchanged), stages its delivered events in LDS (16 B
+//                   each), counts them per destination BUCKET of 2^shift hosts,
+//                   reserves one run per nonempty bucket with one atomic on
+//                   the bucket's counter, and writes its runs in bucket order
+//                   (consecutive lanes store consecutive records) into the
+//                   bucket's region of the stage: bucket b at [b * cap, ...).
+//   k_part_sort     one workgroup per bucket: its events into registers, a
+//                   count per destination (LDS), the bucket's output base (the
+//                   sum of the earlier buckets' totals) and the destination
+//                   offsets, the events placed into LDS grouped by
+//                   destination, then one wave per destination segment ranks
+//                   it by event_compare (wave_rank_segment) and writes it at
+//                   its final place -- no slab, no separate scan or sort pass.
+// Stage record (16 B): {time - tbase, srcHostEventID, pkt_index, src << shift
+// | destination - bucket base}.  An event that does not fit it (time offset
+// or srcHostEventID of 32 bits or more, src >= 2^(32 - shift)) or that finds
+// its bucket's region full goes whole to the wide list (and counts in wcnt[b]);
+// a bucket with wide events, or with more events than k_part_sort holds in
+// LDS, takes the listed path: its events are placed unsorted at their
+// destination ranges of the staging array and every segment is listed for
+// k_segsort_mid / k_segsort_merge (skewed destinations).
+constexpr int kPartBlock = 1024;   // k_part_scatter / k_part_sort workgroup
+constexpr int kPartCH = 4096;      // records per k_part_scatter workgroup (4 per thread)
+constexpr int kPartLdsEv = 7168;   // events k_part_sort holds in LDS (7 per thread)
+constexpr uint32_t kPartMaxDst = 64; // destinations per bucket (shift <= 6)
+constexpr uint32_t kPartMaxBuckets = 4096;
+
+struct PartGeo {
+    uint32_t host_lo, H; // destination host range
+    uint32_t shift, nb;  // bucket = (dst - host_lo) >> shift
+    uint32_t cap;        // stage records per bucket
+    unsigned long long tbase;
+};
+
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* total, uint32_t* ws) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (int k = 0; k < nw; k++) {
+        if (k < w) base += ws[k];
+        tot += ws[k];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+template <int kB = 4>
+__global__ __launch_bounds__(kPartBlock) void k_part_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
+                                                             uint64_t barrier, uint64_t end_time, uint64_t boot_end,
+                                                             PartGeo g, uint4* __restrict__ stage,
+                                                             uint32_t* __restrict__ gcnt, uint32_t* __restrict__ wcnt,
+                                                             uint8_t* __restrict__ status,
+                                                             unsigned long long* counters, ShdDeliv* __restrict__ wide,
+                                                             uint32_t* __restrict__ nwide) {
+    extern __shared__ uint4 part_smem[];
+    uint4* ev = part_smem;                                       // kPartCH staged events (w = ~0: none)
+    uint16_t* rk = reinterpret_cast<uint16_t*>(ev + kPartCH);    // rank inside its bucket
+    uint16_t* perm = rk + kPartCH;                               // bucket order -> staged slot
+    uint32_t* hist = reinterpret_cast<uint32_t*>(perm + kPartCH); // nb
+    uint32_t* lofs = hist + g.nb;                                // nb + 1 (scan per thread run)
+    uint32_t* gb = lofs + g.nb + 1;                              // nb
+    __shared__ uint32_t wsum[kPartBlock / 64];
+    __shared__ unsigned long long wmin[kPartBlock / 64];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < g.nb; b += kPartBlock) hist[b] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * kPartCH;
+    const size_t A = (size_t)c.A;
+    const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
+    const uint2* __restrict__ ptab = reinterpret_cast<const uint2*>(c.ptab);
+    const uint32_t smax = g.shift ? (0xFFFFFFFFu >> g.shift) : 0xFFFFFFFFu; // src hosts that fit the record
+    unsigned long long mn = ~0ull;
+    static_assert(kPartCH % (kPartBlock * kB) == 0, "chunk");
+    for (int k0 = 0; k0 < kPartCH / kPartBlock; k0 += kB) {
+        ShdPkt p[kB];
+        bool live[kB];
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            const size_t i = base + (size_t)(k0 + k) * kPartBlock + threadIdx.x;
+            live[k] = i < n;
+            if (live[k]) p[k] = ld_pkt(&recs[i]);
+        }
+        int si[kB], di[kB];
+        uint32_t ts[kB], td[kB];
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            const bool known = live[k] && p[k].src_host < c.nhosts && p[k].dst_host < c.nhosts;
+            uint2 hs = make_uint2(~0u, ~0u), hd = make_uint2(~0u, ~0u);
+            if (known) {
+                hs = host_info[p[k].src_host];
+                hd = host_info[p[k].dst_host];
+            }
+            si[k] = hs.x == ~0u ? -1 : (int)hs.x;
+            di[k] = hd.x == ~0u ? -1 : (int)hd.x;
+            ts[k] = hs.y;
+            td[k] = hd.y;
+        }
+        size_t ei[kB];
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            int oi = si[k], oj = di[k];
+            if (oi >= 0 && oj >= 0) {
+                if (c.mode == 0) {
+                    if (oi != oj && td[k] < ts[k]) oi = di[k], oj = si[k]; // owner: row touched first
+                } else if (c.mode == 2) {
+                    const size_t b = (size_t)oi * A + (size_t)oj;
+                    if (!((c.pair_bits[b >> 5] >> (b & 31)) & 1u)) oi = di[k], oj = si[k];
+                }
+            }
+            if (oi < c.row_lo || oi >= c.row_hi) si[k] = -1; // another rank's row: not decided here
+            ei[k] = (size_t)(oi < 0 ? 0 : oi) * A + (size_t)(oj < 0 ? 0 : oj);
+        }
+        ShdEntry e[kB];
+        uint2 q[kB];
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            q[k] = make_uint2(kPtabFallback, 0u);
+            if (ptab && si[k] >= 0 && di[k] >= 0) {
+                const unsigned long long v =
+                    __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ptab) + ei[k]);
+                q[k] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kB; k++)
+            if (si[k] >= 0 && di[k] >= 0 && q[k].x == kPtabFallback) e[k] = c.tab[ei[k]];
+#pragma unroll
+        for (int k = 0; k < kB; k++) {
+            const uint32_t li = (uint32_t)((k0 + k) * kPartBlock + threadIdx.x);
+            uint8_t st = 0xff; // unregistered host: not delivered
+            uint64_t t = 0;
+            if (live[k] && si[k] >= 0 && di[k] >= 0) {
+                uint32_t rs = p[k].rng_state;
+                const uint32_t r = (uint32_t)glibc_rand_r(&rs);
+                bool keep;
+                uint64_t delay;
+                if (q[k].x != kPtabFallback) {
+                    keep = r <= q[k].y; // == (chance <= rel), see kPtabFallback
+                    delay = q[k].x;
+                } else {
+                    keep = (double)r / 2147483647.0 <= e[k].rel; // random_nextDouble, worker.c:545
+                    delay = (uint64_t)ceil(e[k].lat * 1000000.0);
+                }
+                st = SHD_DROPPED_LOSS;
+                if (p[k].now < boot_end || keep || p[k].payload_len == 0) {
+                    t = p[k].now + delay;                                   // worker.c:548-549
+                    if (t >= end_time) st = SHD_DROPPED_END;                // scheduler.c:236-239
+                    else {
+                        if (p[k].src_host != p[k].dst_host && t < barrier) t = barrier; // host_single.c:187-192
+                        st = SHD_DELIVERED;
+                    }
+                }
+            }
+            const bool dl = st == SHD_DELIVERED;
+            const uint32_t dr = p[k].dst_host - g.host_lo;
+            const bool fits = dl && c_fits(t, g.tbase, p[k].seq) && p[k].src_host <= smax && dr < g.H;
+            uint4 sv = make_uint4(0u, 0u, 0u, ~0u);
+            if (fits) {
+                rk[li] = (uint16_t)atomicAdd(&hist[dr >> g.shift], 1u); // LDS
+                sv = make_uint4((uint32_t)(t - g.tbase), (uint32_t)p[k].seq, p[k].src_host, p[k].dst_host);
+            }
+            ev[li] = sv;
+            const uint32_t ws = wave_alloc(dl && !fits, nwide, lane); // (every lane: ballot)
+            if (dl && !fits) {
+                st_ev(&wide[ws], ShdDeliv{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)(base + li) + c.idx_base,
+                                          0u});
+                if (dr < g.H) atomicAdd(&wcnt[dr >> g.shift], 1u);
+            }
+            if (dl && t >= barrier && t < mn) mn = t; // worker.c:350-363
+            if (live[k]) status[base + li] = st;
+        }
+    }
+    __syncthreads();
+    // bucket order inside the workgroup, and one run per nonempty bucket
+    {
+        const uint32_t per = (g.nb + kPartBlock - 1) / kPartBlock, b0 = threadIdx.x * per;
+        uint32_t s = 0;
+        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) s += hist[b0 + k];
+        uint32_t tot;
+        uint32_t pre = block_excl_scan_n(s, &tot, wsum);
+        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) {
+            const uint32_t h = hist[b0 + k];
+            lofs[b0 + k] = pre;
+            gb[b0 + k] = h ? atomicAdd(&gcnt[b0 + k], h) : 0u;
+            pre += h;
+        }
+        if (threadIdx.x == 0) lofs[g.nb] = tot;
+    }
+    __syncthreads();
+    for (uint32_t li = threadIdx.x; li < (uint32_t)kPartCH; li += kPartBlock) {
+        const uint32_t w = ev[li].w;
+        if (w != ~0u) perm[lofs[(w - g.host_lo) >> g.shift] + rk[li]] = (uint16_t)li;
+    }
+    __syncthreads();
+    const uint32_t total = lofs[g.nb];
+    const uint32_t mask = (1u << g.shift) - 1u;
+    for (uint32_t p0 = 0; p0 < total; p0 += kPartBlock) { // (uniform trip count: every lane takes the ballot)
+        const uint32_t pp = p0 + threadIdx.x;
+        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t b = 0, li = 0;
+        size_t j = 0;
+        bool in = false;
+        if (pp < total) {
+            li = perm[pp];
+            e = ev[li];
+            b = (e.w - g.host_lo) >> g.shift;
+            j = (size_t)gb[b] + (pp - lofs[b]);
+            in = j < g.cap;
+        }
+        if (in) { // runs of a bucket: consecutive lanes, consecutive records
+            const uint4 r = make_uint4(e.x, e.y, (uint32_t)(base + li) + c.idx_base, (e.z << g.shift) | ((e.w - g.host_lo) & mask));
+            stage[(size_t)b * g.cap + j] = r;
+        }
+        const bool full = pp < total && !in; // the bucket's region is full: whole event to the wide list
+        const uint32_t ws = wave_alloc(full, nwide, lane);
+        if (full) {
+            st_ev(&wide[ws], ShdDeliv{g.tbase + e.x, (unsigned long long)e.y, e.z, e.w,
+                                      (uint32_t)(base + li) + c.idx_base, 0u});
+            atomicAdd(&wcnt[b], 1u);
+        }
+    }
+    mn = wave_min_u64(mn);
+    if (lane == 0) wmin[threadIdx.x >> 6] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = wmin[0];
+        for (int k = 1; k < kPartBlock / 64; k++) m = wmin[k] < m ? wmin[k] : m;
+        if (m != ~0ull) atomicMin(&counters[1], m);
+    }
+}
+
+// One workgroup per bucket (see above).  nbig / big / scr: the listed
+// segments (k_segsort_mid); fault: nbig[2] guard bits.
+__global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
+                                                          const uint32_t* __restrict__ gcnt,
+                                                          const uint32_t* __restrict__ wcnt,
+                                                          const ShdDeliv* __restrict__ wide,
+                                                          const uint32_t* __restrict__ nwide, uint32_t wide_cap,
+                                                          uint32_t* __restrict__ offsets, ShdDeliv* __restrict__ out,
+                                                          ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
+                                                          uint32_t* __restrict__ nbig,
+                                                          unsigned long long* __restrict__ counters, uint32_t lds_keys) {
+    __shared__ uint4 lev[kPartLdsEv];
+    __shared__ unsigned long long keys[kPartBlock / 64][64 * 4 + 8];
+    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kPartBlock / 64];
+    __shared__ uint32_t s_base;
+    const uint32_t b = blockIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t d0 = b << g.shift;
+    const uint32_t nd = min(1u << g.shift, g.H - d0);
+    const uint32_t mask = (1u << g.shift) - 1u;
+    const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
+    const bool listed = tot > (uint32_t)kPartLdsEv || nw > 0; // (block-uniform)
+    // this bucket's output base: the totals of the buckets before it
+    {
+        uint32_t s = 0;
+        for (uint32_t k = threadIdx.x; k < b; k += kPartBlock) s += min(gcnt[k], g.cap) + wcnt[k];
+        uint32_t t;
+        (void)block_excl_scan_n(s, &t, wsum);
+        if (threadIdx.x == 0) s_base = t;
+    }
+    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kPartBlock) cnt[j] = cur[j] = 0;
+    __syncthreads();
+    const uint32_t obase = s_base;
+    const uint4* sb = stage + (size_t)b * g.cap;
+    uint4 e[kPartLdsEv / kPartBlock];
+    if (!listed) {
+#pragma unroll
+        for (int k = 0; k < kPartLdsEv / kPartBlock; k++) {
+            const uint32_t i = (uint32_t)k * kPartBlock + threadIdx.x;
+            if (i < ns) {
+                const shd_v4u v = __builtin_nontemporal_load(reinterpret_cast<const shd_v4u*>(sb) + i);
+                e[k] = make_uint4(v.x, v.y, v.z, v.w);
+                atomicAdd(&cnt[e[k].w & mask], 1u);
+            }
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < ns; i += kPartBlock) atomicAdd(&cnt[sb[i].w & mask], 1u);
+        const uint32_t m = *nwide;
+        if (m > wide_cap) {
+            if (threadIdx.x == 0) atomicOr(nbig + 2, kFaultOvfCap);
+        } else if (nw) {
+            for (uint32_t i = threadIdx.x; i < m; i += kPartBlock) {
+                const uint32_t dr = wide[i].dst_host - g.host_lo;
+                if (dr < g.H && (dr >> g.shift) == b) atomicAdd(&cnt[dr & mask], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) { // destination offsets (nd <= 64: one wave)
+        const uint32_t v = threadIdx.x < nd ? cnt[threadIdx.x] : 0u;
+        const uint32_t inc = wave_incl_scan(v, lane);
+        if (threadIdx.x < nd) {
+            loc[threadIdx.x] = inc - v;
+            offsets[d0 + threadIdx.x] = obase + inc - v;
+        }
+        if (threadIdx.x == 63) loc[nd] = inc;
+    }
+    if (b == gridDim.x - 1 && threadIdx.x == 0) {
+        offsets[g.H] = obase + tot;
+        counters[0] = obase + tot; // the round's delivered count
+    }
+    __syncthreads();
+    if (!listed) {
+#pragma unroll
+        for (int k = 0; k < kPartLdsEv / kPartBlock; k++) {
+            const uint32_t i = (uint32_t)k * kPartBlock + threadIdx.x;
+            if (i < ns) {
+                const uint32_t dl = e[k].w & mask;
+                lev[loc[dl] + atomicAdd(&cur[dl], 1u)] = e[k];
+            }
+        }
+        __syncthreads();
+        unsigned long long* lk = lds_keys ? keys[wv] : nullptr;
+        for (uint32_t j = wv; j < nd; j += kPartBlock / 64) {
+            const uint32_t nj = cnt[j], o = loc[j], dh = g.host_lo + d0 + j;
+            if (nj == 0) continue;
+            auto load = [&](uint32_t i) {
+                const uint4 r = lev[o + i];
+                return Ev{g.tbase + r.x, (unsigned long long)r.y, r.w >> g.shift, r.z};
+            };
+            if (nj <= 64) wave_rank_segment<1, 1>(load, nj, dh, out, obase + o, lane, lk);
+            else if (nj <= 128) wave_rank_segment<2, 1>(load, nj, dh, out, obase + o, lane, lk);
+            else if (nj <= (uint32_t)kSmallSeg) wave_rank_segment<4, 1>(load, nj, dh, out, obase + o, lane, lk);
+            else { // a larger segment: unsorted to its range of the staging array, listed
+                for (uint32_t i = lane; i < nj; i += 64) {
+                    const Ev v = load(i);
+                    st_ev(&scr[obase + o + i], ShdDeliv{v.t, v.q, v.s, dh, v.ix, 0u});
+                }
+                if (lane == 0) {
+                    const uint32_t k = atomicAdd(nbig, 1u);
+                    if (k < g.H) big[k] = d0 + j;
+                    else atomicOr(nbig + 2, kFaultBigCap);
+                }
+            }
+        }
+        return;
+    }
+    // listed bucket: every event unsorted to its destination's range of the
+    // staging array, every nonempty segment listed (k_segsort_mid / _merge)
+    for (uint32_t i = threadIdx.x; i < ns; i += kPartBlock) {
+        const uint4 r = sb[i];
+        const uint32_t dl = r.w & mask;
+        st_ev(&scr[obase + loc[dl] + atomicAdd(&cur[dl], 1u)],
+              ShdDeliv{g.tbase + r.x, (unsigned long long)r.y, r.w >> g.shift, g.host_lo + d0 + dl, r.z, 0u});
+    }
+    const uint32_t m = *nwide;
+    if (nw && m <= wide_cap)
+        for (uint32_t i = threadIdx.x; i < m; i += kPartBlock) {
+            ShdDeliv r = ld_ev(&wide[i]);
+            const uint32_t dr = r.dst_host - g.host_lo;
+            if (dr < g.H && (dr >> g.shift) == b) {
+                r.pad = 0;
+                st_ev(&scr[obase + loc[dr & mask] + atomicAdd(&cur[dr & mask], 1u)], r);
+            }
+        }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nd; j += kPartBlock)
+        if (cnt[j] > 0) {
+            const uint32_t k = atomicAdd(nbig, 1u);
+            if (k < g.H) big[k] = d0 + j;
+            else atomicOr(nbig + 2, kFaultBigCap);
+        }
+}
+
 // the round's fault word when no merge kernel runs: the stage guards only
 __global__ void k_fault_word(const uint32_t* __restrict__ nbig, MergeMeta mm) {
     if (threadIdx.x == 0) {
@@ -1947,6 +2321,8 @@ struct Ws {
     ShdDeliv* slab = nullptr;
     size_t cap_cslab = 0;     // ... and their compact 16-B form (CSlab)
     uint4* cslab = nullptr;
+    size_t cap_pstage = 0;    // part pipeline: the bucket regions of the stage (16-B records)
+    uint4* pstage = nullptr;
     uint32_t* meta = nullptr; // big-segment merge metadata (MergeMeta)
     uint32_t cap_meta = 0;    // merge segments it holds
     uint32_t* fault = nullptr; // pinned host copy of the last round's merge fault word (meta hdr[3])
@@ -2042,6 +2418,18 @@ int cslab_reserve(Ws& w, uint32_t H) {
     w.cap_cslab = 0;
     int rc = hip_status(hipMalloc((void**)&w.cslab, sizeof(uint4) * need), "hipMalloc ws.cslab");
     if (!rc) w.cap_cslab = need;
+    return rc;
+}
+
+int pstage_reserve(Ws& w, size_t need) {
+    if (need <= w.cap_pstage) return 0;
+    if (int rc = ws_quiesce(w)) return rc;
+    (void)hipFree(w.pstage);
+    w.pstage = nullptr;
+    w.cap_pstage = 0;
+    const size_t cap = need + need / 8 + 1024;
+    int rc = hip_status(hipMalloc((void**)&w.pstage, sizeof(uint4) * cap), "hipMalloc ws.pstage");
+    if (!rc) w.cap_pstage = cap;
     return rc;
 }
 
@@ -2379,12 +2767,33 @@ int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const 
 // (per-destination counters + a placement pass over the batch) or "bucket"
 // (atomic-free bucket partition).  The slab pipeline needs H x kSlab x 32 B
 // of HBM (100k hosts: 0.8 GB); above kMaxSlabBytes it falls back to rank.
-enum Pipeline { kBucketPipe = 0, kRankPipe = 1, kSlabPipe = 2 };
+enum Pipeline { kBucketPipe = 0, kRankPipe = 1, kSlabPipe = 2, kPartPipe = 3 };
 constexpr size_t kMaxSlabBytes = 32ull << 30;
+
+// Geometry of the part pipeline for n records over H destinations: the
+// widest buckets (shift <= 6) whose expected load stays within the LDS sort's
+// capacity with room for the spread of a uniform load; false when the
+// buckets would be too many for the scatter's LDS histogram.
+bool part_geometry(uint32_t host_lo, uint32_t H, size_t n, unsigned long long tbase, PartGeo* g) {
+    if (!H) return false;
+    uint32_t shift = 6;
+    while (shift > 0 && (double)n * (double)(1u << shift) / (double)H > 6144.0) shift--;
+    const uint32_t nb = (uint32_t)(((size_t)H + (1u << shift) - 1) >> shift);
+    if (nb > kPartMaxBuckets || (uint64_t)H > (0xFFFFFFFFull >> shift) + 1ull) return false;
+    g->host_lo = host_lo;
+    g->H = H;
+    g->shift = shift;
+    g->nb = nb;
+    g->cap = (uint32_t)((double)n * (double)(1u << shift) / (double)H * 1.25) + 256u;
+    g->tbase = tbase;
+    return true;
+}
+
 int pipeline_for(uint32_t H, bool slab_ok) {
     const char* v = getenv("SHD_PACKET_PIPELINE");
     if (v && strcmp(v, "bucket") == 0) return kBucketPipe;
     if (v && strcmp(v, "rank") == 0) return kRankPipe;
+    if (v && strcmp(v, "part") == 0) return kPartPipe;
     if (!slab_ok || (size_t)H * kSlab * sizeof(ShdDeliv) > kMaxSlabBytes) return kRankPipe;
     return kSlabPipe;
 }
@@ -2443,6 +2852,7 @@ extern "C" void shd_dev_ws_free(void* p) {
     (void)hipFree(w->nbig);
     (void)hipFree(w->slab);
     (void)hipFree(w->cslab);
+    (void)hipFree(w->pstage);
     (void)hipFree(w->meta);
     if (w->fault) (void)hipHostFree(w->fault);
     (void)hipFree(w->xdev);
@@ -2514,6 +2924,54 @@ extern "C" int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes,
     return 0;
 }
 
+// The part pipeline's round (see k_part_scatter): reset, partitioned
+// scatter, per-bucket LDS sort, listed segments.  Stage timing: 0 scatter, 1
+// (no scan), 2 (no placement), 3 the bucket sort and the listed segments.
+int part_attr() {
+    static bool done = false;
+    if (done) return 0;
+    const size_t lds = (size_t)kPartCH * 20 + 12u * kPartMaxBuckets + 4;
+    int rc = hip_status(hipFuncSetAttribute((const void*)k_part_scatter<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)lds),
+                        "hipFuncSetAttribute k_part_scatter");
+    done = rc == 0;
+    return rc;
+}
+
+int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
+               uint64_t bootstrap_end, const PartGeo& g, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,
+               uint64_t* d_counters, hipStream_t s) {
+    int rc;
+    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 2 * (size_t)g.nb, g.H)) ||
+        (rc = pstage_reserve(w, (size_t)g.nb * g.cap)))
+        return rc;
+    unsigned long long* counters = (unsigned long long*)d_counters;
+    uint32_t* gcnt = w.cnt1;
+    uint32_t* wcnt = w.cnt1 + g.nb;
+    if ((rc = dbg_ranges(w, d_status, n, d_out, d_dst_offsets, g.H))) return rc;
+    hipLaunchKernelGGL(k_round_init, dim3(grid_for(2 * g.nb, 256, 4096)), dim3(256), 0, s, w.nbig, counters, w.cnt1,
+                       2 * g.nb);
+    mark(0, s);
+    if (n) {
+        const size_t lds = (size_t)kPartCH * 20 + 12u * g.nb + 4;
+        hipLaunchKernelGGL(k_part_scatter<4>, dim3((unsigned)((n + kPartCH - 1) / kPartCH)), dim3(kPartBlock), lds, s,
+                           *c, d_recs, n, barrier, end_time, bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters,
+                           w.st2, w.nbig + 1);
+    }
+    mark(1, s);
+    mark(2, s);
+    if ((rc = hip_status(hipGetLastError(), "k_part_scatter launch")) || (rc = dbg_sync(s, "k_part_scatter"))) return rc;
+    mark(3, s);
+    hipLaunchKernelGGL(k_part_sort, dim3(g.nb), dim3(kPartBlock), 0, s, g, w.pstage, gcnt, wcnt, w.st2, w.nbig + 1,
+                       (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, lds_keys());
+    if ((rc = hip_status(hipGetLastError(), "k_part_sort launch")) || (rc = dbg_sync(s, "k_part_sort"))) return rc;
+    if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s, counters)) || (rc = dbg_sync(s, "listed segments")))
+        return rc;
+    mark(4, s);
+    if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
+    return ws_end(w, s);
+}
+
 extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                                     uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out,
                                     uint32_t* d_dst_offsets, uint8_t* d_status, uint64_t* d_counters, void* stream) {
@@ -2521,7 +2979,18 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
     Ws& w = *static_cast<Ws*>(c->ws);
     const uint32_t H = c->nhosts;
-    const int pipe = pipeline_for(H, true);
+    int pipe = pipeline_for(H, true);
+    if (pipe == kPartPipe) {
+        PartGeo g;
+        if (part_geometry(0, H, n, barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull, &g)) {
+            int rc = part_round(w, c, d_recs, n, barrier, end_time, bootstrap_end, g, d_out, d_dst_offsets, d_status,
+                                d_counters, s);
+            if (rc || stream) return rc;
+            if ((rc = hip_status(hipStreamSynchronize(s), "packet round"))) return rc;
+            return ws_faults(w, true, s);
+        }
+        pipe = kSlabPipe; // (buckets too many for the scatter's histogram: the slab form)
+    }
     const bool rk = pipe != kBucketPipe;
     Bucketing bk;
     int rc = make_bucketing(0, H, n, &bk);
@@ -2600,6 +3069,17 @@ else if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
     if (stream) return 0;
     if ((rc = hip_status(hipStreamSynchronize(s), "packet round"))) return rc;
     return ws_faults(w, true, s);
+}
+
+// Which grouping pipeline a round of n records over nhosts destinations runs
+// (0 bucket, 1 rank, 2 slab, 3 part), for tooling and benchmarks.
+extern "C" int shd_round_pipeline_of(uint32_t nhosts, size_t n, int* pipe) {
+    if (!pipe) return -EINVAL;
+    int p = pipeline_for(nhosts, true);
+    PartGeo g;
+    if (p == kPartPipe && !part_geometry(0, nhosts, n, 0, &g)) p = kSlabPipe;
+    *pipe = p;
+    return 0;
 }
 
 extern "C" int shd_round_timing_enable(int enable) {

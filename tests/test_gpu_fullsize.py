@@ -105,12 +105,13 @@ def test_c2_full_table_bit_exact(ns):
 
 
 @pytest.mark.timeout(500)
-def test_c3_uniform_unrestricted_round_bit_exact():
+def test_c3_uniform_unrestricted_round_bit_exact(monkeypatch):
     """configs[3] at full size with the bench's own distribution: 10M packets,
     senders and destinations uniform over all 100k hosts (segments of ~92
     events: the k_segsort_dst register sort), the oracle holding all 19,870
     rows released in slot order.  Statuses, delivery times, order, segment
-    offsets and the min delivered time must all be equal."""
+    offsets and the min delivered time must all be equal -- for the slab and
+    the part pipelines (SHD_PACKET_PIPELINE)."""
     import torch
     H, V = 100_000, 20_000
     gml = synth.sparse_graph_gml(V, 0x5EED0002)
@@ -131,14 +132,17 @@ def test_c3_uniform_unrestricted_round_bit_exact():
     orc.preload(sv, tab[:, :, 0], tab[:, :, 1])
     del tab
     pk = synth.packet_batch(10_000_000, H, 0x5EED0003, 100_000_000, 10_000_000, st)  # the bench's batch
-    out, offs, status, mt = device_round(top, pk, H)
     oout, ostatus, omt = orc.round(ips_o, pk, BARRIER, END)
-    assert np.array_equal(status, ostatus)
-    assert mt == omt
-    assert offs[-1] == len(out) == len(oout)
-    assert np.array_equal(np.diff(offs), np.bincount(oout["dst_host"], minlength=H))
-    assert np.array_equal(out, oout)
-    assert np.diff(offs).max() < 256  # uniform: every segment on the register-sort path
+    for pipe in ("slab", "part"):
+        monkeypatch.setenv("SHD_PACKET_PIPELINE", pipe)
+        out, offs, status, mt = device_round(top, pk, H)
+        assert np.array_equal(status, ostatus), pipe
+        assert mt == omt, pipe
+        assert offs[-1] == len(out) == len(oout), pipe
+        assert np.array_equal(np.diff(offs), np.bincount(oout["dst_host"], minlength=H)), pipe
+        assert np.array_equal(out, oout), pipe
+        assert np.diff(offs).max() < 256  # uniform: every segment on the register-sort path
+        del out
 
 
 @pytest.fixture(scope="module")

@@ -183,10 +183,11 @@ def test_unattached_address():
 
 
 @pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor", "slab_readlane", "slab_noagg", "rank_noagg",
-                        "slab_unfused", "slab_wide"])
+                        "slab_unfused", "slab_wide", "part", "part_readlane"])
 def pipeline(request, monkeypatch):
-    """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE, the slab
-    layout SHD_SLAB_LAYOUT, the segment sort's pass-1 key broadcast
+    """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE: bucket,
+    rank, slab, part -- the LDS-staged bucket partition + per-bucket LDS sort;
+    the slab layout SHD_SLAB_LAYOUT, the segment sort's pass-1 key broadcast
     SHD_SEGSORT_LDS, the wave-aggregated destination slots SHD_DEST_AGG and
     the folded overflow placement SHD_ROUND_FUSE and the compact 16-B slab
     records SHD_SLAB_COMPACT, read per launch)."""
