@@ -185,8 +185,10 @@ int shd_topology_build_rows_device(ShdTopology* top, int row_lo, int row_hi, voi
  * table itself is built by the Dijkstra kernels).  Bit-identical to the
  * table's latencies; graphs whose edge latencies are all whole ms and with at
  * most 16,384 vertices (-ENOTSUP otherwise).  Releases nothing (no lookup
- * side effects).  Synchronous. */
-int shd_topology_latency_table_fw(ShdTopology* top, void* d_lat);
+ * side effects).  Enqueued on stream (hipStream_t) without waiting, on the
+ * topology's persistent distance scratch (calls on other streams wait for its
+ * last use); stream NULL: synchronous. */
+int shd_topology_latency_table_fw(ShdTopology* top, void* d_lat, void* stream);
 int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
 /* Adopts a device table WITHOUT a host mirror (tables larger than host RAM
  * wants: A = 86k slots is 120 GB).  Nothing is released at adoption: as in

@@ -24,6 +24,7 @@
 
 #include <cerrno>
 #include <cstdint>
+#include <new>
 
 #include "shd_internal.h"
 
@@ -207,23 +208,67 @@ int hip_rc(hipError_t e, const char* what) {
 
 } // namespace
 
-extern "C" int shd_dev_fw_latency(const ShdGraphDev* gp, double* d_lat) {
+// Grow-only distance matrix of a caller (one per topology), and the event
+// that marks the end of its last use: a call on another stream waits for it.
+struct FwScratch {
+    int device = -1;
+    uint32_t* D = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool used = false;
+};
+
+extern "C" int shd_dev_fw_latency(const ShdGraphDev* gp, double* d_lat, void** scratch, void* stream) {
     const ShdGraphDev g = *gp;
     if (!g.sl) return shd_fail(-ENOTSUP, "min-plus latencies need whole-ms edge latencies");
     if (g.V > kMaxV) return shd_fail(-ENOTSUP, "min-plus latencies: %d vertices > %d", g.V, kMaxV);
+    if (!scratch) return shd_fail(-EINVAL, "min-plus scratch");
     const int Vp = (g.V + kT - 1) / kT * kT, nb = Vp / kT;
-    uint32_t* D = nullptr;
-    int rc = hip_rc(hipMalloc((void**)&D, (size_t)Vp * Vp * 4), "hipMalloc distances");
+    hipStream_t s = (hipStream_t)stream;
+    int dev = 0;
+    int rc = hip_rc(hipGetDevice(&dev), "hipGetDevice");
     if (rc) return rc;
-    hipLaunchKernelGGL(k_fw_init, dim3(1024), dim3(256), 0, nullptr, D, Vp);
-    hipLaunchKernelGGL(k_fw_edges, dim3(g.V < 4096 ? g.V : 4096), dim3(256), 0, nullptr, g, D, Vp);
-    for (int kb = 0; kb < nb; kb++) {
-        hipLaunchKernelGGL(k_fw_cross, dim3(nb > 1 ? 2 * (nb - 1) : 1), dim3(256), 0, nullptr, D, Vp, kb, nb);
-        if (nb > 1) hipLaunchKernelGGL(k_fw_prod, dim3(nb - 1, nb - 1), dim3(256), 0, nullptr, D, Vp, kb);
+    FwScratch* w = static_cast<FwScratch*>(*scratch);
+    if (!w) {
+        w = new (std::nothrow) FwScratch();
+        if (!w) return -ENOMEM;
+        *scratch = w;
     }
-    hipLaunchKernelGGL(k_fw_rows, dim3(g.A < 4096 ? g.A : 4096), dim3(256), 0, nullptr, g, D, Vp, d_lat);
-    rc = hip_rc(hipGetLastError(), "min-plus launch");
-    if (!rc) rc = hip_rc(hipDeviceSynchronize(), "min-plus");
-    (void)hipFree(D);
-    return rc;
+    if (w->device >= 0 && w->device != dev) return shd_fail(-EINVAL, "min-plus scratch of device %d used on %d", w->device, dev);
+    w->device = dev;
+    if (!w->done && (rc = hip_rc(hipEventCreateWithFlags(&w->done, hipEventDisableTiming), "hipEventCreate"))) return rc;
+    const size_t need = (size_t)Vp * Vp;
+    if (need > w->cap) {
+        if (w->used && (rc = hip_rc(hipEventSynchronize(w->done), "min-plus scratch quiesce"))) return rc;
+        (void)hipFree(w->D);
+        w->D = nullptr;
+        w->cap = 0;
+        if ((rc = hip_rc(hipMalloc((void**)&w->D, need * 4), "hipMalloc distances"))) return rc;
+        w->cap = need;
+    } else if (w->used && (rc = hip_rc(hipStreamWaitEvent(s, w->done, 0), "hipStreamWaitEvent"))) {
+        return rc;
+    }
+    uint32_t* D = w->D;
+    hipLaunchKernelGGL(k_fw_init, dim3(1024), dim3(256), 0, s, D, Vp);
+    hipLaunchKernelGGL(k_fw_edges, dim3(g.V < 4096 ? g.V : 4096), dim3(256), 0, s, g, D, Vp);
+    for (int kb = 0; kb < nb; kb++) {
+        hipLaunchKernelGGL(k_fw_cross, dim3(nb > 1 ? 2 * (nb - 1) : 1), dim3(256), 0, s, D, Vp, kb, nb);
+        if (nb > 1) hipLaunchKernelGGL(k_fw_prod, dim3(nb - 1, nb - 1), dim3(256), 0, s, D, Vp, kb);
+    }
+    hipLaunchKernelGGL(k_fw_rows, dim3(g.A < 4096 ? g.A : 4096), dim3(256), 0, s, g, D, Vp, d_lat);
+    if ((rc = hip_rc(hipGetLastError(), "min-plus launch"))) return rc;
+    w->used = true;
+    return hip_rc(hipEventRecord(w->done, s), "hipEventRecord");
+}
+
+extern "C" void shd_dev_fw_scratch_free(void* scratch) {
+    FwScratch* w = static_cast<FwScratch*>(scratch);
+    if (!w) return;
+    int cur = -1;
+    if (w->device >= 0 && hipGetDevice(&cur) == hipSuccess && cur != w->device) (void)hipSetDevice(w->device);
+    if (w->used) (void)hipEventSynchronize(w->done);
+    (void)hipFree(w->D);
+    if (w->done) (void)hipEventDestroy(w->done);
+    if (cur >= 0 && cur != w->device) (void)hipSetDevice(cur);
+    delete w;
 }

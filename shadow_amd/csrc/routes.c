@@ -284,13 +284,15 @@ int shd_topology_build_rows_device(ShdTopology* t, int row_lo, int row_hi, void*
     return rc;
 }
 
-int shd_topology_latency_table_fw(ShdTopology* t, void* d_lat) {
+int shd_topology_latency_table_fw(ShdTopology* t, void* d_lat, void* stream) {
     if (!t || !d_lat) return -EINVAL;
     pthread_mutex_lock(&t->setup_mu);
     int rc = prepare(t);
     ShdGraphDev g = graph_dev(t);
-    if (!rc) rc = shd_dev_fw_latency(&g, (double*)d_lat);
+    if (!rc) rc = shd_dev_init(t->device);
+    if (!rc) rc = shd_dev_fw_latency(&g, (double*)d_lat, &t->fw_scratch, stream);
     pthread_mutex_unlock(&t->setup_mu);
+    if (!rc && !stream) rc = shd_dev_stream_sync(NULL); /* (NULL stream: the call is synchronous) */
     return rc;
 }
 

@@ -107,8 +107,11 @@ void shd_dev_stream_free(void* s);
 int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab);
 /* The A x A latency half of the table (lat_ms doubles, row-major) by blocked
  * min-plus Floyd-Warshall (minplus.hip); whole-ms graphs only (-ENOTSUP
- * otherwise), V <= 16384.  Synchronous. */
-int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat);
+ * otherwise), V <= 16384.  Enqueued on stream (hipStream_t or NULL), no
+ * waiting; *scratch: the caller's grow-only distance matrix (NULL the first
+ * time), freed with shd_dev_fw_scratch_free. */
+int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat, void** scratch, void* stream);
+void shd_dev_fw_scratch_free(void* scratch);
 /* min latency over the entries (i, j), i < j, lat >= 0, of rows [row_lo,
  * row_hi) of an A-column table (rows: row i at rows + (i - row_lo) * A); -1 if none */
 int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out);

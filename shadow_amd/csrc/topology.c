@@ -491,6 +491,7 @@ void shd_topology_free(ShdTopology* t) {
     if (!t) return;
     shd_topology_release_device(t);
     shd_dev_ws_free(t->ws);
+    shd_dev_fw_scratch_free(t->fw_scratch);
     for (int w = 0; w < t->nworkers; w++) free(t->wbuf[w].recs);
     free(t->wbuf);
     pthread_mutex_destroy(&t->setup_mu);

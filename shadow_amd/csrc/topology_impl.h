@@ -169,6 +169,7 @@ struct ShdTopology {
 
     /* device workspace of the round pipeline (packet.hip) */
     void* ws;
+    void* fw_scratch; /* min-plus Floyd-Warshall distances (minplus.hip) */
 
     /* synchronisation (see the header comment) */
     int ready; /* table built and adopted: lookups may proceed (atomic) */

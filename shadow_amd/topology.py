@@ -120,10 +120,11 @@ class Topology:
     def build_rows_device(self, row_lo: int, row_hi: int, d_table_ptr: int):
         check(lib().shd_topology_build_rows_device(self._h, row_lo, row_hi, C.c_void_p(d_table_ptr)))
 
-    def latency_table_fw(self, d_lat_ptr: int):
+    def latency_table_fw(self, d_lat_ptr: int, stream: int = 0):
         """The A x A latency column by blocked min-plus Floyd-Warshall into
-        device memory (A*A doubles); whole-ms graphs only."""
-        check(lib().shd_topology_latency_table_fw(self._h, C.c_void_p(d_lat_ptr)))
+        device memory (A*A doubles); whole-ms graphs only.  stream 0:
+        synchronous; else enqueued on that hipStream_t."""
+        check(lib().shd_topology_latency_table_fw(self._h, C.c_void_p(d_lat_ptr), C.c_void_p(stream)))
 
     def adopt_table_device(self, d_table_ptr: int):
         check(lib().shd_topology_adopt_table_device(self._h, C.c_void_p(d_table_ptr)))

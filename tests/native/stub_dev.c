@@ -63,11 +63,14 @@ void stub_entry(int i, int j, double* lat, double* rel) {
     *rel = 0.5 + (double)((i * 29 + j * 53) % 41) / 100.0;
 }
 
-int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat) {
+int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat, void** scratch, void* stream) {
     (void)g;
     (void)d_lat;
+    (void)scratch;
+    (void)stream;
     return -ENOTSUP;
 }
+void shd_dev_fw_scratch_free(void* scratch) { (void)scratch; }
 
 int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab) {
     (void)use_sp;
