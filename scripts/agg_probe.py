@@ -63,7 +63,9 @@ def main():
             nl = C.c_int()
             _lib.check(lib.shd_round_timing_read(st, 4, C.byref(nl)))
             _lib.check(lib.shd_round_timing_enable(0))
-            print(f"{name}={agg} rep {rep}: round {dt:.4f} ms, scatter {st[0] / max(nl.value, 1):.4f} ms", flush=True)
+            k = max(nl.value, 1)
+            print(f"{name}={agg} rep {rep}: round {dt:.4f} ms, scatter {st[0] / k:.4f} ms, scan {st[1] / k:.4f}, "
+                  f"place {st[2] / k:.4f}, sort {st[3] / k:.4f} ms", flush=True)
             outs[agg] = (d_out.clone(), d_off.clone(), d_status.clone())
     same = all(all(torch.equal(a, b) for a, b in zip(outs[vals[0]], outs[v])) for v in vals[1:])
     print(f"outputs identical: {same}", flush=True)

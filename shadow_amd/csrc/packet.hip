@@ -1920,7 +1920,7 @@ __global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__
 // event beyond the table gather: the destination counter's atomic and a 16-B
 // partial-line store into a 147 MB slab (profiles/r04a_ubench_part.log: the
 // gather floor 0.318 ms, with the slab form 0.573 ms).  Here:
-//   k_part_scatter  a workgroup decides kPartCH records (the scatter's decision,
+//   k_part_scatter  a workgroup decides 4,096 records (the scatter's decision,
 //                   unchanged), stages its delivered events in LDS (16 B
 //                   each), counts them per destination BUCKET of 2^shift hosts,
 //                   reserves one run per nonempty bucket with one atomic on
@@ -1943,7 +1943,6 @@ __global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__
 // destination ranges of the staging array and every segment is listed for
 // k_segsort_mid / k_segsort_merge (skewed destinations).
 constexpr int kPartBlock = 1024;   // k_part_scatter / k_part_sort workgroup
-constexpr int kPartCH = 4096;      // records per k_part_scatter workgroup (4 per thread)
 constexpr int kPartLdsEv = 7168;   // events k_part_sort holds in LDS (7 per thread)
 constexpr uint32_t kPartMaxDst = 64; // destinations per bucket (shift <= 6)
 constexpr uint32_t kPartMaxBuckets = 4096;
@@ -1970,39 +1969,49 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* tota
     return base + inc - v;
 }
 
-template <int kB = 4>
-__global__ __launch_bounds__(kPartBlock) void k_part_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
-                                                             uint64_t barrier, uint64_t end_time, uint64_t boot_end,
-                                                             PartGeo g, uint4* __restrict__ stage,
-                                                             uint32_t* __restrict__ gcnt, uint32_t* __restrict__ wcnt,
-                                                             uint8_t* __restrict__ status,
-                                                             unsigned long long* counters, ShdDeliv* __restrict__ wide,
-                                                             uint32_t* __restrict__ nwide) {
+// kWG threads decide kCH records (kCH / kWG per thread, in batches of 4).
+// kLds: the delivered events are staged in LDS and written in bucket order
+// (consecutive lanes, consecutive records of a run); else each thread keeps
+// its events in registers and stores them at their run positions itself (LDS
+// holds only the bucket counts: more workgroups per CU).
+template <int kWG, int kCH, bool kLds>
+__global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
+                                                      uint64_t barrier, uint64_t end_time, uint64_t boot_end,
+                                                      PartGeo g, uint4* __restrict__ stage,
+                                                      uint32_t* __restrict__ gcnt, uint32_t* __restrict__ wcnt,
+                                                      uint8_t* __restrict__ status, unsigned long long* counters,
+                                                      ShdDeliv* __restrict__ wide, uint32_t* __restrict__ nwide) {
+    constexpr int kB = 4;
+    constexpr int kR = kCH / kWG; // records per thread
+    static_assert(kCH % (kWG * kB) == 0, "chunk");
     extern __shared__ uint4 part_smem[];
-    uint4* ev = part_smem;                                       // kPartCH staged events (w = ~0: none)
-    uint16_t* rk = reinterpret_cast<uint16_t*>(ev + kPartCH);    // rank inside its bucket
-    uint16_t* perm = rk + kPartCH;                               // bucket order -> staged slot
-    uint32_t* hist = reinterpret_cast<uint32_t*>(perm + kPartCH); // nb
-    uint32_t* lofs = hist + g.nb;                                // nb + 1 (scan per thread run)
-    uint32_t* gb = lofs + g.nb + 1;                              // nb
-    __shared__ uint32_t wsum[kPartBlock / 64];
-    __shared__ unsigned long long wmin[kPartBlock / 64];
+    // kLds: ev[kCH] | rk[kCH] u16 | perm[kCH] u16 | hist[nb] | lofs[nb + 1] | gb[nb]; else hist[nb] | gb[nb]
+    uint4* ev = part_smem;
+    uint16_t* rk = reinterpret_cast<uint16_t*>(ev + (kLds ? kCH : 0));
+    uint16_t* perm = rk + (kLds ? kCH : 0);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(perm + (kLds ? kCH : 0));
+    uint32_t* lofs = hist + g.nb;
+    uint32_t* gb = kLds ? lofs + g.nb + 1 : hist + g.nb;
+    __shared__ uint32_t wsum[kWG / 64];
+    __shared__ unsigned long long wmin[kWG / 64];
     const int lane = threadIdx.x & 63;
-    for (uint32_t b = threadIdx.x; b < g.nb; b += kPartBlock) hist[b] = 0;
+    for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) hist[b] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * kPartCH;
+    const size_t base = (size_t)blockIdx.x * kCH;
     const size_t A = (size_t)c.A;
     const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
     const uint2* __restrict__ ptab = reinterpret_cast<const uint2*>(c.ptab);
     const uint32_t smax = g.shift ? (0xFFFFFFFFu >> g.shift) : 0xFFFFFFFFu; // src hosts that fit the record
+    const uint32_t mask = (1u << g.shift) - 1u;
     unsigned long long mn = ~0ull;
-    static_assert(kPartCH % (kPartBlock * kB) == 0, "chunk");
-    for (int k0 = 0; k0 < kPartCH / kPartBlock; k0 += kB) {
+    uint4 rv[kLds ? 1 : kR]; // register staging: {record fields..., dst}, w = ~0: none
+    uint32_t rr[kLds ? 1 : kR];
+    for (int k0 = 0; k0 < kR; k0 += kB) {
         ShdPkt p[kB];
         bool live[kB];
 #pragma unroll
         for (int k = 0; k < kB; k++) {
-            const size_t i = base + (size_t)(k0 + k) * kPartBlock + threadIdx.x;
+            const size_t i = base + (size_t)(k0 + k) * kWG + threadIdx.x;
             live[k] = i < n;
             if (live[k]) p[k] = ld_pkt(&recs[i]);
         }
@@ -2052,7 +2061,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ShdPktCtx c, const 
             if (si[k] >= 0 && di[k] >= 0 && q[k].x == kPtabFallback) e[k] = c.tab[ei[k]];
 #pragma unroll
         for (int k = 0; k < kB; k++) {
-            const uint32_t li = (uint32_t)((k0 + k) * kPartBlock + threadIdx.x);
+            const uint32_t li = (uint32_t)((k0 + k) * kWG + threadIdx.x);
             uint8_t st = 0xff; // unregistered host: not delivered
             uint64_t t = 0;
             if (live[k] && si[k] >= 0 && di[k] >= 0) {
@@ -2081,11 +2090,18 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ShdPktCtx c, const 
             const uint32_t dr = p[k].dst_host - g.host_lo;
             const bool fits = dl && c_fits(t, g.tbase, p[k].seq) && p[k].src_host <= smax && dr < g.H;
             uint4 sv = make_uint4(0u, 0u, 0u, ~0u);
+            uint32_t rank = 0;
             if (fits) {
-                rk[li] = (uint16_t)atomicAdd(&hist[dr >> g.shift], 1u); // LDS
+                rank = atomicAdd(&hist[dr >> g.shift], 1u); // LDS
                 sv = make_uint4((uint32_t)(t - g.tbase), (uint32_t)p[k].seq, p[k].src_host, p[k].dst_host);
             }
-            ev[li] = sv;
+            if (kLds) {
+                ev[li] = sv;
+                if (fits) rk[li] = (uint16_t)rank;
+            } else {
+                rv[kLds ? 0 : k0 + k] = sv;
+                rr[kLds ? 0 : k0 + k] = rank;
+            }
             const uint32_t ws = wave_alloc(dl && !fits, nwide, lane); // (every lane: ballot)
             if (dl && !fits) {
                 st_ev(&wide[ws], ShdDeliv{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)(base + li) + c.idx_base,
@@ -2097,13 +2113,13 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ShdPktCtx c, const 
         }
     }
     __syncthreads();
-    // bucket order inside the workgroup, and one run per nonempty bucket
-    {
-        const uint32_t per = (g.nb + kPartBlock - 1) / kPartBlock, b0 = threadIdx.x * per;
-        uint32_t s = 0;
-        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) s += hist[b0 + k];
+    // one run per nonempty bucket (and, with LDS staging, bucket order inside the workgroup)
+    if (kLds) {
+        const uint32_t per = (g.nb + kWG - 1) / kWG, b0 = threadIdx.x * per;
+        uint32_t sum = 0;
+        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) sum += hist[b0 + k];
         uint32_t tot;
-        uint32_t pre = block_excl_scan_n(s, &tot, wsum);
+        uint32_t pre = block_excl_scan_n(sum, &tot, wsum);
         for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) {
             const uint32_t h = hist[b0 + k];
             lofs[b0 + k] = pre;
@@ -2111,38 +2127,54 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ShdPktCtx c, const 
             pre += h;
         }
         if (threadIdx.x == 0) lofs[g.nb] = tot;
+    } else {
+        for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) {
+            const uint32_t h = hist[b];
+            gb[b] = h ? atomicAdd(&gcnt[b], h) : 0u;
+        }
     }
     __syncthreads();
-    for (uint32_t li = threadIdx.x; li < (uint32_t)kPartCH; li += kPartBlock) {
-        const uint32_t w = ev[li].w;
-        if (w != ~0u) perm[lofs[(w - g.host_lo) >> g.shift] + rk[li]] = (uint16_t)li;
-    }
-    __syncthreads();
-    const uint32_t total = lofs[g.nb];
-    const uint32_t mask = (1u << g.shift) - 1u;
-    for (uint32_t p0 = 0; p0 < total; p0 += kPartBlock) { // (uniform trip count: every lane takes the ballot)
-        const uint32_t pp = p0 + threadIdx.x;
-        uint4 e = make_uint4(0u, 0u, 0u, 0u);
-        uint32_t b = 0, li = 0;
-        size_t j = 0;
-        bool in = false;
-        if (pp < total) {
-            li = perm[pp];
-            e = ev[li];
-            b = (e.w - g.host_lo) >> g.shift;
-            j = (size_t)gb[b] + (pp - lofs[b]);
-            in = j < g.cap;
-        }
-        if (in) { // runs of a bucket: consecutive lanes, consecutive records
-            const uint4 r = make_uint4(e.x, e.y, (uint32_t)(base + li) + c.idx_base, (e.z << g.shift) | ((e.w - g.host_lo) & mask));
-            stage[(size_t)b * g.cap + j] = r;
-        }
-        const bool full = pp < total && !in; // the bucket's region is full: whole event to the wide list
+    auto put = [&](bool valid, const uint4& e, uint32_t li, size_t j) { // (every lane: ballot inside)
+        const uint32_t b = valid ? (e.w - g.host_lo) >> g.shift : 0u;
+        const bool in = valid && j < g.cap;
+        if (in) // runs of a bucket, consecutive records
+            stage[(size_t)b * g.cap + j] =
+                make_uint4(e.x, e.y, (uint32_t)(base + li) + c.idx_base, (e.z << g.shift) | ((e.w - g.host_lo) & mask));
+        const bool full = valid && !in; // the bucket's region is full: whole event to the wide list
         const uint32_t ws = wave_alloc(full, nwide, lane);
         if (full) {
             st_ev(&wide[ws], ShdDeliv{g.tbase + e.x, (unsigned long long)e.y, e.z, e.w,
                                       (uint32_t)(base + li) + c.idx_base, 0u});
             atomicAdd(&wcnt[b], 1u);
+        }
+    };
+    if (kLds) {
+        for (uint32_t li = threadIdx.x; li < (uint32_t)kCH; li += kWG) {
+            const uint32_t w = ev[li].w;
+            if (w != ~0u) perm[lofs[(w - g.host_lo) >> g.shift] + rk[li]] = (uint16_t)li;
+        }
+        __syncthreads();
+        const uint32_t total = lofs[g.nb];
+        for (uint32_t p0 = 0; p0 < total; p0 += kWG) { // (uniform trip count)
+            const uint32_t pp = p0 + threadIdx.x;
+            const bool valid = pp < total;
+            uint4 e = make_uint4(0u, 0u, 0u, 0u);
+            uint32_t li = 0;
+            size_t j = 0;
+            if (valid) {
+                li = perm[pp];
+                e = ev[li];
+                const uint32_t b = (e.w - g.host_lo) >> g.shift;
+                j = (size_t)gb[b] + (pp - lofs[b]);
+            }
+            put(valid, e, li, j);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < (kLds ? 1 : kR); k++) {
+            const bool valid = rv[k].w != ~0u;
+            const size_t j = valid ? (size_t)gb[(rv[k].w - g.host_lo) >> g.shift] + rr[k] : 0;
+            put(valid, rv[k], (uint32_t)(k * kWG + threadIdx.x), j);
         }
     }
     mn = wave_min_u64(mn);
@@ -2150,7 +2182,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_scatter(ShdPktCtx c, const 
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long m = wmin[0];
-        for (int k = 1; k < kPartBlock / 64; k++) m = wmin[k] < m ? wmin[k] : m;
+        for (int k = 1; k < kWG / 64; k++) m = wmin[k] < m ? wmin[k] : m;
         if (m != ~0ull) atomicMin(&counters[1], m);
     }
 }
@@ -2927,15 +2959,39 @@ extern "C" int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes,
 // The part pipeline's round (see k_part_scatter): reset, partitioned
 // scatter, per-bucket LDS sort, listed segments.  Stage timing: 0 scatter, 1
 // (no scan), 2 (no placement), 3 the bucket sort and the listed segments.
+// k_part_scatter instances (SHD_PART_SCATTER, measurement knob): 0 LDS
+// staging, 1024 threads x 4096 records (default); 1 registers, 1024 x 4096;
+// 2 registers, 512 x 2048; 3 registers, 256 x 2048 (8 per thread)
+struct PartCfg {
+    const void* fn;
+    int wg, ch;
+    bool lds;
+};
+PartCfg part_cfg() {
+    const char* v = getenv("SHD_PART_SCATTER");
+    const int k = v ? atoi(v) : 0;
+    if (k == 1) return {(const void*)k_part_scatter<1024, 4096, false>, 1024, 4096, false};
+    if (k == 2) return {(const void*)k_part_scatter<512, 2048, false>, 512, 2048, false};
+    if (k == 3) return {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false};
+    return {(const void*)k_part_scatter<1024, 4096, true>, 1024, 4096, true};
+}
+size_t part_lds(const PartCfg& f, uint32_t nb) {
+    return f.lds ? (size_t)f.ch * 20 + 12u * nb + 4 : 8u * nb;
+}
 int part_attr() {
     static bool done = false;
     if (done) return 0;
-    const size_t lds = (size_t)kPartCH * 20 + 12u * kPartMaxBuckets + 4;
-    int rc = hip_status(hipFuncSetAttribute((const void*)k_part_scatter<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)lds),
-                        "hipFuncSetAttribute k_part_scatter");
-    done = rc == 0;
-    return rc;
+    const PartCfg cfgs[] = {{(const void*)k_part_scatter<1024, 4096, true>, 1024, 4096, true},
+                            {(const void*)k_part_scatter<1024, 4096, false>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<512, 2048, false>, 512, 2048, false},
+                            {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false}};
+    for (const PartCfg& f : cfgs)
+        if (int rc = hip_status(hipFuncSetAttribute(f.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)part_lds(f, kPartMaxBuckets)),
+                                "hipFuncSetAttribute k_part_scatter"))
+            return rc;
+    done = true;
+    return 0;
 }
 
 int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
@@ -2953,10 +3009,17 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
                        2 * g.nb);
     mark(0, s);
     if (n) {
-        const size_t lds = (size_t)kPartCH * 20 + 12u * g.nb + 4;
-        hipLaunchKernelGGL(k_part_scatter<4>, dim3((unsigned)((n + kPartCH - 1) / kPartCH)), dim3(kPartBlock), lds, s,
-                           *c, d_recs, n, barrier, end_time, bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters,
-                           w.st2, w.nbig + 1);
+        const PartCfg f = part_cfg();
+        const dim3 grid((unsigned)((n + f.ch - 1) / f.ch)), blk(f.wg);
+        const size_t lds = part_lds(f, g.nb);
+#define SHD_PART_LAUNCH(WG, CH, L)                                                                                  \
+    hipLaunchKernelGGL((k_part_scatter<WG, CH, L>), grid, blk, lds, s, *c, d_recs, n, barrier, end_time,           \
+                       bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters, w.st2, w.nbig + 1)
+        if (f.lds) SHD_PART_LAUNCH(1024, 4096, true);
+        else if (f.wg == 1024) SHD_PART_LAUNCH(1024, 4096, false);
+        else if (f.wg == 512) SHD_PART_LAUNCH(512, 2048, false);
+        else SHD_PART_LAUNCH(256, 2048, false);
+#undef SHD_PART_LAUNCH
     }
     mark(1, s);
     mark(2, s);
