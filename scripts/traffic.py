@@ -2,8 +2,11 @@
 """Folds rocprofv3 PMC passes into per-launch HBM traffic (bytes) per bench
 stage, as MI355X_MICROARCH.md §HBM prescribes for gfx950: FETCH_SIZE counts
 64 B per TCC_EA0_RDREQ while the requests are 128-B lines (x2 correction,
-cross-checked against TCC_EA0_RDREQ_sum in the third pass); WRITE_SIZE is
-taken as is (it equals 64 B x WRREQ_64B + 32 B x the other write requests).
+cross-checked against TCC_EA0_RDREQ_sum in the third pass; calibrated for
+random 8..128-B gathers too -- one 128-B request each --
+profiles/r04b_fetch_calibration.json); WRITE_SIZE is taken as is (it equals
+64 B x WRREQ_64B + 32 B x the other write requests; a random 16-B store and a
+device-scope atomic are one 32-B write request each).
 Usage: scripts/traffic.py OUT.json [--suffix S] [--source TEXT] PASS_CSV...
 (--suffix appends S to the routing keys and merges into an existing OUT.json,
 e.g. routing_slab_c4 from a C4 build's passes)"""
@@ -12,7 +15,7 @@ import json
 import re
 import sys
 
-STAGE = {"k_pkt_scatter": "packet_scatter", "k_place_rank": "place", "k_place_bucket": "place",
+STAGE = {"k_pkt_scatter": "packet_scatter", "k_part_scatter": "packet_scatter", "k_part_sort": "segment_sort", "k_place_rank": "place", "k_place_bucket": "place",
          "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_slab<256>": "routing_slab",
          "k_sssp_islab<false>": "routing_islab", "k_sssp_ilds": "routing_ilds",
          "k_sssp_lds<true>": "routing_lds", "k_scan_one": "scan"}

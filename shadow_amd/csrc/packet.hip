@@ -1942,10 +1942,9 @@ __global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__
 // LDS, takes the listed path: its events are placed unsorted at their
 // destination ranges of the staging array and every segment is listed for
 // k_segsort_mid / k_segsort_merge (skewed destinations).
-constexpr int kPartBlock = 1024;   // k_part_scatter / k_part_sort workgroup
-constexpr int kPartLdsEv = 7168;   // events k_part_sort holds in LDS (7 per thread)
 constexpr uint32_t kPartMaxDst = 64; // destinations per bucket (shift <= 6)
-constexpr uint32_t kPartMaxBuckets = 4096;
+constexpr uint32_t kPartMaxBuckets = 8192;  // register-staged scatter: 8 B of LDS per bucket
+constexpr uint32_t kPartMaxBucketsLds = 4096; // LDS-staged scatter: + 20 B per record
 
 struct PartGeo {
     uint32_t host_lo, H; // destination host range
@@ -2187,9 +2186,11 @@ __global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt*
     }
 }
 
-// One workgroup per bucket (see above).  nbig / big / scr: the listed
-// segments (k_segsort_mid); fault: nbig[2] guard bits.
-__global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
+// One workgroup of kWG threads per bucket of at most kCap events held in
+// LDS (7 per thread; see above).  nbig / big / scr: the listed segments
+// (k_segsort_mid); fault: nbig[2] guard bits.
+template <int kWG, int kCap>
+__global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
                                                           const uint32_t* __restrict__ wcnt,
                                                           const ShdDeliv* __restrict__ wide,
@@ -2198,9 +2199,9 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
                                                           ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
-    __shared__ uint4 lev[kPartLdsEv];
-    __shared__ unsigned long long keys[kPartBlock / 64][64 * 4 + 8];
-    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kPartBlock / 64];
+    __shared__ uint4 lev[kCap];
+    __shared__ unsigned long long keys[kWG / 64][64 * 4 + 8];
+    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kWG / 64];
     __shared__ uint32_t s_base;
     const uint32_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2208,24 +2209,24 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
     const uint32_t nd = min(1u << g.shift, g.H - d0);
     const uint32_t mask = (1u << g.shift) - 1u;
     const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
-    const bool listed = tot > (uint32_t)kPartLdsEv || nw > 0; // (block-uniform)
+    const bool listed = tot > (uint32_t)kCap || nw > 0; // (block-uniform)
     // this bucket's output base: the totals of the buckets before it
     {
         uint32_t s = 0;
-        for (uint32_t k = threadIdx.x; k < b; k += kPartBlock) s += min(gcnt[k], g.cap) + wcnt[k];
+        for (uint32_t k = threadIdx.x; k < b; k += kWG) s += min(gcnt[k], g.cap) + wcnt[k];
         uint32_t t;
         (void)block_excl_scan_n(s, &t, wsum);
         if (threadIdx.x == 0) s_base = t;
     }
-    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kPartBlock) cnt[j] = cur[j] = 0;
+    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
     __syncthreads();
     const uint32_t obase = s_base;
     const uint4* sb = stage + (size_t)b * g.cap;
-    uint4 e[kPartLdsEv / kPartBlock];
+    uint4 e[kCap / kWG];
     if (!listed) {
 #pragma unroll
-        for (int k = 0; k < kPartLdsEv / kPartBlock; k++) {
-            const uint32_t i = (uint32_t)k * kPartBlock + threadIdx.x;
+        for (int k = 0; k < kCap / kWG; k++) {
+            const uint32_t i = (uint32_t)k * kWG + threadIdx.x;
             if (i < ns) {
                 const shd_v4u v = __builtin_nontemporal_load(reinterpret_cast<const shd_v4u*>(sb) + i);
                 e[k] = make_uint4(v.x, v.y, v.z, v.w);
@@ -2233,12 +2234,12 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
             }
         }
     } else {
-        for (uint32_t i = threadIdx.x; i < ns; i += kPartBlock) atomicAdd(&cnt[sb[i].w & mask], 1u);
+        for (uint32_t i = threadIdx.x; i < ns; i += kWG) atomicAdd(&cnt[sb[i].w & mask], 1u);
         const uint32_t m = *nwide;
         if (m > wide_cap) {
             if (threadIdx.x == 0) atomicOr(nbig + 2, kFaultOvfCap);
         } else if (nw) {
-            for (uint32_t i = threadIdx.x; i < m; i += kPartBlock) {
+            for (uint32_t i = threadIdx.x; i < m; i += kWG) {
                 const uint32_t dr = wide[i].dst_host - g.host_lo;
                 if (dr < g.H && (dr >> g.shift) == b) atomicAdd(&cnt[dr & mask], 1u);
             }
@@ -2261,8 +2262,8 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
     __syncthreads();
     if (!listed) {
 #pragma unroll
-        for (int k = 0; k < kPartLdsEv / kPartBlock; k++) {
-            const uint32_t i = (uint32_t)k * kPartBlock + threadIdx.x;
+        for (int k = 0; k < kCap / kWG; k++) {
+            const uint32_t i = (uint32_t)k * kWG + threadIdx.x;
             if (i < ns) {
                 const uint32_t dl = e[k].w & mask;
                 lev[loc[dl] + atomicAdd(&cur[dl], 1u)] = e[k];
@@ -2270,7 +2271,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
         }
         __syncthreads();
         unsigned long long* lk = lds_keys ? keys[wv] : nullptr;
-        for (uint32_t j = wv; j < nd; j += kPartBlock / 64) {
+        for (uint32_t j = wv; j < nd; j += kWG / 64) {
             const uint32_t nj = cnt[j], o = loc[j], dh = g.host_lo + d0 + j;
             if (nj == 0) continue;
             auto load = [&](uint32_t i) {
@@ -2296,7 +2297,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
     }
     // listed bucket: every event unsorted to its destination's range of the
     // staging array, every nonempty segment listed (k_segsort_mid / _merge)
-    for (uint32_t i = threadIdx.x; i < ns; i += kPartBlock) {
+    for (uint32_t i = threadIdx.x; i < ns; i += kWG) {
         const uint4 r = sb[i];
         const uint32_t dl = r.w & mask;
         st_ev(&scr[obase + loc[dl] + atomicAdd(&cur[dl], 1u)],
@@ -2304,7 +2305,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
     }
     const uint32_t m = *nwide;
     if (nw && m <= wide_cap)
-        for (uint32_t i = threadIdx.x; i < m; i += kPartBlock) {
+        for (uint32_t i = threadIdx.x; i < m; i += kWG) {
             ShdDeliv r = ld_ev(&wide[i]);
             const uint32_t dr = r.dst_host - g.host_lo;
             if (dr < g.H && (dr >> g.shift) == b) {
@@ -2313,7 +2314,7 @@ __global__ __launch_bounds__(kPartBlock) void k_part_sort(PartGeo g, const uint4
             }
         }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < nd; j += kPartBlock)
+    for (uint32_t j = threadIdx.x; j < nd; j += kWG)
         if (cnt[j] > 0) {
             const uint32_t k = atomicAdd(nbig, 1u);
             if (k < g.H) big[k] = d0 + j;
@@ -2802,14 +2803,25 @@ int group_and_sort_rank(Ws& w, const ShdDeliv* in, const uint8_t* status, const 
 enum Pipeline { kBucketPipe = 0, kRankPipe = 1, kSlabPipe = 2, kPartPipe = 3 };
 constexpr size_t kMaxSlabBytes = 32ull << 30;
 
+// k_part_sort instances (SHD_PART_SORT, measurement knob): 0: 1024 threads,
+// 7,168 events in LDS (one workgroup per CU); 1: 512 threads, 3,584 (two);
+// 2: 256 threads, 1,792 (four).  The buckets are sized for the instance.
+int part_sort_cfg() {
+    const char* v = getenv("SHD_PART_SORT");
+    const int k = v ? atoi(v) : 0;
+    return k >= 0 && k <= 2 ? k : 0;
+}
+constexpr int kPartSortCap[3] = {7168, 3584, 1792};
+
 // Geometry of the part pipeline for n records over H destinations: the
 // widest buckets (shift <= 6) whose expected load stays within the LDS sort's
-// capacity with room for the spread of a uniform load; false when the
-// buckets would be too many for the scatter's LDS histogram.
+// capacity with room for the spread of a uniform load (6/7 of it); false
+// when the buckets would be too many for the scatter's LDS histogram.
 bool part_geometry(uint32_t host_lo, uint32_t H, size_t n, unsigned long long tbase, PartGeo* g) {
     if (!H) return false;
+    const double target = kPartSortCap[part_sort_cfg()] * 6.0 / 7.0;
     uint32_t shift = 6;
-    while (shift > 0 && (double)n * (double)(1u << shift) / (double)H > 6144.0) shift--;
+    while (shift > 0 && (double)n * (double)(1u << shift) / (double)H > target) shift--;
     const uint32_t nb = (uint32_t)(((size_t)H + (1u << shift) - 1) >> shift);
     if (nb > kPartMaxBuckets || (uint64_t)H > (0xFFFFFFFFull >> shift) + 1ull) return false;
     g->host_lo = host_lo;
@@ -2960,16 +2972,18 @@ extern "C" int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes,
 // scatter, per-bucket LDS sort, listed segments.  Stage timing: 0 scatter, 1
 // (no scan), 2 (no placement), 3 the bucket sort and the listed segments.
 // k_part_scatter instances (SHD_PART_SCATTER, measurement knob): 0 LDS
-// staging, 1024 threads x 4096 records (default); 1 registers, 1024 x 4096;
+// staging, 1024 threads x 4096 records; 1 registers, 1024 x 4096 (default:
+// round 0.670 vs 0.734-0.744 ms, profiles/r04b_part_scatter_variants.log);
 // 2 registers, 512 x 2048; 3 registers, 256 x 2048 (8 per thread)
 struct PartCfg {
     const void* fn;
     int wg, ch;
     bool lds;
 };
-PartCfg part_cfg() {
+PartCfg part_cfg(uint32_t nb) {
     const char* v = getenv("SHD_PART_SCATTER");
-    const int k = v ? atoi(v) : 0;
+    int k = v ? atoi(v) : 1;
+    if (k == 0 && nb > kPartMaxBucketsLds) k = 1; // (the LDS-staged form's histogram limit)
     if (k == 1) return {(const void*)k_part_scatter<1024, 4096, false>, 1024, 4096, false};
     if (k == 2) return {(const void*)k_part_scatter<512, 2048, false>, 512, 2048, false};
     if (k == 3) return {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false};
@@ -2987,7 +3001,7 @@ int part_attr() {
                             {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false}};
     for (const PartCfg& f : cfgs)
         if (int rc = hip_status(hipFuncSetAttribute(f.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    (int)part_lds(f, kPartMaxBuckets)),
+                                                    (int)part_lds(f, f.lds ? kPartMaxBucketsLds : kPartMaxBuckets)),
                                 "hipFuncSetAttribute k_part_scatter"))
             return rc;
     done = true;
@@ -3009,7 +3023,7 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
                        2 * g.nb);
     mark(0, s);
     if (n) {
-        const PartCfg f = part_cfg();
+        const PartCfg f = part_cfg(g.nb);
         const dim3 grid((unsigned)((n + f.ch - 1) / f.ch)), blk(f.wg);
         const size_t lds = part_lds(f, g.nb);
 #define SHD_PART_LAUNCH(WG, CH, L)                                                                                  \
@@ -3025,8 +3039,16 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
     mark(2, s);
     if ((rc = hip_status(hipGetLastError(), "k_part_scatter launch")) || (rc = dbg_sync(s, "k_part_scatter"))) return rc;
     mark(3, s);
-    hipLaunchKernelGGL(k_part_sort, dim3(g.nb), dim3(kPartBlock), 0, s, g, w.pstage, gcnt, wcnt, w.st2, w.nbig + 1,
-                       (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, lds_keys());
+    {
+        const int sc = part_sort_cfg();
+#define SHD_PART_SORT_LAUNCH(WG, CAP)                                                                                 \
+    hipLaunchKernelGGL((k_part_sort<WG, CAP>), dim3(g.nb), dim3(WG), 0, s, g, w.pstage, gcnt, wcnt, w.st2, w.nbig + 1, \
+                       (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, lds_keys())
+        if (sc == 1) SHD_PART_SORT_LAUNCH(512, 3584);
+        else if (sc == 2) SHD_PART_SORT_LAUNCH(256, 1792);
+        else SHD_PART_SORT_LAUNCH(1024, 7168);
+#undef SHD_PART_SORT_LAUNCH
+    }
     if ((rc = hip_status(hipGetLastError(), "k_part_sort launch")) || (rc = dbg_sync(s, "k_part_sort"))) return rc;
     if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s, counters)) || (rc = dbg_sync(s, "listed segments")))
         return rc;
