@@ -3,8 +3,10 @@
 // core/scheduler/scheduler.c:232-255, scheduler_policy_host_single.c:174-220,
 // core/work/event.c:109-152, utility/random.c:32-43).
 //
-// Pipeline over one round's batch (device-resident, one stream), default
-// "slab" (SHD_PACKET_PIPELINE=slab):
+// Pipeline over one round's batch (device-resident, one stream): the default
+// is "part" (k_part_scatter + k_part_sort, below); the earlier default
+// "slab" (SHD_PACKET_PIPELINE=slab), which the regroup after an exchange and
+// the exchanged round's sender side still use:
 //   k_pkt_scatter<2> per record: host->slot gathers, owner resolution of the
 //                  reference cache (touch order / pair bits), 16 B table
 //                  gather, the sender's reserved rand_r draw, drop rule,
@@ -2833,11 +2835,13 @@ bool part_geometry(uint32_t host_lo, uint32_t H, size_t n, unsigned long long tb
     return true;
 }
 
-int pipeline_for(uint32_t H, bool slab_ok) {
+// part_ok: the caller runs the part pipeline (the decided round: default; the
+// regroup of already-decided events has no part form and takes the slab's)
+int pipeline_for(uint32_t H, bool slab_ok, bool part_ok = false) {
     const char* v = getenv("SHD_PACKET_PIPELINE");
     if (v && strcmp(v, "bucket") == 0) return kBucketPipe;
     if (v && strcmp(v, "rank") == 0) return kRankPipe;
-    if (v && strcmp(v, "part") == 0) return kPartPipe;
+    if (part_ok && !(v && strcmp(v, "slab") == 0)) return kPartPipe;
     if (!slab_ok || (size_t)H * kSlab * sizeof(ShdDeliv) > kMaxSlabBytes) return kRankPipe;
     return kSlabPipe;
 }
@@ -3064,7 +3068,7 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
     Ws& w = *static_cast<Ws*>(c->ws);
     const uint32_t H = c->nhosts;
-    int pipe = pipeline_for(H, true);
+    int pipe = pipeline_for(H, true, true);
     if (pipe == kPartPipe) {
         PartGeo g;
         if (part_geometry(0, H, n, barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull, &g)) {
@@ -3074,7 +3078,7 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
             if ((rc = hip_status(hipStreamSynchronize(s), "packet round"))) return rc;
             return ws_faults(w, true, s);
         }
-        pipe = kSlabPipe; // (buckets too many for the scatter's histogram: the slab form)
+        pipe = pipeline_for(H, true); // (buckets too many for the scatter's histogram: the slab form)
     }
     const bool rk = pipe != kBucketPipe;
     Bucketing bk;
@@ -3160,9 +3164,9 @@ else if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
 // (0 bucket, 1 rank, 2 slab, 3 part), for tooling and benchmarks.
 extern "C" int shd_round_pipeline_of(uint32_t nhosts, size_t n, int* pipe) {
     if (!pipe) return -EINVAL;
-    int p = pipeline_for(nhosts, true);
+    int p = pipeline_for(nhosts, true, true);
     PartGeo g;
-    if (p == kPartPipe && !part_geometry(0, nhosts, n, 0, &g)) p = kSlabPipe;
+    if (p == kPartPipe && !part_geometry(0, nhosts, n, 0, &g)) p = pipeline_for(nhosts, true);
     *pipe = p;
     return 0;
 }
@@ -3281,7 +3285,8 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
     if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
     Ws& w = *static_cast<Ws*>(c->ws);
     const uint32_t H = c->nhosts;
-    if (pipeline_for(H, true) != kSlabPipe) return shd_fail(-ENOTSUP, "the exchanged round needs the slab pipeline");
+    const int pipe = pipeline_for(H, true);
+    if (pipe == kBucketPipe || pipe == kRankPipe) return shd_fail(-ENOTSUP, "the exchanged round needs the slab pipeline");
     Bucketing bk;
     int rc = make_bucketing(0, H, n, &bk);
     if (rc) return rc;
