@@ -13,13 +13,13 @@
 // edges at 2L, topology.c:1431-1576), latency 0 -> 1 ms, unreachable -1.
 //
 // Layout: a Vp x Vp u32 distance matrix (Vp = V rounded up to 64), 64 x 64
-// tiles.  Round kb: the diagonal tile closes over its own 64 vertices (64
-// dependent steps, redone by each workgroup of the next phase rather than
-// launched alone), the tiles of row and column kb relax through it (64 steps
-// each), then every other tile takes one min-plus
-// product of its row-kb and column-kb tiles, both staged in LDS (16 KB
-// each; 256 threads, a 4 x 4 register block per thread, two 16-B LDS reads
-// and 32 VALU per k).  The products are the O(V^3) part.
+// tiles.  Round kb, two launches: the tiles of row and column kb take one
+// min-plus product with the (closed) diagonal tile, then every other tile one
+// product of its row-kb and column-kb tiles, both staged in LDS.  The only
+// dependent chain -- the next round's diagonal tile closing over its own 64
+// vertices -- runs in the one workgroup of the second launch that produced
+// that tile, so a round is two product launches deep.  The products are the
+// O(V^3) part.
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
@@ -49,11 +49,10 @@ __global__ __launch_bounds__(256) void k_fw_edges(ShdGraphDev g, uint32_t* __res
         }
 }
 
-// The dependent phases (the diagonal tile closing over itself, the row and
-// column tiles relaxing through it) keep each thread's 4 x 4 block in
-// registers; step k needs the tile's current row k and/or column k, which
-// the 16 threads owning them publish to a double-buffered LDS line before
-// the step's single barrier.
+// The diagonal tile's closure keeps each thread's 4 x 4 block in registers;
+// step k needs the tile's current row k and column k, which the 16 threads
+// owning them publish to a double-buffered LDS line before the step's single
+// barrier.
 __device__ __forceinline__ void ld_block(uint32_t (&d)[4][4], const uint32_t* D, int Vp, int ti, int tj, int ty, int tx) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -93,10 +92,10 @@ __device__ __forceinline__ void relax(uint32_t (&d)[4][4], const uint4 cv, const
         }
 }
 
-// the diagonal tile's closure (phase 1) in registers, from D
-__device__ __forceinline__ void close_diag(uint32_t (&d)[4][4], uint32_t (*rowb)[kT], uint32_t (*colb)[kT],
-                                           const uint32_t* D, int Vp, int kb, int ty, int tx) {
-    ld_block(d, D, Vp, kb, kb, ty, tx);
+// closes the tile held in registers over its own 64 vertices (64 dependent
+// steps)
+__device__ __forceinline__ void close_regs(uint32_t (&d)[4][4], uint32_t (*rowb)[kT], uint32_t (*colb)[kT], int ty,
+                                           int tx) {
     for (int k = 0; k < kT; k++) {
         const int p = k & 1;
         if (ty == (k >> 2)) *reinterpret_cast<uint4*>(&rowb[p][tx * 4]) = blk_row(d, k & 3);
@@ -106,59 +105,58 @@ __device__ __forceinline__ void close_diag(uint32_t (&d)[4][4], uint32_t (*rowb)
     }
 }
 
-// round kb, phases 1 + 2: every workgroup closes the diagonal tile itself
-// (the same 64 steps in each, in parallel: one launch less per round; block
-// 0 stores it), then relaxes its tile of row or column kb through it
-// (blockIdx.x < nb - 1: row tiles, through the diagonal tile's columns;
-// else column tiles, through its rows)
-__global__ __launch_bounds__(256) void k_fw_cross(uint32_t* __restrict__ D, int Vp, int kb, int nb) {
-    __shared__ __attribute__((aligned(16))) uint32_t dg[kT][kT]; // row tiles: transposed (dg[k][a] = diag[a][k])
-    __shared__ __attribute__((aligned(16))) uint32_t lb[2][kT], rowb[2][kT], colb[2][kT];
+// round 0's diagonal tile (later rounds' are closed by k_fw_tiles)
+__global__ __launch_bounds__(256) void k_fw_close(uint32_t* __restrict__ D, int Vp) {
+    __shared__ __attribute__((aligned(16))) uint32_t rowb[2][kT], colb[2][kT];
     const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
     uint32_t d[4][4];
-    close_diag(d, rowb, colb, D, Vp, kb, ty, tx);
-    if (nb == 1 || blockIdx.x == 0) st_block(d, D, Vp, kb, kb, ty, tx);
-    if (nb == 1) return;
-    const bool row = (int)blockIdx.x < nb - 1;
-    int j = row ? (int)blockIdx.x : (int)blockIdx.x - (nb - 1);
-    if (j >= kb) j++;
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            if (row) dg[tx * 4 + c][ty * 4 + r] = d[r][c];
-            else dg[ty * 4 + r][tx * 4 + c] = d[r][c];
-        }
-    if (row) ld_block(d, D, Vp, kb, j, ty, tx);
-    else ld_block(d, D, Vp, j, kb, ty, tx);
-    __syncthreads();
-    for (int k = 0; k < kT; k++) {
-        const int p = k & 1;
-        if (row) { // d[a][b] = min(d[a][b], diag[a][k] + d[k][b]): row k of this tile
-            if (ty == (k >> 2)) *reinterpret_cast<uint4*>(&lb[p][tx * 4]) = blk_row(d, k & 3);
-            __syncthreads();
-            relax(d, *reinterpret_cast<const uint4*>(&dg[k][ty * 4]), *reinterpret_cast<const uint4*>(&lb[p][tx * 4]));
-        } else { // d[a][b] = min(d[a][b], d[a][k] + diag[k][b]): column k of this tile
-            if (tx == (k >> 2)) *reinterpret_cast<uint4*>(&lb[p][ty * 4]) = blk_col(d, k & 3);
-            __syncthreads();
-            relax(d, *reinterpret_cast<const uint4*>(&lb[p][ty * 4]), *reinterpret_cast<const uint4*>(&dg[k][tx * 4]));
-        }
-    }
-    if (row) st_block(d, D, Vp, kb, j, ty, tx);
-    else st_block(d, D, Vp, j, kb, ty, tx);
+    ld_block(d, D, Vp, 0, 0, ty, tx);
+    close_regs(d, rowb, colb, ty, tx);
+    st_block(d, D, Vp, 0, 0, ty, tx);
 }
 
-// round kb, phase 3: every tile (i, j), i, j != kb: d = min(d, rowtile (+) coltile)
-__global__ __launch_bounds__(256) void k_fw_prod(uint32_t* __restrict__ D, int Vp, int kb) {
-    __shared__ __attribute__((aligned(16))) uint32_t at[kT][kT]; // D[i][kb] transposed: at[k][i]
-    __shared__ __attribute__((aligned(16))) uint32_t bt[kT][kT]; // D[kb][j]: bt[k][j]
-    int ti = blockIdx.y, tj = blockIdx.x;
-    if (ti >= kb) ti++;
-    if (tj >= kb) tj++;
-    for (int q = threadIdx.x; q < kT * kT; q += 256) {
-        const int r = q / kT, c = q % kT;
-        at[c][r] = D[(size_t)(ti * kT + r) * Vp + kb * kT + c];
-        bt[r][c] = D[(size_t)(kb * kT + r) * Vp + tj * kT + c];
+// Round kb with its diagonal tile C already closed.  Every tile (i, j) takes
+// one min-plus product: d = min(d, D[i][kb] (+) D[kb][j]), both operands
+// staged in LDS (a 4 x 4 register block per thread, two 16-B LDS reads and
+// 32 VALU per k).  cross: the tiles of row and column kb -- for a row tile
+// that is C (+) R, for a column tile L (+) C: with C closed (zero diagonal)
+// one product is the whole relaxation through block kb, because a path's
+// last vertex in block kb splits it into a C part and an R part.  The
+// operands are staged before the tile is written, and no workgroup writes
+// another's operand (C is not written), so the update is in place.  prod:
+// every other tile, through the updated row and column tiles; the workgroup
+// of tile (kb + 1, kb + 1) then closes it for the next round (block 0, so
+// that the round's dependent chain starts first).
+template <bool kCross>
+__global__ __launch_bounds__(256) void k_fw_tiles(uint32_t* __restrict__ D, int Vp, int kb, int nb) {
+    __shared__ __attribute__((aligned(16))) uint32_t at[kT][kT + 4]; // D[i][kb] transposed: at[k][i]
+    __shared__ __attribute__((aligned(16))) uint32_t bt[kT][kT];     // D[kb][j]: bt[k][j]
+    int ti, tj;
+    bool close = false;
+    if (kCross) {
+        const int q = (int)blockIdx.x;
+        const bool row = q < nb - 1;
+        int o = row ? q : q - (nb - 1);
+        if (o >= kb) o++;
+        ti = row ? kb : o;
+        tj = row ? o : kb;
+    } else {
+        int q = (int)blockIdx.x;
+        const int nk = kb + 1 < nb ? kb + 1 : -1; // the next round's diagonal tile, taken by block 0
+        if (nk >= 0) {
+            const int qn = (nk - (nk > kb)) * (nb - 1) + (nk - (nk > kb)); // its linear index
+            if (q == 0) q = qn, close = true;
+            else if (q <= qn) q--;
+        }
+        ti = q / (nb - 1), tj = q % (nb - 1);
+        if (ti >= kb) ti++;
+        if (tj >= kb) tj++;
+    }
+    for (int q = threadIdx.x; q < kT * kT / 4; q += 256) {
+        const int r = q / (kT / 4), c = (q % (kT / 4)) * 4;
+        const uint4 a = *reinterpret_cast<const uint4*>(&D[(size_t)(ti * kT + r) * Vp + kb * kT + c]);
+        at[c][r] = a.x, at[c + 1][r] = a.y, at[c + 2][r] = a.z, at[c + 3][r] = a.w;
+        *reinterpret_cast<uint4*>(&bt[r][c]) = *reinterpret_cast<const uint4*>(&D[(size_t)(kb * kT + r) * Vp + tj * kT + c]);
     }
     const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
     uint32_t d[4][4];
@@ -167,6 +165,11 @@ __global__ __launch_bounds__(256) void k_fw_prod(uint32_t* __restrict__ D, int V
 #pragma unroll 8
     for (int k = 0; k < kT; k++)
         relax(d, *reinterpret_cast<const uint4*>(&at[k][ty * 4]), *reinterpret_cast<const uint4*>(&bt[k][tx * 4]));
+    if (!kCross && close) { // (block-uniform)
+        __syncthreads();
+        close_regs(d, reinterpret_cast<uint32_t(*)[kT]>(&at[0][0]), reinterpret_cast<uint32_t(*)[kT]>(&bt[0][0]), ty,
+                   tx);
+    }
     st_block(d, D, Vp, ti, tj, ty, tx);
 }
 
@@ -251,9 +254,10 @@ extern "C" int shd_dev_fw_latency(const ShdGraphDev* gp, double* d_lat, void** s
     uint32_t* D = w->D;
     hipLaunchKernelGGL(k_fw_init, dim3(1024), dim3(256), 0, s, D, Vp);
     hipLaunchKernelGGL(k_fw_edges, dim3(g.V < 4096 ? g.V : 4096), dim3(256), 0, s, g, D, Vp);
-    for (int kb = 0; kb < nb; kb++) {
-        hipLaunchKernelGGL(k_fw_cross, dim3(nb > 1 ? 2 * (nb - 1) : 1), dim3(256), 0, s, D, Vp, kb, nb);
-        if (nb > 1) hipLaunchKernelGGL(k_fw_prod, dim3(nb - 1, nb - 1), dim3(256), 0, s, D, Vp, kb);
+    hipLaunchKernelGGL(k_fw_close, dim3(1), dim3(256), 0, s, D, Vp);
+    for (int kb = 0; nb > 1 && kb < nb; kb++) {
+        hipLaunchKernelGGL(k_fw_tiles<true>, dim3(2 * (nb - 1)), dim3(256), 0, s, D, Vp, kb, nb);
+        hipLaunchKernelGGL(k_fw_tiles<false>, dim3((nb - 1) * (nb - 1)), dim3(256), 0, s, D, Vp, kb, nb);
     }
     hipLaunchKernelGGL(k_fw_rows, dim3(g.A < 4096 ? g.A : 4096), dim3(256), 0, s, g, D, Vp, d_lat);
     if ((rc = hip_rc(hipGetLastError(), "min-plus launch"))) return rc;

@@ -2324,6 +2324,73 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
         }
 }
 
+// The exchanged round's sender side on the part pipeline (see
+// k_group_wire): one workgroup per bucket counts its events per destination,
+// writes the destination offsets (the bucket's base: the earlier buckets'
+// totals) and places every event, unsorted, at its destination's range of
+// the wire array -- the owners sort the union of what they receive.
+__global__ __launch_bounds__(256) void k_part_wire(PartGeo g, const uint4* __restrict__ stage,
+                                                   const uint32_t* __restrict__ gcnt, const uint32_t* __restrict__ wcnt,
+                                                   const ShdDeliv* __restrict__ wide, const uint32_t* __restrict__ nwide,
+                                                   uint32_t wide_cap, uint32_t* __restrict__ offsets,
+                                                   Wire* __restrict__ wire, unsigned long long* __restrict__ counters,
+                                                   uint32_t* __restrict__ fault) {
+    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[4], s_base;
+    const uint32_t b = blockIdx.x;
+    const uint32_t d0 = b << g.shift;
+    const uint32_t nd = min(1u << g.shift, g.H - d0);
+    const uint32_t mask = (1u << g.shift) - 1u;
+    const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
+    {
+        uint32_t sm = 0;
+        for (uint32_t k = threadIdx.x; k < b; k += 256) sm += min(gcnt[k], g.cap) + wcnt[k];
+        uint32_t t;
+        (void)block_excl_scan_n(sm, &t, wsum);
+        if (threadIdx.x == 0) s_base = t;
+    }
+    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += 256) cnt[j] = cur[j] = 0;
+    __syncthreads();
+    const uint32_t obase = s_base;
+    const uint4* sb = stage + (size_t)b * g.cap;
+    const uint32_t m = *nwide;
+    const bool wide_ok = m <= wide_cap;
+    if (!wide_ok && b == 0 && threadIdx.x == 0) atomicOr(fault, kFaultOvfCap);
+    for (uint32_t i = threadIdx.x; i < ns; i += 256) atomicAdd(&cnt[sb[i].w & mask], 1u);
+    if (nw && wide_ok)
+        for (uint32_t i = threadIdx.x; i < m; i += 256) {
+            const uint32_t dr = wide[i].dst_host - g.host_lo;
+            if (dr < g.H && (dr >> g.shift) == b) atomicAdd(&cnt[dr & mask], 1u);
+        }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t v = threadIdx.x < nd ? cnt[threadIdx.x] : 0u;
+        const uint32_t inc = wave_incl_scan(v, (int)threadIdx.x);
+        if (threadIdx.x < nd) {
+            loc[threadIdx.x] = inc - v;
+            offsets[d0 + threadIdx.x] = obase + inc - v;
+        }
+    }
+    if (b == gridDim.x - 1 && threadIdx.x == 0) {
+        offsets[g.H] = obase + tot;
+        counters[0] = obase + tot;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < ns; i += 256) {
+        const uint4 r = sb[i];
+        const uint32_t dl = r.w & mask;
+        st_wire(&wire[obase + loc[dl] + atomicAdd(&cur[dl], 1u)], g.tbase + r.x, (unsigned long long)r.y,
+                r.w >> g.shift, r.z);
+    }
+    if (nw && wide_ok)
+        for (uint32_t i = threadIdx.x; i < m; i += 256) {
+            const ShdDeliv r = ld_ev(&wide[i]);
+            const uint32_t dr = r.dst_host - g.host_lo;
+            if (dr < g.H && (dr >> g.shift) == b)
+                st_wire(&wire[obase + loc[dr & mask] + atomicAdd(&cur[dr & mask], 1u)], r.time, r.seq, r.src_host,
+                        r.pkt_index);
+        }
+}
+
 // the round's fault word when no merge kernel runs: the stage guards only
 __global__ void k_fault_word(const uint32_t* __restrict__ nbig, MergeMeta mm) {
     if (threadIdx.x == 0) {
@@ -3012,17 +3079,12 @@ int part_attr() {
     return 0;
 }
 
-int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
-               uint64_t bootstrap_end, const PartGeo& g, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,
-               uint64_t* d_counters, hipStream_t s) {
-    int rc;
-    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 2 * (size_t)g.nb, g.H)) ||
-        (rc = pstage_reserve(w, (size_t)g.nb * g.cap)))
-        return rc;
-    unsigned long long* counters = (unsigned long long*)d_counters;
+// reset + k_part_scatter of a part round (counters, gcnt / wcnt in cnt1)
+int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
+               uint64_t bootstrap_end, const PartGeo& g, uint8_t* d_status, unsigned long long* counters,
+               hipStream_t s) {
     uint32_t* gcnt = w.cnt1;
     uint32_t* wcnt = w.cnt1 + g.nb;
-    if ((rc = dbg_ranges(w, d_status, n, d_out, d_dst_offsets, g.H))) return rc;
     hipLaunchKernelGGL(k_round_init, dim3(grid_for(2 * g.nb, 256, 4096)), dim3(256), 0, s, w.nbig, counters, w.cnt1,
                        2 * g.nb);
     mark(0, s);
@@ -3041,7 +3103,22 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
     }
     mark(1, s);
     mark(2, s);
-    if ((rc = hip_status(hipGetLastError(), "k_part_scatter launch")) || (rc = dbg_sync(s, "k_part_scatter"))) return rc;
+    int rc = hip_status(hipGetLastError(), "k_part_scatter launch");
+    return rc ? rc : dbg_sync(s, "k_part_scatter");
+}
+
+int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
+               uint64_t bootstrap_end, const PartGeo& g, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,
+               uint64_t* d_counters, hipStream_t s) {
+    int rc;
+    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 2 * (size_t)g.nb, g.H)) ||
+        (rc = pstage_reserve(w, (size_t)g.nb * g.cap)))
+        return rc;
+    unsigned long long* counters = (unsigned long long*)d_counters;
+    uint32_t* gcnt = w.cnt1;
+    uint32_t* wcnt = w.cnt1 + g.nb;
+    if ((rc = dbg_ranges(w, d_status, n, d_out, d_dst_offsets, g.H))) return rc;
+    if ((rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, g, d_status, counters, s))) return rc;
     mark(3, s);
     {
         const int sc = part_sort_cfg();
@@ -3285,6 +3362,28 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
     if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
     Ws& w = *static_cast<Ws*>(c->ws);
     const uint32_t H = c->nhosts;
+    const unsigned long long tb = barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull;
+    PartGeo pg;
+    if (pipeline_for(H, true, true) == kPartPipe && part_geometry(0, H, n, tb, &pg)) {
+        // the part scatter, then the bucket's events grouped by destination
+        // straight into the wire array (k_part_wire)
+        unsigned long long* counters = (unsigned long long*)d_counters;
+        int rc;
+        if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 2 * (size_t)pg.nb, H)) ||
+            (rc = pstage_reserve(w, (size_t)pg.nb * pg.cap)) ||
+            (rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, pg, d_status, counters, s)))
+            return rc;
+        mark(3, s);
+        hipLaunchKernelGGL(k_part_wire, dim3(pg.nb), dim3(256), 0, s, pg, w.pstage, w.cnt1, w.cnt1 + pg.nb, w.st2,
+                           w.nbig + 1, (uint32_t)w.cap_n, d_off, static_cast<Wire*>(d_wire), counters, w.nbig + 2);
+        if ((rc = hip_status(hipGetLastError(), "k_part_wire launch"))) return rc;
+        mark(4, s);
+        if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
+        if ((rc = dbg_sync(s, "grouped part round"))) return rc;
+        hipLaunchKernelGGL(k_fault_word, dim3(1), dim3(64), 0, s, w.nbig, merge_meta(w, counters));
+        if ((rc = copy_faults(w, s))) return rc;
+        return ws_end(w, s);
+    }
     const int pipe = pipeline_for(H, true);
     if (pipe == kBucketPipe || pipe == kRankPipe) return shd_fail(-ENOTSUP, "the exchanged round needs the slab pipeline");
     Bucketing bk;
