@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r03l_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r04f_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
@@ -98,6 +98,7 @@ def gpu_state(dev_index):
 # (independent random 16-B requests, by footprint and write share), the
 # bound the scatter and the slab SSSP kernels are compared against beside
 # their byte fraction.
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 32-bit VALU lane-ops/s (MI355X_MICROARCH: 32 lanes/cycle/SIMD)
 CEILING_JSON = os.path.join(ROOT, "profiles", "r04_request_ceiling.json")
 
 
@@ -343,7 +344,12 @@ def main():
             tj = json.load(f)
         # the PMC passes measured the default N=1 workload (10M packets, 100k
         # hosts): attached only to a line of that workload
-        if STAGES[dom] in tj and world == 1 and P == 10_000_000 and H == 100_000:
+        # and only when the record is of the kernel this line's stage ran (a
+        # record without a kernel name is of the slab pipeline's kernels)
+        rec = tj.get(STAGES[dom]) or {}
+        want = kernels[dom].split()[0]
+        have = rec.get("kernel", {"packet_scatter": "k_pkt_scatter", "segment_sort": "k_segsort_dst"}.get(STAGES[dom]))
+        if rec and have == want and world == 1 and P == 10_000_000 and H == 100_000:
             traffic = tj[STAGES[dom]]["bytes"]
             traffic_src = os.path.relpath(args.traffic, ROOT) + ": " + tj.get("_source", "")
 
@@ -404,7 +410,8 @@ def main():
 
     # ------------------------------------------------------------ C1 routing
     if not args.no_routing:
-        g1 = synth.complete_graph_gml(1000, 0x5EED0001)
+        g1_v = 1000
+        g1 = synth.complete_graph_gml(g1_v, 0x5EED0001)
         t1 = Topology(g1, device=local)
         scenario.register_hosts(t1, 5000, seed=1)
         A1 = t1.slot_count()
@@ -431,6 +438,7 @@ def main():
             t1.latency_table_fw(fw1.data_ptr())
         torch.cuda.synchronize(dev)
         t_fw1 = max_over_ranks((time.perf_counter() - s0) / reps)
+        fw_vp = (g1_v + 63) // 64 * 64
         fw_same = bool(torch.equal(fw1.view(A1, A1), tab1.view(A1, A1, 2)[:, :, 0])) if world == 1 else None
         del fw1
         info1 = t1.info()
@@ -441,7 +449,12 @@ def main():
             "value": 5000.0 ** 2 / tr, "unit": "routed host-pairs/s", "vertex_pairs_per_s": A1 * A1 / tr,
             "ms_per_table": tr * 1e3, "kernel": "k_sssp_ilds (igraph-exact Dijkstra, 1 wave/source, row in LDS, u32 keys)",
             "latency_only_minplus": {"ms": t_fw1 * 1e3, "kernel": "blocked min-plus Floyd-Warshall, 64x64 LDS tiles "
-                                     "(shd_topology_latency_table_fw)", "equals_table_latencies": fw_same},
+                                     "(shd_topology_latency_table_fw)", "equals_table_latencies": fw_same,
+                                     # 2 Vp^3 u32 ops (one add, one min per relaxation) against the
+                                     # chip's 32-bit VALU rate: 256 CUs x 4 SIMDs x 32 lanes/cycle x 2.4 GHz
+                                     "valu_roofline": {"ops": 2.0 * fw_vp ** 3, "achieved": 2.0 * fw_vp ** 3 / t_fw1 / 1e12,
+                                                       "peak": VALU_PEAK_TOPS, "unit": "T int32 ops/s",
+                                                       "frac": 2.0 * fw_vp ** 3 / t_fw1 / 1e12 / VALU_PEAK_TOPS}},
             "roofline": routing_roofline(A1, tr, 20.0 * 2 * info1["edges"] + 4 * 1001, max(h1 - l1, 0), 1000,
                                          tj.get("routing_ilds_c1") if world == 1 else None, bound=C1_BOUND),
             "c3_table": {"config": "the C3 rounds' table: V=%d sparse graph, H=%d hosts, A=%d" % (V, H, A),
@@ -607,10 +620,12 @@ def main():
                 t4.adopt_table_shard_device_resident(shard4.ptr, l4, h4, float(mn.item()))
             cap4 = 2 * n4
             d_pool4 = torch.from_numpy(pool4.view(np.int32)).to(dev)
-            d_st4 = [torch.from_numpy(st4.view(np.int32)).to(dev), torch.empty(len(pool4), dtype=torch.int32,
-                                                                               device=dev)]
-            d_sq4 = [torch.from_numpy(sq4.view(np.int64)).to(dev), torch.empty(len(pool4), dtype=torch.int64,
-                                                                               device=dev)]
+            # round r reads the carried states from [r % 2] and writes [(r + 1) % 2];
+            # the simulated rounds start at r = 1, so the carry starts in [1]
+            d_st4 = [torch.empty(len(pool4), dtype=torch.int32, device=dev),
+                     torch.from_numpy(st4.view(np.int32)).to(dev)]
+            d_sq4 = [torch.empty(len(pool4), dtype=torch.int64, device=dev),
+                     torch.from_numpy(sq4.view(np.int64)).to(dev)]
             r_recs = torch.empty(n4 * 32, dtype=torch.uint8, device=dev)
             r_in = torch.empty(cap4 * 32, dtype=torch.uint8, device=dev) if world > 1 else r_recs
             r_scr = torch.empty(n4 * 32, dtype=torch.uint8, device=dev) if world > 1 else None
@@ -660,6 +675,12 @@ def main():
             torch.cuda.synchronize(dev)
             barrier()
             tp4 = max_over_ranks(time.perf_counter() - s0)
+            # the carry reached every round: each sender's event counter advanced
+            # by m per round since the state the simulated rounds started from
+            sq_now = d_sq4[rnd[0] % 2].cpu().numpy().view(np.uint64)
+            carry_ok = bool(np.array_equal(sq_now, sq4.astype(np.uint64) + np.uint64(m4 * (rnd[0] - 1))))
+            if not carry_ok:
+                raise SystemExit("C4 rounds: the carried event counters are not the expected ones")
             st4ms = (C.c_double * 4)()
             nl4 = C.c_int()
             _lib.check(lib4.shd_round_timing_read(st4ms, 4, C.byref(nl4)))
@@ -672,6 +693,7 @@ def main():
                 "packets_per_s": n4 * world * args.c4_rounds / tp4, "ms_per_round": tp4 / args.c4_rounds * 1e3,
                 "handoff_ms_per_round_rank0": sum(st4ms[k] for k in range(4)) / max(nl4.value, 1),
                 "delivered_last_round_rank0": int(r_cnt.cpu().numpy().view(np.uint64)[0]),
+                "carry_checked": carry_ok,
                 "per_round_advance": "barrier += 10 ms; every sender's rand_r state and event counter carried on the "
                                      "device; new destinations each round (shd_synth_sends_device, in the timed "
                                      "loop; handoff_ms = the decide/group/sort stages alone)",

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box recipe (run through gpurun from the repo root):
 #   scripts/gpu_run.sh TAG STEP [STEP ...]
-# STEP: test[:EXPR]  pytest -m gpu (optionally -k EXPR), full output in gpurun_out/TAG/
+# STEP: test[:EXPR]  pytest -m gpu (optionally -k EXPR, commas for spaces), full output in gpurun_out/TAG/
 #       probe:ARGS   scripts/agg_probe.py ARGS (commas for spaces): in-process A/B of a knob
 #       ubench:NAME  scripts/NAME (a microbenchmark binary built here)
 #       rehearse[:ARGS]  bench.py at N=2 on one GPU over gloo (torch.distributed.run)
@@ -30,7 +30,7 @@ for step in "$@"; do
     test)
         L=$D/pytest$i.log
         if [ -n "$arg" ]; then
-            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread -k "$arg" \
+            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread -k "${arg//,/ }" \
                 > $L 2>&1 || { tail -60 $L; exit 1; }
         else
             timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread \

@@ -15,6 +15,9 @@ import json
 import re
 import sys
 
+# (a run measures one pipeline: its scatter and sort kernels name the stage;
+# the record keeps the kernel, and bench.py attaches a record only to a line
+# whose stage ran that kernel)
 STAGE = {"k_pkt_scatter": "packet_scatter", "k_part_scatter": "packet_scatter", "k_part_sort": "segment_sort", "k_place_rank": "place", "k_place_bucket": "place",
          "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_slab<256>": "routing_slab",
          "k_sssp_islab<false>": "routing_islab", "k_sssp_ilds": "routing_ilds",
@@ -53,7 +56,7 @@ def main():
         rq = agg.get((k, "TCC_EA0_RDREQ_sum"))
         wq = agg.get((k, "TCC_EA0_WRREQ_sum"))
         key = st + suffix if st.startswith("routing") else st
-        res[key] = {"bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
+        res[key] = {"kernel": k, "bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
                    "rd_requests": sum(rq) / len(rq) if rq else None,
                    "wr_requests": sum(wq) / len(wq) if wq else None}
     if suffix:

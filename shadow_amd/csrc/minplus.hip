@@ -34,19 +34,25 @@ constexpr int kT = 64;                  // tile edge
 constexpr uint32_t kInfD = 0x3FFFFFFFu; // unreachable; two of them still fit a u32
 constexpr int kMaxV = 16384;            // Vp^2 x 4 B = 1 GiB
 
-__global__ __launch_bounds__(256) void k_fw_init(uint32_t* __restrict__ D, int Vp) {
-    const size_t n = (size_t)Vp * Vp;
-    for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < n; q += (size_t)gridDim.x * 256)
-        D[q] = (q / Vp == q % Vp) ? 0u : kInfD;
-}
-
-// direct edges (igraph_incident mode OUT: an undirected edge is in both lists)
-__global__ __launch_bounds__(256) void k_fw_edges(ShdGraphDev g, uint32_t* __restrict__ D, int Vp) {
-    for (int u = blockIdx.x; u < g.V; u += gridDim.x)
-        for (int k = g.inc_off[u] + threadIdx.x; k < g.inc_off[u + 1]; k += 256) {
-            const int v = g.inc_nbr[k];
-            if (v != u) atomicMin(&D[(size_t)u * Vp + v], (uint32_t)g.inc_w[k]);
-        }
+// row u of the distance matrix: 0 on the diagonal, the direct edges
+// (igraph_incident mode OUT: an undirected edge is in both lists; the
+// lightest of parallel edges), unreachable elsewhere -- built in LDS, one
+// workgroup per row, stored once
+__global__ __launch_bounds__(256) void k_fw_init(ShdGraphDev g, uint32_t* __restrict__ D, int Vp) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t row[];
+    for (int u = blockIdx.x; u < Vp; u += gridDim.x) {
+        for (int j = threadIdx.x; j < Vp; j += 256) row[j] = j == u ? 0u : kInfD;
+        __syncthreads();
+        if (u < g.V)
+            for (int k = g.inc_off[u] + threadIdx.x; k < g.inc_off[u + 1]; k += 256) {
+                const int v = g.inc_nbr[k];
+                if (v != u) atomicMin(&row[v], (uint32_t)g.inc_w[k]);
+            }
+        __syncthreads();
+        for (int j = threadIdx.x * 4; j < Vp; j += 1024)
+            *reinterpret_cast<uint4*>(&D[(size_t)u * Vp + j]) = *reinterpret_cast<const uint4*>(&row[j]);
+        __syncthreads();
+    }
 }
 
 // The diagonal tile's closure keeps each thread's 4 x 4 block in registers;
@@ -66,21 +72,6 @@ __device__ __forceinline__ void st_block(const uint32_t (&d)[4][4], uint32_t* D,
         *reinterpret_cast<uint4*>(&D[(size_t)(ti * kT + ty * 4 + r) * Vp + tj * kT + tx * 4]) =
             make_uint4(d[r][0], d[r][1], d[r][2], d[r][3]);
 }
-// row k%4 of the block (its owner publishes it) / column k%4
-__device__ __forceinline__ uint4 blk_row(const uint32_t (&d)[4][4], int r) {
-    uint4 o = make_uint4(d[0][0], d[0][1], d[0][2], d[0][3]);
-#pragma unroll
-    for (int q = 1; q < 4; q++)
-        if (r == q) o = make_uint4(d[q][0], d[q][1], d[q][2], d[q][3]);
-    return o;
-}
-__device__ __forceinline__ uint4 blk_col(const uint32_t (&d)[4][4], int c) {
-    uint4 o = make_uint4(d[0][0], d[1][0], d[2][0], d[3][0]);
-#pragma unroll
-    for (int q = 1; q < 4; q++)
-        if (c == q) o = make_uint4(d[0][q], d[1][q], d[2][q], d[3][q]);
-    return o;
-}
 __device__ __forceinline__ void relax(uint32_t (&d)[4][4], const uint4 cv, const uint4 rv) {
     const uint32_t a[4] = {cv.x, cv.y, cv.z, cv.w}, b[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
@@ -96,13 +87,17 @@ __device__ __forceinline__ void relax(uint32_t (&d)[4][4], const uint4 cv, const
 // steps)
 __device__ __forceinline__ void close_regs(uint32_t (&d)[4][4], uint32_t (*rowb)[kT], uint32_t (*colb)[kT], int ty,
                                            int tx) {
-    for (int k = 0; k < kT; k++) {
-        const int p = k & 1;
-        if (ty == (k >> 2)) *reinterpret_cast<uint4*>(&rowb[p][tx * 4]) = blk_row(d, k & 3);
-        if (tx == (k >> 2)) *reinterpret_cast<uint4*>(&colb[p][ty * 4]) = blk_col(d, k & 3);
-        __syncthreads();
-        relax(d, *reinterpret_cast<const uint4*>(&colb[p][ty * 4]), *reinterpret_cast<const uint4*>(&rowb[p][tx * 4]));
-    }
+    // (k = 4 kk + r with r a compile-time constant: a runtime index into d
+    // would put the block in scratch memory)
+    for (int kk = 0; kk < kT / 4; kk++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int p = r & 1;
+            if (ty == kk) *reinterpret_cast<uint4*>(&rowb[p][tx * 4]) = make_uint4(d[r][0], d[r][1], d[r][2], d[r][3]);
+            if (tx == kk) *reinterpret_cast<uint4*>(&colb[p][ty * 4]) = make_uint4(d[0][r], d[1][r], d[2][r], d[3][r]);
+            __syncthreads();
+            relax(d, *reinterpret_cast<const uint4*>(&colb[p][ty * 4]), *reinterpret_cast<const uint4*>(&rowb[p][tx * 4]));
+        }
 }
 
 // round 0's diagonal tile (later rounds' are closed by k_fw_tiles)
@@ -152,15 +147,23 @@ __global__ __launch_bounds__(256) void k_fw_tiles(uint32_t* __restrict__ D, int 
         if (ti >= kb) ti++;
         if (tj >= kb) tj++;
     }
-    for (int q = threadIdx.x; q < kT * kT / 4; q += 256) {
-        const int r = q / (kT / 4), c = (q % (kT / 4)) * 4;
-        const uint4 a = *reinterpret_cast<const uint4*>(&D[(size_t)(ti * kT + r) * Vp + kb * kT + c]);
-        at[c][r] = a.x, at[c + 1][r] = a.y, at[c + 2][r] = a.z, at[c + 3][r] = a.w;
-        *reinterpret_cast<uint4*>(&bt[r][c]) = *reinterpret_cast<const uint4*>(&D[(size_t)(kb * kT + r) * Vp + tj * kT + c]);
+    // the three tiles' loads all in flight before the first LDS store
+    uint4 av[4], bv[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const int q = (int)threadIdx.x + 256 * m, r = q >> 4, c = (q & 15) * 4;
+        av[m] = *reinterpret_cast<const uint4*>(&D[(size_t)(ti * kT + r) * Vp + kb * kT + c]);
+        bv[m] = *reinterpret_cast<const uint4*>(&D[(size_t)(kb * kT + r) * Vp + tj * kT + c]);
     }
     const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
     uint32_t d[4][4];
     ld_block(d, D, Vp, ti, tj, ty, tx);
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        const int q = (int)threadIdx.x + 256 * m, r = q >> 4, c = (q & 15) * 4;
+        at[c][r] = av[m].x, at[c + 1][r] = av[m].y, at[c + 2][r] = av[m].z, at[c + 3][r] = av[m].w;
+        *reinterpret_cast<uint4*>(&bt[r][c]) = bv[m];
+    }
     __syncthreads();
 #pragma unroll 8
     for (int k = 0; k < kT; k++)
@@ -252,8 +255,7 @@ extern "C" int shd_dev_fw_latency(const ShdGraphDev* gp, double* d_lat, void** s
         return rc;
     }
     uint32_t* D = w->D;
-    hipLaunchKernelGGL(k_fw_init, dim3(1024), dim3(256), 0, s, D, Vp);
-    hipLaunchKernelGGL(k_fw_edges, dim3(g.V < 4096 ? g.V : 4096), dim3(256), 0, s, g, D, Vp);
+    hipLaunchKernelGGL(k_fw_init, dim3(Vp < 4096 ? Vp : 4096), dim3(256), (size_t)Vp * 4, s, g, D, Vp);
     hipLaunchKernelGGL(k_fw_close, dim3(1), dim3(256), 0, s, D, Vp);
     for (int kb = 0; nb > 1 && kb < nb; kb++) {
         hipLaunchKernelGGL(k_fw_tiles<true>, dim3(2 * (nb - 1)), dim3(256), 0, s, D, Vp, kb, nb);

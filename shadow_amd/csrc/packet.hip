@@ -2212,29 +2212,33 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
     const uint32_t mask = (1u << g.shift) - 1u;
     const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
     const bool listed = tot > (uint32_t)kCap || nw > 0; // (block-uniform)
-    // this bucket's output base: the totals of the buckets before it
-    {
-        uint32_t s = 0;
-        for (uint32_t k = threadIdx.x; k < b; k += kWG) s += min(gcnt[k], g.cap) + wcnt[k];
-        uint32_t t;
-        (void)block_excl_scan_n(s, &t, wsum);
-        if (threadIdx.x == 0) s_base = t;
-    }
     for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
-    __syncthreads();
-    const uint32_t obase = s_base;
     const uint4* sb = stage + (size_t)b * g.cap;
     uint4 e[kCap / kWG];
-    if (!listed) {
+    if (!listed) { // the bucket's records in flight while the base is summed
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++) {
             const uint32_t i = (uint32_t)k * kWG + threadIdx.x;
             if (i < ns) {
                 const shd_v4u v = __builtin_nontemporal_load(reinterpret_cast<const shd_v4u*>(sb) + i);
                 e[k] = make_uint4(v.x, v.y, v.z, v.w);
-                atomicAdd(&cnt[e[k].w & mask], 1u);
             }
         }
+    }
+    // this bucket's output base: the totals of the buckets before it
+    {
+        uint32_t s = 0;
+        for (uint32_t k = threadIdx.x; k < b; k += kWG) s += min(gcnt[k], g.cap) + wcnt[k];
+        uint32_t t;
+        (void)block_excl_scan_n(s, &t, wsum); // (its barriers also order the cnt reset)
+        if (threadIdx.x == 0) s_base = t;
+    }
+    __syncthreads();
+    const uint32_t obase = s_base;
+    if (!listed) {
+#pragma unroll
+        for (int k = 0; k < kCap / kWG; k++)
+            if ((uint32_t)k * kWG + threadIdx.x < ns) atomicAdd(&cnt[e[k].w & mask], 1u);
     } else {
         for (uint32_t i = threadIdx.x; i < ns; i += kWG) atomicAdd(&cnt[sb[i].w & mask], 1u);
         const uint32_t m = *nwide;
@@ -2873,12 +2877,16 @@ enum Pipeline { kBucketPipe = 0, kRankPipe = 1, kSlabPipe = 2, kPartPipe = 3 };
 constexpr size_t kMaxSlabBytes = 32ull << 30;
 
 // k_part_sort instances (SHD_PART_SORT, measurement knob): 0: 1024 threads,
-// 7,168 events in LDS (one workgroup per CU); 1: 512 threads, 3,584 (two);
-// 2: 256 threads, 1,792 (four).  The buckets are sized for the instance.
+// 7,168 events in LDS (one workgroup per CU); 1 (default): 512 threads, 3,584
+// (two per CU); 2: 256 threads, 1,792 (four).  The buckets are sized for the
+// instance.  C3 (profiles/r04c_part_sort_cfg.log): round 0.664 ms with 1 --
+// sort 0.184 ms, scatter 0.440 ms over 6,250 buckets -- vs 0.676 with 0 (sort
+// 0.214, scatter 0.418 over 3,125); 2 needs 12,500 buckets, above the
+// scatter's 8,192, and C3 falls back to the slab form.
 int part_sort_cfg() {
     const char* v = getenv("SHD_PART_SORT");
-    const int k = v ? atoi(v) : 0;
-    return k >= 0 && k <= 2 ? k : 0;
+    const int k = v ? atoi(v) : 1;
+    return k >= 0 && k <= 2 ? k : 1;
 }
 constexpr int kPartSortCap[3] = {7168, 3584, 1792};
 

@@ -1432,8 +1432,12 @@ __host__ __device__ __forceinline__ int blk_count(long V) {
 } // namespace ik
 
 // Slab per wave: nblk 128-B heap blocks, then V 16-B records.
-template <bool kStats>
-__global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8))) void k_sssp_islab(
+// kWpe: waves per SIMD (SHD_SSSP_WPE: 8 default; 7 and 6 trade occupancy for
+// fewer register spills -- 8 waves leave 64 VGPRs and 78 SGPRs, and the
+// compiler spills 23 VGPRs to scratch and 35 SGPRs to VGPR lanes; 7: 18 and
+// 26; 6: 6 and 11)
+template <bool kStats, int kWpe = 8>
+__global__ __launch_bounds__(64 * kSlabWaves) __attribute__((amdgpu_waves_per_eu(kWpe, kWpe))) void k_sssp_islab(
     ShdGraphDev g, int row_lo, int row_hi, ShdEntry* __restrict__ tab, char* __restrict__ slab, size_t slab_stride,
     size_t nblk, unsigned* __restrict__ err, unsigned long long* __restrict__ stats) {
     using namespace ik;
@@ -1841,7 +1845,9 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
             (rc = hip_status(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
                              "hipDeviceGetAttribute")))
             return rc;
-        long waves = (long)cus * kWavesPerCU;
+        int wpe = 8;
+        if (const char* e = getenv("SHD_SSSP_WPE")) wpe = atoi(e) == 7 ? 7 : atoi(e) == 6 ? 6 : 8;
+        long waves = (long)cus * 4 * wpe;
         if (const char* e = getenv("SHD_SSSP_WAVES")) {
             const long x = atol(e);
             if (x > 0) waves = x;
@@ -1868,6 +1874,12 @@ extern "C" int shd_dev_build_rows(const ShdGraphDev* gp, int use_sp, int row_lo,
             (void)hipMemset(stats, 0, 8 * ik::kStN);
             hipLaunchKernelGGL(k_sssp_islab<true>, dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo, row_hi,
                                tab, slab, stride, nblk, err, stats);
+        } else if (wpe == 7) {
+            hipLaunchKernelGGL((k_sssp_islab<false, 7>), dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo,
+                               row_hi, tab, slab, stride, nblk, err, nullptr);
+        } else if (wpe == 6) {
+            hipLaunchKernelGGL((k_sssp_islab<false, 6>), dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo,
+                               row_hi, tab, slab, stride, nblk, err, nullptr);
         } else {
             hipLaunchKernelGGL(k_sssp_islab<false>, dim3(grid), dim3(64 * kSlabWaves), lds, nullptr, g, row_lo, row_hi,
                                tab, slab, stride, nblk, err, nullptr);
