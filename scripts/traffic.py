@@ -18,14 +18,15 @@ import sys
 # (a run measures one pipeline: its scatter and sort kernels name the stage;
 # the record keeps the kernel, and bench.py attaches a record only to a line
 # whose stage ran that kernel)
-STAGE = {"k_pkt_scatter": "packet_scatter", "k_part_scatter": "packet_scatter", "k_part_sort": "segment_sort", "k_place_rank": "place", "k_place_bucket": "place",
-         "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf", "k_sssp_slab<256>": "routing_slab",
-         "k_sssp_islab<false>": "routing_islab", "k_sssp_ilds": "routing_ilds",
-         "k_sssp_lds<true>": "routing_lds", "k_scan_one": "scan"}
+# (kernel names without their template arguments)
+STAGE = {"k_pkt_scatter": "packet_scatter", "k_part_scatter": "packet_scatter", "k_part_sort": "segment_sort",
+         "k_place_rank": "place", "k_place_bucket": "place", "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf",
+         "k_sssp_slab": "routing_slab", "k_sssp_islab": "routing_islab", "k_sssp_ilds": "routing_ilds",
+         "k_sssp_lds": "routing_lds", "k_scan_one": "scan"}
 
 
 def kname(n):
-    m = re.search(r"(k_\w+(?:<\w+>)?)", n)
+    m = re.search(r"(k_\w+)", n)
     return m.group(1) if m else n
 
 
@@ -44,7 +45,6 @@ def main():
     for f in files:
         for r in csv.DictReader(open(f)):
             k = kname(r["Kernel_Name"])
-            k = k.split("<", 1)[0]  # template instances (k_pkt_scatter<2, 4, 0, true>, k_segsort_dst<3>)
             agg.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
     res = {}
     for k, st in STAGE.items():

@@ -2188,6 +2188,40 @@ __global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt*
     }
 }
 
+// The wide list (events whose record did not fit the 16-B stage form, or
+// whose bucket region was full) grouped by bucket into `grouped`, so that a
+// bucket reads only its own (wcnt[b] events from the earlier buckets'
+// total): every workgroup scans the per-bucket counts into LDS, then places
+// its share of the list with per-bucket cursors.  Exits at once when the list
+// is empty (the usual round).
+__global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* __restrict__ wide,
+                                                     const uint32_t* __restrict__ nwide, uint32_t wide_cap,
+                                                     const uint32_t* __restrict__ wcnt, uint32_t* __restrict__ wcur,
+                                                     ShdDeliv* __restrict__ grouped) {
+    const uint32_t m = *nwide;
+    if (m == 0 || m > wide_cap) return; // (block-uniform; an overfull list is the sort's fault to report)
+    __shared__ uint32_t woff[kPartMaxBuckets];
+    __shared__ uint32_t wsum[16];
+    const uint32_t per = (g.nb + 1023) / 1024, b0 = threadIdx.x * per;
+    uint32_t sm = 0;
+    for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) sm += wcnt[b0 + k];
+    uint32_t tot;
+    uint32_t pre = block_excl_scan_n(sm, &tot, wsum);
+    for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) {
+        woff[b0 + k] = pre;
+        pre += wcnt[b0 + k];
+    }
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < m; i += gridDim.x * 1024) {
+        const ShdDeliv r = ld_ev(&wide[i]);
+        const uint32_t dr = r.dst_host - g.host_lo;
+        if (dr < g.H) {
+            const uint32_t b = dr >> g.shift;
+            st_ev(&grouped[woff[b] + atomicAdd(&wcur[b], 1u)], r);
+        }
+    }
+}
+
 // One workgroup of kWG threads per bucket of at most kCap events held in
 // LDS (7 per thread; see above).  nbig / big / scr: the listed segments
 // (k_segsort_mid); fault: nbig[2] guard bits.
@@ -2204,7 +2238,7 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
     __shared__ uint4 lev[kCap];
     __shared__ unsigned long long keys[kWG / 64][64 * 4 + 8];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kWG / 64];
-    __shared__ uint32_t s_base;
+    __shared__ uint32_t s_base, s_wbase;
     const uint32_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t d0 = b << g.shift;
@@ -2225,16 +2259,24 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
             }
         }
     }
-    // this bucket's output base: the totals of the buckets before it
+    // this bucket's output base: the totals of the buckets before it (and,
+    // when it has wide events, their place in the grouped list: the earlier
+    // buckets' wide counts)
     {
-        uint32_t s = 0;
-        for (uint32_t k = threadIdx.x; k < b; k += kWG) s += min(gcnt[k], g.cap) + wcnt[k];
-        uint32_t t;
+        uint32_t s = 0, sw = 0;
+        for (uint32_t k = threadIdx.x; k < b; k += kWG) {
+            const uint32_t x = wcnt[k];
+            s += min(gcnt[k], g.cap) + x;
+            sw += x;
+        }
+        uint32_t t, tw = 0;
         (void)block_excl_scan_n(s, &t, wsum); // (its barriers also order the cnt reset)
-        if (threadIdx.x == 0) s_base = t;
+        if (nw) (void)block_excl_scan_n(sw, &tw, wsum);
+        if (threadIdx.x == 0) s_base = t, s_wbase = tw;
     }
     __syncthreads();
     const uint32_t obase = s_base;
+    const ShdDeliv* wb = wide + s_wbase; // this bucket's wide events (k_wide_group)
     if (!listed) {
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++)
@@ -2244,11 +2286,8 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
         const uint32_t m = *nwide;
         if (m > wide_cap) {
             if (threadIdx.x == 0) atomicOr(nbig + 2, kFaultOvfCap);
-        } else if (nw) {
-            for (uint32_t i = threadIdx.x; i < m; i += kWG) {
-                const uint32_t dr = wide[i].dst_host - g.host_lo;
-                if (dr < g.H && (dr >> g.shift) == b) atomicAdd(&cnt[dr & mask], 1u);
-            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < nw; i += kWG) atomicAdd(&cnt[(wb[i].dst_host - g.host_lo) & mask], 1u);
         }
     }
     __syncthreads();
@@ -2309,15 +2348,12 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
         st_ev(&scr[obase + loc[dl] + atomicAdd(&cur[dl], 1u)],
               ShdDeliv{g.tbase + r.x, (unsigned long long)r.y, r.w >> g.shift, g.host_lo + d0 + dl, r.z, 0u});
     }
-    const uint32_t m = *nwide;
-    if (nw && m <= wide_cap)
-        for (uint32_t i = threadIdx.x; i < m; i += kWG) {
-            ShdDeliv r = ld_ev(&wide[i]);
-            const uint32_t dr = r.dst_host - g.host_lo;
-            if (dr < g.H && (dr >> g.shift) == b) {
-                r.pad = 0;
-                st_ev(&scr[obase + loc[dr & mask] + atomicAdd(&cur[dr & mask], 1u)], r);
-            }
+    if (nw && *nwide <= wide_cap)
+        for (uint32_t i = threadIdx.x; i < nw; i += kWG) {
+            ShdDeliv r = ld_ev(&wb[i]);
+            const uint32_t dl = (r.dst_host - g.host_lo) & mask;
+            r.pad = 0;
+            st_ev(&scr[obase + loc[dl] + atomicAdd(&cur[dl], 1u)], r);
         }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nd; j += kWG)
@@ -2339,32 +2375,35 @@ __global__ __launch_bounds__(256) void k_part_wire(PartGeo g, const uint4* __res
                                                    uint32_t wide_cap, uint32_t* __restrict__ offsets,
                                                    Wire* __restrict__ wire, unsigned long long* __restrict__ counters,
                                                    uint32_t* __restrict__ fault) {
-    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[4], s_base;
+    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[4], s_base, s_wbase;
     const uint32_t b = blockIdx.x;
     const uint32_t d0 = b << g.shift;
     const uint32_t nd = min(1u << g.shift, g.H - d0);
     const uint32_t mask = (1u << g.shift) - 1u;
     const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
     {
-        uint32_t sm = 0;
-        for (uint32_t k = threadIdx.x; k < b; k += 256) sm += min(gcnt[k], g.cap) + wcnt[k];
-        uint32_t t;
+        uint32_t sm = 0, sw = 0;
+        for (uint32_t k = threadIdx.x; k < b; k += 256) {
+            const uint32_t x = wcnt[k];
+            sm += min(gcnt[k], g.cap) + x;
+            sw += x;
+        }
+        uint32_t t, tw = 0;
         (void)block_excl_scan_n(sm, &t, wsum);
-        if (threadIdx.x == 0) s_base = t;
+        if (nw) (void)block_excl_scan_n(sw, &tw, wsum);
+        if (threadIdx.x == 0) s_base = t, s_wbase = tw;
     }
     for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += 256) cnt[j] = cur[j] = 0;
     __syncthreads();
     const uint32_t obase = s_base;
+    const ShdDeliv* wb = wide + s_wbase; // this bucket's wide events (k_wide_group)
     const uint4* sb = stage + (size_t)b * g.cap;
     const uint32_t m = *nwide;
     const bool wide_ok = m <= wide_cap;
     if (!wide_ok && b == 0 && threadIdx.x == 0) atomicOr(fault, kFaultOvfCap);
     for (uint32_t i = threadIdx.x; i < ns; i += 256) atomicAdd(&cnt[sb[i].w & mask], 1u);
-    if (nw && wide_ok)
-        for (uint32_t i = threadIdx.x; i < m; i += 256) {
-            const uint32_t dr = wide[i].dst_host - g.host_lo;
-            if (dr < g.H && (dr >> g.shift) == b) atomicAdd(&cnt[dr & mask], 1u);
-        }
+    if (wide_ok)
+        for (uint32_t i = threadIdx.x; i < nw; i += 256) atomicAdd(&cnt[(wb[i].dst_host - g.host_lo) & mask], 1u);
     __syncthreads();
     if (threadIdx.x < 64) {
         const uint32_t v = threadIdx.x < nd ? cnt[threadIdx.x] : 0u;
@@ -2385,13 +2424,11 @@ __global__ __launch_bounds__(256) void k_part_wire(PartGeo g, const uint4* __res
         st_wire(&wire[obase + loc[dl] + atomicAdd(&cur[dl], 1u)], g.tbase + r.x, (unsigned long long)r.y,
                 r.w >> g.shift, r.z);
     }
-    if (nw && wide_ok)
-        for (uint32_t i = threadIdx.x; i < m; i += 256) {
-            const ShdDeliv r = ld_ev(&wide[i]);
-            const uint32_t dr = r.dst_host - g.host_lo;
-            if (dr < g.H && (dr >> g.shift) == b)
-                st_wire(&wire[obase + loc[dr & mask] + atomicAdd(&cur[dr & mask], 1u)], r.time, r.seq, r.src_host,
-                        r.pkt_index);
+    if (wide_ok)
+        for (uint32_t i = threadIdx.x; i < nw; i += 256) {
+            const ShdDeliv r = ld_ev(&wb[i]);
+            const uint32_t dl = (r.dst_host - g.host_lo) & mask;
+            st_wire(&wire[obase + loc[dl] + atomicAdd(&cur[dl], 1u)], r.time, r.seq, r.src_host, r.pkt_index);
         }
 }
 
@@ -2786,12 +2823,21 @@ struct Timing {
     bool on = false;
     int n = 0;
     hipEvent_t ev[kMaxTimed][kStages + 1];
+    int8_t at[kMaxTimed][kStages + 1]; // the event a boundary reads (a stage with no kernels: the previous one)
     bool created = false;
 };
 Timing g_tm;
 
 void mark(int stage, hipStream_t s) {
-    if (g_tm.on && g_tm.n < kMaxTimed) (void)hipEventRecord(g_tm.ev[g_tm.n][stage], s);
+    if (g_tm.on && g_tm.n < kMaxTimed) {
+        (void)hipEventRecord(g_tm.ev[g_tm.n][stage], s);
+        g_tm.at[g_tm.n][stage] = (int8_t)stage;
+    }
+}
+// a boundary with nothing launched since the previous one: no event of its
+// own (an event record costs the stream ~5 us)
+void mark_same(int stage, int prev) {
+    if (g_tm.on && g_tm.n < kMaxTimed) g_tm.at[g_tm.n][stage] = g_tm.at[g_tm.n][prev];
 }
 
 // scan of the count matrix, atomic-free placement into bucket regions,
@@ -3093,8 +3139,8 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
                hipStream_t s) {
     uint32_t* gcnt = w.cnt1;
     uint32_t* wcnt = w.cnt1 + g.nb;
-    hipLaunchKernelGGL(k_round_init, dim3(grid_for(2 * g.nb, 256, 4096)), dim3(256), 0, s, w.nbig, counters, w.cnt1,
-                       2 * g.nb);
+    hipLaunchKernelGGL(k_round_init, dim3(grid_for(3 * g.nb, 256, 4096)), dim3(256), 0, s, w.nbig, counters, w.cnt1,
+                       3 * g.nb);
     mark(0, s);
     if (n) {
         const PartCfg f = part_cfg(g.nb);
@@ -3108,9 +3154,13 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         else if (f.wg == 512) SHD_PART_LAUNCH(512, 2048, false);
         else SHD_PART_LAUNCH(256, 2048, false);
 #undef SHD_PART_LAUNCH
+        // the wide list by bucket (w.tmp: unused by this pipeline), for the
+        // second pass to read its buckets' own
+        hipLaunchKernelGGL(k_wide_group, dim3(64), dim3(1024), 0, s, g, w.st2, w.nbig + 1, (uint32_t)w.cap_n, wcnt,
+                           w.cnt1 + 2 * g.nb, w.tmp);
     }
     mark(1, s);
-    mark(2, s);
+    mark_same(2, 1);
     int rc = hip_status(hipGetLastError(), "k_part_scatter launch");
     return rc ? rc : dbg_sync(s, "k_part_scatter");
 }
@@ -3119,7 +3169,7 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
                uint64_t bootstrap_end, const PartGeo& g, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,
                uint64_t* d_counters, hipStream_t s) {
     int rc;
-    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 2 * (size_t)g.nb, g.H)) ||
+    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 3 * (size_t)g.nb, g.H)) ||
         (rc = pstage_reserve(w, (size_t)g.nb * g.cap)))
         return rc;
     unsigned long long* counters = (unsigned long long*)d_counters;
@@ -3127,11 +3177,11 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
     uint32_t* wcnt = w.cnt1 + g.nb;
     if ((rc = dbg_ranges(w, d_status, n, d_out, d_dst_offsets, g.H))) return rc;
     if ((rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, g, d_status, counters, s))) return rc;
-    mark(3, s);
+    mark_same(3, 2);
     {
         const int sc = part_sort_cfg();
 #define SHD_PART_SORT_LAUNCH(WG, CAP)                                                                                 \
-    hipLaunchKernelGGL((k_part_sort<WG, CAP>), dim3(g.nb), dim3(WG), 0, s, g, w.pstage, gcnt, wcnt, w.st2, w.nbig + 1, \
+    hipLaunchKernelGGL((k_part_sort<WG, CAP>), dim3(g.nb), dim3(WG), 0, s, g, w.pstage, gcnt, wcnt, w.tmp, w.nbig + 1, \
                        (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, lds_keys())
         if (sc == 1) SHD_PART_SORT_LAUNCH(512, 3584);
         else if (sc == 2) SHD_PART_SORT_LAUNCH(256, 1792);
@@ -3275,7 +3325,8 @@ extern "C" int shd_round_timing_read(double* stage_ms, int nstages, int* launche
         if (hipEventSynchronize(g_tm.ev[i][kStages]) != hipSuccess) return shd_fail(-EIO, "hipEventSynchronize");
         for (int k = 0; k < nstages; k++) {
             float ms = 0.f;
-            if (hipEventElapsedTime(&ms, g_tm.ev[i][k], g_tm.ev[i][k + 1]) != hipSuccess)
+            const int a = g_tm.at[i][k], b = g_tm.at[i][k + 1];
+            if (a != b && hipEventElapsedTime(&ms, g_tm.ev[i][a], g_tm.ev[i][b]) != hipSuccess)
                 return shd_fail(-EIO, "hipEventElapsedTime");
             stage_ms[k] += ms;
         }
@@ -3377,12 +3428,12 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
         // straight into the wire array (k_part_wire)
         unsigned long long* counters = (unsigned long long*)d_counters;
         int rc;
-        if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 2 * (size_t)pg.nb, H)) ||
+        if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 3 * (size_t)pg.nb, H)) ||
             (rc = pstage_reserve(w, (size_t)pg.nb * pg.cap)) ||
             (rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, pg, d_status, counters, s)))
             return rc;
-        mark(3, s);
-        hipLaunchKernelGGL(k_part_wire, dim3(pg.nb), dim3(256), 0, s, pg, w.pstage, w.cnt1, w.cnt1 + pg.nb, w.st2,
+        mark_same(3, 2);
+        hipLaunchKernelGGL(k_part_wire, dim3(pg.nb), dim3(256), 0, s, pg, w.pstage, w.cnt1, w.cnt1 + pg.nb, w.tmp,
                            w.nbig + 1, (uint32_t)w.cap_n, d_off, static_cast<Wire*>(d_wire), counters, w.nbig + 2);
         if ((rc = hip_status(hipGetLastError(), "k_part_wire launch"))) return rc;
         mark(4, s);

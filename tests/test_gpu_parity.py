@@ -494,6 +494,21 @@ def test_compact_slab_fallbacks(pipeline):
     assert (out["seq"] >= 1 << 32).sum() > 1000 and (out["time"] < barrier - 2**31).sum() > 100
 
 
+def test_all_events_wide(pipeline):
+    """Every event outside the compact forms (srcHostEventIDs of 2^32 and
+    more: a host's event counter in a long simulation), so every bucket of
+    the part pipeline has wide events: each reads only its own from the
+    bucket-grouped wide list (k_wide_group); outputs equal the oracle's."""
+    gml, H = GRAPHS["sparse300_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    pk = synth.packet_batch(120000, H, 0x5EED0430, 100_000_000, 10_000_000, st)
+    pk["seq"] += np.uint64(3 << 32)
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert len(out) > 100000
+
+
 def test_device_api_unknown_hosts_not_delivered(pipeline):
     """Records naming host ids outside the registered range get status 0xff and
     no event; every other record is decided exactly as the oracle does."""
