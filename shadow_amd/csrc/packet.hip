@@ -1975,7 +1975,10 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* tota
 // (consecutive lanes, consecutive records of a run); else each thread keeps
 // its events in registers and stores them at their run positions itself (LDS
 // holds only the bucket counts: more workgroups per CU).
-template <int kWG, int kCH, bool kLds>
+// kProbe (SHD_PART_PROBE, measurement only -- outputs deliberately wrong):
+// 1 no table gather, 2 no run-reservation atomics, 3 no stage stores, 4 no
+// host->slot gathers
+template <int kWG, int kCH, bool kLds, int kProbe = 0>
 __global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
                                                       uint64_t barrier, uint64_t end_time, uint64_t boot_end,
                                                       PartGeo g, uint4* __restrict__ stage,
@@ -2022,7 +2025,10 @@ __global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt*
         for (int k = 0; k < kB; k++) {
             const bool known = live[k] && p[k].src_host < c.nhosts && p[k].dst_host < c.nhosts;
             uint2 hs = make_uint2(~0u, ~0u), hd = make_uint2(~0u, ~0u);
-            if (known) {
+            if (known && kProbe == 4) {
+                hs = make_uint2(p[k].src_host % (uint32_t)A, 0u);
+                hd = make_uint2(p[k].dst_host % (uint32_t)A, 1u);
+            } else if (known) {
                 hs = host_info[p[k].src_host];
                 hd = host_info[p[k].dst_host];
             }
@@ -2050,8 +2056,8 @@ __global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt*
         uint2 q[kB];
 #pragma unroll
         for (int k = 0; k < kB; k++) {
-            q[k] = make_uint2(kPtabFallback, 0u);
-            if (ptab && si[k] >= 0 && di[k] >= 0) {
+            q[k] = make_uint2(kProbe == 1 ? 1000000u : kPtabFallback, kProbe == 1 ? 0xFFFFFFFFu : 0u);
+            if (kProbe != 1 && ptab && si[k] >= 0 && di[k] >= 0) {
                 const unsigned long long v =
                     __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ptab) + ei[k]);
                 q[k] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
@@ -2131,14 +2137,15 @@ __global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt*
     } else {
         for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) {
             const uint32_t h = hist[b];
-            gb[b] = h ? atomicAdd(&gcnt[b], h) : 0u;
+            if (kProbe == 2) gb[b] = (blockIdx.x * 37u + b) % (g.cap > 64 ? g.cap - 64 : 1u);
+            else gb[b] = h ? atomicAdd(&gcnt[b], h) : 0u;
         }
     }
     __syncthreads();
     auto put = [&](bool valid, const uint4& e, uint32_t li, size_t j) { // (every lane: ballot inside)
         const uint32_t b = valid ? (e.w - g.host_lo) >> g.shift : 0u;
         const bool in = valid && j < g.cap;
-        if (in) // runs of a bucket, consecutive records
+        if (in && kProbe != 3) // runs of a bucket, consecutive records
             stage[(size_t)b * g.cap + j] =
                 make_uint4(e.x, e.y, (uint32_t)(base + li) + c.idx_base, (e.z << g.shift) | ((e.w - g.host_lo) & mask));
         const bool full = valid && !in; // the bucket's region is full: whole event to the wide list
@@ -3105,6 +3112,11 @@ struct PartCfg {
     int wg, ch;
     bool lds;
 };
+int part_probe() {
+    const char* v = getenv("SHD_PART_PROBE");
+    const int k = v ? atoi(v) : 0;
+    return k >= 1 && k <= 4 ? k : 0;
+}
 PartCfg part_cfg(uint32_t nb) {
     const char* v = getenv("SHD_PART_SCATTER");
     int k = v ? atoi(v) : 1;
@@ -3146,10 +3158,16 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         const PartCfg f = part_cfg(g.nb);
         const dim3 grid((unsigned)((n + f.ch - 1) / f.ch)), blk(f.wg);
         const size_t lds = part_lds(f, g.nb);
-#define SHD_PART_LAUNCH(WG, CH, L)                                                                                  \
-    hipLaunchKernelGGL((k_part_scatter<WG, CH, L>), grid, blk, lds, s, *c, d_recs, n, barrier, end_time,           \
+#define SHD_PART_LAUNCH(WG, CH, L, ...)                                                                             \
+    hipLaunchKernelGGL((k_part_scatter<WG, CH, L, ##__VA_ARGS__>), grid, blk, lds, s, *c, d_recs, n, barrier, end_time, \
                        bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters, w.st2, w.nbig + 1)
-        if (f.lds) SHD_PART_LAUNCH(1024, 4096, true);
+        const int pr = part_probe();
+        if (pr && !f.lds && f.wg == 1024) {
+            if (pr == 1) SHD_PART_LAUNCH(1024, 4096, false, 1);
+            else if (pr == 2) SHD_PART_LAUNCH(1024, 4096, false, 2);
+            else if (pr == 3) SHD_PART_LAUNCH(1024, 4096, false, 3);
+            else SHD_PART_LAUNCH(1024, 4096, false, 4);
+        } else if (f.lds) SHD_PART_LAUNCH(1024, 4096, true);
         else if (f.wg == 1024) SHD_PART_LAUNCH(1024, 4096, false);
         else if (f.wg == 512) SHD_PART_LAUNCH(512, 2048, false);
         else SHD_PART_LAUNCH(256, 2048, false);
