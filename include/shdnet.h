@@ -189,6 +189,16 @@ int shd_topology_build_rows_device(ShdTopology* top, int row_lo, int row_hi, voi
  * topology's persistent distance scratch (calls on other streams wait for its
  * last use); stream NULL: synchronous. */
 int shd_topology_latency_table_fw(ShdTopology* top, void* d_lat, void* stream);
+/* Latencies only, for sparse graphs: rows [row_lo, row_hi) of the lat_ms
+ * column ((row_hi - row_lo) x A doubles, row - row_lo major) into d_lat, by a
+ * bucketed frontier SSSP per source (Dial's algorithm: a ring of
+ * max-latency + 1 distance buckets, each settled bucket's edges relaxed
+ * edge-parallel by one wave; csrc/frontier.hip).  Same entries as the
+ * table's latency column (tie-independent, as for the min-plus entry above),
+ * no lookup side effects; graphs whose edge latencies are all whole ms (at
+ * most 65,535) -- -ENOTSUP otherwise.  Synchronous on stream (hipStream_t,
+ * NULL: the null stream). */
+int shd_topology_latency_rows_frontier(ShdTopology* top, int row_lo, int row_hi, void* d_lat, void* stream);
 int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
 /* Adopts a device table WITHOUT a host mirror (tables larger than host RAM
  * wants: A = 86k slots is 120 GB).  Nothing is released at adoption: as in

@@ -58,6 +58,7 @@ PROTOS = {
     "shd_device_copy": (C.c_int, [C.c_int, _P, _P, C.c_size_t]),
     "shd_topology_build_rows_device": (C.c_int, [_P, C.c_int, C.c_int, _P]),
     "shd_topology_latency_table_fw": (C.c_int, [_P, _P, _P]),
+    "shd_topology_latency_rows_frontier": (C.c_int, [_P, C.c_int, C.c_int, _P, _P]),
     "shd_topology_adopt_table_device": (C.c_int, [_P, _P]),
     "shd_topology_adopt_table_device_resident": (C.c_int, [_P, _P]),
     "shd_topology_adopt_table_shards": (C.c_int, [_P, C.c_int, _P, _P, _P]),

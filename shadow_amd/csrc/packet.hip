@@ -1945,7 +1945,7 @@ __global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__
 // destination ranges of the staging array and every segment is listed for
 // k_segsort_mid / k_segsort_merge (skewed destinations).
 constexpr uint32_t kPartMaxDst = 64; // destinations per bucket (shift <= 6)
-constexpr uint32_t kPartMaxBuckets = 8192;  // register-staged scatter: 8 B of LDS per bucket
+constexpr uint32_t kPartMaxBuckets = 16384; // register-staged scatter: 8 B of LDS per bucket
 constexpr uint32_t kPartMaxBucketsLds = 4096; // LDS-staged scatter: + 20 B per record
 
 struct PartGeo {
@@ -1978,8 +1978,11 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* tota
 // kProbe (SHD_PART_PROBE, measurement only -- outputs deliberately wrong):
 // 1 no table gather, 2 no run-reservation atomics, 3 no stage stores, 4 no
 // host->slot gathers
-template <int kWG, int kCH, bool kLds, int kProbe = 0>
-__global__ __launch_bounds__(kWG) void k_part_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
+// kOcc: waves per SIMD the registers are sized for (0: the compiler's
+// choice -- 71 VGPRs, one 1,024-thread workgroup per CU; 8: two per CU, with
+// spills)
+template <int kWG, int kCH, bool kLds, int kProbe = 0, int kOcc = 0>
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc : 4, 8))) void k_part_scatter(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
                                                       uint64_t barrier, uint64_t end_time, uint64_t boot_end,
                                                       PartGeo g, uint4* __restrict__ stage,
                                                       uint32_t* __restrict__ gcnt, uint32_t* __restrict__ wcnt,
@@ -2207,7 +2210,7 @@ __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* 
                                                      ShdDeliv* __restrict__ grouped) {
     const uint32_t m = *nwide;
     if (m == 0 || m > wide_cap) return; // (block-uniform; an overfull list is the sort's fault to report)
-    __shared__ uint32_t woff[kPartMaxBuckets];
+    extern __shared__ uint32_t woff[]; // [nb]
     __shared__ uint32_t wsum[16];
     const uint32_t per = (g.nb + 1023) / 1024, b0 = threadIdx.x * per;
     uint32_t sm = 0;
@@ -3124,6 +3127,7 @@ PartCfg part_cfg(uint32_t nb) {
     if (k == 1) return {(const void*)k_part_scatter<1024, 4096, false>, 1024, 4096, false};
     if (k == 2) return {(const void*)k_part_scatter<512, 2048, false>, 512, 2048, false};
     if (k == 3) return {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false};
+    if (k == 4) return {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false};
     return {(const void*)k_part_scatter<1024, 4096, true>, 1024, 4096, true};
 }
 size_t part_lds(const PartCfg& f, uint32_t nb) {
@@ -3135,7 +3139,16 @@ int part_attr() {
     const PartCfg cfgs[] = {{(const void*)k_part_scatter<1024, 4096, true>, 1024, 4096, true},
                             {(const void*)k_part_scatter<1024, 4096, false>, 1024, 4096, false},
                             {(const void*)k_part_scatter<512, 2048, false>, 512, 2048, false},
-                            {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false}};
+                            {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 1>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 2>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 3>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 4>, 1024, 4096, false}};
+    if (int rc = hip_status(hipFuncSetAttribute((const void*)k_wide_group, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)(4 * kPartMaxBuckets)),
+                            "hipFuncSetAttribute k_wide_group"))
+        return rc;
     for (const PartCfg& f : cfgs)
         if (int rc = hip_status(hipFuncSetAttribute(f.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                     (int)part_lds(f, f.lds ? kPartMaxBucketsLds : kPartMaxBuckets)),
@@ -3168,13 +3181,14 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
             else if (pr == 3) SHD_PART_LAUNCH(1024, 4096, false, 3);
             else SHD_PART_LAUNCH(1024, 4096, false, 4);
         } else if (f.lds) SHD_PART_LAUNCH(1024, 4096, true);
+        else if (f.fn == (const void*)k_part_scatter<1024, 4096, false, 0, 8>) SHD_PART_LAUNCH(1024, 4096, false, 0, 8);
         else if (f.wg == 1024) SHD_PART_LAUNCH(1024, 4096, false);
         else if (f.wg == 512) SHD_PART_LAUNCH(512, 2048, false);
         else SHD_PART_LAUNCH(256, 2048, false);
 #undef SHD_PART_LAUNCH
         // the wide list by bucket (w.tmp: unused by this pipeline), for the
         // second pass to read its buckets' own
-        hipLaunchKernelGGL(k_wide_group, dim3(64), dim3(1024), 0, s, g, w.st2, w.nbig + 1, (uint32_t)w.cap_n, wcnt,
+        hipLaunchKernelGGL(k_wide_group, dim3(64), dim3(1024), 4 * (size_t)g.nb, s, g, w.st2, w.nbig + 1, (uint32_t)w.cap_n, wcnt,
                            w.cnt1 + 2 * g.nb, w.tmp);
     }
     mark(1, s);

@@ -296,6 +296,22 @@ int shd_topology_latency_table_fw(ShdTopology* t, void* d_lat, void* stream) {
     return rc;
 }
 
+int shd_topology_latency_rows_frontier(ShdTopology* t, int row_lo, int row_hi, void* d_lat, void* stream) {
+    if (!t || !d_lat) return -EINVAL;
+    pthread_mutex_lock(&t->setup_mu);
+    int rc = prepare(t);
+    if (!rc && (row_lo < 0 || row_hi > t->A || row_lo > row_hi)) rc = shd_fail(-EINVAL, "row range out of bounds");
+    ShdGraphDev g = graph_dev(t);
+    double wmax = 0.0;
+    for (int e = 0; !rc && e < t->E; e++)
+        if (t->e_ms[e] > wmax) wmax = t->e_ms[e];
+    if (!rc) rc = shd_dev_init(t->device);
+    if (!rc) rc = shd_dev_frontier_latency(&g, row_lo, row_hi, wmax > 2147483647.0 ? -1 : (int)wmax, (double*)d_lat,
+                                           stream);
+    pthread_mutex_unlock(&t->setup_mu);
+    return rc;
+}
+
 /* ---- single-process multi-GPU build (shd_topology_build_shards) ---- */
 
 /* The device graph arrays of prepare(), with their sizes (bytes). */

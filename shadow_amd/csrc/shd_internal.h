@@ -112,6 +112,9 @@ int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi,
  * time), freed with shd_dev_fw_scratch_free. */
 int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat, void** scratch, void* stream);
 void shd_dev_fw_scratch_free(void* scratch);
+/* Latency rows [row_lo, row_hi) by the bucketed frontier SSSP (frontier.hip):
+ * whole-ms graphs, wmax = the largest edge latency in ms; synchronous. */
+int shd_dev_frontier_latency(const ShdGraphDev* g, int row_lo, int row_hi, int wmax, double* d_lat, void* stream);
 /* min latency over the entries (i, j), i < j, lat >= 0, of rows [row_lo,
  * row_hi) of an A-column table (rows: row i at rows + (i - row_lo) * A); -1 if none */
 int shd_dev_min_upper(const ShdEntry* rows, int A, int row_lo, int row_hi, double* out);

@@ -126,6 +126,13 @@ class Topology:
         synchronous; else enqueued on that hipStream_t."""
         check(lib().shd_topology_latency_table_fw(self._h, C.c_void_p(d_lat_ptr), C.c_void_p(stream)))
 
+    def latency_rows_frontier(self, row_lo: int, row_hi: int, d_lat_ptr: int, stream: int = 0):
+        """Rows [row_lo, row_hi) of the latency column by the bucketed frontier
+        SSSP into device memory ((row_hi - row_lo) * A doubles); whole-ms
+        graphs only; synchronous."""
+        check(lib().shd_topology_latency_rows_frontier(self._h, row_lo, row_hi, C.c_void_p(d_lat_ptr),
+                                                       C.c_void_p(stream)))
+
     def adopt_table_device(self, d_table_ptr: int):
         check(lib().shd_topology_adopt_table_device(self._h, C.c_void_p(d_table_ptr)))
 

@@ -71,6 +71,15 @@ int shd_dev_fw_latency(const ShdGraphDev* g, double* d_lat, void** scratch, void
     return -ENOTSUP;
 }
 void shd_dev_fw_scratch_free(void* scratch) { (void)scratch; }
+int shd_dev_frontier_latency(const ShdGraphDev* g, int row_lo, int row_hi, int wmax, double* d_lat, void* stream) {
+    (void)g;
+    (void)row_lo;
+    (void)row_hi;
+    (void)wmax;
+    (void)d_lat;
+    (void)stream;
+    return -ENOTSUP;
+}
 
 int shd_dev_build_rows(const ShdGraphDev* g, int use_sp, int row_lo, int row_hi, ShdEntry* tab) {
     (void)use_sp;

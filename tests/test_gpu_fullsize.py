@@ -100,6 +100,13 @@ def test_c2_full_table_bit_exact(ns):
         bad += [int(x) for x in rows[diff]]
         print(f"[c2] rows {b}..{b + len(rows)} of {A} compared ({time.perf_counter() - t0:.1f}s)", flush=True)
     assert not bad, f"{len(bad)} rows differ, first {bad[:8]}"
+    if not ns:  # whole-ms: the frontier SSSP's latencies equal the table's, every row
+        d = torch.empty(A * A, dtype=torch.float64, device="cuda")
+        t1 = time.perf_counter()
+        top.latency_rows_frontier(0, A, d.data_ptr())
+        print(f"[c2] frontier latencies of all {A} rows in {time.perf_counter() - t1:.3f}s", flush=True)
+        assert torch.equal(d.view(A, A), full.view(A, A, 2)[:, :, 0])
+        del d
     del full
     torch.cuda.empty_cache()
 
@@ -181,6 +188,27 @@ def test_c4_sampled_rows_bit_exact(c4):
            if not (np.array_equal(bits(got[i, :, 0]), bits(olat[i])) and np.array_equal(bits(got[i, :, 1]),
                                                                                      bits(orel[i])))]
     assert not bad, f"rows differ: {bad[:8]}"
+
+
+@pytest.mark.timeout(600)
+def test_c4_frontier_latencies_all_rows(c4):
+    """The frontier SSSP's latencies for all 86,603 rows of C4 against the
+    heap kernel's table (an independent algorithm: Dial's buckets vs igraph's
+    binary heap), in blocks of 8,192 rows compared on the device."""
+    import time
+
+    import torch
+    top, A, full = c4["top"], c4["A"], c4["full"]
+    blk = 8192
+    d = torch.empty(blk * A, dtype=torch.float64, device="cuda")
+    t0 = time.perf_counter()
+    for b in range(0, A, blk):
+        e = min(A, b + blk)
+        top.latency_rows_frontier(b, e, d.data_ptr())
+        assert torch.equal(d[:(e - b) * A].view(e - b, A), full.view(A, A, 2)[b:e, :, 0]), f"rows {b}..{e}"
+        print(f"[c4] frontier rows {b}..{e} equal ({time.perf_counter() - t0:.1f}s)", flush=True)
+    del d
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.timeout(400)

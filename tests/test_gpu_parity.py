@@ -758,6 +758,39 @@ def test_minplus_latencies_equal_table(name):
     assert np.array_equal(bits(fw), bits(lat)), name
 
 
+@pytest.mark.parametrize("name", ["complete30_ms", "complete25_dir", "sparse300_ms", "sparse5000_hbm", "dense4400_hbm"])
+def test_frontier_latencies_equal_table(name):
+    """shd_topology_latency_rows_frontier (bucketed frontier SSSP, one wave per
+    source): the latency half of the table, bit for bit, self paths and
+    directed graphs included -- all rows, and a sub-range written from its
+    first row."""
+    import torch
+    gml, H = GRAPHS[name]
+    top, orc, _, _ = make_pair(gml, H)
+    lat, rel, sv = top.table()
+    A = len(sv)
+    d = torch.full((A * A,), 7.0, dtype=torch.float64, device="cuda")
+    top.latency_rows_frontier(0, A, d.data_ptr())
+    assert np.array_equal(bits(d.cpu().numpy().reshape(A, A)), bits(lat)), name
+    lo, hi = A // 3, A // 3 + max(1, A // 4)
+    d2 = torch.full(((hi - lo) * A,), 7.0, dtype=torch.float64, device="cuda")
+    top.latency_rows_frontier(lo, hi, d2.data_ptr())
+    assert np.array_equal(bits(d2.cpu().numpy().reshape(hi - lo, A)), bits(lat[lo:hi])), name
+
+
+def test_frontier_needs_whole_ms():
+    """Fractional-ms latencies: the frontier entry declines (-ENOTSUP)."""
+    import torch
+    gml, H = GRAPHS["sparse300_ns"]
+    top, _, _, _ = make_pair(gml, H)
+    A = top.slot_count()
+    d = torch.empty(A * A, dtype=torch.float64, device="cuda")
+    from shadow_amd._lib import ShdError
+    with pytest.raises(ShdError) as ei:
+        top.latency_rows_frontier(0, A, d.data_ptr())
+    assert ei.value.code == -95  # ENOTSUP
+
+
 def test_minplus_needs_whole_ms():
     """Fractional-ms latencies: the min-plus entry declines (-ENOTSUP)."""
     import torch
