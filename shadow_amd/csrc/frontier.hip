@@ -53,8 +53,8 @@ __device__ __forceinline__ void wave_sync_mem() {
 }
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 
-// per-wave LDS: head[nbk] | tail[nbk] | fill[nbk] | offs[64] | starts[64]
-__host__ __device__ constexpr size_t dial_lds_words(int nbk) { return 3 * (size_t)nbk + 128; }
+// per-wave LDS: head[nbk] | tail[nbk] | fill[nbk] | offs[64] | starts[64] | htab[64]
+__host__ __device__ constexpr size_t dial_lds_words(int nbk) { return 3 * (size_t)nbk + 192; }
 
 // rows: rowlist[0 .. nrows) (or row_lo + i when rowlist is null); a row whose
 // chunk pool ran out is appended to redo (for a second launch with the
@@ -71,6 +71,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_sssp_dial(ShdGraphDev g, int ro
     uint32_t* fill = tail + nbk;
     uint32_t* offs = fill + nbk;
     uint32_t* starts = offs + 64;
+    uint32_t* htab = starts + 64;
     uint32_t* dist = reinterpret_cast<uint32_t*>(slab + (size_t)gw * stride);
     uint32_t* pool = dist + Vp;
     uint32_t* nxt = pool + (size_t)nchunk * 64;
@@ -84,7 +85,8 @@ __global__ __launch_bounds__(64 * kWaves) void k_sssp_dial(ShdGraphDev g, int ro
         for (int v = lane; v < Vp; v += 64) dist[v] = kInf;
         for (int b = lane; b < nbk; b += 64) head[b] = kNone, fill[b] = 0u;
         wave_sync_mem();
-        uint32_t bump = 0, ftop = 0; // chunk allocation (wave-uniform)
+        uint32_t bump = 0, ftop = 0, fsafe = 0; // chunk allocation (wave-uniform); fsafe: free-stack
+                                                // entries stored before the last fence
         bool failed = false;
         // the source: bucket 0
         bump = 1;
@@ -112,14 +114,17 @@ __global__ __launch_bounds__(64 * kWaves) void k_sssp_dial(ShdGraphDev g, int ro
                 ftop++;
                 pending -= n;
                 c = nx;
-                // settled (stale entries: the vertex improved since it was pushed)
-                const bool live = v >= 0 && dist[v] == cur;
-                uint32_t deg = 0, st = 0;
-                if (live) {
-                    const int a = g.inc_off[v];
-                    deg = (uint32_t)(g.inc_off[v + 1] - a);
-                    st = (uint32_t)(a + v); // (sl: one sentinel per list before it)
+                // settled (stale entries: the vertex improved since it was
+                // pushed); its distance and list bounds in one round trip
+                uint32_t dv = kInf;
+                int a0 = 0, a1 = 0;
+                if (v >= 0) {
+                    dv = dist[v];
+                    a0 = g.inc_off[v];
+                    a1 = g.inc_off[v + 1];
                 }
+                const bool live = v >= 0 && dv == cur;
+                const uint32_t deg = live ? (uint32_t)(a1 - a0) : 0u;
                 uint32_t incl = deg;
                 for (int o = 1; o < 64; o <<= 1) {
                     const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
@@ -127,28 +132,46 @@ __global__ __launch_bounds__(64 * kWaves) void k_sssp_dial(ShdGraphDev g, int ro
                 }
                 const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 offs[lane] = incl - deg;
-                starts[lane] = st;
-                wave_sync_mem();
-                for (uint32_t e0 = 0; e0 < T; e0 += 64) {
-                    const uint32_t e = e0 + (uint32_t)lane;
-                    const bool act = e < T;
-                    int o = 0; // the last lane whose edges start at or before e
-#pragma unroll
-                    for (int s = 32; s > 0; s >>= 1)
-                        if (offs[o + s] <= e) o += s;
+                starts[lane] = (uint32_t)(a0 + v); // (sl: one sentinel per list before it)
+                __asm__ volatile("" ::: "memory"); // (LDS: the wave's own accesses stay in order)
+                // batch e0's entries (issued one batch ahead of their use)
+                auto entry = [&](uint32_t e) {
                     Ent en{-1, 0u, 0.0};
-                    if (act) en = sl[starts[o] + (e - offs[o])];
+                    if (e < T) {
+                        int o = 0; // the last lane whose edges start at or before e
+#pragma unroll
+                        for (int s = 32; s > 0; s >>= 1)
+                            if (offs[o + s] <= e) o += s;
+                        en = sl[starts[o] + (e - offs[o])];
+                    }
+                    return en;
+                };
+                Ent en = entry((uint32_t)lane);
+                for (uint32_t e0 = 0; e0 < T; e0 += 64) {
+                    const Ent nx_en = entry(e0 + 64 + (uint32_t)lane);
+                    const bool act = e0 + (uint32_t)lane < T;
                     const uint32_t alt = cur + en.w;
                     bool imp = act && alt < dist[en.nbr];
-                    bool push = false;
-                    while (__ballot(imp)) { // equal neighbours in one batch settle on their minimum
-                        if (imp) dist[en.nbr] = alt;
-                        wave_sync_mem();
-                        if (imp) {
-                            const uint32_t now = dist[en.nbr];
-                            push |= now == alt;
-                            imp = now > alt;
+                    bool push = imp;
+                    // two lanes improving the same neighbour: found through an
+                    // LDS table (neighbour mod 64: a collision is only a false
+                    // alarm); then they settle on the minimum by store and re-read
+                    if (imp) htab[en.nbr & 63] = (uint32_t)lane;
+                    __asm__ volatile("" ::: "memory");
+                    const bool clash = imp && htab[en.nbr & 63] != (uint32_t)lane;
+                    if (__ballot(clash)) {
+                        push = false;
+                        while (__ballot(imp)) {
+                            if (imp) dist[en.nbr] = alt;
+                            wave_sync_mem();
+                            if (imp) {
+                                const uint32_t now = dist[en.nbr];
+                                push |= now == alt;
+                                imp = now > alt;
+                            }
                         }
+                    } else if (imp) {
+                        dist[en.nbr] = alt;
                     }
                     // pushes, grouped by bucket
                     const uint32_t bk = b + en.w >= (uint32_t)nbk ? b + en.w - (uint32_t)nbk : b + en.w;
@@ -166,9 +189,18 @@ __global__ __launch_bounds__(64 * kWaves) void k_sssp_dial(ShdGraphDev g, int ro
                         uint32_t need = (empty ? 1u : 0u) + ((empty ? 0u : tc) + cnt > 64u ? 1u : 0u);
                         uint32_t got[2] = {kNone, kNone};
                         for (uint32_t q = 0; q < need; q++) {
-                            if (ftop > 0) got[q] = uni(fstk[--ftop]);
-                            else if (bump < nchunk) got[q] = bump++;
-                            else failed = true;
+                            if (ftop > 0) {
+                                if (ftop > fsafe) { // (an entry stored since the last fence)
+                                    wave_sync_mem();
+                                    fsafe = ftop;
+                                }
+                                got[q] = uni(fstk[--ftop]);
+                                fsafe = ftop < fsafe ? ftop : fsafe;
+                            } else if (bump < nchunk) {
+                                got[q] = bump++;
+                            } else {
+                                failed = true;
+                            }
                         }
                         if (failed) break;
                         if (empty) {
@@ -195,7 +227,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_sssp_dial(ShdGraphDev g, int ro
                         pending += cnt;
                         if (bk == bb) push = false;
                     }
+                    // the batch's stores seen by the next batch's gathers
                     wave_sync_mem();
+                    fsafe = ftop;
+                    en = nx_en;
                     if (failed) break;
                 }
             }
