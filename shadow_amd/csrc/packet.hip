@@ -1946,6 +1946,7 @@ __global__ __launch_bounds__(256) void k_group_wire(const ShdDeliv* __restrict__
 // k_segsort_mid / k_segsort_merge (skewed destinations).
 constexpr uint32_t kPartMaxDst = 64; // destinations per bucket (shift <= 6)
 constexpr uint32_t kPartMaxBuckets = 16384; // register-staged scatter: 8 B of LDS per bucket
+constexpr uint32_t kTinySeg = 16;           // part sort: segments ranked one thread per event
 constexpr uint32_t kPartMaxBucketsLds = 4096; // LDS-staged scatter: + 20 B per record
 
 struct PartGeo {
@@ -2235,7 +2236,10 @@ __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* 
 // One workgroup of kWG threads per bucket of at most kCap events held in
 // LDS (7 per thread; see above).  nbig / big / scr: the listed segments
 // (k_segsort_mid); fault: nbig[2] guard bits.
-template <int kWG, int kCap>
+// kKeyE: the per-wave LDS key array holds segments of up to 64 kKeyE events
+// (larger ones up to kSmallSeg take the readlane form): 4, or 2 for the
+// instance sized for three workgroups per CU
+template <int kWG, int kCap, int kKeyE = 4>
 __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
                                                           const uint32_t* __restrict__ wcnt,
@@ -2246,7 +2250,7 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
     __shared__ uint4 lev[kCap];
-    __shared__ unsigned long long keys[kWG / 64][64 * 4 + 8];
+    __shared__ unsigned long long keys[kWG / 64][64 * kKeyE + 8];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kWG / 64];
     __shared__ uint32_t s_base, s_wbase;
     const uint32_t b = blockIdx.x;
@@ -2325,17 +2329,41 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
             }
         }
         __syncthreads();
+        // segments of at most kTinySeg events (many destinations per bucket,
+        // few events each: C4's rounds): one thread per event, its rank the
+        // count of its segment's events before it in event_compare order
+        // (time, src, srcHostEventID -- the stage record's time offset, src and
+        // 32-bit id compare as the full values do)
+        for (uint32_t i = threadIdx.x; i < ns; i += kWG) {
+            const uint4 r = lev[i];
+            const uint32_t dl = r.w & mask, nj = cnt[dl];
+            if (nj > kTinySeg) continue;
+            const uint32_t o = loc[dl], sr = r.w >> g.shift;
+            uint32_t rank = 0;
+            for (uint32_t j = o; j < o + nj; j++) {
+                const uint4 x = lev[j];
+                const uint32_t sx = x.w >> g.shift;
+                rank += (uint32_t)(x.x < r.x || (x.x == r.x && (sx < sr || (sx == sr && x.y < r.y))));
+            }
+            const unsigned long long t = g.tbase + r.x;
+            shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[obase + o + rank]);
+            const shd_v4u a = {(uint32_t)t, (uint32_t)(t >> 32), r.y, 0u};
+            const shd_v4u c2 = {sr, g.host_lo + d0 + dl, r.z, 0u};
+            __builtin_nontemporal_store(a, q);
+            __builtin_nontemporal_store(c2, q + 1);
+        }
         unsigned long long* lk = lds_keys ? keys[wv] : nullptr;
         for (uint32_t j = wv; j < nd; j += kWG / 64) {
             const uint32_t nj = cnt[j], o = loc[j], dh = g.host_lo + d0 + j;
-            if (nj == 0) continue;
+            if (nj <= kTinySeg) continue;
             auto load = [&](uint32_t i) {
                 const uint4 r = lev[o + i];
                 return Ev{g.tbase + r.x, (unsigned long long)r.y, r.w >> g.shift, r.z};
             };
             if (nj <= 64) wave_rank_segment<1, 1>(load, nj, dh, out, obase + o, lane, lk);
             else if (nj <= 128) wave_rank_segment<2, 1>(load, nj, dh, out, obase + o, lane, lk);
-            else if (nj <= (uint32_t)kSmallSeg) wave_rank_segment<4, 1>(load, nj, dh, out, obase + o, lane, lk);
+            else if (nj <= (uint32_t)kSmallSeg)
+                wave_rank_segment<4, 1>(load, nj, dh, out, obase + o, lane, kKeyE >= 4 ? lk : nullptr);
             else { // a larger segment: unsorted to its range of the staging array, listed
                 for (uint32_t i = lane; i < nj; i += 64) {
                     const Ev v = load(i);
@@ -2942,9 +2970,9 @@ constexpr size_t kMaxSlabBytes = 32ull << 30;
 int part_sort_cfg() {
     const char* v = getenv("SHD_PART_SORT");
     const int k = v ? atoi(v) : 1;
-    return k >= 0 && k <= 2 ? k : 1;
+    return k >= 0 && k <= 3 ? k : 1;
 }
-constexpr int kPartSortCap[3] = {7168, 3584, 1792};
+constexpr int kPartSortCap[4] = {7168, 3584, 1792, 2304};
 
 // Geometry of the part pipeline for n records over H destinations: the
 // widest buckets (shift <= 6) whose expected load stays within the LDS sort's
@@ -3212,11 +3240,12 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
     mark_same(3, 2);
     {
         const int sc = part_sort_cfg();
-#define SHD_PART_SORT_LAUNCH(WG, CAP)                                                                                 \
-    hipLaunchKernelGGL((k_part_sort<WG, CAP>), dim3(g.nb), dim3(WG), 0, s, g, w.pstage, gcnt, wcnt, w.tmp, w.nbig + 1, \
+#define SHD_PART_SORT_LAUNCH(WG, CAP, ...)                                                                            \
+    hipLaunchKernelGGL((k_part_sort<WG, CAP, ##__VA_ARGS__>), dim3(g.nb), dim3(WG), 0, s, g, w.pstage, gcnt, wcnt, w.tmp, w.nbig + 1, \
                        (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, lds_keys())
         if (sc == 1) SHD_PART_SORT_LAUNCH(512, 3584);
         else if (sc == 2) SHD_PART_SORT_LAUNCH(256, 1792);
+        else if (sc == 3) SHD_PART_SORT_LAUNCH(512, 2304, 2);
         else SHD_PART_SORT_LAUNCH(1024, 7168);
 #undef SHD_PART_SORT_LAUNCH
     }
