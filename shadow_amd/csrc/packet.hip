@@ -2239,8 +2239,8 @@ __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* 
 // kKeyE: the per-wave LDS key array holds segments of up to 64 kKeyE events
 // (larger ones up to kSmallSeg take the readlane form): 4, or 2 for the
 // instance sized for three workgroups per CU
-template <int kWG, int kCap, int kKeyE = 4>
-__global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
+template <int kWG, int kCap, int kKeyE>
+__device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
                                                           const uint32_t* __restrict__ wcnt,
                                                           const ShdDeliv* __restrict__ wide,
@@ -2250,7 +2250,7 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
     __shared__ uint4 lev[kCap];
-    __shared__ unsigned long long keys[kWG / 64][64 * kKeyE + 8];
+    __shared__ unsigned long long keys[kWG / 64][kKeyE ? 64 * kKeyE + 8 : 1];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kWG / 64];
     __shared__ uint32_t s_base, s_wbase;
     const uint32_t b = blockIdx.x;
@@ -2352,7 +2352,7 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
             __builtin_nontemporal_store(a, q);
             __builtin_nontemporal_store(c2, q + 1);
         }
-        unsigned long long* lk = lds_keys ? keys[wv] : nullptr;
+        unsigned long long* lk = lds_keys && kKeyE ? keys[wv] : nullptr;
         for (uint32_t j = wv; j < nd; j += kWG / 64) {
             const uint32_t nj = cnt[j], o = loc[j], dh = g.host_lo + d0 + j;
             if (nj <= kTinySeg) continue;
@@ -2361,7 +2361,7 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
                 return Ev{g.tbase + r.x, (unsigned long long)r.y, r.w >> g.shift, r.z};
             };
             if (nj <= 64) wave_rank_segment<1, 1>(load, nj, dh, out, obase + o, lane, lk);
-            else if (nj <= 128) wave_rank_segment<2, 1>(load, nj, dh, out, obase + o, lane, lk);
+            else if (nj <= 128) wave_rank_segment<2, 1>(load, nj, dh, out, obase + o, lane, kKeyE >= 2 ? lk : nullptr);
             else if (nj <= (uint32_t)kSmallSeg)
                 wave_rank_segment<4, 1>(load, nj, dh, out, obase + o, lane, kKeyE >= 4 ? lk : nullptr);
             else { // a larger segment: unsorted to its range of the staging array, listed
@@ -2400,6 +2400,33 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
             if (k < g.H) big[k] = d0 + j;
             else atomicOr(nbig + 2, kFaultBigCap);
         }
+}
+
+// the kernels: the compiler's register choice, or sized for kOcc waves per
+// SIMD (SHD_PART_SORT=4: no LDS keys, 63 VGPRs, four workgroups per CU)
+template <int kWG, int kCap, int kKeyE = 4>
+__global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
+                                                          const uint32_t* __restrict__ gcnt,
+                                                          const uint32_t* __restrict__ wcnt,
+                                                          const ShdDeliv* __restrict__ wide,
+                                                          const uint32_t* __restrict__ nwide, uint32_t wide_cap,
+                                                          uint32_t* __restrict__ offsets, ShdDeliv* __restrict__ out,
+                                                          ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
+                                                          uint32_t* __restrict__ nbig,
+                                                          unsigned long long* __restrict__ counters, uint32_t lds_keys) {
+    part_sort_body<kWG, kCap, kKeyE>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig, counters, lds_keys);
+}
+template <int kWG, int kCap, int kKeyE, int kOcc>
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc, kOcc))) void k_part_sort_occ(PartGeo g, const uint4* __restrict__ stage,
+                                                          const uint32_t* __restrict__ gcnt,
+                                                          const uint32_t* __restrict__ wcnt,
+                                                          const ShdDeliv* __restrict__ wide,
+                                                          const uint32_t* __restrict__ nwide, uint32_t wide_cap,
+                                                          uint32_t* __restrict__ offsets, ShdDeliv* __restrict__ out,
+                                                          ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
+                                                          uint32_t* __restrict__ nbig,
+                                                          unsigned long long* __restrict__ counters, uint32_t lds_keys) {
+    part_sort_body<kWG, kCap, kKeyE>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig, counters, lds_keys);
 }
 
 // The exchanged round's sender side on the part pipeline (see
@@ -2961,18 +2988,20 @@ enum Pipeline { kBucketPipe = 0, kRankPipe = 1, kSlabPipe = 2, kPartPipe = 3 };
 constexpr size_t kMaxSlabBytes = 32ull << 30;
 
 // k_part_sort instances (SHD_PART_SORT, measurement knob): 0: 1024 threads,
-// 7,168 events in LDS (one workgroup per CU); 1 (default): 512 threads, 3,584
-// (two per CU); 2: 256 threads, 1,792 (four).  The buckets are sized for the
-// instance.  C3 (profiles/r04c_part_sort_cfg.log): round 0.664 ms with 1 --
-// sort 0.184 ms, scatter 0.440 ms over 6,250 buckets -- vs 0.676 with 0 (sort
-// 0.214, scatter 0.418 over 3,125); 2 needs 12,500 buckets, above the
-// scatter's 8,192, and C3 falls back to the slab form.
+// 7,168 events in LDS (one workgroup per CU); 1: 512 threads, 3,584 (two per
+// CU); 2: 256 threads, 1,792 (four); 3 (default): 512 threads, 2,304, keys
+// for segments up to 128 in LDS (46 KB, 71 VGPRs: three per CU).  The buckets
+// are sized for the instance.  C3: round 0.611-0.616 ms with 3 (sort 0.159 ms)
+// vs 0.635-0.643 with 1 (sort 0.183, profiles/r04l_part_sort_3wg.log), 0.676
+// with 0; 2 needs 12,500 buckets (scatter 0.475 ms, profiles/r04i_part_sort_256.log);
+// 4: instance 3 without the LDS keys at 63 VGPRs, four per CU: sort 0.197 ms
+// (profiles/r04m_part_sort_occ8.log).
 int part_sort_cfg() {
     const char* v = getenv("SHD_PART_SORT");
-    const int k = v ? atoi(v) : 1;
-    return k >= 0 && k <= 3 ? k : 1;
+    const int k = v ? atoi(v) : 3;
+    return k >= 0 && k <= 4 ? k : 3;
 }
-constexpr int kPartSortCap[4] = {7168, 3584, 1792, 2304};
+constexpr int kPartSortCap[5] = {7168, 3584, 1792, 2304, 2304};
 
 // Geometry of the part pipeline for n records over H destinations: the
 // widest buckets (shift <= 6) whose expected load stays within the LDS sort's
@@ -3246,6 +3275,10 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         if (sc == 1) SHD_PART_SORT_LAUNCH(512, 3584);
         else if (sc == 2) SHD_PART_SORT_LAUNCH(256, 1792);
         else if (sc == 3) SHD_PART_SORT_LAUNCH(512, 2304, 2);
+        else if (sc == 4)
+            hipLaunchKernelGGL((k_part_sort_occ<512, 2304, 0, 8>), dim3(g.nb), dim3(512), 0, s, g, w.pstage, gcnt, wcnt,
+                               w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters,
+                               lds_keys());
         else SHD_PART_SORT_LAUNCH(1024, 7168);
 #undef SHD_PART_SORT_LAUNCH
     }

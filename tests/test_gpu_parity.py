@@ -183,7 +183,7 @@ def test_unattached_address():
 
 
 @pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor", "slab_readlane", "slab_noagg", "rank_noagg",
-                        "slab_unfused", "slab_wide", "part", "part_readlane", "part_lds", "part_s1", "part_s2", "part_s3"])
+                        "slab_unfused", "slab_wide", "part", "part_readlane", "part_lds", "part_s1", "part_s2", "part_s3", "part_s4"])
 def pipeline(request, monkeypatch):
     """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE: bucket,
     rank, slab, part -- the LDS-staged bucket partition + per-bucket LDS sort;
