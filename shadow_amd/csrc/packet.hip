@@ -2533,7 +2533,8 @@ struct Ws {
     uint4* pstage = nullptr;
     uint32_t* meta = nullptr; // big-segment merge metadata (MergeMeta)
     uint32_t cap_meta = 0;    // merge segments it holds
-    uint32_t* fault = nullptr; // pinned host copy of the last round's merge fault word (meta hdr[3])
+    uint32_t* fault = nullptr; // pinned host buffer the sticky fault word is read into
+    hipStream_t rd = nullptr;  // the stream that read uses (non-blocking)
     void* xdev = nullptr;      // exchange scratch (xchg.hip: route counts / offsets, event cuts), grow-only
     size_t cap_xdev = 0;
     void* xhost = nullptr;     // its pinned host side (read back on the launch stream)
@@ -2690,13 +2691,9 @@ int mid_attr() {
 // memory at the end of a round, on its stream.  The device only ORs into the
 // sticky word, so a round that finishes before the host looked cannot hide
 // an earlier round's fault.
-int copy_faults(Ws& w, hipStream_t s) {
-    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
-        w.fault = nullptr;
-        return shd_fail(-ENOMEM, "hipHostMalloc fault word");
-    }
-    return hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 4, hipMemcpyDeviceToHost, s), "fault word D2H");
-}
+// (the sticky word stays on the device; ws_faults reads it once the
+// workspace's last use has completed -- nothing on the round's stream)
+int copy_faults(Ws&, hipStream_t) { return 0; }
 
 // listed segments: LDS runs, then the merge passes of the larger ones.  A
 // round's fault (tiles that gave up waiting for their segment's previous
@@ -2726,9 +2723,23 @@ int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDel
 // destination segment may be mis-sorted), the merge metadata overflowed or a
 // stage guard fired.
 int ws_faults(Ws& w, bool completed, hipStream_t s) {
-    if (!w.used || !w.fault) return 0;
+    if (!w.used || !w.meta) return 0;
     if (!completed && hipEventQuery(w.done) != hipSuccess) return 0;
-    const uint32_t f = __atomic_load_n(w.fault, __ATOMIC_ACQUIRE);
+    // the word, read on a stream of the workspace's own (it waits for nothing
+    // else: the use it reports on has completed)
+    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
+        w.fault = nullptr;
+        return shd_fail(-ENOMEM, "hipHostMalloc fault word");
+    }
+    if (!w.rd && hipStreamCreateWithFlags(&w.rd, hipStreamNonBlocking) != hipSuccess) {
+        w.rd = nullptr;
+        return shd_fail(-EIO, "hipStreamCreate fault read");
+    }
+    if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 4, hipMemcpyDeviceToHost, w.rd),
+                            "fault word D2H"))
+        return rc;
+    if (int rc = hip_status(hipStreamSynchronize(w.rd), "fault word read")) return rc;
+    const uint32_t f = *w.fault;
     if (!f) return 0;
     *w.fault = 0;
     (void)(s ? hipMemsetAsync(w.meta + kStickyFault, 0, 4, s) : hipMemset(w.meta + kStickyFault, 0, 4));
@@ -3091,6 +3102,7 @@ extern "C" void shd_dev_ws_free(void* p) {
     (void)hipFree(w->pstage);
     (void)hipFree(w->meta);
     if (w->fault) (void)hipHostFree(w->fault);
+    if (w->rd) (void)hipStreamDestroy(w->rd);
     (void)hipFree(w->xdev);
     if (w->xhost) (void)hipHostFree(w->xhost);
     if (w->done) (void)hipEventDestroy(w->done);
