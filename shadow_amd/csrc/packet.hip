@@ -870,6 +870,26 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v)
     return v;
 }
 
+// The exchange's wire record (24 B): a delivered event without its
+// destination (the block and offsets say it) and without the slot word.
+// 25 % fewer bytes over xGMI than the 32-B ShdDeliv.
+struct Wire {
+    unsigned long long t, q;
+    uint32_t s, ix;
+};
+static_assert(sizeof(Wire) == 24, "wire record");
+__device__ __forceinline__ Ev ld_wire(const Wire* p) {
+    const uint2* w = reinterpret_cast<const uint2*>(p); // 8-B aligned
+    const uint2 a = w[0], b = w[1], c = w[2];
+    return Ev{((unsigned long long)a.y << 32) | a.x, ((unsigned long long)b.y << 32) | b.x, c.x, c.y};
+}
+__device__ __forceinline__ void st_wire(Wire* p, unsigned long long t, unsigned long long q, uint32_t src,
+                                        uint32_t ix) {
+    uint2* w = reinterpret_cast<uint2*>(p);
+    w[0] = make_uint2((uint32_t)t, (uint32_t)(t >> 32));
+    w[1] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
+    w[2] = make_uint2(src, ix);
+}
 template <int E, int kNT = 0, typename Load>
 __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* __restrict__ out, uint32_t o,
                                   int lane, unsigned long long* lk = nullptr) {
@@ -963,7 +983,9 @@ __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* _
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)(e * 64 + lane);
         if (i >= n) continue;
-        if (kNT) {
+        if (kNT == 2) { // the exchange's 24-B wire record (out is a Wire array)
+            st_wire(reinterpret_cast<Wire*>(out) + o + rank[e], v[e].t, v[e].q, v[e].s, v[e].ix);
+        } else if (kNT) {
             shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[o + rank[e]]);
             const shd_v4u a = {(uint32_t)v[e].t, (uint32_t)(v[e].t >> 32), (uint32_t)v[e].q, (uint32_t)(v[e].q >> 32)};
             const shd_v4u b = {v[e].s, d, v[e].ix, 0u};
@@ -1298,14 +1320,74 @@ __device__ void lds_sort_run(const ShdDeliv* src, ShdDeliv* dst, uint32_t b, uin
     __syncthreads();
 }
 
+// Listed segments of kSmallSeg < n <= kMedSeg events (the owners' segments
+// of a weak-scaled exchange: ~92 N events per destination at N ranks): one
+// wave each, a bitonic network over the segment in the wave's LDS region
+// (padded to a power of two) -- no workgroup barriers: a wave's LDS accesses
+// stay in order.  O(n log^2 n) compare-exchanges, against the register rank
+// sort's O(n^2) (whose tie pass -- equal time and sender, frequent when most
+// deliveries are clamped to the barrier -- is slower still) and
+// k_segsort_mid's 1,024-thread network per segment, one segment per
+// workgroup at a time.  k_segsort_mid then skips these segments.
+constexpr uint32_t kMedSeg = 1024;
+constexpr int kMedWaves = 2; // waves per workgroup (LDS: kMedSeg x 24 B each)
+__global__ __launch_bounds__(64 * kMedWaves) void k_segsort_medium(const ShdDeliv* __restrict__ unsorted,
+                                                                   const uint32_t* __restrict__ off,
+                                                                   const uint32_t* __restrict__ big,
+                                                                   const uint32_t* __restrict__ nbig,
+                                                                   ShdDeliv* __restrict__ out, uint32_t cap_big) {
+    __shared__ Ev sv_all[kMedWaves][kMedSeg];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    Ev* sv = sv_all[wv];
+    const uint32_t nb_raw = nbig[0];
+    const uint32_t nb = nb_raw <= cap_big ? nb_raw : 0u; // (an overfull list is k_segsort_mid's to report)
+    const uint32_t wave = blockIdx.x * kMedWaves + wv, nwaves = gridDim.x * kMedWaves;
+    for (uint32_t q = wave; q < nb; q += nwaves) {
+        const uint32_t d = big[q];
+        const uint32_t b = off[d], n = off[d + 1] - b;
+        if (n <= (uint32_t)kSmallSeg || n > kMedSeg) continue;
+        uint32_t N = 512;
+        while (N < n) N <<= 1;
+        const uint32_t dh = (uint32_t)__builtin_amdgcn_readfirstlane((int)unsorted[b].dst_host);
+        for (uint32_t i = lane; i < N; i += 64) {
+            if (i < n) {
+                const ShdDeliv r = ld_ev(&unsorted[b + i]);
+                sv[i] = Ev{r.time, r.seq, r.src_host, r.pkt_index};
+            } else {
+                sv[i] = Ev{~0ull, ~0ull, ~0u, ~0u};
+            }
+        }
+        for (uint32_t k = 2; k <= N; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1)
+                for (uint32_t p = lane; p < (N >> 1); p += 64) { // pair p: i = its lower index
+                    const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), l = i | j;
+                    const Ev x = sv[i], y = sv[l];
+                    if (((i & k) == 0) ? ev_lt(y, x) : ev_lt(x, y)) {
+                        sv[i] = y;
+                        sv[l] = x;
+                    }
+                }
+        for (uint32_t i = lane; i < n; i += 64) {
+            const Ev e = sv[i];
+            shd_v4u* qd = reinterpret_cast<shd_v4u*>(&out[b + i]);
+            const shd_v4u a0 = {(uint32_t)e.t, (uint32_t)(e.t >> 32), (uint32_t)e.q, (uint32_t)(e.q >> 32)};
+            const shd_v4u a1 = {e.s, dh, e.ix, 0u};
+            __builtin_nontemporal_store(a0, qd);
+            __builtin_nontemporal_store(a1, qd + 1);
+        }
+    }
+}
+
 // Every listed segment's kChunk-event runs, dealt round-robin over the
 // workgroups (a segment of up to kChunk events is one run, sorted straight
-// into `out`).  Workgroup 0 also builds the merge metadata.
+// into `out`).  Workgroup 0 also builds the merge metadata.  skip_med:
+// segments of kSmallSeg < n <= kMedSeg events are k_segsort_medium's.
 __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* unsorted,
                                                              const uint32_t* __restrict__ off,
                                                              const uint32_t* __restrict__ big,
                                                              const uint32_t* __restrict__ nbig, ShdDeliv* out,
-                                                             ShdDeliv* scratch, MergeMeta mm, uint32_t rank_small) {
+                                                             ShdDeliv* scratch, MergeMeta mm, uint32_t rank_small,
+                                                             uint32_t skip_med) {
     extern __shared__ __attribute__((aligned(16))) char mid_smem[];
     Ev* sv = reinterpret_cast<Ev*>(mid_smem);
     __shared__ uint32_t sb[kMidThreads], sn[kMidThreads], sst[kMidThreads + 1];
@@ -1324,7 +1406,7 @@ __global__ __launch_bounds__(kMidThreads) void k_segsort_mid(const ShdDeliv* uns
             b = off[d];
             n = off[d + 1] - b;
         }
-        const uint32_t nch = (n + kChunk - 1) / kChunk;
+        const uint32_t nch = (skip_med && n > (uint32_t)kSmallSeg && n <= kMedSeg) ? 0u : (n + kChunk - 1) / kChunk;
         uint32_t total;
         const uint32_t st = block_excl_scan_1k(nch, &total, ws);
         total = bu(total);
@@ -1773,26 +1855,6 @@ __global__ __launch_bounds__(256) void k_segsort_dst(ShdDeliv* __restrict__ scr,
 // scatter into destination slabs, only the per-destination union of W runs.
 constexpr uint32_t kMaxRuns = 64; // = xchg.hip kMaxWorld
 
-// The exchange's wire record (24 B): a delivered event without its
-// destination (the block and offsets say it) and without the slot word.
-// 25 % fewer bytes over xGMI than the 32-B ShdDeliv.
-struct Wire {
-    unsigned long long t, q;
-    uint32_t s, ix;
-};
-static_assert(sizeof(Wire) == 24, "wire record");
-__device__ __forceinline__ Ev ld_wire(const Wire* p) {
-    const uint2* w = reinterpret_cast<const uint2*>(p); // 8-B aligned
-    const uint2 a = w[0], b = w[1], c = w[2];
-    return Ev{((unsigned long long)a.y << 32) | a.x, ((unsigned long long)b.y << 32) | b.x, c.x, c.y};
-}
-__device__ __forceinline__ void st_wire(Wire* p, unsigned long long t, unsigned long long q, uint32_t src,
-                                        uint32_t ix) {
-    uint2* w = reinterpret_cast<uint2*>(p);
-    w[0] = make_uint2((uint32_t)t, (uint32_t)(t >> 32));
-    w[1] = make_uint2((uint32_t)q, (uint32_t)(q >> 32));
-    w[2] = make_uint2(src, ix);
-}
 // element i of a run-merge input: a ShdDeliv (kFmt 0) or a Wire (kFmt 1)
 template <int kFmt>
 __device__ __forceinline__ Ev ld_run(const void* in, uint32_t i) {
@@ -1814,8 +1876,11 @@ __global__ __launch_bounds__(256) void k_runs_count(const uint32_t* __restrict__
 // start and source index of each run) are read as one segment and ranked
 // like a slab segment; segments above kSmallSeg events are copied to their
 // final range of the staging array and listed for k_segsort_mid / _merge.
+// (self < W: run `self` is read from in_self -- this rank's own block, never
+// sent through the transport -- at its element index, the others from in)
 template <int kFmt>
-__global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, const uint32_t* __restrict__ rofs,
+__global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, const void* __restrict__ in_self,
+                                                   uint32_t self, const uint32_t* __restrict__ rofs,
                                                    const uint32_t* __restrict__ bbase, uint32_t W, uint32_t Hr,
                                                    const uint32_t* __restrict__ off, uint32_t host_lo,
                                                    ShdDeliv* __restrict__ out, ShdDeliv* __restrict__ scr,
@@ -1836,7 +1901,7 @@ __global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, 
         if ((uint32_t)lane < W) {
             const uint32_t a = rofs[(size_t)lane * (Hr + 1) + d];
             len = rofs[(size_t)lane * (Hr + 1) + d + 1] - a;
-            src = bbase[lane] + a;
+            src = ((uint32_t)lane == self ? 0u : bbase[lane]) + a;
         }
         const uint32_t inc = wave_incl_scan(len, lane);
         if ((uint32_t)lane < W) {
@@ -1847,19 +1912,19 @@ __global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        auto at = [&](uint32_t i) { // source index of segment element i (i < n)
+        auto get = [&](uint32_t i) { // segment element i (i < n), from its run
             uint32_t k = 0;
             while (rs[k + 1] <= i) k++;
-            return rb[k] + (i - rs[k]);
+            return ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
         };
         if (n <= (uint32_t)kSmallSeg) {
-            auto load = [&](uint32_t i) { return ld_run<kFmt>(in, at(i)); };
+            auto load = [&](uint32_t i) { return get(i); };
             if (n <= 64) wave_rank_segment<1>(load, n, d + host_lo, out, o, lane, lk);
             else if (n <= 128) wave_rank_segment<2>(load, n, d + host_lo, out, o, lane, lk);
             else wave_rank_segment<4>(load, n, d + host_lo, out, o, lane, lk);
         } else {
             for (uint32_t i = lane; i < n; i += 64) {
-                const Ev e = ld_run<kFmt>(in, at(i));
+                const Ev e = get(i);
                 st_ev(&scr[o + i], ShdDeliv{e.t, e.q, e.s, d + host_lo, e.ix, 0u});
             }
             if (lane == 0) {
@@ -1872,6 +1937,181 @@ __global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+// rank of x (element i of run k) in the union of sorted runs staged one
+// after another in v (run j at [rs[j], rs[j+1])): its index in its run +
+// the elements before it in every other run, ties to the lower run (the
+// union's stable order)
+__device__ __forceinline__ uint32_t merged_rank(const Ev* v, const uint32_t* rs, uint32_t W, uint32_t k, uint32_t i,
+                                                const Ev& x) {
+    uint32_t rank = i - rs[k];
+    for (uint32_t j = 0; j < W; j++) {
+        if (j == k) continue;
+        uint32_t lo = rs[j], hi = rs[j + 1];
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (j < k ? !ev_lt(x, v[mid]) : ev_lt(v[mid], x)) lo = mid + 1;
+            else hi = mid;
+        }
+        rank += lo - rs[j];
+    }
+    return rank;
+}
+
+__device__ __forceinline__ void st_deliv_nt(ShdDeliv* p, const Ev& x, uint32_t dh) {
+    shd_v4u* q = reinterpret_cast<shd_v4u*>(p);
+    const shd_v4u a0 = {(uint32_t)x.t, (uint32_t)(x.t >> 32), (uint32_t)x.q, (uint32_t)(x.q >> 32)};
+    const shd_v4u a1 = {x.s, dh, x.ix, 0u};
+    __builtin_nontemporal_store(a0, q);
+    __builtin_nontemporal_store(a1, q + 1);
+}
+
+// The merge of sorted runs for segments of up to kSmallSeg events: one wave
+// per destination, its runs staged in the wave's LDS, every element placed
+// by merged_rank (no workgroup barrier; k_runs_merge takes the longer ones).
+template <int kFmt>
+__global__ __launch_bounds__(256) void k_runs_merge_wave(const void* __restrict__ in, const void* __restrict__ in_self,
+                                                         uint32_t self, const uint32_t* __restrict__ rofs,
+                                                         const uint32_t* __restrict__ bbase, uint32_t W, uint32_t Hr,
+                                                         const uint32_t* __restrict__ off, uint32_t host_lo,
+                                                         ShdDeliv* __restrict__ out, uint32_t* __restrict__ longl,
+                                                         uint32_t* __restrict__ nlong) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wv;
+    const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+    __shared__ Ev sv_all[4][kSmallSeg];
+    __shared__ uint16_t inv_all[4][kSmallSeg];
+    __shared__ uint32_t rs_all[4][kMaxRuns + 1], rb_all[4][kMaxRuns];
+    Ev* v = sv_all[wv];
+    uint16_t* inv = inv_all[wv];
+    uint32_t* rs = rs_all[wv];
+    uint32_t* rb = rb_all[wv];
+    for (uint32_t d = wave; d < Hr; d += nwaves) {
+        const uint32_t o = off[d], n = off[d + 1] - o;
+        if (n == 0) continue;
+        if (n > (uint32_t)kSmallSeg) { // (k_runs_merge's, listed)
+            if (lane == 0) longl[atomicAdd(nlong, 1u)] = d;
+            continue;
+        }
+        uint32_t len = 0, src = 0;
+        if ((uint32_t)lane < W) {
+            const uint32_t a = rofs[(size_t)lane * (Hr + 1) + d];
+            len = rofs[(size_t)lane * (Hr + 1) + d + 1] - a;
+            src = ((uint32_t)lane == self ? 0u : bbase[lane]) + a;
+        }
+        const uint32_t inc = wave_incl_scan(len, lane);
+        if ((uint32_t)lane < W) {
+            rs[lane] = inc - len;
+            rb[lane] = src;
+        }
+        if (lane == 0) rs[W] = n;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        uint32_t kk[kSmallSeg / 64];
+#pragma unroll
+        for (int j = 0; j < kSmallSeg / 64; j++) {
+            const uint32_t i = lane + 64 * j;
+            uint32_t k = 0;
+            if (i < n) {
+                while (rs[k + 1] <= i) k++;
+                v[i] = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
+            }
+            kk[j] = k;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        // the permutation in LDS, then the segment written in order (whole
+        // lines, not 32-B pieces scattered over the segment)
+#pragma unroll
+        for (int j = 0; j < kSmallSeg / 64; j++) {
+            const uint32_t i = lane + 64 * j;
+            if (i < n) inv[merged_rank(v, rs, W, kk[j], i, v[i])] = (uint16_t)i;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t dh = d + host_lo;
+        for (uint32_t p = lane; p < n; p += 64) st_deliv_nt(&out[o + p], v[inv[p]], dh);
+        // the run table and the stage are rewritten for the next destination
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+}
+
+// The owner's merge when every run is sorted (the senders' sorted wire, or
+// their sorted rounds), segments above kSmallSeg events: one workgroup per
+// destination, its W runs staged in LDS one after another, each element
+// placed by merged_rank (a binary search per other run) -- O(n W log n)
+// work per segment instead of the rank sort's O(n^2), and no listed-segment
+// passes up to kMergeMax events.  Larger segments go unsorted to the
+// staging array and are listed, as in k_runs_sort.
+constexpr uint32_t kMergeMax = 2048;
+template <int kFmt>
+__global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in, const void* __restrict__ in_self,
+                                                    uint32_t self, const uint32_t* __restrict__ rofs,
+                                                    const uint32_t* __restrict__ bbase, uint32_t W, uint32_t Hr,
+                                                    const uint32_t* __restrict__ off, uint32_t host_lo,
+                                                    ShdDeliv* __restrict__ out, ShdDeliv* __restrict__ scr,
+                                                    uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
+                                                    const uint32_t* __restrict__ longl,
+                                                    const uint32_t* __restrict__ nlong) {
+    __shared__ Ev sv[kMergeMax];
+    __shared__ uint16_t inv[kMergeMax];
+    __shared__ uint32_t rs[kMaxRuns + 1], rb[kMaxRuns];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t m = *nlong; // (the destinations k_runs_merge_wave listed)
+    for (uint32_t li = blockIdx.x; li < m; li += gridDim.x) {
+        const uint32_t d = longl[li];
+        const uint32_t o = off[d], n = off[d + 1] - o;
+        if (tid < 64) {
+            uint32_t len = 0, src = 0;
+            if (tid < W) {
+                const uint32_t a = rofs[(size_t)tid * (Hr + 1) + d];
+                len = rofs[(size_t)tid * (Hr + 1) + d + 1] - a;
+                src = (tid == self ? 0u : bbase[tid]) + a;
+            }
+            const uint32_t inc = wave_incl_scan(len, (int)tid);
+            if (tid < W) {
+                rs[tid] = inc - len;
+                rb[tid] = src;
+            }
+            if (tid == 0) rs[W] = n;
+        }
+        __syncthreads();
+        auto run_of = [&](uint32_t i) {
+            uint32_t k = 0;
+            while (rs[k + 1] <= i) k++;
+            return k;
+        };
+        const uint32_t dh = d + host_lo;
+        if (n > kMergeMax) { // unsorted (runs one after another) to the staging array, listed
+            for (uint32_t i = tid; i < n; i += 256) {
+                const uint32_t k = run_of(i);
+                const Ev e = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
+                st_ev(&scr[o + i], ShdDeliv{e.t, e.q, e.s, dh, e.ix, 0u});
+            }
+            if (tid == 0) {
+                const uint32_t k = atomicAdd(nbig, 1u);
+                if (k < Hr) big[k] = d;
+                else atomicOr(nbig + 2, kFaultBigCap);
+            }
+            __syncthreads();
+            continue;
+        }
+        for (uint32_t i = tid; i < n; i += 256) {
+            const uint32_t k = run_of(i);
+            sv[i] = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += 256) inv[merged_rank(sv, rs, W, run_of(i), i, sv[i])] = (uint16_t)i;
+        __syncthreads();
+        for (uint32_t p = tid; p < n; p += 256) st_deliv_nt(&out[o + p], sv[inv[p]], dh);
+        __syncthreads();
     }
 }
 
@@ -2239,7 +2479,10 @@ __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* 
 // kKeyE: the per-wave LDS key array holds segments of up to 64 kKeyE events
 // (larger ones up to kSmallSeg take the readlane form): 4, or 2 for the
 // instance sized for three workgroups per CU
-template <int kWG, int kCap, int kKeyE>
+// kWire: the sorted segments go out as the exchange's 24-B wire records
+// (`out` is then a Wire array; listed segments are staged and listed as
+// always -- their sorted ShdDeliv form is converted by k_listed_wire)
+template <int kWG, int kCap, int kKeyE, bool kWire>
 __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
                                                           const uint32_t* __restrict__ wcnt,
@@ -2346,11 +2589,15 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                 rank += (uint32_t)(x.x < r.x || (x.x == r.x && (sx < sr || (sx == sr && x.y < r.y))));
             }
             const unsigned long long t = g.tbase + r.x;
-            shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[obase + o + rank]);
-            const shd_v4u a = {(uint32_t)t, (uint32_t)(t >> 32), r.y, 0u};
-            const shd_v4u c2 = {sr, g.host_lo + d0 + dl, r.z, 0u};
-            __builtin_nontemporal_store(a, q);
-            __builtin_nontemporal_store(c2, q + 1);
+            if (kWire) {
+                st_wire(reinterpret_cast<Wire*>(out) + obase + o + rank, t, (unsigned long long)r.y, sr, r.z);
+            } else {
+                shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[obase + o + rank]);
+                const shd_v4u a = {(uint32_t)t, (uint32_t)(t >> 32), r.y, 0u};
+                const shd_v4u c2 = {sr, g.host_lo + d0 + dl, r.z, 0u};
+                __builtin_nontemporal_store(a, q);
+                __builtin_nontemporal_store(c2, q + 1);
+            }
         }
         unsigned long long* lk = lds_keys && kKeyE ? keys[wv] : nullptr;
         for (uint32_t j = wv; j < nd; j += kWG / 64) {
@@ -2360,10 +2607,12 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                 const uint4 r = lev[o + i];
                 return Ev{g.tbase + r.x, (unsigned long long)r.y, r.w >> g.shift, r.z};
             };
-            if (nj <= 64) wave_rank_segment<1, 1>(load, nj, dh, out, obase + o, lane, lk);
-            else if (nj <= 128) wave_rank_segment<2, 1>(load, nj, dh, out, obase + o, lane, kKeyE >= 2 ? lk : nullptr);
+            constexpr int kOut = kWire ? 2 : 1;
+            if (nj <= 64) wave_rank_segment<1, kOut>(load, nj, dh, out, obase + o, lane, lk);
+            else if (nj <= 128)
+                wave_rank_segment<2, kOut>(load, nj, dh, out, obase + o, lane, kKeyE >= 2 ? lk : nullptr);
             else if (nj <= (uint32_t)kSmallSeg)
-                wave_rank_segment<4, 1>(load, nj, dh, out, obase + o, lane, kKeyE >= 4 ? lk : nullptr);
+                wave_rank_segment<4, kOut>(load, nj, dh, out, obase + o, lane, kKeyE >= 4 ? lk : nullptr);
             else { // a larger segment: unsorted to its range of the staging array, listed
                 for (uint32_t i = lane; i < nj; i += 64) {
                     const Ev v = load(i);
@@ -2404,7 +2653,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
 
 // the kernels: the compiler's register choice, or sized for kOcc waves per
 // SIMD (SHD_PART_SORT=4: no LDS keys, 63 VGPRs, four workgroups per CU)
-template <int kWG, int kCap, int kKeyE = 4>
+template <int kWG, int kCap, int kKeyE = 4, bool kWire = false>
 __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
                                                           const uint32_t* __restrict__ wcnt,
@@ -2414,7 +2663,8 @@ __global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __res
                                                           ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
-    part_sort_body<kWG, kCap, kKeyE>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig, counters, lds_keys);
+    part_sort_body<kWG, kCap, kKeyE, kWire>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig,
+                                           counters, lds_keys);
 }
 template <int kWG, int kCap, int kKeyE, int kOcc>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc, kOcc))) void k_part_sort_occ(PartGeo g, const uint4* __restrict__ stage,
@@ -2426,7 +2676,27 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc, kOcc)
                                                           ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
-    part_sort_body<kWG, kCap, kKeyE>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig, counters, lds_keys);
+    part_sort_body<kWG, kCap, kKeyE, false>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig,
+                                           counters, lds_keys);
+}
+
+// The sorted wire's listed segments: the listed kernels sorted them as
+// ShdDeliv into `sorted` (at their event offsets); copied here into the wire
+// array at the same offsets (one wave per listed destination).
+__global__ __launch_bounds__(256) void k_listed_wire(const ShdDeliv* __restrict__ sorted, const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig,
+                                                     uint32_t cap_big, Wire* __restrict__ wire) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nb_raw = nbig[0];
+    const uint32_t nb = nb_raw <= cap_big ? nb_raw : 0u;
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+    for (uint32_t q = wave; q < nb; q += nwaves) {
+        const uint32_t d = big[q];
+        for (uint32_t i = off[d] + lane; i < off[d + 1]; i += 64) {
+            const ShdDeliv r = ld_ev(&sorted[i]);
+            st_wire(&wire[i], r.time, r.seq, r.src_host, r.pkt_index);
+        }
+    }
 }
 
 // The exchanged round's sender side on the part pipeline (see
@@ -2434,41 +2704,62 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc, kOcc)
 // writes the destination offsets (the bucket's base: the earlier buckets'
 // totals) and places every event, unsorted, at its destination's range of
 // the wire array -- the owners sort the union of what they receive.
-__global__ __launch_bounds__(256) void k_part_wire(PartGeo g, const uint4* __restrict__ stage,
+template <int kWG, int kR>
+__global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __restrict__ stage,
                                                    const uint32_t* __restrict__ gcnt, const uint32_t* __restrict__ wcnt,
                                                    const ShdDeliv* __restrict__ wide, const uint32_t* __restrict__ nwide,
                                                    uint32_t wide_cap, uint32_t* __restrict__ offsets,
                                                    Wire* __restrict__ wire, unsigned long long* __restrict__ counters,
                                                    uint32_t* __restrict__ fault) {
-    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[4], s_base, s_wbase;
+    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kWG / 64], s_base, s_wbase;
     const uint32_t b = blockIdx.x;
     const uint32_t d0 = b << g.shift;
     const uint32_t nd = min(1u << g.shift, g.H - d0);
     const uint32_t mask = (1u << g.shift) - 1u;
     const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
+    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
+    // the bucket's records (up to kR per thread in registers, read once: the
+    // count pass and the placement use them), in flight while the base is summed
+    const uint4* sb = stage + (size_t)b * g.cap;
+    const bool held = ns <= (uint32_t)(kWG * kR); // (block-uniform)
+    uint4 e[kR];
+    if (held) {
+#pragma unroll
+        for (int k = 0; k < kR; k++) {
+            const uint32_t i = (uint32_t)k * kWG + threadIdx.x;
+            if (i < ns) {
+                const shd_v4u v = __builtin_nontemporal_load(reinterpret_cast<const shd_v4u*>(sb) + i);
+                e[k] = make_uint4(v.x, v.y, v.z, v.w);
+            }
+        }
+    }
     {
         uint32_t sm = 0, sw = 0;
-        for (uint32_t k = threadIdx.x; k < b; k += 256) {
+        for (uint32_t k = threadIdx.x; k < b; k += kWG) {
             const uint32_t x = wcnt[k];
             sm += min(gcnt[k], g.cap) + x;
             sw += x;
         }
         uint32_t t, tw = 0;
-        (void)block_excl_scan_n(sm, &t, wsum);
+        (void)block_excl_scan_n(sm, &t, wsum); // (its barriers also order the cnt reset)
         if (nw) (void)block_excl_scan_n(sw, &tw, wsum);
         if (threadIdx.x == 0) s_base = t, s_wbase = tw;
     }
-    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += 256) cnt[j] = cur[j] = 0;
     __syncthreads();
     const uint32_t obase = s_base;
     const ShdDeliv* wb = wide + s_wbase; // this bucket's wide events (k_wide_group)
-    const uint4* sb = stage + (size_t)b * g.cap;
     const uint32_t m = *nwide;
     const bool wide_ok = m <= wide_cap;
     if (!wide_ok && b == 0 && threadIdx.x == 0) atomicOr(fault, kFaultOvfCap);
-    for (uint32_t i = threadIdx.x; i < ns; i += 256) atomicAdd(&cnt[sb[i].w & mask], 1u);
+    if (held) {
+#pragma unroll
+        for (int k = 0; k < kR; k++)
+            if ((uint32_t)k * kWG + threadIdx.x < ns) atomicAdd(&cnt[e[k].w & mask], 1u);
+    } else {
+        for (uint32_t i = threadIdx.x; i < ns; i += kWG) atomicAdd(&cnt[sb[i].w & mask], 1u);
+    }
     if (wide_ok)
-        for (uint32_t i = threadIdx.x; i < nw; i += 256) atomicAdd(&cnt[(wb[i].dst_host - g.host_lo) & mask], 1u);
+        for (uint32_t i = threadIdx.x; i < nw; i += kWG) atomicAdd(&cnt[(wb[i].dst_host - g.host_lo) & mask], 1u);
     __syncthreads();
     if (threadIdx.x < 64) {
         const uint32_t v = threadIdx.x < nd ? cnt[threadIdx.x] : 0u;
@@ -2483,14 +2774,20 @@ __global__ __launch_bounds__(256) void k_part_wire(PartGeo g, const uint4* __res
         counters[0] = obase + tot;
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ns; i += 256) {
-        const uint4 r = sb[i];
+    auto place = [&](const uint4& r) {
         const uint32_t dl = r.w & mask;
         st_wire(&wire[obase + loc[dl] + atomicAdd(&cur[dl], 1u)], g.tbase + r.x, (unsigned long long)r.y,
                 r.w >> g.shift, r.z);
+    };
+    if (held) {
+#pragma unroll
+        for (int k = 0; k < kR; k++)
+            if ((uint32_t)k * kWG + threadIdx.x < ns) place(e[k]);
+    } else {
+        for (uint32_t i = threadIdx.x; i < ns; i += kWG) place(sb[i]);
     }
     if (wide_ok)
-        for (uint32_t i = threadIdx.x; i < nw; i += 256) {
+        for (uint32_t i = threadIdx.x; i < nw; i += kWG) {
             const ShdDeliv r = ld_ev(&wb[i]);
             const uint32_t dl = (r.dst_host - g.host_lo) & mask;
             st_wire(&wire[obase + loc[dl] + atomicAdd(&cur[dl], 1u)], r.time, r.seq, r.src_host, r.pkt_index);
@@ -2506,6 +2803,7 @@ __global__ void k_fault_word(const uint32_t* __restrict__ nbig, MergeMeta mm) {
 }
 
 // ---- workspace (grow-only, one per topology; see shd_dev_ws_new) ----
+constexpr size_t kXmatWords = 64 * 66; // the exchange's count matrix at the largest world (xchg.hip kMaxWorld)
 struct Ws {
     int device = -1;           // device the buffers live on
     hipEvent_t done = nullptr; // recorded after the last launch that used the buffers
@@ -2539,6 +2837,8 @@ struct Ws {
     size_t cap_xdev = 0;
     void* xhost = nullptr;     // its pinned host side (read back on the launch stream)
     size_t cap_xhost = 0;
+    uint64_t* xmat = nullptr;  // the exchange's count matrix (kXmatWords u64), device and pinned host
+    uint64_t* hxmat = nullptr;
 };
 
 int hip_status(hipError_t e, const char* what) {
@@ -2705,8 +3005,15 @@ int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDel
     if (int rc = mid_attr()) return rc;
     const MergeMeta mm = merge_meta(w, flag);
     const char* mr = getenv("SHD_MID_RANK");
+    const char* md = getenv("SHD_MEDIUM_SEG"); // 0: segments up to kMedSeg through k_segsort_mid as before
+    const bool med = !(md && strcmp(md, "0") == 0);
+    if (med) {
+        hipLaunchKernelGGL(k_segsort_medium, dim3(2048), dim3(64 * kMedWaves), 0, s, unsorted, offsets, w.big, w.nbig,
+                           out, mm.cap_big);
+        if (int rc = hip_status(hipGetLastError(), "k_segsort_medium launch")) return rc;
+    }
     hipLaunchKernelGGL(k_segsort_mid, dim3(256), dim3(kMidThreads), kMidLds, s, unsorted, offsets, w.big, w.nbig,
-                       out, w.st1, mm, (uint32_t)!(mr && strcmp(mr, "0") == 0));
+                       out, w.st1, mm, (uint32_t)!(mr && strcmp(mr, "0") == 0), (uint32_t)med);
     if (int rc = hip_status(hipGetLastError(), "k_segsort_mid launch")) return rc;
     hipLaunchKernelGGL(k_segsort_merge, dim3(512), dim3(256), 0, s, out, w.st1, mm);
     if (int rc = hip_status(hipGetLastError(), "k_segsort_merge launch")) return rc;
@@ -3105,6 +3412,8 @@ extern "C" void shd_dev_ws_free(void* p) {
     if (w->rd) (void)hipStreamDestroy(w->rd);
     (void)hipFree(w->xdev);
     if (w->xhost) (void)hipHostFree(w->xhost);
+    (void)hipFree(w->xmat);
+    if (w->hxmat) (void)hipHostFree(w->hxmat);
     if (w->done) (void)hipEventDestroy(w->done);
     delete w;
 }
@@ -3144,6 +3453,26 @@ extern "C" int shd_dev_ptab_build(const ShdEntry* tab, size_t nent, void* d_out,
 // round allocates nothing: hipFree / hipHostFree synchronise the device.
 // Callers run on one stream and synchronise it before returning, so a grow
 // only waits for the workspace's last round.
+// The exchange's count matrix (world x (world + 2) u64, device + pinned
+// host), allocated once per workspace.
+extern "C" int shd_dev_ws_xmat(void* ws, size_t words, uint64_t** d, uint64_t** h) {
+    if (!ws) return shd_fail(-ENOMEM, "no round workspace");
+    Ws& w = *static_cast<Ws*>(ws);
+    if (words > kXmatWords) return shd_fail(-EINVAL, "count matrix of %zu words", words);
+    if (!w.xmat) {
+        if (int rc = hip_status(hipMalloc((void**)&w.xmat, 8 * kXmatWords), "hipMalloc count matrix")) return rc;
+        if (hipHostMalloc((void**)&w.hxmat, 8 * kXmatWords, hipHostMallocDefault) != hipSuccess) {
+            w.hxmat = nullptr;
+            (void)hipFree(w.xmat);
+            w.xmat = nullptr;
+            return shd_fail(-ENOMEM, "hipHostMalloc count matrix");
+        }
+    }
+    *d = w.xmat;
+    *h = w.hxmat;
+    return 0;
+}
+
 extern "C" int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, void** h) {
     if (!ws) return shd_fail(-ENOMEM, "no round workspace");
     Ws& w = *static_cast<Ws*>(ws);
@@ -3487,9 +3816,10 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
 // the n events of the blocks back to back (block k from d_bbase[k], a device
 // array of W + 1 prefix counts), d_rofs the W per-block offset arrays over
 // the host range [host_lo, host_hi).  Output as shd_dev_deliv_sort.
-extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, size_t n, const uint32_t* d_rofs,
-                                        const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi,
-                                        ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream) {
+extern "C" int shd_dev_deliv_merge_runs_self(void* ws, const void* d_in, const void* d_self, uint32_t self, int wire,
+                                             int sorted, size_t n, const uint32_t* d_rofs, const uint32_t* d_bbase,
+                                             uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
+                                             uint32_t* d_dst_offsets, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (!ws) return shd_fail(-ENOMEM, "no round workspace");
     if (W < 1 || W > kMaxRuns) return shd_fail(-EINVAL, "%u runs outside 1..%u", W, kMaxRuns);
@@ -3502,12 +3832,30 @@ extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, si
     if ((rc = hip_status(hipMemsetAsync(w.nbig, 0, 12, s), "memset nbig"))) return rc;
     hipLaunchKernelGGL(k_runs_count, dim3(grid_for(H, 256, 4096)), dim3(256), 0, s, d_rofs, W, H, w.cnt1);
     scan_counts(w.cnt1, (size_t)H, d_dst_offsets, w.bsum, nullptr, s);
-    if (wire)
-        hipLaunchKernelGGL(k_runs_sort<1>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_rofs, d_bbase, W, H,
-                           d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
+    if (!d_self) self = 0xffffffffu;
+    if (sorted) { // (every run sorted: merge by binary searches)
+        // the segments above kSmallSeg events are listed in w.rnk (at most
+        // n / (kSmallSeg + 1) of them), counted in w.cnt1[H] (free after the scan)
+        uint32_t* nlong = w.cnt1 + H;
+        if ((rc = hip_status(hipMemsetAsync(nlong, 0, 4, s), "memset nlong"))) return rc;
+        const unsigned g = grid_for(H, 1, 1024), gw = grid_for(H, 4, 16384);
+        if (wire) {
+            hipLaunchKernelGGL(k_runs_merge_wave<1>, dim3(gw), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W,
+                               H, d_dst_offsets, host_lo, d_out, w.rnk, nlong);
+            hipLaunchKernelGGL(k_runs_merge<1>, dim3(g), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
+                               d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, w.rnk, nlong);
+        } else {
+            hipLaunchKernelGGL(k_runs_merge_wave<0>, dim3(gw), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W,
+                               H, d_dst_offsets, host_lo, d_out, w.rnk, nlong);
+            hipLaunchKernelGGL(k_runs_merge<0>, dim3(g), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
+                               d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, w.rnk, nlong);
+        }
+    } else if (wire)
+        hipLaunchKernelGGL(k_runs_sort<1>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_self, self, d_rofs,
+                           d_bbase, W, H, d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
     else
-        hipLaunchKernelGGL(k_runs_sort<0>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_rofs, d_bbase, W, H,
-                           d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
+        hipLaunchKernelGGL(k_runs_sort<0>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_self, self, d_rofs,
+                           d_bbase, W, H, d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, lds_keys());
     if ((rc = hip_status(hipGetLastError(), "k_runs_sort launch"))) return rc;
     if ((rc = dbg_sync(s, "k_runs_sort"))) return rc;
     if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s, nullptr))) return rc;
@@ -3517,13 +3865,22 @@ extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, si
     return ws_faults(w, true, s);
 }
 
+extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, int sorted, size_t n, const uint32_t* d_rofs,
+                                        const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi,
+                                        ShdDeliv* d_out, uint32_t* d_dst_offsets, void* stream) {
+    return shd_dev_deliv_merge_runs_self(ws, d_in, nullptr, 0xffffffffu, wire, sorted, n, d_rofs, d_bbase, W, host_lo,
+                                         host_hi, d_out, d_dst_offsets, stream);
+}
+
 // The sender's side of shd_round_process_exchange: the slab round up to the
 // per-destination offsets (d_off, H + 1), then the grouped, unsorted wire
 // records (k_group_wire) instead of the segment sort.  Slab pipeline only.
 extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                                             uint64_t end_time, uint64_t bootstrap_end, void* d_wire, uint32_t* d_off,
-                                            uint8_t* d_status, uint64_t* d_counters, void* stream) {
+                                            uint8_t* d_status, uint64_t* d_counters, void* stream, int sort_wire,
+                                            int* sorted_out) {
     hipStream_t s = (hipStream_t)stream;
+    if (sorted_out) *sorted_out = 0;
     if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
     Ws& w = *static_cast<Ws*>(c->ws);
     const uint32_t H = c->nhosts;
@@ -3539,9 +3896,37 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
             (rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, pg, d_status, counters, s)))
             return rc;
         mark_same(3, 2);
-        hipLaunchKernelGGL(k_part_wire, dim3(pg.nb), dim3(256), 0, s, pg, w.pstage, w.cnt1, w.cnt1 + pg.nb, w.tmp,
-                           w.nbig + 1, (uint32_t)w.cap_n, d_off, static_cast<Wire*>(d_wire), counters, w.nbig + 2);
-        if ((rc = hip_status(hipGetLastError(), "k_part_wire launch"))) return rc;
+        // sort_wire: every destination's run goes out sorted (the part sort
+        // writing wire records; listed segments sorted by the listed kernels
+        // into w.st2 -- the wide list's first copy, free by then -- and
+        // converted), so the owners merge sorted runs; else unsorted runs
+        // (k_part_wire), the owners sort their union
+        const bool wsorted = sort_wire != 0;
+        if (wsorted) {
+            ShdDeliv* wout = static_cast<ShdDeliv*>(d_wire); // (a Wire array: kWire)
+            const int sc = part_sort_cfg();
+#define SHD_WIRE_SORT_LAUNCH(WG, CAP, KE)                                                                             \
+    hipLaunchKernelGGL((k_part_sort<WG, CAP, KE, true>), dim3(pg.nb), dim3(WG), 0, s, pg, w.pstage, w.cnt1,            \
+                       w.cnt1 + pg.nb, w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_off, wout, w.st1, w.big, w.nbig, counters, \
+                       lds_keys())
+            if (sc == 0) SHD_WIRE_SORT_LAUNCH(1024, 7168, 4);
+            else if (sc == 1) SHD_WIRE_SORT_LAUNCH(512, 3584, 4);
+            else if (sc == 2) SHD_WIRE_SORT_LAUNCH(256, 1792, 4);
+            else SHD_WIRE_SORT_LAUNCH(512, 2304, 2);
+#undef SHD_WIRE_SORT_LAUNCH
+            if ((rc = hip_status(hipGetLastError(), "k_part_sort (wire) launch")) ||
+                (rc = sort_listed(w, w.st1, d_off, w.st2, s, counters)))
+                return rc;
+            hipLaunchKernelGGL(k_listed_wire, dim3(1024), dim3(256), 0, s, w.st2, d_off, w.big, w.nbig,
+                               merge_meta(w, counters).cap_big, static_cast<Wire*>(d_wire));
+            if ((rc = hip_status(hipGetLastError(), "k_listed_wire launch"))) return rc;
+        } else {
+            hipLaunchKernelGGL((k_part_wire<512, 5>), dim3(pg.nb), dim3(512), 0, s, pg, w.pstage, w.cnt1,
+                               w.cnt1 + pg.nb, w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_off, static_cast<Wire*>(d_wire),
+                               counters, w.nbig + 2);
+            if ((rc = hip_status(hipGetLastError(), "k_part_wire launch"))) return rc;
+        }
+        if (sorted_out) *sorted_out = wsorted ? 1 : 0;
         mark(4, s);
         if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
         if ((rc = dbg_sync(s, "grouped part round"))) return rc;

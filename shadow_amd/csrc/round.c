@@ -371,7 +371,7 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
             free(h);
         }
         if (!rc)
-            rc = shd_dev_deliv_merge_runs(sm->ws, sm->d_recv, 0, tot, sm->d_rofs, sm->d_rofs + (size_t)S * (hi - lo + 1),
+            rc = shd_dev_deliv_merge_runs(sm->ws, sm->d_recv, 0, 1, tot, sm->d_rofs, sm->d_rofs + (size_t)S * (hi - lo + 1),
                                           (uint32_t)S, lo, hi, sm->d_fin, sm->d_fin_off, sm->stream);
         if (!rc) rc = shd_dev_stream_sync(sm->stream);
         if (!rc) rc = shd_dev_ws_check_faults(sm->ws);

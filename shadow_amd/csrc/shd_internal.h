@@ -162,6 +162,9 @@ void shd_dev_ws_free(void* ws);
 /* grow-only exchange scratch of a workspace: dev_bytes of device memory and
  * host_bytes of pinned host memory (either pointer may be NULL) */
 int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, void** h);
+/* The exchange's count matrix (words <= 64 x 66 u64: device + pinned host),
+ * allocated on first use and kept. */
+int shd_dev_ws_xmat(void* ws, size_t words, uint64_t** d, uint64_t** h);
 /* The workspace's round faults after its last use (waits for it): 0, or -EIO
  * once per faulted round (merge spin-out, metadata overflow, stage guard). */
 int shd_dev_ws_check_faults(void* ws);
@@ -174,16 +177,27 @@ int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_l
  * destination in event_compare order (the exchange's output): block k starts
  * at event d_bbase[k] of d_in (W + 1 prefix counts, device), d_rofs holds
  * per block the (host_hi - host_lo + 1) destination offsets relative to the
- * block.  No scatter: the runs are read in place. */
-int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, size_t n, const uint32_t* d_rofs,
+ * block.  No scatter: the runs are read in place.  sorted: every run is in
+ * event_compare order inside each destination (merged, not sorted). */
+int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, int sorted, size_t n, const uint32_t* d_rofs,
                              const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                              uint32_t* d_dst_offsets, void* stream);
+/* The same with run `self` read from d_self (this rank's own block, at its
+ * element index: never sent through the transport); d_self NULL: none.
+ * sorted: every run is sorted (a merge instead of the union's sort). */
+int shd_dev_deliv_merge_runs_self(void* ws, const void* d_in, const void* d_self, uint32_t self, int wire, int sorted,
+                                  size_t n, const uint32_t* d_rofs, const uint32_t* d_bbase, uint32_t W,
+                                  uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out, uint32_t* d_dst_offsets,
+                                  void* stream);
 /* The sender's side of an exchanged round: decided events grouped by
- * destination, unsorted, as 24-B wire records {time, seq, src, pkt_index}
- * into d_wire, destination offsets (H + 1) into d_off; slab pipeline only. */
+ * destination as 24-B wire records {time, seq, src, pkt_index} into d_wire,
+ * destination offsets (H + 1) into d_off.  sort_wire: each destination's
+ * run in event_compare order (the part pipeline only); *sorted_out says
+ * whether they are. */
 int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                                  uint64_t end_time, uint64_t bootstrap_end, void* d_wire, uint32_t* d_off,
-                                 uint8_t* d_status, uint64_t* d_counters, void* stream);
+                                 uint8_t* d_status, uint64_t* d_counters, void* stream, int sort_wire,
+                                 int* sorted_out);
 /* decide + group + exchange + merge in one call (shd_round_process_exchange) */
 int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                            uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds, void* d_wire_send,

@@ -128,6 +128,24 @@ __global__ void k_cuts(const uint32_t* __restrict__ offsets, RouteArgs ra, uint3
     if (r <= ra.world) cuts[r] = offsets[ra.bounds[r]];
 }
 
+// This rank's row of the exchange's count matrix: the events for each owner
+// rank (the cuts of the destination offsets at the owners' host bounds), its
+// receive capacity and whether its own stage failed (then the offsets are
+// not read; bit 0 of the flag word) and whether its runs are sorted (bit 1);
+// the cuts themselves for the payload's base.
+__global__ void k_count_row(const uint32_t* __restrict__ offsets, RouteArgs ra, uint32_t* __restrict__ cuts,
+                            uint64_t* __restrict__ row, uint64_t cap, int failed, int sorted) {
+    const int r = threadIdx.x, W = ra.world;
+    if (failed) {
+        if (r < W) row[r] = 0ull;
+        if (r == 0) row[W] = cap, row[W + 1] = 1ull;
+        return;
+    }
+    if (r <= W) cuts[r] = offsets[ra.bounds[r]];
+    if (r < W) row[r] = (uint64_t)(offsets[ra.bounds[r + 1]] - offsets[ra.bounds[r]]);
+    if (r == 0) row[W] = cap, row[W + 1] = sorted ? 2ull : 0ull;
+}
+
 int make_args(const uint32_t* bounds, int world, RouteArgs* ra) {
     if (world < 1 || world > kMaxWorld) return shd_fail(-EINVAL, "world %d outside 1..%d", world, kMaxWorld);
     ra->world = world;
@@ -238,8 +256,10 @@ int rccl_alltoall_u64(void* user, const uint64_t* send, uint64_t* recv) {
     return 0;
 }
 
-int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
-                   const uint64_t* recv_bytes, void* stream) {
+// send_off: peer r's block at d_send + send_off[r] (NULL: blocks contiguous
+// in rank order)
+int rccl_alltoallv_off(void* user, const void* d_send, const uint64_t* send_bytes, const uint64_t* send_off,
+                       void* d_recv, const uint64_t* recv_bytes, void* stream) {
     Rccl* t = static_cast<Rccl*>(user);
     const int W = t->x.world;
     hipStream_t s = (hipStream_t)stream;
@@ -247,8 +267,9 @@ int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, v
     if (rc) return rc;
     uint64_t so = 0, ro = 0;
     for (int r = 0; r < W; r++) {
+        const uint64_t at = send_off ? send_off[r] : so;
         if (send_bytes[r] &&
-            (rc = nccl_status(ncclSend((const char*)d_send + so, send_bytes[r], ncclChar, r, t->comm, s), "ncclSend")))
+            (rc = nccl_status(ncclSend((const char*)d_send + at, send_bytes[r], ncclChar, r, t->comm, s), "ncclSend")))
             break;
         if (recv_bytes[r] &&
             (rc = nccl_status(ncclRecv((char*)d_recv + ro, recv_bytes[r], ncclChar, r, t->comm, s), "ncclRecv")))
@@ -258,6 +279,10 @@ int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, v
     }
     const int rc2 = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
     return rc ? rc : rc2;
+}
+int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
+                   const uint64_t* recv_bytes, void* stream) {
+    return rccl_alltoallv_off(user, d_send, send_bytes, nullptr, d_recv, recv_bytes, stream);
 }
 
 // All-gather of variable blocks, in place: rank r's block is bytes
@@ -350,12 +375,18 @@ extern "C" int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const
 // xchg_scratch_words): [cuts | H + W slices | W x (H_me + 1) received offsets
 // | W + 1 block bases]; host (pinned): [cuts | block bases].
 namespace {
+int local_allgatherv(void* user, void* d_buf, const uint64_t* off, void* stream);
+int local_alltoallv_off(void* user, const void* d_send, const uint64_t* send_bytes, const uint64_t* send_off,
+                        void* d_recv, const uint64_t* recv_bytes, void* stream);
 size_t xchg_scratch_words(uint32_t H, int W, uint32_t Hm) {
     return (kMaxWorld + 1) + ((size_t)H + W) + (size_t)W * (Hm + 1) + (W + 1);
 }
 // local_rc != 0: this rank's own round failed; it still joins the count
-// all-to-all (exchange_blocks) so that every rank fails together.
-int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, size_t elem_bytes, int wire,
+// all-to-all (exchange_blocks) so that every rank fails together.  sorted:
+// this rank's runs are in event_compare order inside every destination; the
+// owner merges instead of sorting when every sender's are (the count
+// matrix says so; without it only for ShdDeliv runs, sorted by contract).
+int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, size_t elem_bytes, int wire, int sorted,
                        const uint32_t* d_dst_offsets, const uint32_t* host_bounds, void* d_recv, size_t recv_cap,
                        ShdDeliv* d_out, uint32_t* d_out_offsets, size_t* n_out, hipStream_t s, uint32_t* dscr,
                        uint32_t* hscr, int local_rc = 0) {
@@ -367,12 +398,96 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
         const char* f = getenv("SHD_DEBUG_FAIL_RANK");
         if (f && atoi(f) == me) local_rc = shd_fail(-EIO, "debug: injected failure of rank %d", me);
     }
-    if (local_rc) { // only the count all-to-all that tells the peers
+    // With an all-gather in the transport, one collective carries the whole
+    // count matrix (every rank's counts for every owner, its receive capacity
+    // and its failure flag): the cuts, the counts and the capacity verdict in
+    // one host round trip instead of three; every rank reads the same matrix,
+    // so all of them fail together.
+    uint64_t *d_mat = nullptr, *h_mat = nullptr;
+    // (the library's own transports: their all-gather takes any device
+    // buffer; a caller's transport may only know the buffers it registered)
+    const bool own = x->allgatherv == rccl_allgatherv || x->allgatherv == local_allgatherv;
+    const bool one_trip = own && shd_dev_ws_xmat(ws, (size_t)W * (W + 2), &d_mat, &h_mat) == 0;
+    if (local_rc && !one_trip) { // only the count all-to-all that tells the peers
         std::vector<uint64_t> none(W, 0);
         size_t nr = 0;
         return exchange_blocks(x, nullptr, none.data(), elem_bytes, nullptr, 0, &nr, s, nullptr, local_rc);
     }
     const uint32_t H = host_bounds[W], lo = host_bounds[me], hi = host_bounds[me + 1], Hm = hi - lo;
+    if (one_trip) {
+        const size_t rw = (size_t)W + 2;
+        uint32_t* d_cuts = local_rc ? nullptr : dscr;
+        hipLaunchKernelGGL(k_count_row, dim3(1), dim3(kMaxWorld + 1), 0, s, local_rc ? nullptr : d_dst_offsets, ra,
+                           d_cuts, d_mat + (size_t)me * rw, (uint64_t)recv_cap, local_rc ? 1 : 0, sorted);
+        uint32_t* d_sl = local_rc ? nullptr : dscr + (kMaxWorld + 1);
+        if (!local_rc)
+            hipLaunchKernelGGL(k_offset_slices,
+                               dim3((unsigned)(((size_t)H + W + 255) / 256 < 4096 ? ((size_t)H + W + 255) / 256 : 4096)),
+                               dim3(256), 0, s, d_dst_offsets, ra, d_sl);
+        std::vector<uint64_t> moff(W + 1);
+        for (int r = 0; r <= W; r++) moff[r] = 8ull * rw * (uint64_t)r;
+        int rc2 = hip_status(hipGetLastError(), "count row launch");
+        if (!rc2) rc2 = x->allgatherv(x->user, d_mat, moff.data(), (void*)s);
+        if (rc2) return rc2 < 0 ? rc2 : -EIO;
+        if ((rc2 = hip_status(hipMemcpyAsync(h_mat, d_mat, 8 * rw * (size_t)W, hipMemcpyDeviceToHost, s), "counts D2H")) ||
+            (!local_rc && (rc2 = hip_status(hipMemcpyAsync(hscr, dscr, 4 * (size_t)(W + 1), hipMemcpyDeviceToHost, s),
+                                            "cuts D2H"))) ||
+            (rc2 = hip_status(hipStreamSynchronize(s), "counts sync")))
+            return rc2;
+        if (local_rc) return local_rc;
+        bool over = false;
+        int all_sorted = 1;
+        for (int r = 0; r < W; r++) {
+            if (h_mat[(size_t)r * rw + W + 1] & 1ull) return shd_fail(-EIO, "rank %d failed before the exchange", r);
+            if (!(h_mat[(size_t)r * rw + W + 1] & 2ull)) all_sorted = 0;
+        }
+        for (int t = 0; t < W; t++) {
+            uint64_t tot = 0;
+            for (int r = 0; r < W; r++) tot += h_mat[(size_t)r * rw + t];
+            if (tot > h_mat[(size_t)t * rw + W]) {
+                if (t == me) return shd_fail(-ENOSPC, "receive %llu elements > capacity %zu", (unsigned long long)tot, recv_cap);
+                over = true;
+            }
+        }
+        if (over) return shd_fail(-ENOSPC, "a peer's receive capacity is too small for this exchange");
+        // this rank's own block stays where it is: the merge reads it from
+        // the send buffer (no copy through the transport)
+        std::vector<uint64_t> sbytes(W), rbytes(W), recv(W), sb(W), rb(W);
+        uint64_t nrecv = 0;
+        for (int r = 0; r < W; r++) {
+            sbytes[r] = r == me ? 0 : h_mat[(size_t)me * rw + r] * elem_bytes;
+            recv[r] = h_mat[(size_t)r * rw + me];
+            rbytes[r] = r == me ? 0 : recv[r] * elem_bytes;
+            nrecv += recv[r];
+        }
+        uint32_t* h_cuts = hscr;
+        std::vector<uint64_t> soff(W);
+        for (int r = 0; r < W; r++) soff[r] = (uint64_t)h_cuts[r] * elem_bytes; // (own block skipped, in place)
+        int rc3 = x->allgatherv == rccl_allgatherv
+                      ? rccl_alltoallv_off(x->user, d_events, sbytes.data(), soff.data(), d_recv, rbytes.data(), (void*)s)
+                      : local_alltoallv_off(x->user, d_events, sbytes.data(), soff.data(), d_recv, rbytes.data(),
+                                            (void*)s);
+        if (rc3) return rc3 < 0 ? rc3 : -EIO;
+        const size_t n_sl = (size_t)H + W;
+        uint32_t* d_ro = d_sl + n_sl;
+        uint32_t* d_bb = d_ro + (size_t)W * (Hm + 1);
+        uint32_t* h_bb = h_cuts + (kMaxWorld + 1);
+        for (int r = 0; r < W; r++) {
+            sb[r] = 4ull * (host_bounds[r + 1] - host_bounds[r] + 1);
+            rb[r] = 4ull * (Hm + 1);
+        }
+        if ((rc3 = x->alltoallv(x->user, d_sl, sb.data(), d_ro, rb.data(), (void*)s))) return rc3 < 0 ? rc3 : -EIO;
+        h_bb[0] = 0;
+        for (int r = 0; r < W; r++) h_bb[r + 1] = h_bb[r] + (r == me ? 0u : (uint32_t)recv[r]);
+        const void* self_block = static_cast<const char*>(d_events) + (size_t)h_cuts[me] * elem_bytes;
+        if ((rc3 = hip_status(hipMemcpyAsync(d_bb, h_bb, 4 * (size_t)(W + 1), hipMemcpyHostToDevice, s), "bases H2D")) ||
+            (rc3 = shd_dev_deliv_merge_runs_self(ws, d_recv, self_block, (uint32_t)me, wire, all_sorted, nrecv, d_ro, d_bb,
+                                                 (uint32_t)W, lo, hi, d_out, d_out_offsets, s)) ||
+            (rc3 = hip_status(hipStreamSynchronize(s), "exchange runs")) || (rc3 = shd_dev_ws_check_faults(ws)))
+            return rc3;
+        *n_out = nrecv;
+        return 0;
+    }
     const size_t n_sl = (size_t)H + W, n_ro = (size_t)W * (Hm + 1);
     uint32_t* d_cuts = dscr;
     uint32_t* d_sl = d_cuts + (kMaxWorld + 1);
@@ -410,8 +525,8 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
     for (int r = 0; r < W; r++) h_bb[r + 1] = h_bb[r] + (uint32_t)recv[r];
     if ((rc = hip_status(hipMemcpyAsync(d_bb, h_bb, 4 * (size_t)(W + 1), hipMemcpyHostToDevice, s), "bases H2D")))
         return rc;
-    if ((rc = shd_dev_deliv_merge_runs(ws, d_recv, wire, nrecv, d_ro, d_bb, (uint32_t)W, lo, hi, d_out, d_out_offsets,
-                                       s)))
+    if ((rc = shd_dev_deliv_merge_runs_self(ws, d_recv, nullptr, 0xffffffffu, wire, wire ? 0 : sorted, nrecv, d_ro,
+                                            d_bb, (uint32_t)W, lo, hi, d_out, d_out_offsets, s)))
         return rc;
     if ((rc = hip_status(hipStreamSynchronize(s), "exchange runs"))) return rc;
     // the sender's round and this merge ran on the workspace: their faults
@@ -433,7 +548,7 @@ extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdD
     void *dscr = nullptr, *hscr = nullptr;
     const int rc = shd_dev_ws_scratch(ws, 4 * xchg_scratch_words(host_bounds[W], W, Hm), 4 * (2 * kMaxWorld + 2),
                                       &dscr, &hscr); // (a failure still joins the first collective)
-    return exchange_runs_core(ws, x, d_events, sizeof(ShdDeliv), 0, d_dst_offsets, host_bounds, d_recv, recv_cap,
+    return exchange_runs_core(ws, x, d_events, sizeof(ShdDeliv), 0, 1, d_dst_offsets, host_bounds, d_recv, recv_cap,
                               d_out, d_out_offsets, n_out, (hipStream_t)stream, static_cast<uint32_t*>(dscr),
                               static_cast<uint32_t*>(hscr), rc);
 }
@@ -455,10 +570,22 @@ extern "C" int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x,
     // (a failed local stage still joins the exchange's first collective)
     int rc = shd_dev_ws_scratch(c->ws, 4 * words, 4 * (2 * kMaxWorld + 2), &dscr, &hscr);
     uint32_t* d_off = static_cast<uint32_t*>(dscr); // the sender's destination offsets (H + 1)
+    // Sorted wire runs (SHD_WIRE_SORTED=1/0 forces them on/off): by default
+    // when an owner's destination would gather more than kSmallSeg events
+    // from the W runs on average (W n / H) -- then its union is past the
+    // one-wave rank sort and a merge of sorted runs is the cheaper side
+    // (profiles/r04y_xchg_probe.log); below, the sender's sort costs more
+    // than the owner's.  Ranks may choose differently: the owners merge
+    // only when every run is sorted.
+    const char* sw = getenv("SHD_WIRE_SORTED");
+    const int sort_wire = sw && strcmp(sw, "1") == 0   ? 1
+                          : sw && strcmp(sw, "0") == 0 ? 0
+                                                       : (double)W * (double)n > 256.0 * (double)(H ? H : 1);
+    int sorted = 0;
     if (!rc)
         rc = shd_dev_packet_round_grouped(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire_send, d_off, d_status,
-                                          d_counters, stream);
-    return exchange_runs_core(c->ws, x, d_wire_send, 24, 1, d_off, host_bounds, d_wire_recv, recv_cap, d_out,
+                                          d_counters, stream, sort_wire, &sorted);
+    return exchange_runs_core(c->ws, x, d_wire_send, 24, 1, sorted, d_off, host_bounds, d_wire_recv, recv_cap, d_out,
                               d_out_offsets, n_out, (hipStream_t)stream, rc ? nullptr : d_off + (H + 1),
                               static_cast<uint32_t*>(hscr), rc);
 }
@@ -564,30 +691,41 @@ int local_alltoall_u64(void* user, const uint64_t* send, uint64_t* recv) {
 
 // every rank publishes its send buffer and per-peer block offsets; each
 // receiver copies its blocks out of the senders' buffers, in rank order
-int local_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
-                    const uint64_t* recv_bytes, void* stream) {
+// (send_off: as rccl_alltoallv_off)
+int local_alltoallv_off(void* user, const void* d_send, const uint64_t* send_bytes, const uint64_t* send_off,
+                        void* d_recv, const uint64_t* recv_bytes, void* stream) {
     Local* t = static_cast<Local*>(user);
     LocalHub* h = t->hub;
     const int W = h->world, me = t->x.rank;
     hipStream_t s = (hipStream_t)stream;
     int rc = hip_status(hipStreamSynchronize(s), "local alltoallv (send side ready)");
     h->src[me] = static_cast<const char*>(d_send);
+    // boff[me]: block r at [2r] (offset) and [2r + 1] (size)
     std::vector<uint64_t>& o = h->boff[me];
-    o.assign(W + 1, 0);
-    for (int r = 0; r < W; r++) o[r + 1] = o[r] + send_bytes[r];
+    o.assign(2 * (size_t)W, 0);
+    uint64_t so = 0;
+    for (int r = 0; r < W; r++) {
+        o[2 * (size_t)r] = send_off ? send_off[r] : so;
+        o[2 * (size_t)r + 1] = send_bytes[r];
+        so += send_bytes[r];
+    }
     hub_wait(h);
     uint64_t at = 0;
     for (int r = 0; r < W && !rc; r++) {
-        if (recv_bytes[r] != h->boff[r][me + 1] - h->boff[r][me]) rc = shd_fail(-EIO, "local alltoallv: block sizes disagree");
+        if (recv_bytes[r] != h->boff[r][2 * (size_t)me + 1]) rc = shd_fail(-EIO, "local alltoallv: block sizes disagree");
         else if (recv_bytes[r])
-            rc = hip_status(hipMemcpyAsync(static_cast<char*>(d_recv) + at, h->src[r] + h->boff[r][me], recv_bytes[r],
-                                           hipMemcpyDefault, s),
+            rc = hip_status(hipMemcpyAsync(static_cast<char*>(d_recv) + at, h->src[r] + h->boff[r][2 * (size_t)me],
+                                           recv_bytes[r], hipMemcpyDefault, s),
                             "local alltoallv copy");
         at += recv_bytes[r];
     }
     if (!rc) rc = hip_status(hipStreamSynchronize(s), "local alltoallv");
     hub_wait(h); // (senders keep their buffers until every receiver copied)
     return rc;
+}
+int local_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, void* d_recv,
+                    const uint64_t* recv_bytes, void* stream) {
+    return local_alltoallv_off(user, d_send, send_bytes, nullptr, d_recv, recv_bytes, stream);
 }
 
 int local_allgatherv(void* user, void* d_buf, const uint64_t* off, void* stream) {

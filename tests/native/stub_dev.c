@@ -165,7 +165,7 @@ int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint32_t host_l
     return shd_fail(-ENOSYS, "stub device: no packet kernels");
 }
 
-int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, size_t n, const uint32_t* d_rofs,
+int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, int sorted, size_t n, const uint32_t* d_rofs,
                              const uint32_t* d_bbase, uint32_t W, uint32_t host_lo, uint32_t host_hi, ShdDeliv* d_out,
                              uint32_t* d_dst_offsets, void* stream) {
     return shd_fail(-ENOSYS, "stub device: no packet kernels");

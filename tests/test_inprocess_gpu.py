@@ -35,10 +35,20 @@ def _gml():
     return synth.sparse_graph_gml(250, 0x5EED0801, ns_variant=True)
 
 
-def _packets(rank, world, st):
+def _packets(rank, world, st, hot=0):
+    """hot > 0: every packet goes to one of `hot` destinations spread over
+    the hosts (long destination segments on the sender and the owner)."""
     from shadow_amd import synth
     lo, hi = rank * H // world, (rank + 1) * H // world
-    return synth.packet_batch(NPK, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, hosts_lo=lo, hosts_hi=hi)
+    if not hot:
+        return synth.packet_batch(NPK, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, hosts_lo=lo, hosts_hi=hi)
+    rng = np.random.default_rng(0x5EED0820 + rank)
+    hosts = np.array([i * H // hot for i in range(hot)] + [H // 2 + 1])
+    src = rng.integers(lo, hi, NPK).astype(np.uint32)
+    k = rng.integers(0, hot, NPK)
+    dst = hosts[k]
+    dst = np.where(dst == src, hosts[(k + 1) % len(hosts)], dst).astype(np.uint32)
+    return synth.packet_batch(NPK, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, pairs=(src, dst))
 
 
 class _UidTransport:
@@ -94,7 +104,7 @@ def _run_ranks(world, fn):
     return res, errs
 
 
-def _setup(world):
+def _setup(world, hot=0):
     import torch
 
     from shadow_amd import Topology, scenario
@@ -111,7 +121,7 @@ def _setup(world):
         cap = NPK * world
         bufs.append(dict(
             tab=torch.zeros(A * A * 2, dtype=torch.float64, device="cuda"),
-            recs=torch.from_numpy(_packets(r, world, tops[r][1]).view(np.uint8)).cuda(),
+            recs=torch.from_numpy(_packets(r, world, tops[r][1], hot).view(np.uint8)).cuda(),
             send=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
             routed=torch.empty(cap * 32, dtype=torch.uint8, device="cuda"),
             off=torch.empty(H + 1, dtype=torch.int32, device="cuda"),
@@ -124,7 +134,7 @@ def _setup(world):
     return gml, tops, A, host_bounds, bufs
 
 
-def _oracle_round(gml, world):
+def _oracle_round(gml, world, hot=0):
     orc = O.OracleTopology(gml)
     from shadow_amd import scenario
     ips, st, verts = scenario.register_hosts(orc, H, 1)
@@ -132,7 +142,7 @@ def _oracle_round(gml, world):
     lat, rel = orc.rows_parallel(sv, sv, 8)
     want_tab = np.stack([lat, rel], axis=-1).tobytes()
     orc.preload(sv, lat, rel)
-    allpk = np.concatenate([_packets(r, world, st) for r in range(world)])
+    allpk = np.concatenate([_packets(r, world, st, hot) for r in range(world)])
     ref, status, mt = orc.round(ips, allpk, BARRIER, END)
     return want_tab, ref, mt
 
@@ -186,6 +196,39 @@ def test_threads_as_ranks(kind, world, fused):
     want_tab, ref, mt = _oracle_round(gml, world)
     for b in bufs:  # every rank's all-gathered table
         assert b["tab"].cpu().numpy().tobytes() == want_tab
+    _check_union(bufs, res, world, host_bounds, ref, mt)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("hot", [1, 2, 6])
+@pytest.mark.parametrize("wire_sorted", ["1", "0"], ids=["sorted_wire", "unsorted_wire"])
+def test_exchange_long_segments(world, hot, wire_sorted, monkeypatch):
+    """Packets aimed at a few hot destinations: sender segments past the
+    part sort's LDS capacity (listed, sorted, converted to wire records) and
+    owner segments past the run merge's LDS stage (kMergeMax: listed) or
+    below it (merged from sorted runs of hundreds); SHD_WIRE_SORTED=0 sends
+    unsorted runs that the owner sorts."""
+    monkeypatch.setenv("SHD_WIRE_SORTED", wire_sorted)
+    gml, tops, A, host_bounds, bufs = _setup(world, hot)
+    xps = _transports("local", world)
+
+    def rank_main(r):
+        top, _ = tops[r]
+        b, xp = bufs[r], xps.ranks[r]
+        top.build_rows_device(0, A, b["tab"].data_ptr())
+        top.adopt_table_device(b["tab"].data_ptr())
+        top.touch_all()
+        return top.process_exchange(xp, b["recs"].data_ptr(), NPK, BARRIER, END, 0, host_bounds,
+                                    b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
+                                    b["recv"].data_ptr(), NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+
+    try:
+        res, errs = _run_ranks(world, rank_main)
+        assert not any(errs), [e for e in errs if e]
+    finally:
+        xps.close()
+    _, ref, mt = _oracle_round(gml, world, hot)
     _check_union(bufs, res, world, host_bounds, ref, mt)
 
 
