@@ -2439,16 +2439,47 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
     }
 }
 
+// The part round's per-bucket counters (w.cnt1): gcnt[nb] (staged events) |
+// wcnt[nb] (wide events) | wcur[nb] (k_wide_group's cursors) | bpre[nb + 1]
+// (each bucket's output base: the earlier buckets' totals) | wpre[nb] (its
+// first event in the grouped wide list).
+constexpr size_t part_cnt_words(uint32_t nb) { return 5 * (size_t)nb + 1; }
+
 // The wide list (events whose record did not fit the 16-B stage form, or
 // whose bucket region was full) grouped by bucket into `grouped`, so that a
 // bucket reads only its own (wcnt[b] events from the earlier buckets'
 // total): every workgroup scans the per-bucket counts into LDS, then places
 // its share of the list with per-bucket cursors.  Exits at once when the list
-// is empty (the usual round).
+// is empty (the usual round).  Workgroup 0 first writes bpre / wpre (one
+// scan here instead of every sort workgroup summing the counts before it).
 __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* __restrict__ wide,
                                                      const uint32_t* __restrict__ nwide, uint32_t wide_cap,
+                                                     const uint32_t* __restrict__ gcnt,
                                                      const uint32_t* __restrict__ wcnt, uint32_t* __restrict__ wcur,
                                                      ShdDeliv* __restrict__ grouped) {
+    if (blockIdx.x == 0) {
+        __shared__ uint32_t ps[16];
+        uint32_t* bpre = wcur + g.nb;
+        uint32_t* wpre = bpre + g.nb + 1;
+        const uint32_t per = (g.nb + 1023) / 1024, b0 = threadIdx.x * per;
+        uint32_t st = 0, sw = 0;
+        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) {
+            const uint32_t x = wcnt[b0 + k];
+            st += min(gcnt[b0 + k], g.cap) + x;
+            sw += x;
+        }
+        uint32_t tt, tw;
+        uint32_t pt = block_excl_scan_n(st, &tt, ps);
+        uint32_t pw = block_excl_scan_n(sw, &tw, ps);
+        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) {
+            const uint32_t x = wcnt[b0 + k];
+            bpre[b0 + k] = pt;
+            wpre[b0 + k] = pw;
+            pt += min(gcnt[b0 + k], g.cap) + x;
+            pw += x;
+        }
+        if (threadIdx.x == 0) bpre[g.nb] = tt;
+    }
     const uint32_t m = *nwide;
     if (m == 0 || m > wide_cap) return; // (block-uniform; an overfull list is the sort's fault to report)
     extern __shared__ uint32_t woff[]; // [nb]
@@ -2494,8 +2525,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
     __shared__ uint4 lev[kCap];
     __shared__ unsigned long long keys[kWG / 64][kKeyE ? 64 * kKeyE + 8 : 1];
-    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kWG / 64];
-    __shared__ uint32_t s_base, s_wbase;
+    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
     const uint32_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t d0 = b << g.shift;
@@ -2506,7 +2536,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
     const uint4* sb = stage + (size_t)b * g.cap;
     uint4 e[kCap / kWG];
-    if (!listed) { // the bucket's records in flight while the base is summed
+    if (!listed) { // the bucket's records
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++) {
             const uint32_t i = (uint32_t)k * kWG + threadIdx.x;
@@ -2516,24 +2546,13 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
             }
         }
     }
-    // this bucket's output base: the totals of the buckets before it (and,
-    // when it has wide events, their place in the grouped list: the earlier
-    // buckets' wide counts)
-    {
-        uint32_t s = 0, sw = 0;
-        for (uint32_t k = threadIdx.x; k < b; k += kWG) {
-            const uint32_t x = wcnt[k];
-            s += min(gcnt[k], g.cap) + x;
-            sw += x;
-        }
-        uint32_t t, tw = 0;
-        (void)block_excl_scan_n(s, &t, wsum); // (its barriers also order the cnt reset)
-        if (nw) (void)block_excl_scan_n(sw, &tw, wsum);
-        if (threadIdx.x == 0) s_base = t, s_wbase = tw;
-    }
-    __syncthreads();
-    const uint32_t obase = s_base;
-    const ShdDeliv* wb = wide + s_wbase; // this bucket's wide events (k_wide_group)
+    // this bucket's output base (the totals of the buckets before it) and
+    // its wide events' place in the grouped list, from k_wide_group's scan
+    // (the counter layout: part_cnt_words)
+    const uint32_t* bpre = gcnt + 3 * (size_t)g.nb;
+    const uint32_t obase = bpre[b];
+    const ShdDeliv* wb = wide + (nw ? bpre[g.nb + 1 + b] : 0u); // this bucket's wide events (k_wide_group)
+    __syncthreads(); // (orders the cnt reset)
     if (!listed) {
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++)
@@ -2701,8 +2720,8 @@ __global__ __launch_bounds__(256) void k_listed_wire(const ShdDeliv* __restrict_
 
 // The exchanged round's sender side on the part pipeline (see
 // k_group_wire): one workgroup per bucket counts its events per destination,
-// writes the destination offsets (the bucket's base: the earlier buckets'
-// totals) and places every event, unsorted, at its destination's range of
+// writes the destination offsets (the bucket's base: k_wide_group's scan of
+// the earlier buckets' totals) and places every event, unsorted, at its destination's range of
 // the wire array -- the owners sort the union of what they receive.
 template <int kWG, int kR>
 __global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __restrict__ stage,
@@ -2711,7 +2730,7 @@ __global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __res
                                                    uint32_t wide_cap, uint32_t* __restrict__ offsets,
                                                    Wire* __restrict__ wire, unsigned long long* __restrict__ counters,
                                                    uint32_t* __restrict__ fault) {
-    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst], wsum[kWG / 64], s_base, s_wbase;
+    __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
     const uint32_t b = blockIdx.x;
     const uint32_t d0 = b << g.shift;
     const uint32_t nd = min(1u << g.shift, g.H - d0);
@@ -2719,7 +2738,7 @@ __global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __res
     const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
     for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
     // the bucket's records (up to kR per thread in registers, read once: the
-    // count pass and the placement use them), in flight while the base is summed
+    // count pass and the placement use them)
     const uint4* sb = stage + (size_t)b * g.cap;
     const bool held = ns <= (uint32_t)(kWG * kR); // (block-uniform)
     uint4 e[kR];
@@ -2733,21 +2752,10 @@ __global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __res
             }
         }
     }
-    {
-        uint32_t sm = 0, sw = 0;
-        for (uint32_t k = threadIdx.x; k < b; k += kWG) {
-            const uint32_t x = wcnt[k];
-            sm += min(gcnt[k], g.cap) + x;
-            sw += x;
-        }
-        uint32_t t, tw = 0;
-        (void)block_excl_scan_n(sm, &t, wsum); // (its barriers also order the cnt reset)
-        if (nw) (void)block_excl_scan_n(sw, &tw, wsum);
-        if (threadIdx.x == 0) s_base = t, s_wbase = tw;
-    }
-    __syncthreads();
-    const uint32_t obase = s_base;
-    const ShdDeliv* wb = wide + s_wbase; // this bucket's wide events (k_wide_group)
+    const uint32_t* bpre = gcnt + 3 * (size_t)g.nb; // (k_wide_group's scan: part_cnt_words)
+    const uint32_t obase = bpre[b];
+    const ShdDeliv* wb = wide + (nw ? bpre[g.nb + 1 + b] : 0u); // this bucket's wide events (k_wide_group)
+    __syncthreads(); // (orders the cnt reset)
     const uint32_t m = *nwide;
     const bool wide_ok = m <= wide_cap;
     if (!wide_ok && b == 0 && threadIdx.x == 0) atomicOr(fault, kFaultOvfCap);
@@ -3526,6 +3534,8 @@ PartCfg part_cfg(uint32_t nb) {
     if (k == 2) return {(const void*)k_part_scatter<512, 2048, false>, 512, 2048, false};
     if (k == 3) return {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false};
     if (k == 4) return {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false};
+    if (k == 5) return {(const void*)k_part_scatter<512, 4096, false>, 512, 4096, false};
+    if (k == 6) return {(const void*)k_part_scatter<1024, 8192, false>, 1024, 8192, false};
     return {(const void*)k_part_scatter<1024, 4096, true>, 1024, 4096, true};
 }
 size_t part_lds(const PartCfg& f, uint32_t nb) {
@@ -3539,6 +3549,8 @@ int part_attr() {
                             {(const void*)k_part_scatter<512, 2048, false>, 512, 2048, false},
                             {(const void*)k_part_scatter<256, 2048, false>, 256, 2048, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<512, 4096, false>, 512, 4096, false},
+                            {(const void*)k_part_scatter<1024, 8192, false>, 1024, 8192, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 1>, 1024, 4096, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 2>, 1024, 4096, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 3>, 1024, 4096, false},
@@ -3580,15 +3592,18 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
             else SHD_PART_LAUNCH(1024, 4096, false, 4);
         } else if (f.lds) SHD_PART_LAUNCH(1024, 4096, true);
         else if (f.fn == (const void*)k_part_scatter<1024, 4096, false, 0, 8>) SHD_PART_LAUNCH(1024, 4096, false, 0, 8);
+        else if (f.wg == 1024 && f.ch == 8192) SHD_PART_LAUNCH(1024, 8192, false);
         else if (f.wg == 1024) SHD_PART_LAUNCH(1024, 4096, false);
+        else if (f.wg == 512 && f.ch == 4096) SHD_PART_LAUNCH(512, 4096, false);
         else if (f.wg == 512) SHD_PART_LAUNCH(512, 2048, false);
         else SHD_PART_LAUNCH(256, 2048, false);
 #undef SHD_PART_LAUNCH
         // the wide list by bucket (w.tmp: unused by this pipeline), for the
         // second pass to read its buckets' own
-        hipLaunchKernelGGL(k_wide_group, dim3(64), dim3(1024), 4 * (size_t)g.nb, s, g, w.st2, w.nbig + 1, (uint32_t)w.cap_n, wcnt,
-                           w.cnt1 + 2 * g.nb, w.tmp);
     }
+    // (also with no records: it writes the sort's bucket bases)
+    hipLaunchKernelGGL(k_wide_group, dim3(64), dim3(1024), 4 * (size_t)g.nb, s, g, w.st2, w.nbig + 1, (uint32_t)w.cap_n,
+                       gcnt, wcnt, w.cnt1 + 2 * g.nb, w.tmp);
     mark(1, s);
     mark_same(2, 1);
     int rc = hip_status(hipGetLastError(), "k_part_scatter launch");
@@ -3599,7 +3614,7 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
                uint64_t bootstrap_end, const PartGeo& g, ShdDeliv* d_out, uint32_t* d_dst_offsets, uint8_t* d_status,
                uint64_t* d_counters, hipStream_t s) {
     int rc;
-    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 3 * (size_t)g.nb, g.H)) ||
+    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, part_cnt_words(g.nb), g.H)) ||
         (rc = pstage_reserve(w, (size_t)g.nb * g.cap)))
         return rc;
     unsigned long long* counters = (unsigned long long*)d_counters;
@@ -3891,7 +3906,7 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
         // straight into the wire array (k_part_wire)
         unsigned long long* counters = (unsigned long long*)d_counters;
         int rc;
-        if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, 3 * (size_t)pg.nb, H)) ||
+        if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, part_cnt_words(pg.nb), H)) ||
             (rc = pstage_reserve(w, (size_t)pg.nb * pg.cap)) ||
             (rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, pg, d_status, counters, s)))
             return rc;
