@@ -983,7 +983,9 @@ __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* _
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)(e * 64 + lane);
         if (i >= n) continue;
-        if (kNT == 2) { // the exchange's 24-B wire record (out is a Wire array)
+        if (kNT == 3) { // the permutation only: out is an LDS index array, element i is item o + i
+            reinterpret_cast<uint16_t*>(out)[o + rank[e]] = (uint16_t)(o + i);
+        } else if (kNT == 2) { // the exchange's 24-B wire record (out is a Wire array)
             st_wire(reinterpret_cast<Wire*>(out) + o + rank[e], v[e].t, v[e].q, v[e].s, v[e].ix);
         } else if (kNT) {
             shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[o + rank[e]]);
@@ -2523,7 +2525,16 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                                                           ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
+    // perm: the segments' ranks go to an LDS permutation and the bucket is
+    // written in order afterwards -- consecutive lanes, consecutive 16-B (8-B
+    // for wire records) pieces of the output, whole lines per instruction
+    // instead of every event's two 16-B stores scattered over its segment
+    // (the instances whose LDS has room for the 2-B index per event; not the
+    // LDS-key-free four-per-CU one)
+    constexpr bool kPermOk = kCap <= 2304 && kKeyE > 0;
     __shared__ uint4 lev[kCap];
+    __shared__ uint16_t inv[kPermOk ? kCap : 1];
+    const bool perm = kPermOk && (lds_keys & 2u);
     __shared__ unsigned long long keys[kWG / 64][kKeyE ? 64 * kKeyE + 8 : 1];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
     const uint32_t b = blockIdx.x;
@@ -2608,7 +2619,9 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                 rank += (uint32_t)(x.x < r.x || (x.x == r.x && (sx < sr || (sx == sr && x.y < r.y))));
             }
             const unsigned long long t = g.tbase + r.x;
-            if (kWire) {
+            if (perm) {
+                inv[o + rank] = (uint16_t)i;
+            } else if (kWire) {
                 st_wire(reinterpret_cast<Wire*>(out) + obase + o + rank, t, (unsigned long long)r.y, sr, r.z);
             } else {
                 shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[obase + o + rank]);
@@ -2618,7 +2631,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                 __builtin_nontemporal_store(c2, q + 1);
             }
         }
-        unsigned long long* lk = lds_keys && kKeyE ? keys[wv] : nullptr;
+        unsigned long long* lk = (lds_keys & 1u) && kKeyE ? keys[wv] : nullptr;
         for (uint32_t j = wv; j < nd; j += kWG / 64) {
             const uint32_t nj = cnt[j], o = loc[j], dh = g.host_lo + d0 + j;
             if (nj <= kTinySeg) continue;
@@ -2627,20 +2640,53 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                 return Ev{g.tbase + r.x, (unsigned long long)r.y, r.w >> g.shift, r.z};
             };
             constexpr int kOut = kWire ? 2 : 1;
-            if (nj <= 64) wave_rank_segment<1, kOut>(load, nj, dh, out, obase + o, lane, lk);
-            else if (nj <= 128)
-                wave_rank_segment<2, kOut>(load, nj, dh, out, obase + o, lane, kKeyE >= 2 ? lk : nullptr);
-            else if (nj <= (uint32_t)kSmallSeg)
-                wave_rank_segment<4, kOut>(load, nj, dh, out, obase + o, lane, kKeyE >= 4 ? lk : nullptr);
-            else { // a larger segment: unsorted to its range of the staging array, listed
+            ShdDeliv* const wo = reinterpret_cast<ShdDeliv*>(inv);
+            if (nj <= 64) {
+                if (perm) wave_rank_segment<1, 3>(load, nj, dh, wo, o, lane, lk);
+                else wave_rank_segment<1, kOut>(load, nj, dh, out, obase + o, lane, lk);
+            } else if (nj <= 128) {
+                if (perm) wave_rank_segment<2, 3>(load, nj, dh, wo, o, lane, kKeyE >= 2 ? lk : nullptr);
+                else wave_rank_segment<2, kOut>(load, nj, dh, out, obase + o, lane, kKeyE >= 2 ? lk : nullptr);
+            } else if (nj <= (uint32_t)kSmallSeg) {
+                if (perm) wave_rank_segment<4, 3>(load, nj, dh, wo, o, lane, kKeyE >= 4 ? lk : nullptr);
+                else wave_rank_segment<4, kOut>(load, nj, dh, out, obase + o, lane, kKeyE >= 4 ? lk : nullptr);
+            } else { // a larger segment: unsorted to its range of the staging array, listed
                 for (uint32_t i = lane; i < nj; i += 64) {
                     const Ev v = load(i);
                     st_ev(&scr[obase + o + i], ShdDeliv{v.t, v.q, v.s, dh, v.ix, 0u});
+                    if (perm) inv[o + i] = 0xFFFFu; // (its place is the listed kernels' to write)
                 }
                 if (lane == 0) {
                     const uint32_t k = atomicAdd(nbig, 1u);
                     if (k < g.H) big[k] = d0 + j;
                     else atomicOr(nbig + 2, kFaultBigCap);
+                }
+            }
+        }
+        if (perm) { // the bucket in output order
+            __syncthreads();
+            if (kWire) {
+                uint2* ob = reinterpret_cast<uint2*>(reinterpret_cast<Wire*>(out) + obase);
+                for (uint32_t u = threadIdx.x; u < 3 * ns; u += kWG) {
+                    const uint32_t p = u / 3, part = u - 3 * p;
+                    const uint32_t i = inv[p];
+                    if (i == 0xFFFFu) continue;
+                    const uint4 r = lev[i];
+                    const unsigned long long t = g.tbase + r.x;
+                    ob[u] = part == 0 ? make_uint2((uint32_t)t, (uint32_t)(t >> 32))
+                            : part == 1 ? make_uint2(r.y, 0u)
+                                        : make_uint2(r.w >> g.shift, r.z);
+                }
+            } else {
+                shd_v4u* ob = reinterpret_cast<shd_v4u*>(out + obase);
+                for (uint32_t h = threadIdx.x; h < 2 * ns; h += kWG) {
+                    const uint32_t i = inv[h >> 1];
+                    if (i == 0xFFFFu) continue;
+                    const uint4 r = lev[i];
+                    const unsigned long long t = g.tbase + r.x;
+                    const shd_v4u a = (h & 1) ? shd_v4u{r.w >> g.shift, g.host_lo + d0 + (r.w & mask), r.z, 0u}
+                                              : shd_v4u{(uint32_t)t, (uint32_t)(t >> 32), r.y, 0u};
+                    __builtin_nontemporal_store(a, ob + h);
                 }
             }
         }
@@ -3085,6 +3131,14 @@ bool staged_partition() {
 uint32_t lds_keys() {
     const char* v = getenv("SHD_SEGSORT_LDS");
     return !(v && strcmp(v, "0") == 0);
+}
+// the part sort's flags word: bit 0 LDS keys, bit 1 (SHD_PART_PERM=1) buckets
+// written in order through the LDS permutation -- measured 3-4 us slower per
+// round than every event stored at its rank (profiles/r04af_part_perm_probe.log:
+// the L2 merges the scattered halves; the extra pass and barrier cost more)
+uint32_t part_sort_flags() {
+    const char* v = getenv("SHD_PART_PERM");
+    return lds_keys() | (v && strcmp(v, "1") == 0 ? 2u : 0u);
 }
 // Compact 16-B slab records (CSlab) with the rank sort; SHD_SLAB_COMPACT=0
 // (or the bitonic segment sort) keeps the 32-B slab
@@ -3627,14 +3681,14 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         const int sc = part_sort_cfg();
 #define SHD_PART_SORT_LAUNCH(WG, CAP, ...)                                                                            \
     hipLaunchKernelGGL((k_part_sort<WG, CAP, ##__VA_ARGS__>), dim3(g.nb), dim3(WG), 0, s, g, w.pstage, gcnt, wcnt, w.tmp, w.nbig + 1, \
-                       (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, lds_keys())
+                       (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, part_sort_flags())
         if (sc == 1) SHD_PART_SORT_LAUNCH(512, 3584);
         else if (sc == 2) SHD_PART_SORT_LAUNCH(256, 1792);
         else if (sc == 3) SHD_PART_SORT_LAUNCH(512, 2304, 2);
         else if (sc == 4)
             hipLaunchKernelGGL((k_part_sort_occ<512, 2304, 0, 8>), dim3(g.nb), dim3(512), 0, s, g, w.pstage, gcnt, wcnt,
                                w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters,
-                               lds_keys());
+                               part_sort_flags());
         else SHD_PART_SORT_LAUNCH(1024, 7168);
 #undef SHD_PART_SORT_LAUNCH
     }
@@ -3923,7 +3977,7 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
 #define SHD_WIRE_SORT_LAUNCH(WG, CAP, KE)                                                                             \
     hipLaunchKernelGGL((k_part_sort<WG, CAP, KE, true>), dim3(pg.nb), dim3(WG), 0, s, pg, w.pstage, w.cnt1,            \
                        w.cnt1 + pg.nb, w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_off, wout, w.st1, w.big, w.nbig, counters, \
-                       lds_keys())
+                       part_sort_flags())
             if (sc == 0) SHD_WIRE_SORT_LAUNCH(1024, 7168, 4);
             else if (sc == 1) SHD_WIRE_SORT_LAUNCH(512, 3584, 4);
             else if (sc == 2) SHD_WIRE_SORT_LAUNCH(256, 1792, 4);
