@@ -284,6 +284,36 @@ int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, v
                    const uint64_t* recv_bytes, void* stream) {
     return rccl_alltoallv_off(user, d_send, send_bytes, nullptr, d_recv, recv_bytes, stream);
 }
+// The exchange's two all-to-alls -- the payload (explicit send offsets) and
+// the destination offset slices (contiguous) -- as ONE send/recv group: one
+// RCCL launch per round instead of two back to back on the stream.
+int rccl_alltoallv2(void* user, const void* d_send, const uint64_t* send_bytes, const uint64_t* send_off,
+                    void* d_recv, const uint64_t* recv_bytes, const void* d_send2, const uint64_t* send2_bytes,
+                    void* d_recv2, const uint64_t* recv2_bytes, void* stream) {
+    Rccl* t = static_cast<Rccl*>(user);
+    const int W = t->x.world;
+    hipStream_t s = (hipStream_t)stream;
+    int rc = nccl_status(ncclGroupStart(), "ncclGroupStart");
+    if (rc) return rc;
+    uint64_t ro = 0, so2 = 0, ro2 = 0;
+    for (int r = 0; r < W && !rc; r++) {
+        if (send_bytes[r])
+            rc = nccl_status(ncclSend((const char*)d_send + send_off[r], send_bytes[r], ncclChar, r, t->comm, s),
+                             "ncclSend");
+        if (!rc && recv_bytes[r])
+            rc = nccl_status(ncclRecv((char*)d_recv + ro, recv_bytes[r], ncclChar, r, t->comm, s), "ncclRecv");
+        if (!rc && send2_bytes[r])
+            rc = nccl_status(ncclSend((const char*)d_send2 + so2, send2_bytes[r], ncclChar, r, t->comm, s),
+                             "ncclSend");
+        if (!rc && recv2_bytes[r])
+            rc = nccl_status(ncclRecv((char*)d_recv2 + ro2, recv2_bytes[r], ncclChar, r, t->comm, s), "ncclRecv");
+        ro += recv_bytes[r];
+        so2 += send2_bytes[r];
+        ro2 += recv2_bytes[r];
+    }
+    const int rc2 = nccl_status(ncclGroupEnd(), "ncclGroupEnd");
+    return rc ? rc : rc2;
+}
 
 // All-gather of variable blocks, in place: rank r's block is bytes
 // [off[r], off[r+1]) of buf.  Every rank sends its block straight to every
@@ -463,11 +493,8 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
         uint32_t* h_cuts = hscr;
         std::vector<uint64_t> soff(W);
         for (int r = 0; r < W; r++) soff[r] = (uint64_t)h_cuts[r] * elem_bytes; // (own block skipped, in place)
-        int rc3 = x->allgatherv == rccl_allgatherv
-                      ? rccl_alltoallv_off(x->user, d_events, sbytes.data(), soff.data(), d_recv, rbytes.data(), (void*)s)
-                      : local_alltoallv_off(x->user, d_events, sbytes.data(), soff.data(), d_recv, rbytes.data(),
-                                            (void*)s);
-        if (rc3) return rc3 < 0 ? rc3 : -EIO;
+        // the payload and the offset slices (H_r + 1 words to peer r, H_me + 1
+        // from each peer): one group on RCCL
         const size_t n_sl = (size_t)H + W;
         uint32_t* d_ro = d_sl + n_sl;
         uint32_t* d_bb = d_ro + (size_t)W * (Hm + 1);
@@ -476,7 +503,14 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
             sb[r] = 4ull * (host_bounds[r + 1] - host_bounds[r] + 1);
             rb[r] = 4ull * (Hm + 1);
         }
-        if ((rc3 = x->alltoallv(x->user, d_sl, sb.data(), d_ro, rb.data(), (void*)s))) return rc3 < 0 ? rc3 : -EIO;
+        int rc3;
+        if (x->allgatherv == rccl_allgatherv)
+            rc3 = rccl_alltoallv2(x->user, d_events, sbytes.data(), soff.data(), d_recv, rbytes.data(), d_sl,
+                                  sb.data(), d_ro, rb.data(), (void*)s);
+        else if (!(rc3 = local_alltoallv_off(x->user, d_events, sbytes.data(), soff.data(), d_recv, rbytes.data(),
+                                              (void*)s)))
+            rc3 = x->alltoallv(x->user, d_sl, sb.data(), d_ro, rb.data(), (void*)s);
+        if (rc3) return rc3 < 0 ? rc3 : -EIO;
         h_bb[0] = 0;
         for (int r = 0; r < W; r++) h_bb[r + 1] = h_bb[r] + (r == me ? 0u : (uint32_t)recv[r]);
         const void* self_block = static_cast<const char*>(d_events) + (size_t)h_cuts[me] * elem_bytes;

@@ -183,7 +183,8 @@ def test_unattached_address():
 
 
 @pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor", "slab_readlane", "slab_noagg", "rank_noagg",
-                        "slab_unfused", "slab_wide", "part", "part_readlane", "part_lds", "part_s1", "part_s2", "part_s3", "part_s4"])
+                        "slab_unfused", "slab_wide", "part", "part_readlane", "part_lds", "part_s1", "part_s2", "part_s3", "part_s4",
+                        "part_s3perm", "part_x5", "part_x6"])
 def pipeline(request, monkeypatch):
     """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE: bucket,
     rank, slab, part -- the LDS-staged bucket partition + per-bucket LDS sort;
@@ -197,10 +198,13 @@ def pipeline(request, monkeypatch):
     monkeypatch.setenv("SHD_DEST_AGG", "0" if request.param.endswith("noagg") else "1")
     monkeypatch.setenv("SHD_ROUND_FUSE", "0" if request.param.endswith("unfused") else "1")
     monkeypatch.setenv("SHD_SLAB_COMPACT", "0" if request.param.endswith("wide") else "1")
-    # part: the scatter's LDS-staged form, the bucket sort's other instances
-    monkeypatch.setenv("SHD_PART_SCATTER", "0" if request.param.endswith("lds") else "1")
-    monkeypatch.setenv("SHD_PART_SORT", request.param[-1] if request.param[:-1].endswith("_s") else "0")
-    return request.param
+    # part: the scatter's LDS-staged form and other instances (_xK), the
+    # bucket sort's other instances (_sK), its in-order write (perm)
+    p = request.param
+    monkeypatch.setenv("SHD_PART_SCATTER", "0" if p.endswith("lds") else p.split("_x")[1] if "_x" in p else "1")
+    monkeypatch.setenv("SHD_PART_SORT", p.split("_s")[1][0] if "_s" in p else "0")
+    monkeypatch.setenv("SHD_PART_PERM", "1" if p.endswith("perm") else "0")
+    return p
 
 
 ROUND_CASES = [
