@@ -1945,19 +1945,37 @@ __global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, 
 // rank of x (element i of run k) in the union of sorted runs staged one
 // after another in v (run j at [rs[j], rs[j+1])): its index in its run +
 // the elements before it in every other run, ties to the lower run (the
-// union's stable order)
+// union's stable order).  The binary searches of 8 runs at a time step in
+// lockstep: their LDS reads are independent, so one step costs one LDS
+// round trip instead of eight (the searches are latency-bound).
 __device__ __forceinline__ uint32_t merged_rank(const Ev* v, const uint32_t* rs, uint32_t W, uint32_t k, uint32_t i,
                                                 const Ev& x) {
     uint32_t rank = i - rs[k];
-    for (uint32_t j = 0; j < W; j++) {
-        if (j == k) continue;
-        uint32_t lo = rs[j], hi = rs[j + 1];
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (j < k ? !ev_lt(x, v[mid]) : ev_lt(v[mid], x)) lo = mid + 1;
-            else hi = mid;
+    for (uint32_t j0 = 0; j0 < W; j0 += 8) {
+        uint32_t lo[8], hi[8], b0[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t j = j0 + u;
+            const bool on = j < W && j != k;
+            lo[u] = b0[u] = on ? rs[j] : 0u;
+            hi[u] = on ? rs[j + 1] : 0u;
         }
-        rank += lo - rs[j];
+        for (bool any = true; any;) {
+            any = false;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (lo[u] < hi[u]) {
+                    const uint32_t mid = (lo[u] + hi[u]) >> 1;
+                    const Ev y = v[mid];
+                    const bool after = j0 + u < k ? !ev_lt(x, y) : ev_lt(y, x);
+                    lo[u] = after ? mid + 1 : lo[u];
+                    hi[u] = after ? hi[u] : mid;
+                    any = true;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) rank += lo[u] - b0[u];
     }
     return rank;
 }
@@ -2052,7 +2070,7 @@ __global__ __launch_bounds__(256) void k_runs_merge_wave(const void* __restrict_
 // work per segment instead of the rank sort's O(n^2), and no listed-segment
 // passes up to kMergeMax events.  Larger segments go unsorted to the
 // staging array and are listed, as in k_runs_sort.
-constexpr uint32_t kMergeMax = 2048;
+constexpr uint32_t kMergeMax = 1024; // (24 KiB of staged events: six workgroups per CU)
 template <int kFmt>
 __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in, const void* __restrict__ in_self,
                                                     uint32_t self, const uint32_t* __restrict__ rofs,
@@ -3907,7 +3925,7 @@ extern "C" int shd_dev_deliv_merge_runs_self(void* ws, const void* d_in, const v
         // n / (kSmallSeg + 1) of them), counted in w.cnt1[H] (free after the scan)
         uint32_t* nlong = w.cnt1 + H;
         if ((rc = hip_status(hipMemsetAsync(nlong, 0, 4, s), "memset nlong"))) return rc;
-        const unsigned g = grid_for(H, 1, 1024), gw = grid_for(H, 4, 16384);
+        const unsigned g = grid_for(H, 1, 2048), gw = grid_for(H, 4, 16384);
         if (wire) {
             hipLaunchKernelGGL(k_runs_merge_wave<1>, dim3(gw), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W,
                                H, d_dst_offsets, host_lo, d_out, w.rnk, nlong);

@@ -32,7 +32,11 @@ def _build(tsan: bool) -> str:
              "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "shadow_amd", "csrc")]
     if tsan:
         flags += ["-fsanitize=thread"]
-    subprocess.check_call(["gcc"] + flags + srcs + ["-o", exe, "-lm"])
+    # (built under a private name and renamed into place: pytest-xdist
+    # workers build the same binary at once and must not run a half-written one)
+    tmp = f"{exe}.{os.getpid()}"
+    subprocess.check_call(["gcc"] + flags + srcs + ["-o", tmp, "-lm"])
+    os.replace(tmp, exe)
     return exe
 
 
