@@ -84,8 +84,15 @@ def local_ranks(N):
 
     try:
         outs = {}
-        for v in ("auto", "1", "0", "auto", "1", "0"):
-            if v == "auto":
+        knob = os.environ.get("XCHG_PROBE_KNOB")  # NAME=v1/v2/...: A/B of another knob instead
+        arms = ("auto", "1", "0", "auto", "1", "0")
+        if knob:
+            kn, kv = knob.split("=")
+            arms = tuple(kv.split("/")) * 2
+        for v in arms:
+            if knob:
+                os.environ[kn] = v
+            elif v == "auto":
                 os.environ.pop("SHD_WIRE_SORTED", None)
             else:
                 os.environ["SHD_WIRE_SORTED"] = v
@@ -93,11 +100,13 @@ def local_ranks(N):
             t0 = time.perf_counter()
             rounds(5)
             dt = (time.perf_counter() - t0) / 5 * 1e3
-            print(f"N={N} SHD_WIRE_SORTED={v}: {dt:.3f} ms per exchanged round (all ranks on one GPU), "
+            print(f"N={N} {knob.split('=')[0] if knob else 'SHD_WIRE_SORTED'}={v}: {dt:.3f} ms per exchanged round "
+                  "(all ranks on one GPU), "
                   f"{sum(nres)} events", flush=True)
             outs[v] = union()
-        print("sorted and unsorted wire unions identical:",
-              bool(np.array_equal(outs["1"], outs["0"]) and np.array_equal(outs["auto"], outs["0"])), flush=True)
+        if not knob:
+            print("sorted and unsorted wire unions identical:",
+                  bool(np.array_equal(outs["1"], outs["0"]) and np.array_equal(outs["auto"], outs["0"])), flush=True)
     finally:
         xps.close()
         for t in tops:

@@ -1948,8 +1948,12 @@ __global__ __launch_bounds__(256) void k_runs_sort(const void* __restrict__ in, 
 // union's stable order).  The binary searches of 8 runs at a time step in
 // lockstep: their LDS reads are independent, so one step costs one LDS
 // round trip instead of eight (the searches are latency-bound).
+// With packed keys (pk != nullptr: pk[i] = (t - tmin) << 24 | src, distinct
+// unless time AND sender are equal) a step reads one 8-B key instead of the
+// 24-B event, and the event only on a key tie.
 __device__ __forceinline__ uint32_t merged_rank(const Ev* v, const uint32_t* rs, uint32_t W, uint32_t k, uint32_t i,
-                                                const Ev& x) {
+                                                const Ev& x, const unsigned long long* pk = nullptr,
+                                                unsigned long long kx = 0) {
     uint32_t rank = i - rs[k];
     for (uint32_t j0 = 0; j0 < W; j0 += 8) {
         uint32_t lo[8], hi[8], b0[8];
@@ -1966,8 +1970,14 @@ __device__ __forceinline__ uint32_t merged_rank(const Ev* v, const uint32_t* rs,
             for (int u = 0; u < 8; u++) {
                 if (lo[u] < hi[u]) {
                     const uint32_t mid = (lo[u] + hi[u]) >> 1;
-                    const Ev y = v[mid];
-                    const bool after = j0 + u < k ? !ev_lt(x, y) : ev_lt(y, x);
+                    bool after;
+                    const unsigned long long ky = pk ? pk[mid] : 0ull;
+                    if (pk && ky != kx) {
+                        after = ky < kx;
+                    } else {
+                        const Ev y = v[mid];
+                        after = j0 + u < k ? !ev_lt(x, y) : ev_lt(y, x);
+                    }
                     lo[u] = after ? mid + 1 : lo[u];
                     hi[u] = after ? hi[u] : mid;
                     any = true;
@@ -1996,8 +2006,7 @@ __global__ __launch_bounds__(256) void k_runs_merge_wave(const void* __restrict_
                                                          uint32_t self, const uint32_t* __restrict__ rofs,
                                                          const uint32_t* __restrict__ bbase, uint32_t W, uint32_t Hr,
                                                          const uint32_t* __restrict__ off, uint32_t host_lo,
-                                                         ShdDeliv* __restrict__ out, uint32_t* __restrict__ longl,
-                                                         uint32_t* __restrict__ nlong) {
+                                                         ShdDeliv* __restrict__ out) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wv;
     const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
@@ -2010,11 +2019,7 @@ __global__ __launch_bounds__(256) void k_runs_merge_wave(const void* __restrict_
     uint32_t* rb = rb_all[wv];
     for (uint32_t d = wave; d < Hr; d += nwaves) {
         const uint32_t o = off[d], n = off[d + 1] - o;
-        if (n == 0) continue;
-        if (n > (uint32_t)kSmallSeg) { // (k_runs_merge's, listed)
-            if (lane == 0) longl[atomicAdd(nlong, 1u)] = d;
-            continue;
-        }
+        if (n == 0 || n > (uint32_t)kSmallSeg) continue; // (longer: k_runs_merge's)
         uint32_t len = 0, src = 0;
         if ((uint32_t)lane < W) {
             const uint32_t a = rofs[(size_t)lane * (Hr + 1) + d];
@@ -2078,16 +2083,18 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
                                                     const uint32_t* __restrict__ off, uint32_t host_lo,
                                                     ShdDeliv* __restrict__ out, ShdDeliv* __restrict__ scr,
                                                     uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
-                                                    const uint32_t* __restrict__ longl,
-                                                    const uint32_t* __restrict__ nlong) {
+                                                    uint32_t probe) {
     __shared__ Ev sv[kMergeMax];
+    __shared__ unsigned long long sk[kMergeMax];
     __shared__ uint16_t inv[kMergeMax];
     __shared__ uint32_t rs[kMaxRuns + 1], rb[kMaxRuns];
+    __shared__ unsigned long long red[3][4];
     const uint32_t tid = threadIdx.x;
-    const uint32_t m = *nlong; // (the destinations k_runs_merge_wave listed)
-    for (uint32_t li = blockIdx.x; li < m; li += gridDim.x) {
-        const uint32_t d = longl[li];
+    // (the destinations above kSmallSeg events, found by scanning: listing
+    // them with one counter would serialise an atomic per destination)
+    for (uint32_t d = blockIdx.x; d < Hr; d += gridDim.x) {
         const uint32_t o = off[d], n = off[d + 1] - o;
+        if (n <= (uint32_t)kSmallSeg) continue; // (block-uniform)
         if (tid < 64) {
             uint32_t len = 0, src = 0;
             if (tid < W) {
@@ -2123,12 +2130,37 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
             __syncthreads();
             continue;
         }
+        unsigned long long tmn = ~0ull, tmx = 0ull, smx = 0ull;
         for (uint32_t i = tid; i < n; i += 256) {
             const uint32_t k = run_of(i);
-            sv[i] = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
+            const Ev e = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
+            sv[i] = e;
+            tmn = e.t < tmn ? e.t : tmn;
+            tmx = e.t > tmx ? e.t : tmx;
+            smx = e.s > smx ? e.s : smx;
         }
+        // packed keys when the segment's time span and sender ids allow
+        tmn = wave_min_u64(tmn);
+        tmx = wave_max_u64(tmx);
+        smx = wave_max_u64(smx);
+        if ((tid & 63) == 0) red[0][tid >> 6] = tmn, red[1][tid >> 6] = tmx, red[2][tid >> 6] = smx;
         __syncthreads();
-        for (uint32_t i = tid; i < n; i += 256) inv[merged_rank(sv, rs, W, run_of(i), i, sv[i])] = (uint16_t)i;
+        unsigned long long a = red[0][0], bx = red[1][0], cx = red[2][0];
+#pragma unroll
+        for (int q = 1; q < 4; q++) {
+            a = red[0][q] < a ? red[0][q] : a;
+            bx = red[1][q] > bx ? red[1][q] : bx;
+            cx = red[2][q] > cx ? red[2][q] : cx;
+        }
+        const bool packed = bx - a < (1ull << 40) && cx < (1ull << 24);
+        if (packed)
+            for (uint32_t i = tid; i < n; i += 256) sk[i] = ((sv[i].t - a) << 24) | sv[i].s;
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += 256) {
+            const Ev x = sv[i];
+            if (probe & 1u) inv[i] = (uint16_t)i; // (SHD_MERGE_PROBE: measurement only, output unsorted)
+            else inv[merged_rank(sv, rs, W, run_of(i), i, x, packed ? sk : nullptr, packed ? sk[i] : 0ull)] = (uint16_t)i;
+        }
         __syncthreads();
         for (uint32_t p = tid; p < n; p += 256) st_deliv_nt(&out[o + p], sv[inv[p]], dh);
         __syncthreads();
@@ -3921,21 +3953,19 @@ extern "C" int shd_dev_deliv_merge_runs_self(void* ws, const void* d_in, const v
     scan_counts(w.cnt1, (size_t)H, d_dst_offsets, w.bsum, nullptr, s);
     if (!d_self) self = 0xffffffffu;
     if (sorted) { // (every run sorted: merge by binary searches)
-        // the segments above kSmallSeg events are listed in w.rnk (at most
-        // n / (kSmallSeg + 1) of them), counted in w.cnt1[H] (free after the scan)
-        uint32_t* nlong = w.cnt1 + H;
-        if ((rc = hip_status(hipMemsetAsync(nlong, 0, 4, s), "memset nlong"))) return rc;
-        const unsigned g = grid_for(H, 1, 2048), gw = grid_for(H, 4, 16384);
+        const unsigned g = grid_for(H, 1, 8192), gw = grid_for(H, 4, 16384);
+        const char* mp = getenv("SHD_MERGE_PROBE"); // (measurement only)
+        const uint32_t mprobe = mp ? (uint32_t)atoi(mp) : 0u;
         if (wire) {
             hipLaunchKernelGGL(k_runs_merge_wave<1>, dim3(gw), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W,
-                               H, d_dst_offsets, host_lo, d_out, w.rnk, nlong);
+                               H, d_dst_offsets, host_lo, d_out);
             hipLaunchKernelGGL(k_runs_merge<1>, dim3(g), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
-                               d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, w.rnk, nlong);
+                               d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, mprobe);
         } else {
             hipLaunchKernelGGL(k_runs_merge_wave<0>, dim3(gw), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W,
-                               H, d_dst_offsets, host_lo, d_out, w.rnk, nlong);
+                               H, d_dst_offsets, host_lo, d_out);
             hipLaunchKernelGGL(k_runs_merge<0>, dim3(g), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
-                               d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, w.rnk, nlong);
+                               d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, mprobe);
         }
     } else if (wire)
         hipLaunchKernelGGL(k_runs_sort<1>, dim3(grid_for(H, 4, 16384)), dim3(256), 0, s, d_in, d_self, self, d_rofs,
