@@ -2913,6 +2913,7 @@ struct Ws {
     hipEvent_t done = nullptr; // recorded after the last launch that used the buffers
     hipStream_t last = nullptr;
     bool used = false;
+    bool checked = false; // the fault word of the last (completed) use has been read
     size_t cap_n = 0;
     ShdDeliv* tmp = nullptr; // decided events in record order
     ShdDeliv* st1 = nullptr; // events partitioned by bucket (bucket) / destination (rank)
@@ -3133,15 +3134,20 @@ int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDel
 // merge tile hit its spin limit (its input may have been incomplete: the
 // destination segment may be mis-sorted), the merge metadata overflowed or a
 // stage guard fired.
-int ws_faults(Ws& w, bool completed, hipStream_t s) {
-    if (!w.used || !w.meta) return 0;
-    if (!completed && hipEventQuery(w.done) != hipSuccess) return 0;
-    // the word, read on a stream of the workspace's own (it waits for nothing
-    // else: the use it reports on has completed)
+int fault_word_buf(Ws& w) {
     if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
         w.fault = nullptr;
         return shd_fail(-ENOMEM, "hipHostMalloc fault word");
     }
+    return 0;
+}
+int fault_report(Ws& w, hipStream_t s);
+int ws_faults(Ws& w, bool completed, hipStream_t s) {
+    if (!w.used || !w.meta || w.checked) return 0;
+    if (!completed && hipEventQuery(w.done) != hipSuccess) return 0;
+    // the word, read on a stream of the workspace's own (it waits for nothing
+    // else: the use it reports on has completed)
+    if (int rc = fault_word_buf(w)) return rc;
     if (!w.rd && hipStreamCreateWithFlags(&w.rd, hipStreamNonBlocking) != hipSuccess) {
         w.rd = nullptr;
         return shd_fail(-EIO, "hipStreamCreate fault read");
@@ -3150,6 +3156,23 @@ int ws_faults(Ws& w, bool completed, hipStream_t s) {
                             "fault word D2H"))
         return rc;
     if (int rc = hip_status(hipStreamSynchronize(w.rd), "fault word read")) return rc;
+    return fault_report(w, s);
+}
+// A synchronous call's end: the fault word copied on the call's own stream
+// behind its launches, one wait for both (not a wait for the round and then
+// another for the word's copy on a side stream)
+int ws_sync(Ws& w, hipStream_t s, const char* what) {
+    if (!w.meta) return hip_status(hipStreamSynchronize(s), what);
+    if (int rc = fault_word_buf(w)) return rc;
+    if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 4, hipMemcpyDeviceToHost, s),
+                            "fault word D2H"))
+        return rc;
+    if (int rc = hip_status(hipStreamSynchronize(s), what)) return rc;
+    return fault_report(w, s);
+}
+// *w.fault holds the word of the workspace's last, completed use
+int fault_report(Ws& w, hipStream_t s) {
+    w.checked = true;
     const uint32_t f = *w.fault;
     if (!f) return 0;
     *w.fault = 0;
@@ -3481,6 +3504,7 @@ int ws_begin(Ws& w, hipStream_t s) {
 int ws_end(Ws& w, hipStream_t s) {
     w.last = s;
     w.used = true;
+    w.checked = false;
     return hip_status(hipEventRecord(w.done, s), "hipEventRecord ws");
 }
 
@@ -3764,8 +3788,7 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
             int rc = part_round(w, c, d_recs, n, barrier, end_time, bootstrap_end, g, d_out, d_dst_offsets, d_status,
                                 d_counters, s);
             if (rc || stream) return rc;
-            if ((rc = hip_status(hipStreamSynchronize(s), "packet round"))) return rc;
-            return ws_faults(w, true, s);
+            return ws_sync(w, s, "packet round");
         }
         pipe = pipeline_for(H, true); // (buckets too many for the scatter's histogram: the slab form)
     }
@@ -3845,8 +3868,7 @@ else if (pipe == kSlabPipe && sb && strcmp(sb, "8") == 0)
     if (!rc) rc = ws_end(w, s);
     if (rc) return rc;
     if (stream) return 0;
-    if ((rc = hip_status(hipStreamSynchronize(s), "packet round"))) return rc;
-    return ws_faults(w, true, s);
+    return ws_sync(w, s, "packet round");
 }
 
 // Which grouping pipeline a round of n records over nhosts destinations runs
@@ -3927,8 +3949,7 @@ extern "C" int shd_dev_deliv_sort(void* ws, const ShdDeliv* d_in, size_t n, uint
     if (!rc) rc = ws_end(w, s);
     if (rc) return rc;
     if (stream) return 0;
-    if ((rc = hip_status(hipStreamSynchronize(s), "deliv sort"))) return rc;
-    return ws_faults(w, true, s);
+    return ws_sync(w, s, "deliv sort");
 }
 
 // Regroup of the exchange's W received blocks (see k_runs_count): d_in holds
@@ -3978,8 +3999,7 @@ extern "C" int shd_dev_deliv_merge_runs_self(void* ws, const void* d_in, const v
     if ((rc = sort_listed(w, w.st1, d_dst_offsets, d_out, s, nullptr))) return rc;
     if ((rc = ws_end(w, s))) return rc; // (not a timed round stage: shd_round_timing_* time the decide side)
     if (stream) return 0;
-    if ((rc = hip_status(hipStreamSynchronize(s), "merge runs"))) return rc;
-    return ws_faults(w, true, s);
+    return ws_sync(w, s, "merge runs");
 }
 
 extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, int sorted, size_t n, const uint32_t* d_rofs,
