@@ -2513,22 +2513,31 @@ __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* 
         __shared__ uint32_t ps[16];
         uint32_t* bpre = wcur + g.nb;
         uint32_t* wpre = bpre + g.nb + 1;
+        // (nb <= kPartMaxBuckets: at most 16 counts per thread, all loads in
+        // flight at once)
+        constexpr int kPer = (int)(kPartMaxBuckets / 1024);
         const uint32_t per = (g.nb + 1023) / 1024, b0 = threadIdx.x * per;
+        uint32_t gv[kPer], wv[kPer];
         uint32_t st = 0, sw = 0;
-        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) {
-            const uint32_t x = wcnt[b0 + k];
-            st += min(gcnt[b0 + k], g.cap) + x;
-            sw += x;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const bool in = (uint32_t)k < per && b0 + k < g.nb;
+            gv[k] = in ? min(gcnt[b0 + k], g.cap) : 0u;
+            wv[k] = in ? wcnt[b0 + k] : 0u;
         }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) st += gv[k] + wv[k], sw += wv[k];
         uint32_t tt, tw;
         uint32_t pt = block_excl_scan_n(st, &tt, ps);
         uint32_t pw = block_excl_scan_n(sw, &tw, ps);
-        for (uint32_t k = 0; k < per && b0 + k < g.nb; k++) {
-            const uint32_t x = wcnt[b0 + k];
-            bpre[b0 + k] = pt;
-            wpre[b0 + k] = pw;
-            pt += min(gcnt[b0 + k], g.cap) + x;
-            pw += x;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            if ((uint32_t)k < per && b0 + k < g.nb) {
+                bpre[b0 + k] = pt;
+                wpre[b0 + k] = pw;
+            }
+            pt += gv[k] + wv[k];
+            pw += wv[k];
         }
         if (threadIdx.x == 0) bpre[g.nb] = tt;
     }
