@@ -2070,12 +2070,17 @@ __global__ __launch_bounds__(256) void k_runs_merge_wave(const void* __restrict_
 
 // The owner's merge when every run is sorted (the senders' sorted wire, or
 // their sorted rounds), segments above kSmallSeg events: one workgroup per
-// destination, its W runs staged in LDS one after another, each element
-// placed by merged_rank (a binary search per other run) -- O(n W log n)
-// work per segment instead of the rank sort's O(n^2), and no listed-segment
-// passes up to kMergeMax events.  Larger segments go unsorted to the
-// staging array and are listed, as in k_runs_sort.
-constexpr uint32_t kMergeMax = 1024; // (24 KiB of staged events: six workgroups per CU)
+// destination, a pairwise merge tree over its W runs in LDS -- each level
+// places every element at its index in its run + its rank in the partner run
+// (one binary search: ties to the lower run, the union's stable order), so an
+// element costs log2(W) searches instead of W - 1 (8 runs: ≈24 key reads
+// instead of ≈56).  The searches compare packed 8-B keys (t - tmin) << 24 |
+// src (the events, re-read from the input, only on a key tie); LDS holds
+// keys, indices and each element's input position (24 KiB: six workgroups per
+// CU), and the sorted segment is written from the input in order.  A segment
+// whose time span or sender ids do not pack, or above kMergeMax events, goes
+// unsorted to the staging array and is listed, as in k_runs_sort.
+constexpr uint32_t kMergeMax = 1024;
 template <int kFmt>
 __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in, const void* __restrict__ in_self,
                                                     uint32_t self, const uint32_t* __restrict__ rofs,
@@ -2084,12 +2089,14 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
                                                     ShdDeliv* __restrict__ out, ShdDeliv* __restrict__ scr,
                                                     uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
                                                     uint32_t probe) {
-    __shared__ Ev sv[kMergeMax];
-    __shared__ unsigned long long sk[kMergeMax];
-    __shared__ uint16_t inv[kMergeMax];
+    constexpr int kPer = (int)(kMergeMax / 256);
+    __shared__ unsigned long long kbuf[2][kMergeMax];
+    __shared__ uint16_t ibuf[2][kMergeMax];
+    __shared__ uint32_t sa[kMergeMax]; // element -> its input position (bit 31: this rank's own block)
     __shared__ uint32_t rs[kMaxRuns + 1], rb[kMaxRuns];
     __shared__ unsigned long long red[3][4];
     const uint32_t tid = threadIdx.x;
+    auto ld_at = [&](uint32_t a) { return ld_run<kFmt>((a >> 31) ? in_self : in, a & 0x7fffffffu); };
     // (the destinations above kSmallSeg events, found by scanning: listing
     // them with one counter would serialise an atomic per destination)
     for (uint32_t d = blockIdx.x; d < Hr; d += gridDim.x) {
@@ -2116,7 +2123,48 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
             return k;
         };
         const uint32_t dh = d + host_lo;
-        if (n > kMergeMax) { // unsorted (runs one after another) to the staging array, listed
+        bool listed = n > kMergeMax; // (block-uniform)
+        Ev ev[kPer];
+        uint32_t ea[kPer];
+        if (!listed) {
+            unsigned long long tmn = ~0ull, tmx = 0ull, smx = 0ull;
+#pragma unroll
+            for (int e = 0; e < kPer; e++) {
+                const uint32_t i = tid + 256u * e;
+                if (i < n) {
+                    const uint32_t k = run_of(i);
+                    ea[e] = (k == self ? 0x80000000u : 0u) | (rb[k] + (i - rs[k]));
+                    ev[e] = ld_at(ea[e]);
+                    tmn = ev[e].t < tmn ? ev[e].t : tmn;
+                    tmx = ev[e].t > tmx ? ev[e].t : tmx;
+                    smx = ev[e].s > smx ? ev[e].s : smx;
+                }
+            }
+            tmn = wave_min_u64(tmn);
+            tmx = wave_max_u64(tmx);
+            smx = wave_max_u64(smx);
+            if ((tid & 63) == 0) red[0][tid >> 6] = tmn, red[1][tid >> 6] = tmx, red[2][tid >> 6] = smx;
+            __syncthreads();
+            unsigned long long a = red[0][0], bx = red[1][0], cx = red[2][0];
+#pragma unroll
+            for (int q = 1; q < 4; q++) {
+                a = red[0][q] < a ? red[0][q] : a;
+                bx = red[1][q] > bx ? red[1][q] : bx;
+                cx = red[2][q] > cx ? red[2][q] : cx;
+            }
+            listed = !(bx - a < (1ull << 40) && cx < (1ull << 24)); // (the keys do not pack: listed)
+            if (!listed)
+#pragma unroll
+                for (int e = 0; e < kPer; e++) {
+                    const uint32_t i = tid + 256u * e;
+                    if (i < n) {
+                        kbuf[0][i] = ((ev[e].t - a) << 24) | ev[e].s;
+                        ibuf[0][i] = (uint16_t)i;
+                        sa[i] = ea[e];
+                    }
+                }
+        }
+        if (listed) { // unsorted (runs one after another) to the staging array, listed
             for (uint32_t i = tid; i < n; i += 256) {
                 const uint32_t k = run_of(i);
                 const Ev e = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
@@ -2130,39 +2178,55 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
             __syncthreads();
             continue;
         }
-        unsigned long long tmn = ~0ull, tmx = 0ull, smx = 0ull;
-        for (uint32_t i = tid; i < n; i += 256) {
-            const uint32_t k = run_of(i);
-            const Ev e = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
-            sv[i] = e;
-            tmn = e.t < tmn ? e.t : tmn;
-            tmx = e.t > tmx ? e.t : tmx;
-            smx = e.s > smx ? e.s : smx;
-        }
-        // packed keys when the segment's time span and sender ids allow
-        tmn = wave_min_u64(tmn);
-        tmx = wave_max_u64(tmx);
-        smx = wave_max_u64(smx);
-        if ((tid & 63) == 0) red[0][tid >> 6] = tmn, red[1][tid >> 6] = tmx, red[2][tid >> 6] = smx;
         __syncthreads();
-        unsigned long long a = red[0][0], bx = red[1][0], cx = red[2][0];
-#pragma unroll
-        for (int q = 1; q < 4; q++) {
-            a = red[0][q] < a ? red[0][q] : a;
-            bx = red[1][q] > bx ? red[1][q] : bx;
-            cx = red[2][q] > cx ? red[2][q] : cx;
+        // the merge tree: runs [rs[r], rs[r+1]) of the current buffer, pairs
+        // (2q, 2q + 1) merged into the other buffer, the boundaries halved
+        int cur = 0;
+        for (uint32_t R = W; R > 1 && !(probe & 1u); R = (R + 1) >> 1) {
+            for (uint32_t i = tid; i < n; i += 256) {
+                const unsigned long long kx = kbuf[cur][i];
+                const uint16_t ix = ibuf[cur][i];
+                uint32_t r = 0;
+                while (rs[r + 1] <= i) r++;
+                const uint32_t p = r ^ 1u;
+                uint32_t pos = i;
+                if (p < R) {
+                    // left element (r even): partner elements strictly before it;
+                    // right element: partner elements before or equal (ties: left first)
+                    const bool left = (r & 1u) == 0;
+                    uint32_t lo = rs[p], hi = rs[p + 1];
+                    const uint32_t base = lo;
+                    bool have_x = false;
+                    Ev ex;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        const unsigned long long ky = kbuf[cur][mid];
+                        bool before;
+                        if (ky != kx) {
+                            before = ky < kx;
+                        } else { // a key tie: the events decide
+                            if (!have_x) ex = ld_at(sa[ix]), have_x = true;
+                            const Ev ey = ld_at(sa[ibuf[cur][mid]]);
+                            before = left ? ev_lt(ey, ex) : !ev_lt(ex, ey);
+                        }
+                        if (before) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    pos = rs[r & ~1u] + (i - rs[r]) + (lo - base);
+                }
+                kbuf[cur ^ 1][pos] = kx;
+                ibuf[cur ^ 1][pos] = ix;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                const uint32_t R2 = (R + 1) >> 1;
+                for (uint32_t q = 1; q < R2; q++) rs[q] = rs[2 * q];
+                rs[R2] = n;
+            }
+            cur ^= 1;
+            __syncthreads();
         }
-        const bool packed = bx - a < (1ull << 40) && cx < (1ull << 24);
-        if (packed)
-            for (uint32_t i = tid; i < n; i += 256) sk[i] = ((sv[i].t - a) << 24) | sv[i].s;
-        __syncthreads();
-        for (uint32_t i = tid; i < n; i += 256) {
-            const Ev x = sv[i];
-            if (probe & 1u) inv[i] = (uint16_t)i; // (SHD_MERGE_PROBE: measurement only, output unsorted)
-            else inv[merged_rank(sv, rs, W, run_of(i), i, x, packed ? sk : nullptr, packed ? sk[i] : 0ull)] = (uint16_t)i;
-        }
-        __syncthreads();
-        for (uint32_t p = tid; p < n; p += 256) st_deliv_nt(&out[o + p], sv[inv[p]], dh);
+        for (uint32_t p = tid; p < n; p += 256) st_deliv_nt(&out[o + p], ld_at(sa[ibuf[cur][p]]), dh);
         __syncthreads();
     }
 }
@@ -3521,6 +3585,11 @@ int ws_end(Ws& w, hipStream_t s) {
 
 // The workspace's faults after its last use, waited for: for callers that
 // synchronised their own streams (multi-shard collect, the exchange).
+extern "C" int shd_dev_ws_sync(void* ws, void* stream) {
+    if (!ws) return hip_status(hipStreamSynchronize((hipStream_t)stream), "stream sync");
+    return ws_sync(*static_cast<Ws*>(ws), (hipStream_t)stream, "stream sync");
+}
+
 extern "C" int shd_dev_ws_check_faults(void* ws) {
     if (!ws) return 0;
     Ws& w = *static_cast<Ws*>(ws);

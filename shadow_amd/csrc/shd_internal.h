@@ -168,6 +168,9 @@ int shd_dev_ws_xmat(void* ws, size_t words, uint64_t** d, uint64_t** h);
 /* The workspace's round faults after its last use (waits for it): 0, or -EIO
  * once per faulted round (merge spin-out, metadata overflow, stage guard). */
 int shd_dev_ws_check_faults(void* ws);
+/* synchronise `stream` (the workspace's last use was launched on it) and
+ * report that use's fault word, copied behind it on the same stream: one wait */
+int shd_dev_ws_sync(void* ws, void* stream);
 int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                          uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out, uint32_t* d_dst_offsets,
                          uint8_t* d_status, uint64_t* d_counters, void* stream);

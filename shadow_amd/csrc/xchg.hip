@@ -517,7 +517,7 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
         if ((rc3 = hip_status(hipMemcpyAsync(d_bb, h_bb, 4 * (size_t)(W + 1), hipMemcpyHostToDevice, s), "bases H2D")) ||
             (rc3 = shd_dev_deliv_merge_runs_self(ws, d_recv, self_block, (uint32_t)me, wire, all_sorted, nrecv, d_ro, d_bb,
                                                  (uint32_t)W, lo, hi, d_out, d_out_offsets, s)) ||
-            (rc3 = hip_status(hipStreamSynchronize(s), "exchange runs")) || (rc3 = shd_dev_ws_check_faults(ws)))
+            (rc3 = shd_dev_ws_sync(ws, (void*)s)))
             return rc3;
         *n_out = nrecv;
         return 0;
@@ -562,10 +562,9 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
     if ((rc = shd_dev_deliv_merge_runs_self(ws, d_recv, nullptr, 0xffffffffu, wire, wire ? 0 : sorted, nrecv, d_ro,
                                             d_bb, (uint32_t)W, lo, hi, d_out, d_out_offsets, s)))
         return rc;
-    if ((rc = hip_status(hipStreamSynchronize(s), "exchange runs"))) return rc;
     // the sender's round and this merge ran on the workspace: their faults
     // are this call's (synchronous) -- reported now, not by a later call
-    if ((rc = shd_dev_ws_check_faults(ws))) return rc;
+    if ((rc = shd_dev_ws_sync(ws, (void*)s))) return rc;
     *n_out = nrecv;
     return 0;
 }
