@@ -2984,6 +2984,7 @@ constexpr size_t kXmatWords = 64 * 66; // the exchange's count matrix at the lar
 struct Ws {
     int device = -1;           // device the buffers live on
     hipEvent_t done = nullptr; // recorded after the last launch that used the buffers
+    hipEvent_t fin = nullptr;  // a synchronous call's end (ws_sync)
     hipStream_t last = nullptr;
     bool used = false;
     bool checked = false; // the fault word of the last (completed) use has been read
@@ -3240,6 +3241,21 @@ int ws_sync(Ws& w, hipStream_t s, const char* what) {
     if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 4, hipMemcpyDeviceToHost, s),
                             "fault word D2H"))
         return rc;
+    // SHD_SYNC_SPIN (default 1): the calling thread polls an event recorded
+    // behind the call's work instead of sleeping in hipStreamSynchronize --
+    // the caller waits anyway, and the poll sees the end sooner than a
+    // wake-up does (the gap before the next round's launches)
+    const char* sp = getenv("SHD_SYNC_SPIN");
+    if (!(sp && strcmp(sp, "0") == 0)) {
+        if (!w.fin && hipEventCreateWithFlags(&w.fin, hipEventDisableTiming) != hipSuccess) w.fin = nullptr;
+        if (w.fin && hipEventRecord(w.fin, s) == hipSuccess) {
+            hipError_t e;
+            while ((e = hipEventQuery(w.fin)) == hipErrorNotReady) {
+            }
+            if (int rc = hip_status(e, what)) return rc;
+            return fault_report(w, s);
+        }
+    }
     if (int rc = hip_status(hipStreamSynchronize(s), what)) return rc;
     return fault_report(w, s);
 }
@@ -3629,6 +3645,7 @@ extern "C" void shd_dev_ws_free(void* p) {
     (void)hipFree(w->xmat);
     if (w->hxmat) (void)hipHostFree(w->hxmat);
     if (w->done) (void)hipEventDestroy(w->done);
+    if (w->fin) (void)hipEventDestroy(w->fin);
     delete w;
 }
 
