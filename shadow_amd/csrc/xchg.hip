@@ -610,8 +610,12 @@ extern "C" int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x,
     // (profiles/r04y_xchg_probe.log); below, the sender's sort costs more
     // than the owner's.  Ranks may choose differently: the owners merge
     // only when every run is sorted.
+    // (a caller's transport takes the three-step exchange, whose owners sort
+    // the wire runs anyway: no sender sort there)
+    const bool own = x->allgatherv == rccl_allgatherv || x->allgatherv == local_allgatherv;
     const char* sw = getenv("SHD_WIRE_SORTED");
-    const int sort_wire = sw && strcmp(sw, "1") == 0   ? 1
+    const int sort_wire = !own                         ? 0
+                          : sw && strcmp(sw, "1") == 0 ? 1
                           : sw && strcmp(sw, "0") == 0 ? 0
                                                        : (double)W * (double)n > 256.0 * (double)(H ? H : 1);
     int sorted = 0;
