@@ -2081,20 +2081,21 @@ __global__ __launch_bounds__(256) void k_runs_merge_wave(const void* __restrict_
 // whose time span or sender ids do not pack, or above kMergeMax events, goes
 // unsorted to the staging array and is listed, as in k_runs_sort.
 constexpr uint32_t kMergeMax = 1024;
+constexpr uint32_t kMergeThreads = 256; // (512: 240 vs 192 us per 8-rank owner merge, profiles/r04av_…)
 template <int kFmt>
-__global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in, const void* __restrict__ in_self,
+__global__ __launch_bounds__(kMergeThreads) void k_runs_merge(const void* __restrict__ in, const void* __restrict__ in_self,
                                                     uint32_t self, const uint32_t* __restrict__ rofs,
                                                     const uint32_t* __restrict__ bbase, uint32_t W, uint32_t Hr,
                                                     const uint32_t* __restrict__ off, uint32_t host_lo,
                                                     ShdDeliv* __restrict__ out, ShdDeliv* __restrict__ scr,
                                                     uint32_t* __restrict__ big, uint32_t* __restrict__ nbig,
                                                     uint32_t probe) {
-    constexpr int kPer = (int)(kMergeMax / 256);
+    constexpr int kPer = (int)(kMergeMax / kMergeThreads);
     __shared__ unsigned long long kbuf[2][kMergeMax];
     __shared__ uint16_t ibuf[2][kMergeMax];
     __shared__ uint32_t sa[kMergeMax]; // element -> its input position (bit 31: this rank's own block)
     __shared__ uint32_t rs[kMaxRuns + 1], rb[kMaxRuns];
-    __shared__ unsigned long long red[3][4];
+    __shared__ unsigned long long red[3][kMergeThreads / 64];
     const uint32_t tid = threadIdx.x;
     auto ld_at = [&](uint32_t a) { return ld_run<kFmt>((a >> 31) ? in_self : in, a & 0x7fffffffu); };
     // (the destinations above kSmallSeg events, found by scanning: listing
@@ -2130,7 +2131,7 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
             unsigned long long tmn = ~0ull, tmx = 0ull, smx = 0ull;
 #pragma unroll
             for (int e = 0; e < kPer; e++) {
-                const uint32_t i = tid + 256u * e;
+                const uint32_t i = tid + kMergeThreads * e;
                 if (i < n) {
                     const uint32_t k = run_of(i);
                     ea[e] = (k == self ? 0x80000000u : 0u) | (rb[k] + (i - rs[k]));
@@ -2147,7 +2148,7 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
             __syncthreads();
             unsigned long long a = red[0][0], bx = red[1][0], cx = red[2][0];
 #pragma unroll
-            for (int q = 1; q < 4; q++) {
+            for (int q = 1; q < (int)(kMergeThreads / 64); q++) {
                 a = red[0][q] < a ? red[0][q] : a;
                 bx = red[1][q] > bx ? red[1][q] : bx;
                 cx = red[2][q] > cx ? red[2][q] : cx;
@@ -2156,7 +2157,7 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
             if (!listed)
 #pragma unroll
                 for (int e = 0; e < kPer; e++) {
-                    const uint32_t i = tid + 256u * e;
+                    const uint32_t i = tid + kMergeThreads * e;
                     if (i < n) {
                         kbuf[0][i] = ((ev[e].t - a) << 24) | ev[e].s;
                         ibuf[0][i] = (uint16_t)i;
@@ -2165,7 +2166,7 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
                 }
         }
         if (listed) { // unsorted (runs one after another) to the staging array, listed
-            for (uint32_t i = tid; i < n; i += 256) {
+            for (uint32_t i = tid; i < n; i += kMergeThreads) {
                 const uint32_t k = run_of(i);
                 const Ev e = ld_run<kFmt>(k == self ? in_self : in, rb[k] + (i - rs[k]));
                 st_ev(&scr[o + i], ShdDeliv{e.t, e.q, e.s, dh, e.ix, 0u});
@@ -2183,7 +2184,7 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
         // (2q, 2q + 1) merged into the other buffer, the boundaries halved
         int cur = 0;
         for (uint32_t R = W; R > 1 && !(probe & 1u); R = (R + 1) >> 1) {
-            for (uint32_t i = tid; i < n; i += 256) {
+            for (uint32_t i = tid; i < n; i += kMergeThreads) {
                 const unsigned long long kx = kbuf[cur][i];
                 const uint16_t ix = ibuf[cur][i];
                 uint32_t r = 0;
@@ -2226,7 +2227,7 @@ __global__ __launch_bounds__(256) void k_runs_merge(const void* __restrict__ in,
             cur ^= 1;
             __syncthreads();
         }
-        for (uint32_t p = tid; p < n; p += 256) st_deliv_nt(&out[o + p], ld_at(sa[ibuf[cur][p]]), dh);
+        for (uint32_t p = tid; p < n; p += kMergeThreads) st_deliv_nt(&out[o + p], ld_at(sa[ibuf[cur][p]]), dh);
         __syncthreads();
     }
 }
@@ -4075,12 +4076,12 @@ extern "C" int shd_dev_deliv_merge_runs_self(void* ws, const void* d_in, const v
         if (wire) {
             hipLaunchKernelGGL(k_runs_merge_wave<1>, dim3(gw), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W,
                                H, d_dst_offsets, host_lo, d_out);
-            hipLaunchKernelGGL(k_runs_merge<1>, dim3(g), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
+            hipLaunchKernelGGL(k_runs_merge<1>, dim3(g), dim3(kMergeThreads), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
                                d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, mprobe);
         } else {
             hipLaunchKernelGGL(k_runs_merge_wave<0>, dim3(gw), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W,
                                H, d_dst_offsets, host_lo, d_out);
-            hipLaunchKernelGGL(k_runs_merge<0>, dim3(g), dim3(256), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
+            hipLaunchKernelGGL(k_runs_merge<0>, dim3(g), dim3(kMergeThreads), 0, s, d_in, d_self, self, d_rofs, d_bbase, W, H,
                                d_dst_offsets, host_lo, d_out, w.st1, w.big, w.nbig, mprobe);
         }
     } else if (wire)
