@@ -149,6 +149,7 @@ int shd_dev_ws_scratch(void* ws, size_t dev_bytes, size_t host_bytes, void** d, 
     return shd_fail(-ENOSYS, "stub device: no exchange scratch");
 }
 int shd_dev_ws_check_faults(void* ws) { return 0; }
+int shd_dev_ws_sync(void* ws, void* stream) { return 0; }
 int shd_dev_mem_info(size_t* free_bytes, size_t* total_bytes) {
     *free_bytes = *total_bytes = (size_t)1 << 40;
     return 0;
