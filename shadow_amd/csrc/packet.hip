@@ -2345,7 +2345,8 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
                                                       PartGeo g, uint4* __restrict__ stage,
                                                       uint32_t* __restrict__ gcnt, uint32_t* __restrict__ wcnt,
                                                       uint8_t* __restrict__ status, unsigned long long* counters,
-                                                      ShdDeliv* __restrict__ wide, uint32_t* __restrict__ nwide) {
+                                                      ShdDeliv* __restrict__ wide, uint32_t* __restrict__ nwide,
+                                                      uint32_t ch) {
     constexpr int kB = 4;
     constexpr int kR = kCH / kWG; // records per thread
     static_assert(kCH % (kWG * kB) == 0, "chunk");
@@ -2362,7 +2363,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
     const int lane = threadIdx.x & 63;
     for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) hist[b] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * kCH;
+    const size_t base = (size_t)blockIdx.x * ch; // (ch <= kCH records per workgroup, see part_front)
     const size_t A = (size_t)c.A;
     const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
     const uint2* __restrict__ ptab = reinterpret_cast<const uint2*>(c.ptab);
@@ -2377,7 +2378,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
 #pragma unroll
         for (int k = 0; k < kB; k++) {
             const size_t i = base + (size_t)(k0 + k) * kWG + threadIdx.x;
-            live[k] = i < n;
+            live[k] = (uint32_t)((k0 + k) * kWG + threadIdx.x) < ch && i < n;
             if (live[k]) p[k] = ld_pkt(&recs[i]);
         }
         int si[kB], di[kB];
@@ -3276,6 +3277,19 @@ int fault_report(Ws& w, hipStream_t s) {
                     (g & kFaultOff) ? ", offsets above the staging area" : "");
 }
 
+// compute units of the current device (cached per device)
+int dev_cus() {
+    static int cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cus[dev] = v;
+    }
+    return cus[dev];
+}
+
 unsigned grid_for(size_t n, unsigned block, unsigned cap) {
     size_t g = (n + block - 1) / block;
     if (g < 1) g = 1;
@@ -3803,11 +3817,21 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
     mark(0, s);
     if (n) {
         const PartCfg f = part_cfg(g.nb);
-        const dim3 grid((unsigned)((n + f.ch - 1) / f.ch)), blk(f.wg);
+        // records per workgroup: at most f.ch, spread so that the grid is a
+        // whole number of waves of one workgroup per CU (no last, partly
+        // filled wave of workgroups: 10M records = 2,560 x 3,907, not
+        // 2,442 x 4,096 on 256 CUs); SHD_PART_EVEN=0: f.ch each
+        uint32_t ch = (uint32_t)f.ch;
+        const char* ev = getenv("SHD_PART_EVEN");
+        if (!(ev && strcmp(ev, "0") == 0)) {
+            const size_t ncu = (size_t)dev_cus(), waves = (n + ncu * f.ch - 1) / (ncu * f.ch);
+            ch = (uint32_t)((n + ncu * waves - 1) / (ncu * waves));
+        }
+        const dim3 grid((unsigned)((n + ch - 1) / ch)), blk(f.wg);
         const size_t lds = part_lds(f, g.nb);
 #define SHD_PART_LAUNCH(WG, CH, L, ...)                                                                             \
     hipLaunchKernelGGL((k_part_scatter<WG, CH, L, ##__VA_ARGS__>), grid, blk, lds, s, *c, d_recs, n, barrier, end_time, \
-                       bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters, w.st2, w.nbig + 1)
+                       bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters, w.st2, w.nbig + 1, ch)
         const int pr = part_probe();
         if (pr && !f.lds && f.wg == 1024) {
             if (pr == 1) SHD_PART_LAUNCH(1024, 4096, false, 1);
