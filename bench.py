@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-routing", action="store_true")
     ap.add_argument("--no-nic", action="store_true", help="skip the receive-side interface leg (§8f-2/-4)")
+    ap.add_argument("--no-host-api", action="store_true", help="skip the host-API (append + collect) leg (§8b)")
+    ap.add_argument("--host-workers", type=int, default=8, help="worker threads appending in the host-API leg")
     ap.add_argument("--c4", type=int, default=1, help="1: also time the C4 routing build (V=100k, H=200k)")
     ap.add_argument("--c4-vertices", type=int, default=100_000)
     ap.add_argument("--c4-hosts", type=int, default=200_000)
@@ -407,6 +409,11 @@ def main():
     # ------------------------------------------- receive side (§8f-2 / -4)
     if not args.no_nic and world == 1:
         result["nic"] = nic_leg(lib, top, d_recs, d_out, d_off, delivered, H, dev, stream)
+
+    # ------------------------- the drop-in host boundary at C3 size (§8b)
+    if world == 1 and not args.no_host_api:
+        result["host_api"] = host_api_leg(lib, top, pk, H, barrier_t, end_t, d_out, d_off, delivered,
+                                          args.host_workers)
 
     # ------------------------------------------------------------ C1 routing
     if not args.no_routing:
@@ -768,6 +775,78 @@ def nic_leg(lib, top, d_recs, d_out, d_off, delivered, H, dev, stream, reps=5):
     }
 
 
+def host_api_leg(lib, top, pk, H, barrier_t, end_t, d_out, d_off, delivered, nworkers=8, reps=5):
+    """The drop-in boundary as Shadow drives it (manager.c:553-573): during the
+    round `nworkers` worker threads call shd_round_append_worker concurrently
+    (each its share of the bench's C3 batch: the send-time lookups, staged in
+    its own pinned buffer), then the scheduler thread calls shd_round_collect
+    at the boundary (records to the device, the round -- path packet
+    counters included -- and events, offsets and statuses back into pinned
+    host buffers from shd_host_buffer_alloc).  Steady state: every row
+    touched, buffers grown by the first (untimed) round.  The collected round
+    is checked against the device round of the timed region."""
+    import threading
+
+    from shadow_amd import _lib, synth
+    P = len(pk)
+    h = top.handle
+    _lib.check(lib.shd_round_set_workers(h, nworkers))
+    bounds = [k * P // nworkers for k in range(nworkers + 1)]
+    chunks = [np.ascontiguousarray(pk[bounds[w]:bounds[w + 1]]) for w in range(nworkers)]
+    bufs = [C.c_void_p() for _ in range(3)]
+    sizes = [P * 32, (H + 1) * 4, P]
+    for b, n in zip(bufs, sizes):
+        _lib.check(lib.shd_host_buffer_alloc(n, C.byref(b)))
+    app, col = [], []
+    nout, mt = C.c_size_t(), C.c_uint64()
+    try:
+        for r in range(reps + 1):
+            _lib.check(lib.shd_round_begin(h, barrier_t, end_t, 0))
+            gate = threading.Barrier(nworkers + 1)
+            rcs = [None] * nworkers
+
+            def work(w):
+                gate.wait()
+                rcs[w] = lib.shd_round_append_worker(h, w, chunks[w].ctypes.data, len(chunks[w]))
+            th = [threading.Thread(target=work, args=(w,)) for w in range(nworkers)]
+            for t in th:
+                t.start()
+            gate.wait()
+            t0 = time.perf_counter()
+            for t in th:
+                t.join()
+            t1 = time.perf_counter()
+            for rc in rcs:
+                _lib.check(rc)
+            _lib.check(lib.shd_round_collect(h, bufs[0], P, C.byref(nout), bufs[1], bufs[2], C.byref(mt)))
+            t2 = time.perf_counter()
+            if r:
+                app.append(t1 - t0)
+                col.append(t2 - t1)
+        nev = int(nout.value)
+        got = np.ctypeslib.as_array(C.cast(bufs[0], C.POINTER(C.c_uint8)), shape=(nev * 32,))
+        offs = np.ctypeslib.as_array(C.cast(bufs[1], C.POINTER(C.c_uint32)), shape=(H + 1,))
+        same = nev == delivered and bool(np.array_equal(got, d_out[:nev * 32].cpu().numpy())) and bool(
+            np.array_equal(offs.view(np.int32), d_off.cpu().numpy()))
+    finally:
+        for b in bufs:
+            lib.shd_host_buffer_free(b)
+    ta, tc = float(np.median(app)), float(np.median(col))
+    moved = 32 * P + 32 * nev + 4 * (H + 1) + P
+    return {
+        "config": f"the bench's C3 batch ({P} packets over {H} hosts) through the drop-in host API: {nworkers} "
+                  "threads append concurrently, then one collect (manager.c:553-573)",
+        "value": P / (ta + tc), "unit": "packets/s", "workers": nworkers, "reps": reps,
+        "append_ms": ta * 1e3, "collect_ms": tc * 1e3, "append_packets_per_s": P / ta,
+        "collect_packets_per_s": P / tc, "collect_host_link_bytes": moved,
+        "collect_host_link_GBps": moved / tc / 1e9,
+        "equals_device_round": same,
+        "what": "append = send-time lookups + staging into each worker's pinned buffer (steady state: no side "
+                "effect left, one copy); collect = records H2D + the round on the device (decide, group, sort, "
+                "path packet counters) + events/offsets/status D2H into pinned buffers; medians over the reps",
+    }
+
+
 def cpu_rows_parallel(orc, sources, targets, threads):
     """Oracle Dijkstra rows on `threads` host threads (ctypes releases the GIL
     inside orc_compute_row; rows are independent, like the reference's rows
@@ -779,10 +858,49 @@ def cpu_rows_parallel(orc, sources, targets, threads):
     return (time.perf_counter() - t0) / len(sources)
 
 
+def cpu_share():
+    """The host cores this job may use, and the evidence for the number:
+    the cgroup CPU quota (/sys/fs/cgroup/cpu.max, cgroup v2; cpu.cfs_quota_us
+    under v1) if one is set, the scheduler affinity, and OMP_NUM_THREADS (the
+    job's CPU share as the GPU box declares it to its jobs; nproc there shows
+    the whole machine).  threads = SHD_CPU_THREADS if set, else the smallest
+    of the affinity and the quota, else of the affinity and the declared
+    share."""
+    quota, src = None, None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                txt = f.read().split()
+        except OSError:
+            continue
+        src = f"{path}: {' '.join(txt)}"
+        if path.endswith("cpu.max") and txt and txt[0] != "max" and len(txt) == 2:
+            quota = int(txt[0]) / int(txt[1])
+        elif path.endswith("cfs_quota_us") and txt and int(txt[0]) > 0:
+            try:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    quota = int(txt[0]) / int(f.read().split()[0])
+            except OSError:
+                pass
+        break
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if os.environ.get("SHD_CPU_THREADS"):
+        n, why = int(os.environ["SHD_CPU_THREADS"]), "SHD_CPU_THREADS"
+    elif quota:
+        n, why = max(1, min(aff, int(quota))), "min(affinity, cgroup quota)"
+    elif omp and omp.isdigit() and int(omp) > 0:
+        n, why = min(aff, int(omp)), "min(affinity, OMP_NUM_THREADS: the job's declared CPU share; no cgroup quota)"
+    else:
+        n, why = aff, "affinity (no quota, no declared share)"
+    return {"threads_used": n, "threads_rule": why, "cgroup_cpu": src, "cgroup_quota_cpus": quota,
+            "affinity_cpus": aff, "omp_num_threads": omp}
+
+
 def host_cpu():
     """The box's CPU as the CPU baseline ran on it (model and
     core count stated): /proc/cpuinfo's model, the machine's CPUs and the
-    ones this process may run on."""
+    share this job may use (cpu_share)."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -792,20 +910,19 @@ def host_cpu():
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
-            "threads_used": int(os.environ.get("SHD_CPU_THREADS", "16"))}
+    return dict({"cpu_model": model, "nproc": os.cpu_count()}, **cpu_share())
 
 
 def cpu_baseline(gml, H, states, top, result, c4_ctx=None, pk=None, c2_hosts=50_000):
     """The oracle (C restatement of worker_sendPacket + per-destination binary
     heaps) timed on this host: the headline figure is the bench's own C3
     batch over the full table on one core; beside it the same batch on the
-    box's 16-thread CPU share and the round-2 bounded subsample."""
+    job's host cores (cpu_share) and the round-2 bounded subsample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ctypes as O  # checker/baseline only
     from shadow_amd import scenario, synth
 
-    threads = int(os.environ.get("SHD_CPU_THREADS", "16"))
+    threads = cpu_share()["threads_used"]
     lat, rel, sv = top.table()
     base = {}
     hostinfo = host_cpu()
@@ -867,9 +984,8 @@ def cpu_baseline(gml, H, states, top, result, c4_ctx=None, pk=None, c2_hosts=50_
     base["routing"] = {"value": 5000.0 ** 2 / full, "unit": "routed host-pairs/s", "cores": 1, "kind": "port",
                        "sample": f"{k} of {len(targets)} C1 source rows (igraph-0.8 Dijkstra restatement), "
                                  f"extrapolated to the full table: {full:.2f}s"}
-    # row-parallel oracle on the box's CPU share ("all N host
-    # cores"); the box exposes 16 CPUs to a job, os.cpu_count() shows the host
-    threads = int(os.environ.get("SHD_CPU_THREADS", "16"))
+    # row-parallel oracle on the job's host cores ("all N host
+    # cores"; the count and its evidence in base["host"], cpu_share())
     per_mt = cpu_rows_parallel(o1, targets, targets, threads)
     base["routing_mt"] = {"value": 5000.0 ** 2 / (per_mt * len(targets)), "unit": "routed host-pairs/s",
                           "cores": threads, "kind": "port",

@@ -297,11 +297,38 @@ int shd_round_staged(ShdTopology* top, size_t* n);
  * UINT64_MAX if none. */
 int shd_round_collect(ShdTopology* top, ShdDeliv* out, size_t cap, size_t* n_out, uint32_t* dst_offsets,
                       uint8_t* status, uint64_t* min_time);
+/* Pinned (page-locked) host memory, e.g. for shd_round_collect's out /
+ * dst_offsets / status: copies into it run at the host link's full rate.
+ * Any host memory works there; this is the fast kind.  Worker staging
+ * buffers are pinned by the library itself. */
+int shd_host_buffer_alloc(size_t bytes, void** out);
+void shd_host_buffer_free(void* p);
+
+/* Path packet counters (topology_incrementPathPacketCounter, worker.c:551):
+ * every round -- shd_round_collect, shd_round_process_device,
+ * shd_round_process_exchange -- counts each kept packet (delivered or
+ * dropped at the end time) at its answering pair on the device, inside the
+ * round's own kernels; shd_topology_get_path_packet_count and the teardown
+ * log read them back.  With a row-sharded table a rank counts the packets
+ * it decides (the pair's total is the sum over ranks). */
+/* Every counter of table rows [row_lo, row_hi) (slots as in
+ * shd_topology_copy_table): counts[(i - row_lo) * A + j] = the packets
+ * counted at pair (i, j), host-side increments included (the count the
+ * teardown log prints for the cached path (i, j)).  Rows this topology does
+ * not hold (another rank's shard) read 0. */
+int shd_topology_copy_path_packet_counts(ShdTopology* top, int row_lo, int row_hi, uint64_t* counts);
+/* The rounds log each kept packet's pair (one store per record, inside the
+ * round's own kernels) and the log is added into the device counters in
+ * bulk: when it fills, before any of the readers above, and here.  Waits for
+ * every round in flight on the topology's device(s).  A benchmark calls it
+ * inside its timed region so that every counted packet is in the time. */
+int shd_topology_path_counts_sync(ShdTopology* top);
 
 /* Device-resident variant (inputs already in HBM; used by benchmarks and the
  * multi-GPU exchange).  All pointers are device pointers; stream is a
- * hipStream_t (NULL = default stream).  Lookup side effects are NOT applied:
- * rows must have been touched (shd_round_append or shd_topology_touch_all).
+ * hipStream_t (NULL = default stream).  The lookup side effects (row touch,
+ * min-jump) are NOT applied: rows must have been touched (shd_round_append
+ * or shd_topology_touch_all); the path packet counters are counted.
  * out needs n entries, dst_offsets nhosts+1, status n; counters[0] =
  * delivered count, counters[1] = min delivered time (both written async).
  * A round whose device-side guards fired (a merge tile that gave up waiting,

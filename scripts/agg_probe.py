@@ -52,11 +52,15 @@ def main():
                 os.environ[name] = agg
             for _ in range(2):
                 run_round()
+            if os.environ.get("PROBE_SYNC_COUNTS") == "1":
+                top.path_counts_sync()  # (the warm-up rounds' counts: outside the timed block)
             torch.cuda.synchronize()
             _lib.check(lib.shd_round_timing_enable(1))
             t0 = time.perf_counter()
             for _ in range(20):
                 run_round()
+            if os.environ.get("PROBE_SYNC_COUNTS") == "1":  # the logged path counts folded in the timed block
+                top.path_counts_sync()
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / 20 * 1e3
             st = (C.c_double * 4)()

@@ -45,6 +45,8 @@ PROTOS = {
     "shd_topology_is_routable": (C.c_int, [_P, C.c_uint32, C.c_uint32, _ip]),
     "shd_topology_increment_path_packet_counter": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "shd_topology_get_path_packet_count": (C.c_int, [_P, C.c_uint32, C.c_uint32, _u64p]),
+    "shd_topology_copy_path_packet_counts": (C.c_int, [_P, C.c_int, C.c_int, _P]),
+    "shd_topology_path_counts_sync": (C.c_int, [_P]),
     "shd_topology_lookup_batch": (C.c_int, [_P, _P, _P, C.c_size_t, _P, _P]),
     "shd_topology_set_min_jump_callback": (C.c_int, [_P, MINJUMP_FN, _P]),
     "shd_topology_get_min_path_latency": (C.c_int, [_P, _dp]),
@@ -73,6 +75,8 @@ PROTOS = {
     "shd_round_append": (C.c_int, [_P, _P, C.c_size_t]),
     "shd_round_staged": (C.c_int, [_P, C.POINTER(C.c_size_t)]),
     "shd_round_collect": (C.c_int, [_P, _P, C.c_size_t, C.POINTER(C.c_size_t), _P, _P, _u64p]),
+    "shd_host_buffer_alloc": (C.c_int, [C.c_size_t, C.POINTER(_P)]),
+    "shd_host_buffer_free": (None, [_P]),
     "shd_round_process_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint64, C.c_uint64, C.c_uint64, _P, _P, _P, _P,
                                            _P]),
     "shd_deliv_sort_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P, _P]),

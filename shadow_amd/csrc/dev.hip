@@ -65,6 +65,25 @@ extern "C" int shd_dev_d2d(void* d, const void* s, size_t bytes) {
     return bytes ? hip_err(hipMemcpy(d, s, bytes, hipMemcpyDeviceToDevice), "hipMemcpy D2D") : 0;
 }
 
+extern "C" int shd_dev_h2d_async(void* d, const void* h, size_t bytes, void* s) {
+    return bytes ? hip_err(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, (hipStream_t)s), "hipMemcpyAsync H2D") : 0;
+}
+
+extern "C" int shd_dev_d2h_async(void* h, const void* d, size_t bytes, void* s) {
+    return bytes ? hip_err(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, (hipStream_t)s), "hipMemcpyAsync D2H") : 0;
+}
+
+// Pinned (page-locked) host memory: the round's staging buffers, so their
+// copies run at the link's rate and asynchronously on the round's stream.
+extern "C" int shd_host_alloc(void** p, size_t bytes) {
+    *p = nullptr;
+    return hip_err(hipHostMalloc(p, bytes ? bytes : 4, hipHostMallocDefault), "hipHostMalloc");
+}
+
+extern "C" void shd_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 extern "C" int shd_dev_memset(void* d, int v, size_t bytes) {
     return bytes ? hip_err(hipMemset(d, v, bytes), "hipMemset") : 0;
 }

@@ -228,6 +228,23 @@ __device__ __forceinline__ bool c_fits(unsigned long long t, unsigned long long 
     return t >= tbase && t - tbase < kCMark && seq <= 0xFFFFFFFFull;
 }
 
+// The round's path packet counter log (ShdPktCtx.plog): record i's key, the
+// flat index of its answering pair, or all-ones when the packet was not kept
+// (dropped by loss, or not decided here).  One coalesced store per record --
+// 4 B (8 B for tables of 2^32 entries or more) instead of a memory-side
+// atomic per kept packet: the atomics ran at the chip's ~25 G/s atomic rate
+// (+0.365 ms on the 10M-packet round, k_part_scatter 0.43 -> 0.795 ms,
+// profiles/r05b_pcnt_atomic_ab.log); the log is added into the dense counters
+// in bulk (shd_dev_pcnt_fold).
+__device__ __forceinline__ void pcnt_log(const ShdPktCtx& c, size_t i, bool kept, size_t key) {
+    if (!c.plog) return;
+    if (c.plog64)
+        __builtin_nontemporal_store(kept ? (unsigned long long)key : ~0ull,
+                                    static_cast<unsigned long long*>(c.plog) + i);
+    else
+        __builtin_nontemporal_store(kept ? (uint32_t)key : ~0u, static_cast<uint32_t*>(c.plog) + i);
+}
+
 // kMode 1 ("rank" pipeline): each delivered event takes its slot in its
 // destination segment from a per-destination global counter (the counter's
 // old value, carried in pad); cnt1 is then the per-destination count array.
@@ -383,8 +400,12 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
                         st[k] = SHD_DELIVERED;
                         tt[k] = t;
                     }
+                    // topology_incrementPathPacketCounter (worker.c:551): every kept packet,
+                    // before the end-time drop, at its answering pair
+                    if (c.pcnt) atomicAdd(c.pcnt + ei[k], 1u);
                 }
             }
+            if (live[k]) pcnt_log(c, idx[k], st[k] == SHD_DELIVERED || st[k] == SHD_DROPPED_END, ei[k]);
         }
 #pragma unroll
         for (int k = 0; k < kB; k++) {
@@ -2453,8 +2474,12 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
                         if (p[k].src_host != p[k].dst_host && t < barrier) t = barrier; // host_single.c:187-192
                         st = SHD_DELIVERED;
                     }
+                    // topology_incrementPathPacketCounter (worker.c:551): every kept packet
+                    // at its answering pair (SHD_PCNT=atomic: a memory-side atomic each)
+                    if (c.pcnt) atomicAdd(c.pcnt + ei[k], 1u);
                 }
             }
+            if (live[k]) pcnt_log(c, base + li, st == SHD_DELIVERED || st == SHD_DROPPED_END, ei[k]);
             const bool dl = st == SHD_DELIVERED;
             const uint32_t dr = p[k].dst_host - g.host_lo;
             const bool fits = dl && c_fits(t, g.tbase, p[k].seq) && p[k].src_host <= smax && dr < g.H;
@@ -3076,6 +3101,9 @@ int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
         (void)hipFree(w.bsum);
         (void)hipFree(w.poff);
         (void)hipFree(w.cursor);
+        // (nulled at once: a failed allocation below leaves no freed pointer
+        // for a retried reserve to free again)
+        w.cnt1 = w.off1 = w.bsum = w.poff = w.cursor = nullptr;
         w.cap_m = 0;
         const size_t cap = m + 1 + (m >> 3) + 4096;
         if ((rc = hip_status(hipMalloc((void**)&w.cnt1, 4 * cap), "hipMalloc ws.cnt1")) ||
@@ -3089,6 +3117,7 @@ int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
     if (H + 1 > w.cap_h) {
         (void)hipFree(w.big);
         (void)hipFree(w.nbig);
+        w.big = w.nbig = nullptr;
         w.cap_h = 0;
         const uint32_t cap = H + 1 + 1024;
         if ((rc = hip_status(hipMalloc((void**)&w.big, 4ull * cap), "hipMalloc ws.big")) ||
@@ -3684,7 +3713,222 @@ __global__ __launch_bounds__(256) void k_ptab_build(const ShdEntry* __restrict__
         out[i] = ptab_entry(tab[i]);
 }
 
+// Path packet counters >= thr move to a list (see shd_dev_pcnt_spill): one
+// wave-aggregated slot reservation per wave, the appended entries zeroed.
+__global__ __launch_bounds__(256) void k_pcnt_spill(uint32_t* __restrict__ cnt, size_t n, uint32_t thr,
+                                                    unsigned long long* __restrict__ list, uint32_t cap,
+                                                    uint32_t* __restrict__ nlist) {
+    const int lane = threadIdx.x & 63;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    // (uniform trip count over the wave: wave_alloc ballots)
+    for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+        const size_t i = i0 + threadIdx.x;
+        const uint32_t v = i < n ? cnt[i] : 0u;
+        const bool hit = i < n && v >= thr && v != 0u;
+        const uint32_t slot = wave_alloc(hit, nlist, lane);
+        if (hit && slot < cap) {
+            list[2 * (size_t)slot] = i;
+            list[2 * (size_t)slot + 1] = v;
+            cnt[i] = 0u;
+        }
+    }
+}
+
+// ---- the counter log's fold (shd_dev_pcnt_fold) ----
+// Key space [0, N) in buckets of 2^S counters (at most kFoldBuckets of
+// them); the log in W chunks, one 1,024-thread workgroup each.
+// 1. k_fold_hist: each chunk's histogram over the buckets (LDS) -> column w
+//    of the bucket-major matrix M[b * W + w];
+// 2. the exclusive scan of M (scan_counts): every (bucket, chunk) run's start;
+// 3. k_fold_scatter: each chunk's keys to their runs (LDS cursors);
+// 4. k_fold_add: one workgroup per bucket adds its keys into LDS counters
+//    (sub-regions of 2^kFoldLds counters: 128 KB) and then each nonzero LDS
+//    counter into the dense table -- the bucket's counters belong to this
+//    workgroup alone, so plain loads and stores, and only the lines with a
+//    nonzero counter move (a dense bucket streams, a sparse one touches few).
+constexpr uint32_t kFoldBuckets = 16384;
+constexpr uint32_t kFoldLds = 15; // log2 of the LDS counters per pass (32K x 4 B)
+constexpr int kFoldWG = 1024;
+constexpr int kFoldUnroll = 4;
+
+template <typename K>
+__global__ __launch_bounds__(kFoldWG) void k_fold_hist(const K* __restrict__ keys, size_t L, uint32_t S, uint32_t B,
+                                                       size_t chunk, uint32_t W, uint32_t* __restrict__ M) {
+    extern __shared__ uint32_t fh[];
+    for (uint32_t b = threadIdx.x; b < B; b += kFoldWG) fh[b] = 0;
+    __syncthreads();
+    const size_t beg = (size_t)blockIdx.x * chunk, end = beg + chunk < L ? beg + chunk : L;
+    for (size_t i0 = beg + threadIdx.x; i0 < end; i0 += (size_t)kFoldWG * kFoldUnroll) {
+        K k[kFoldUnroll];
+#pragma unroll
+        for (int u = 0; u < kFoldUnroll; u++) {
+            const size_t i = i0 + (size_t)u * kFoldWG;
+            k[u] = i < end ? __builtin_nontemporal_load(keys + i) : (K)~(K)0;
+        }
+#pragma unroll
+        for (int u = 0; u < kFoldUnroll; u++)
+            if (k[u] != (K)~(K)0) atomicAdd(&fh[(uint32_t)(k[u] >> S)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < B; b += kFoldWG) M[(size_t)b * W + blockIdx.x] = fh[b];
+}
+
+template <typename K>
+__global__ __launch_bounds__(kFoldWG) void k_fold_scatter(const K* __restrict__ keys, size_t L, uint32_t S, uint32_t B,
+                                                          size_t chunk, uint32_t W, const uint32_t* __restrict__ off,
+                                                          K* __restrict__ part) {
+    extern __shared__ uint32_t fo[];
+    for (uint32_t b = threadIdx.x; b < B; b += kFoldWG) fo[b] = off[(size_t)b * W + blockIdx.x];
+    __syncthreads();
+    const size_t beg = (size_t)blockIdx.x * chunk, end = beg + chunk < L ? beg + chunk : L;
+    for (size_t i0 = beg + threadIdx.x; i0 < end; i0 += (size_t)kFoldWG * kFoldUnroll) {
+        K k[kFoldUnroll];
+#pragma unroll
+        for (int u = 0; u < kFoldUnroll; u++) {
+            const size_t i = i0 + (size_t)u * kFoldWG;
+            k[u] = i < end ? __builtin_nontemporal_load(keys + i) : (K)~(K)0;
+        }
+#pragma unroll
+        for (int u = 0; u < kFoldUnroll; u++)
+            if (k[u] != (K)~(K)0) part[atomicAdd(&fo[(uint32_t)(k[u] >> S)], 1u)] = k[u];
+    }
+}
+
+template <typename K>
+__global__ __launch_bounds__(kFoldWG) void k_fold_add(const K* __restrict__ part, const uint32_t* __restrict__ off,
+                                                      uint32_t W, uint32_t S, uint32_t* __restrict__ dense,
+                                                      unsigned long long N) {
+    extern __shared__ uint32_t fc[];
+    const uint32_t b = blockIdx.x;
+    const size_t beg = off[(size_t)b * W], end = off[(size_t)(b + 1) * W];
+    if (beg == end) return; // (block-uniform)
+    const uint32_t R = S < kFoldLds ? S : kFoldLds;
+    const uint32_t nsub = 1u << (S - R);
+    const unsigned long long bbase = (unsigned long long)b << S;
+    for (uint32_t sub = 0; sub < nsub; sub++) {
+        const unsigned long long sbase = bbase + ((unsigned long long)sub << R);
+        if (sbase >= N) break;
+        for (uint32_t j = threadIdx.x; j < (1u << R); j += kFoldWG) fc[j] = 0;
+        __syncthreads();
+        for (size_t i0 = beg + threadIdx.x; i0 < end; i0 += (size_t)kFoldWG * kFoldUnroll) {
+            K k[kFoldUnroll];
+#pragma unroll
+            for (int u = 0; u < kFoldUnroll; u++) {
+                const size_t i = i0 + (size_t)u * kFoldWG;
+                k[u] = i < end ? part[i] : (K)~(K)0;
+            }
+#pragma unroll
+            for (int u = 0; u < kFoldUnroll; u++) {
+                const unsigned long long rel = (unsigned long long)k[u] - sbase;
+                if (k[u] != (K)~(K)0 && rel < (1ull << R)) atomicAdd(&fc[(uint32_t)rel], 1u);
+            }
+        }
+        __syncthreads();
+        const unsigned long long rem = N - sbase;
+        const uint32_t lim = rem < (1ull << R) ? (uint32_t)rem : (1u << R);
+        for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
+            const uint32_t v = fc[j];
+            if (v) dense[sbase + j] += v;
+        }
+        __syncthreads();
+    }
+}
+
+struct FoldScratch {
+    void* part = nullptr;
+    size_t cap_part = 0; // bytes
+    uint32_t* M = nullptr;
+    size_t cap_M = 0; // words
+    uint32_t* bsum = nullptr;
+    size_t cap_bsum = 0;
+};
+
+template <typename K>
+int pcnt_fold(const K* log, size_t L, uint32_t* dense, unsigned long long N, FoldScratch& f, hipStream_t s) {
+    uint32_t S = kFoldLds;
+    while ((N - 1) >> S >= kFoldBuckets) S++;
+    const uint32_t B = (uint32_t)(((N - 1) >> S) + 1);
+    size_t chunk = (L + 1023) / 1024;
+    if (chunk < (1u << 16)) chunk = 1u << 16;
+    const uint32_t W = (uint32_t)((L + chunk - 1) / chunk);
+    const size_t m = (size_t)B * W;
+    int rc = 0;
+    auto grow = [&](void** p, size_t* cap, size_t need, const char* what) {
+        if (need <= *cap) return 0;
+        (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        const size_t c = need + need / 8;
+        if (int r = hip_status(hipMalloc(p, c), what)) return r;
+        *cap = c;
+        return 0;
+    };
+    size_t cm = f.cap_M * 4, cb = f.cap_bsum * 4;
+    if ((rc = grow(&f.part, &f.cap_part, L * sizeof(K), "hipMalloc fold part")) ||
+        (rc = grow((void**)&f.M, &cm, 4 * (m + 1), "hipMalloc fold matrix")) ||
+        (rc = grow((void**)&f.bsum, &cb, 4 * (m / kScanTile + 2), "hipMalloc fold scan")))
+        return rc;
+    f.cap_M = cm / 4;
+    f.cap_bsum = cb / 4;
+    static bool attr = false;
+    if (!attr) {
+        if ((rc = hip_status(hipFuncSetAttribute((const void*)k_fold_add<uint32_t>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 << kFoldLds),
+                             "hipFuncSetAttribute k_fold_add")) ||
+            (rc = hip_status(hipFuncSetAttribute((const void*)k_fold_add<unsigned long long>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 << kFoldLds),
+                             "hipFuncSetAttribute k_fold_add")))
+            return rc;
+        attr = true;
+    }
+    K* part = static_cast<K*>(f.part);
+    hipLaunchKernelGGL(k_fold_hist<K>, dim3(W), dim3(kFoldWG), 4 * (size_t)B, s, log, L, S, B, chunk, W, f.M);
+    scan_counts(f.M, m, f.M, f.bsum, nullptr, s);
+    hipLaunchKernelGGL(k_fold_scatter<K>, dim3(W), dim3(kFoldWG), 4 * (size_t)B, s, log, L, S, B, chunk, W, f.M,
+                       part);
+    // (the scatter's cursors live in LDS: M still holds every run's start, so
+    // bucket b spans [M[b * W], M[(b + 1) * W]))
+    hipLaunchKernelGGL(k_fold_add<K>, dim3(B), dim3(kFoldWG), (size_t)4 << (S < kFoldLds ? S : kFoldLds), s, part,
+                       f.M, W, S, dense, N);
+    return hip_status(hipGetLastError(), "pcnt fold launch");
+}
+
 } // namespace
+
+extern "C" int shd_dev_pcnt_fold(const void* log, int log64, size_t L, uint32_t* dense, uint64_t N, void** scratch,
+                                 void* stream) {
+    if (!L || !N) return 0;
+    if (!*scratch && !(*scratch = new (std::nothrow) FoldScratch())) return shd_fail(-ENOMEM, "fold scratch");
+    FoldScratch& f = *static_cast<FoldScratch*>(*scratch);
+    hipStream_t s = (hipStream_t)stream;
+    return log64 ? pcnt_fold(static_cast<const unsigned long long*>(log), L, dense, N, f, s)
+                 : pcnt_fold(static_cast<const uint32_t*>(log), L, dense, N, f, s);
+}
+
+extern "C" void shd_dev_pcnt_scratch_free(void* scratch) {
+    if (!scratch) return;
+    FoldScratch* f = static_cast<FoldScratch*>(scratch);
+    (void)hipFree(f->part);
+    (void)hipFree(f->M);
+    (void)hipFree(f->bsum);
+    delete f;
+}
+
+extern "C" int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, size_t cap,
+                                  uint32_t* d_nlist, size_t* appended) {
+    *appended = 0;
+    if (!n) return 0;
+    if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;
+    int rc = hip_status(hipMemset(d_nlist, 0, 4), "hipMemset spill count");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_pcnt_spill, dim3(grid_for(n, 256, 8192)), dim3(256), 0, nullptr, cnt, n, thr,
+                       (unsigned long long*)d_list, (uint32_t)cap, d_nlist);
+    if ((rc = hip_status(hipGetLastError(), "k_pcnt_spill launch"))) return rc;
+    uint32_t m = 0;
+    if ((rc = hip_status(hipMemcpy(&m, d_nlist, 4, hipMemcpyDeviceToHost), "spill count D2H"))) return rc;
+    *appended = m < cap ? m : cap;
+    return 0;
+}
 
 extern "C" int shd_dev_ptab_build(const ShdEntry* tab, size_t nent, void* d_out, void* stream) {
     if (!nent) return 0;

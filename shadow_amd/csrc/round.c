@@ -32,7 +32,7 @@ int shd_round_set_workers(ShdTopology* t, int nworkers) {
         ShdWorkerBuf* nb = (ShdWorkerBuf*)calloc((size_t)nworkers, sizeof(ShdWorkerBuf));
         if (!nb) rc = -ENOMEM;
         else {
-            for (int w = 0; w < t->nworkers; w++) free(t->wbuf[w].recs);
+            for (int w = 0; w < t->nworkers; w++) shd_host_free(t->wbuf[w].recs);
             free(t->wbuf);
             t->wbuf = nb;
             t->nworkers = nworkers;
@@ -63,28 +63,53 @@ static int rec_slots(const ShdTopology* t, const ShdPkt* p, int* si, int* di) {
     return 0;
 }
 
+/* Grows worker buffer b (pinned host memory: the collect copies it to the
+ * device asynchronously at the link's rate) to hold `need` records. */
+static int wbuf_reserve(ShdWorkerBuf* b, size_t need) {
+    if (need <= b->cap) return 0;
+    size_t nc = b->cap ? b->cap : 4096;
+    while (nc < need) nc *= 2;
+    ShdPkt* s = NULL;
+    int rc = shd_host_alloc((void**)&s, sizeof(ShdPkt) * nc);
+    if (rc) return rc;
+    if (b->n) memcpy(s, b->recs, sizeof(ShdPkt) * b->n);
+    shd_host_free(b->recs);
+    b->recs = s;
+    b->cap = nc;
+    return 0;
+}
+
 int shd_round_append_worker(ShdTopology* t, int worker, const ShdPkt* recs, size_t n) {
     if (!t || (!recs && n) || worker < 0 || worker >= t->nworkers) return shd_fail(-EINVAL, "bad append arguments");
     int rc = shd_ensure_routes(t);
     if (rc) return rc;
     if (!__atomic_load_n(&t->lookups_started, __ATOMIC_RELAXED)) __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
-    /* validate the whole batch before any side effect or copy */
-    int si, di;
-    for (size_t i = 0; i < n; i++)
-        if (rec_slots(t, &recs[i], &si, &di)) return shd_fail(-ENOENT, "packet %zu references an unattached host", i);
+    /* validate the whole batch before any side effect or copy; note whether
+     * any send can still have a lookup side effect (a first touch of its row,
+     * a first self or direct pair) -- none in the steady state, where the
+     * batch is then one copy.  (Every attached pair of a validated graph is
+     * routable: strongly connected, or complete for direct paths.) */
+    const uint32_t* hs = t->h_host_info; /* {slot, -} per host, UINT32_MAX: unattached */
+    const uint32_t H = t->nhosts;
+    size_t pending = 0;
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t s = recs[i].src_host, d = recs[i].dst_host;
+        if (s >= H || d >= H || hs[2 * (size_t)s] == SHD_UNTOUCHED || hs[2 * (size_t)d] == SHD_UNTOUCHED)
+            return shd_fail(-ENOENT, "packet %zu references an unattached host", i);
+        pending += (size_t)shd_resolve_pending(t, (int)hs[2 * (size_t)s], (int)hs[2 * (size_t)d]);
+    }
     ShdWorkerBuf* b = &t->wbuf[worker];
-    if (b->n + n > b->cap) {
-        size_t nc = b->cap ? b->cap : 4096;
-        while (nc < b->n + n) nc *= 2;
-        ShdPkt* s = (ShdPkt*)realloc(b->recs, sizeof(ShdPkt) * nc);
-        if (!s) return -ENOMEM;
-        b->recs = s;
-        b->cap = nc;
+    if ((rc = wbuf_reserve(b, b->n + n))) return rc;
+    if (!pending) {
+        if (n) memcpy(b->recs + b->n, recs, sizeof(ShdPkt) * n);
+        b->n += n;
+        return 0;
     }
     for (size_t i = 0; i < n && !rc; i++) {
-        rec_slots(t, &recs[i], &si, &di);
+        const int si = (int)hs[2 * (size_t)recs[i].src_host], di = (int)hs[2 * (size_t)recs[i].dst_host];
         int oi, oj;
-        rc = shd_resolve(t, si, di, &oi, &oj); /* topology_getReliability's lookup, at send time */
+        if (shd_resolve_pending(t, si, di))
+            rc = shd_resolve(t, si, di, &oi, &oj); /* topology_getReliability's lookup, at send time */
         if (!rc) b->recs[b->n++] = recs[i];
     }
     /* device-resident rows first touched here are queued; launched in batches
@@ -94,6 +119,13 @@ int shd_round_append_worker(ShdTopology* t, int worker, const ShdPkt* recs, size
 }
 
 int shd_round_append(ShdTopology* t, const ShdPkt* recs, size_t n) { return shd_round_append_worker(t, 0, recs, n); }
+
+int shd_host_buffer_alloc(size_t bytes, void** out) {
+    if (!out) return -EINVAL;
+    return shd_host_alloc(out, bytes);
+}
+
+void shd_host_buffer_free(void* p) { shd_host_free(p); }
 
 int shd_round_staged(ShdTopology* t, size_t* n) {
     if (!t || !n) return -EINVAL;
@@ -122,79 +154,94 @@ static int gather_staged(ShdTopology* t, size_t* n_out) {
     return 0;
 }
 
-/* topology_incrementPathPacketCounter for every kept packet of the staged
- * batch (worker.c:551), delivered or discarded at the end time alike; the
- * lookups were made at append, so this only resolves owners and counts.
- * Only an allocation failure of the counter map stops it halfway; the
- * caller has already consumed the batch, so a retry cannot count twice. */
-static int count_kept(ShdTopology* t, size_t n, const uint8_t* status) {
+/* The collect's device buffers for n records over H hosts (grow-only; the
+ * previous round on the collect stream has completed). */
+static int collect_reserve(ShdTopology* t, size_t n, uint32_t H) {
     int rc = 0;
-    pthread_mutex_lock(&t->pkt_mu);
-    for (size_t i = 0; i < n && !rc; i++)
-        if (status[i] != SHD_DROPPED_LOSS) {
-            int si, di, oi, oj;
-            rec_slots(t, &t->staged[i], &si, &di);
-            if (!(rc = shd_resolve(t, si, di, &oi, &oj))) rc = shd_count_packet_locked(t, oi, oj, 1);
-        }
-    pthread_mutex_unlock(&t->pkt_mu);
-    return rc;
+    if (!t->cstream && (rc = shd_dev_stream_new(&t->cstream))) return rc;
+    if (!t->h_ccnt && (rc = shd_host_alloc((void**)&t->h_ccnt, 16))) return rc;
+    if (!t->d_ccnt && (rc = shd_dev_malloc((void**)&t->d_ccnt, 16))) return rc;
+    if (!n) n = 1;
+    if (n > t->cap_c) {
+        shd_dev_free(t->d_crecs);
+        shd_dev_free(t->d_cout);
+        shd_dev_free(t->d_cstat);
+        t->d_crecs = NULL;
+        t->d_cout = NULL;
+        t->d_cstat = NULL;
+        t->cap_c = 0;
+        const size_t cap = n + n / 8 + 1024;
+        if ((rc = shd_dev_malloc((void**)&t->d_crecs, sizeof(ShdPkt) * cap)) ||
+            (rc = shd_dev_malloc((void**)&t->d_cout, sizeof(ShdDeliv) * cap)) ||
+            (rc = shd_dev_malloc((void**)&t->d_cstat, cap)))
+            return rc;
+        t->cap_c = cap;
+    }
+    if (H + 1 > t->cap_coff) {
+        shd_dev_free(t->d_coff);
+        t->d_coff = NULL;
+        t->cap_coff = 0;
+        if ((rc = shd_dev_malloc((void**)&t->d_coff, sizeof(uint32_t) * ((size_t)H + 1)))) return rc;
+        t->cap_coff = H + 1;
+    }
+    return 0;
 }
 
+/* The round boundary on one device: the worker buffers (pinned) go to the
+ * device on the collect stream, the round runs there (path packet counters
+ * included, on the device), and the outputs come back on the same stream:
+ * one wait for the event count, one for the copies.  No allocation in the
+ * steady state. */
 static int collect_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_out, uint32_t* dst_offsets,
                           uint8_t* status, uint64_t* min_time) {
     size_t n = 0;
     int rc = shd_ensure_routes(t);
     if (rc) return rc;
-    if ((rc = gather_staged(t, &n))) return rc;
+    for (int w = 0; w < t->nworkers; w++) n += t->wbuf[w].n;
     if (cap < n && out) return shd_fail(-ENOSPC, "output capacity %zu < %zu records", cap, n);
     if ((rc = shd_dev_init(t->device))) return rc;
-    ShdPkt* d_recs = NULL;
-    ShdDeliv* d_out = NULL;
-    uint32_t* d_off = NULL;
-    uint8_t* d_status = NULL;
-    uint64_t* d_cnt = NULL;
-    uint8_t* h_status = NULL;
-    size_t nn = n ? n : 1;
-    if ((rc = shd_dev_malloc((void**)&d_recs, sizeof(ShdPkt) * nn)) ||
-        (rc = shd_dev_malloc((void**)&d_out, sizeof(ShdDeliv) * nn)) ||
-        (rc = shd_dev_malloc((void**)&d_off, sizeof(uint32_t) * ((size_t)t->nhosts + 1))) ||
-        (rc = shd_dev_malloc((void**)&d_status, nn)) || (rc = shd_dev_malloc((void**)&d_cnt, 16)))
-        goto done;
-    if (n && (rc = shd_dev_h2d(d_recs, t->staged, sizeof(ShdPkt) * n))) goto done;
-    if ((rc = shd_sync_touch(t)) || (rc = shd_ensure_ptab(t))) goto done;
+    if ((rc = collect_reserve(t, n, t->nhosts))) return rc;
+    void* s = t->cstream;
+    size_t at = 0;
+    for (int w = 0; w < t->nworkers && !rc; w++) {
+        rc = shd_dev_h2d_async(t->d_crecs + at, t->wbuf[w].recs, sizeof(ShdPkt) * t->wbuf[w].n, s);
+        at += t->wbuf[w].n;
+    }
+    if (rc) return rc;
+    if ((rc = shd_sync_touch(t)) || (rc = shd_pcnt_ensure(t, &t->pcnt, t->tab_row_lo, t->tab_row_hi, n)) ||
+        (rc = shd_ensure_ptab(t)))
+        return rc;
     ShdPktCtx c;
     shd_pkt_ctx(t, &c);
-    rc = shd_dev_packet_round(&c, d_recs, n, t->barrier, t->end_time, t->bootstrap_end, d_out, d_off, d_status,
-                              d_cnt, NULL);
+    rc = shd_dev_packet_round(&c, t->d_crecs, n, t->barrier, t->end_time, t->bootstrap_end, t->d_cout, t->d_coff,
+                              t->d_cstat, t->d_ccnt, s);
     if (shd_ptab_release_for_retry(t, rc)) {
         shd_pkt_ctx(t, &c);
-        rc = shd_dev_packet_round(&c, d_recs, n, t->barrier, t->end_time, t->bootstrap_end, d_out, d_off, d_status,
-                                  d_cnt, NULL);
+        rc = shd_dev_packet_round(&c, t->d_crecs, n, t->barrier, t->end_time, t->bootstrap_end, t->d_cout, t->d_coff,
+                                  t->d_cstat, t->d_ccnt, s);
     }
-    if (rc) goto done;
-    uint64_t cnt[2];
-    if ((rc = shd_dev_d2h(cnt, d_cnt, 16))) goto done;
-    if (n_out) *n_out = (size_t)cnt[0];
-    if (min_time) *min_time = cnt[1];
-    if (out && cnt[0] && (rc = shd_dev_d2h(out, d_out, sizeof(ShdDeliv) * (size_t)cnt[0]))) goto done;
-    if (dst_offsets && (rc = shd_dev_d2h(dst_offsets, d_off, sizeof(uint32_t) * ((size_t)t->nhosts + 1)))) goto done;
-    h_status = status ? status : (uint8_t*)malloc(nn);
-    if (!h_status) {
-        rc = -ENOMEM;
-        goto done;
+    shd_pcnt_commit(&t->pcnt, rc);
+    if (!rc) rc = shd_dev_d2h_async(t->h_ccnt, t->d_ccnt, 16, s);
+    if (!rc) rc = shd_dev_ws_sync(c.ws, s); /* (the round's own fault report) */
+    if (rc) {
+        (void)shd_dev_stream_sync(s); /* nothing of this round stays in flight */
+        return rc;
     }
-    if ((rc = shd_dev_d2h(h_status, d_status, n))) goto done;
-    /* the round is decided: its records leave the staging buffers whatever
-     * happens below (a retried collect must not count them twice) */
+    /* the round is decided and counted: its records leave the staging
+     * buffers whatever happens below (a retried collect must not count them
+     * twice) */
     for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0;
-    rc = count_kept(t, n, h_status);
-done:
-    if (h_status != status) free(h_status);
-    shd_dev_free(d_recs);
-    shd_dev_free(d_out);
-    shd_dev_free(d_off);
-    shd_dev_free(d_status);
-    shd_dev_free(d_cnt);
+    const uint64_t nev = t->h_ccnt[0], mt = t->h_ccnt[1];
+    if (out && nev) rc = shd_dev_d2h_async(out, t->d_cout, sizeof(ShdDeliv) * (size_t)nev, s);
+    if (!rc && dst_offsets)
+        rc = shd_dev_d2h_async(dst_offsets, t->d_coff, sizeof(uint32_t) * ((size_t)t->nhosts + 1), s);
+    if (!rc && status) rc = shd_dev_d2h_async(status, t->d_cstat, n, s);
+    const int rcs = shd_dev_stream_sync(s);
+    if (!rc) rc = rcs;
+    if (!rc) {
+        if (n_out) *n_out = (size_t)nev;
+        if (min_time) *min_time = mt;
+    }
     return rc;
 }
 
@@ -295,7 +342,7 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
         if ((rc = shd_dev_init(s->device))) break;
         if (!s->stream && (rc = shd_dev_stream_new(&s->stream))) break;
         if (!s->ws && (rc = shd_dev_ws_new(&s->ws))) break;
-        if ((rc = sync_shard_touch(t, s))) break;
+        if ((rc = sync_shard_touch(t, s)) || (rc = shd_pcnt_ensure(t, &s->pcnt, s->lo, s->hi, nk))) break;
         GROW(s->d_recs, s->cap_n, nk, sizeof(ShdPkt));
         GROW(s->d_out, s->cap_n, nk, sizeof(ShdDeliv));
         GROW(s->d_status, s->cap_n, nk, 1);
@@ -318,8 +365,10 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
         c.row_hi = s->hi;
         c.idx_base = (uint32_t)pbeg[k];
         c.ptab = NULL; /* shards decide from their f64 rows */
+        shd_pcnt_ctx(&s->pcnt, &c); /* path packet counters of the shard's rows */
         rc = shd_dev_packet_round(&c, s->d_recs, nk, t->barrier, t->end_time, t->bootstrap_end, s->d_out, s->d_off,
                                   s->d_status, s->d_cnt, s->stream);
+        shd_pcnt_commit(&s->pcnt, rc);
     }
     for (int k = 0; k < S && !rc; k++) {
         ShdShard* s = &t->shards[k];
@@ -391,17 +440,9 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
     if (min_time) *min_time = mt;
     if (out)
         for (size_t i = 0; i < obase; i++) out[i].pkt_index = perm[out[i].pkt_index];
-    {
-        uint8_t* st = status ? status : (uint8_t*)malloc(nn);
-        if (!st) {
-            rc = -ENOMEM;
-            goto done;
-        }
-        for (size_t q = 0; q < n; q++) st[perm[q]] = pst[q]; /* partition order -> record order */
-        for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0; /* decided (see collect_locked) */
-        rc = count_kept(t, n, st);
-        if (st != status) free(st);
-    }
+    if (status)
+        for (size_t q = 0; q < n; q++) status[perm[q]] = pst[q]; /* partition order -> record order */
+    for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0; /* decided and counted (see collect_locked) */
 done:
     free(perm);
     free(owner);
@@ -436,7 +477,8 @@ int shd_round_process_device(ShdTopology* t, const ShdPkt* d_recs, size_t n, uin
     if (!__atomic_load_n(&t->lookups_started, __ATOMIC_RELAXED)) __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
     if (t->nshards > 1) return shd_fail(-ENOTSUP, "a multi-shard table runs its rounds with shd_round_process_shards");
     pthread_mutex_lock(&t->round_mu);
-    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t)) && !(rc = shd_ensure_ptab(t))) {
+    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t)) &&
+        !(rc = shd_pcnt_ensure(t, &t->pcnt, t->tab_row_lo, t->tab_row_hi, n)) && !(rc = shd_ensure_ptab(t))) {
         ShdPktCtx c;
         shd_pkt_ctx(t, &c);
         rc = shd_dev_packet_round(&c, d_recs, n, barrier, end_time, bootstrap_end, d_out, d_dst_offsets, d_status,
@@ -446,6 +488,7 @@ int shd_round_process_device(ShdTopology* t, const ShdPkt* d_recs, size_t n, uin
             rc = shd_dev_packet_round(&c, d_recs, n, barrier, end_time, bootstrap_end, d_out, d_dst_offsets,
                                       d_status, d_counters, stream);
         }
+        shd_pcnt_commit(&t->pcnt, rc);
     }
     pthread_mutex_unlock(&t->round_mu);
     return rc;
@@ -555,12 +598,14 @@ int shd_round_process_exchange(ShdTopology* t, const ShdTransport* x, const ShdP
     if (t->nshards > 1) return shd_fail(-ENOTSUP, "a multi-shard table runs its rounds with shd_round_collect");
     if (!__atomic_load_n(&t->lookups_started, __ATOMIC_RELAXED)) __atomic_store_n(&t->lookups_started, 1, __ATOMIC_RELEASE);
     pthread_mutex_lock(&t->round_mu);
-    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t)) && !(rc = shd_ensure_ptab(t))) {
+    if (!(rc = shd_dev_init(t->device)) && !(rc = shd_sync_touch(t)) &&
+        !(rc = shd_pcnt_ensure(t, &t->pcnt, t->tab_row_lo, t->tab_row_hi, n)) && !(rc = shd_ensure_ptab(t))) {
         ShdPktCtx c;
         shd_pkt_ctx(t, &c);
         rc = c.ws ? shd_dev_round_exchange(&c, x, d_recs, n, barrier, end_time, bootstrap_end, host_bounds, d_send,
                                            d_status, d_counters, d_recv, recv_cap, d_out, d_out_offsets, n_out, stream)
                   : -ENOMEM;
+        shd_pcnt_commit(&t->pcnt, rc);
     }
     pthread_mutex_unlock(&t->round_mu);
     return rc;

@@ -226,6 +226,7 @@ static int adopt(ShdTopology* t, ShdEntry* d_tab, int owned) {
     if (rc) return rc;
     if (t->d_tab && t->d_tab_owned && t->d_tab != d_tab) shd_dev_free(t->d_tab);
     shd_ptab_drop(t);
+    if ((rc = shd_pcnt_drop(t, &t->pcnt))) return rc; /* (the counts so far stay, in the host map) */
     t->d_tab = d_tab;
     t->d_tab_owned = owned;
     t->tab_row_lo = 0;
@@ -491,6 +492,254 @@ int shd_ptab_release_for_retry(ShdTopology* t, int rc) {
     return 1;
 }
 
+/* ---- device path packet counters (topology_incrementPathPacketCounter of
+ * every kept packet, worker.c:551 / topology.c:1983-1993, counted by the
+ * round kernels) ----
+ * Dense u32 counters per resident table entry.  The round kernels log each
+ * record's answering-pair key (one coalesced store per record, inside the
+ * round) and the log is added into the counters in bulk -- when it is full,
+ * before anything reads the counters (shd_pcnt_sync), or when the caller
+ * asks (shd_topology_path_counts_sync) -- by shd_dev_pcnt_fold.  The
+ * per-packet device atomic (SHD_PCNT=atomic) costs the round +0.365 ms at
+ * C3. */
+
+/* SHD_PCNT: "log" (default), "atomic" (one device atomic per kept packet,
+ * the A/B form), "0" (measurement only: counts are not kept). */
+static int pcnt_mode(void) {
+    const char* v = getenv("SHD_PCNT");
+    if (v && strcmp(v, "0") == 0) return 0;
+    if (v && strcmp(v, "atomic") == 0) return 2;
+    return 1;
+}
+
+/* Spill threshold: counters >= T move to the host map once the packets
+ * counted since the last spill could reach T (T + T < 2^32: no counter
+ * wraps).  SHD_PCNT_SPILL_AT (tests) lowers T. */
+static uint64_t pcnt_spill_at(void) {
+    const char* v = getenv("SHD_PCNT_SPILL_AT");
+    const uint64_t x = v ? strtoull(v, NULL, 10) : 0;
+    return x >= 1 && x <= (1ull << 31) ? x : (1ull << 31);
+}
+
+/* Log capacity in records: SHD_PCNT_LOG (tests), else 2^28 (1 GB of u32
+ * keys, ~27 rounds of 10M packets), at least one round. */
+static size_t pcnt_log_cap(size_t n) {
+    const char* v = getenv("SHD_PCNT_LOG");
+    size_t c = v ? (size_t)strtoull(v, NULL, 10) : ((size_t)1 << 28);
+    if (c < 1) c = 1;
+    return c > n ? c : n;
+}
+
+static int pcnt_dev(ShdTopology* t, const ShdPcnt* p) {
+    for (const ShdShard* s = t->shards; s < t->shards + t->nshards; s++)
+        if (p == &s->pcnt) return s->device;
+    return t->device;
+}
+
+/* Adds the log into the counters (synchronous: every round that wrote it
+ * has finished -- they may have run on any stream). */
+static int pcnt_fold(ShdTopology* t, ShdPcnt* p) {
+    if (!p->alloc || !p->log_fill) return 0;
+    int rc = shd_dev_init(p->device);
+    if (!rc) rc = shd_dev_sync();
+    if (!rc)
+        rc = shd_dev_pcnt_fold(p->log, p->log64, p->log_fill, p->base, (uint64_t)(p->hi) * (uint64_t)t->A, &p->fold,
+                               NULL);
+    if (!rc) rc = shd_dev_sync();
+    if (!rc) p->log_fill = 0;
+    shd_dev_init(t->device);
+    return rc;
+}
+
+/* Moves every counter >= thr of p into the host map (pkt_mu taken here). */
+static int pcnt_spill(ShdTopology* t, ShdPcnt* p, uint32_t thr) {
+    if (!p->alloc || p->hi <= p->lo) return 0;
+    int rc = pcnt_fold(t, p);
+    if (rc) return rc;
+    const size_t A = (size_t)t->A, n = (size_t)(p->hi - p->lo) * A;
+    const size_t cap = n < (1u << 22) ? n : (1u << 22);
+    rc = shd_dev_init(p->device);
+    if (!rc) rc = shd_dev_sync(); /* rounds on any stream have counted */
+    uint64_t* d_list = NULL;
+    uint32_t* d_n = NULL;
+    uint64_t* h = (uint64_t*)malloc(16 * cap);
+    if (!h) rc = -ENOMEM;
+    if (!rc && !(rc = shd_dev_malloc((void**)&d_list, 16 * cap))) rc = shd_dev_malloc((void**)&d_n, 4);
+    for (size_t got = cap; !rc && got == cap;) {
+        if ((rc = shd_dev_pcnt_spill(p->alloc, n, thr, d_list, cap, d_n, &got)) || !got) break;
+        if ((rc = shd_dev_d2h(h, d_list, 16 * got))) break;
+        pthread_mutex_lock(&t->pkt_mu);
+        if (!(rc = shd_count_reserve_locked(t, got)))
+            for (size_t k = 0; k < got && !rc; k++)
+                rc = shd_count_packet_locked(t, p->lo + (int)(h[2 * k] / A), (int)(h[2 * k] % A), h[2 * k + 1]);
+        pthread_mutex_unlock(&t->pkt_mu);
+    }
+    shd_dev_free(d_list);
+    shd_dev_free(d_n);
+    free(h);
+    shd_dev_init(t->device);
+    return rc;
+}
+
+int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
+    p->cur = NULL;
+    const int mode = pcnt_mode();
+    if (!mode || hi <= lo) return 0;
+    int rc = 0;
+    if (p->alloc && (p->lo != lo || p->hi != hi) && (rc = shd_pcnt_drop(t, p))) return rc;
+    const int dev = pcnt_dev(t, p);
+    if (!p->alloc) {
+        const size_t bytes = (size_t)(hi - lo) * (size_t)t->A * 4;
+        void* d = NULL;
+        rc = shd_dev_malloc(&d, bytes);
+        if (rc == -ENOMEM && t->d_ptab_alloc) { /* the counters are not optional, the 8-B table is */
+            shd_ptab_drop(t);
+            t->ptab_unavailable = 1;
+            rc = shd_dev_malloc(&d, bytes);
+        }
+        if (!rc && ((rc = shd_dev_memset(d, 0, bytes)) || (rc = shd_dev_sync()))) shd_dev_free(d);
+        if (rc) return rc;
+        p->alloc = (uint32_t*)d;
+        p->base = p->alloc - (ptrdiff_t)lo * (ptrdiff_t)t->A;
+        p->lo = lo;
+        p->hi = hi;
+        p->device = dev;
+        p->budget = 0;
+        p->log64 = (uint64_t)hi * (uint64_t)t->A >= 0xFFFFFFFFull; /* keys are flat entry indices */
+    }
+    const uint64_t T = pcnt_spill_at();
+    if (p->budget + n >= T) { /* a counter below T could otherwise pass 2^32 - 1 */
+        if ((rc = pcnt_spill(t, p, (uint32_t)T))) return rc;
+        p->budget = 0;
+    }
+    p->budget += n;
+    if (mode == 2) return shd_dev_init(dev);
+    const size_t ksz = p->log64 ? 8 : 4;
+    if (p->log_fill + n > p->log_cap) {
+        if ((rc = pcnt_fold(t, p))) return rc;
+        if (n > p->log_cap || !p->log) {
+            shd_dev_init(dev);
+            shd_dev_free(p->log);
+            p->log = NULL;
+            p->log_cap = 0;
+            const size_t cap = pcnt_log_cap(n);
+            if ((rc = shd_dev_malloc(&p->log, cap * ksz))) return rc;
+            p->log_cap = cap;
+        }
+    }
+    /* this round's slice; shd_pcnt_commit adds it to the log once the round
+     * is launched (a round that fails before leaves it out) */
+    p->cur = (char*)p->log + p->log_fill * ksz;
+    p->cur_n = n;
+    return shd_dev_init(dev);
+}
+
+void shd_pcnt_ctx(const ShdPcnt* p, ShdPktCtx* c) {
+    c->plog = p->cur;
+    c->plog64 = (uint32_t)p->log64;
+    c->pcnt = pcnt_mode() == 2 ? p->base : NULL;
+}
+
+void shd_pcnt_commit(ShdPcnt* p, int rc) {
+    if (!rc && p->cur) p->log_fill += p->cur_n;
+    p->cur = NULL;
+    p->cur_n = 0;
+}
+
+int shd_pcnt_sync(ShdTopology* t) {
+    int rc = 0;
+    pthread_mutex_lock(&t->round_mu);
+    rc = pcnt_fold(t, &t->pcnt);
+    for (int k = 0; k < t->nshards && !rc; k++) rc = pcnt_fold(t, &t->shards[k].pcnt);
+    pthread_mutex_unlock(&t->round_mu);
+    return rc;
+}
+
+int shd_topology_path_counts_sync(ShdTopology* t) {
+    if (!t) return -EINVAL;
+    return shd_pcnt_sync(t);
+}
+
+int shd_pcnt_drop(ShdTopology* t, ShdPcnt* p) {
+    if (!p->alloc) return 0;
+    int rc = pcnt_spill(t, p, 1u); /* (folds the log first) */
+    shd_dev_init(p->device);
+    shd_dev_free(p->alloc);
+    shd_dev_free(p->log);
+    shd_dev_pcnt_scratch_free(p->fold);
+    memset(p, 0, sizeof *p);
+    shd_dev_init(t->device);
+    return rc;
+}
+
+void shd_pcnt_discard(ShdTopology* t) {
+    ShdPcnt* ps[SHD_MAX_SHARDS + 1];
+    int n = 0;
+    ps[n++] = &t->pcnt;
+    for (int k = 0; k < t->nshards; k++) ps[n++] = &t->shards[k].pcnt;
+    for (int k = 0; k < n; k++)
+        if (ps[k]->alloc) {
+            shd_dev_init(ps[k]->device);
+            shd_dev_free(ps[k]->alloc);
+            shd_dev_free(ps[k]->log);
+            shd_dev_pcnt_scratch_free(ps[k]->fold);
+            memset(ps[k], 0, sizeof *ps[k]);
+        }
+    shd_dev_init(t->device);
+}
+
+static ShdPcnt* pcnt_of(ShdTopology* t, int row) {
+    ShdPcnt* p = &t->pcnt;
+    if (t->nshards > 1) {
+        ShdShard* s = shd_shard_of(t, row);
+        p = s ? &s->pcnt : NULL;
+    }
+    return p && p->alloc && row >= p->lo && row < p->hi ? p : NULL;
+}
+
+/* (the readers run shd_pcnt_sync first: the log is folded) */
+int shd_pcnt_read(ShdTopology* t, int row, int col, uint64_t* v) {
+    *v = 0;
+    ShdPcnt* p = pcnt_of(t, row);
+    if (!p) return 0;
+    uint32_t x = 0;
+    int rc = shd_dev_init(p->device);
+    if (!rc) rc = shd_dev_sync();
+    if (!rc) rc = shd_dev_d2h(&x, p->base + (size_t)row * (size_t)t->A + (size_t)col, 4);
+    *v = x;
+    shd_dev_init(t->device);
+    return rc;
+}
+
+int shd_pcnt_read_row(ShdTopology* t, int row, uint64_t* out) { return shd_pcnt_read_rows(t, row, row + 1, out); }
+
+int shd_pcnt_read_rows(ShdTopology* t, int lo, int hi, uint64_t* out) {
+    const size_t A = (size_t)t->A;
+    const size_t chunk_rows = A ? ((size_t)1 << 24) / A + 1 : 1; /* ~64 MB of u32 per copy */
+    uint32_t* x = NULL;
+    int rc = 0;
+    for (int i = lo; i < hi && !rc;) {
+        ShdPcnt* p = pcnt_of(t, i);
+        if (!p) {
+            i++;
+            continue;
+        }
+        int e = hi < p->hi ? hi : p->hi;
+        if ((size_t)(e - i) > chunk_rows) e = i + (int)chunk_rows;
+        const size_t m = (size_t)(e - i) * A;
+        if (!x && !(x = (uint32_t*)malloc(4 * (chunk_rows < (size_t)(hi - lo) ? chunk_rows : (size_t)(hi - lo)) * A)))
+            return -ENOMEM;
+        if (!(rc = shd_dev_init(p->device)) && !(rc = shd_dev_sync()))
+            rc = shd_dev_d2h(x, p->base + (size_t)i * A, 4 * m);
+        uint64_t* o = out + (size_t)(i - lo) * A;
+        for (size_t k = 0; !rc && k < m; k++) o[k] += x[k];
+        i = e;
+    }
+    free(x);
+    shd_dev_init(t->device);
+    return rc;
+}
+
 void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->tab = t->d_tab;
     c->A = t->A;
@@ -503,6 +752,7 @@ void shd_pkt_ctx(ShdTopology* t, ShdPktCtx* c) {
     c->row_hi = t->tab_row_hi;
     c->idx_base = 0;
     c->ptab = ptab_enabled() ? t->d_ptab : NULL;
+    shd_pcnt_ctx(&t->pcnt, c); /* (shd_pcnt_ensure ran first) */
     if (!t->ws) shd_dev_ws_new(&t->ws); /* (a failure leaves ws NULL: the launch reports -ENOMEM) */
     c->ws = t->ws;
 }

@@ -94,6 +94,13 @@ int shd_dev_d2d(void* d, const void* s, size_t bytes);
 int shd_dev_h2d(void* d, const void* h, size_t bytes);
 int shd_dev_d2h(void* h, const void* d, size_t bytes);
 int shd_dev_memset(void* d, int v, size_t bytes);
+/* copies enqueued on a stream (hipStream_t behind void*); the host side
+ * should be pinned (shd_host_alloc) for them to be asynchronous */
+int shd_dev_h2d_async(void* d, const void* h, size_t bytes, void* stream);
+int shd_dev_d2h_async(void* h, const void* d, size_t bytes, void* stream);
+/* pinned host memory */
+int shd_host_alloc(void** p, size_t bytes);
+void shd_host_free(void* p);
 int shd_dev_sync(void);
 /* a stream on the calling thread's device (hipStream_t behind void*) */
 int shd_dev_stream_new(void** s);
@@ -148,7 +155,37 @@ typedef struct {
     int row_lo, row_hi;        /* rows of tab present (a shard: others are never read) */
     uint32_t idx_base;         /* added to the record index an event carries (pkt_index) */
     const void* ptab;          /* NULL or the 8-B packet-path table {delay_ns, keep threshold} indexed as tab */
+    /* path packet counters (topology_incrementPathPacketCounter, worker.c:551)
+     * of every kept packet (delivered or dropped at the end time), at its
+     * answering pair's flat entry index (oi * A + oj):
+     *   plog: this round's slice of the counter log -- record i writes its
+     *         key (u32, or u64 when plog64) or all-ones (not kept) at
+     *         plog[i]; shd_dev_pcnt_fold adds logged keys into the dense
+     *         counters (default, SHD_PCNT=log);
+     *   pcnt: the dense u32 counters themselves, one device atomic per kept
+     *         packet (SHD_PCNT=atomic, the A/B form);
+     * both NULL: SHD_PCNT=0 (measurement only: counts are not kept). */
+    void* plog;
+    uint32_t plog64;
+    uint32_t* pcnt;
 } ShdPktCtx;
+
+/* Path packet counter spill (packet.hip): every entry of cnt[0, n) that is
+ * >= thr is appended to list as {index (u64), value (u64)} (at most cap
+ * entries; *d_nlist, device, counts all that qualified) and zeroed -- only
+ * the appended ones.  Synchronous on the calling thread's device.  Returns
+ * the number of entries appended in *appended (host). */
+int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, size_t cap, uint32_t* d_nlist,
+                       size_t* appended);
+/* Adds the L logged keys of `log` (u32 or u64 flat entry indices below N,
+ * all-ones = nothing) into the dense counters (N u32): a bucket partition
+ * of the keys (histogram, scan, scatter) and one workgroup per bucket that
+ * accumulates its keys in LDS and adds its counters to the dense table
+ * (exclusive owner: plain read-modify-write of the touched lines).  Enqueued
+ * on stream; *scratch: grow-only buffers (NULL the first time), freed with
+ * shd_dev_pcnt_scratch_free. */
+int shd_dev_pcnt_fold(const void* log, int log64, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream);
+void shd_dev_pcnt_scratch_free(void* scratch);
 
 /* The 8-B packet-path table of nent entries of tab ({u32 delay_ns =
  * ceil(lat * 1e6), u32 keep threshold over the 31-bit rand_r output}, or a

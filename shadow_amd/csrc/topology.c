@@ -489,10 +489,19 @@ out:
 
 void shd_topology_free(ShdTopology* t) {
     if (!t) return;
+    shd_pcnt_discard(t);
     shd_topology_release_device(t);
     shd_dev_ws_free(t->ws);
     shd_dev_fw_scratch_free(t->fw_scratch);
-    for (int w = 0; w < t->nworkers; w++) free(t->wbuf[w].recs);
+    if (t->cstream) shd_dev_stream_sync(t->cstream);
+    shd_dev_free(t->d_crecs);
+    shd_dev_free(t->d_cout);
+    shd_dev_free(t->d_cstat);
+    shd_dev_free(t->d_coff);
+    shd_dev_free(t->d_ccnt);
+    shd_host_free(t->h_ccnt);
+    shd_dev_stream_free(t->cstream);
+    for (int w = 0; w < t->nworkers; w++) shd_host_free(t->wbuf[w].recs);
     free(t->wbuf);
     pthread_mutex_destroy(&t->setup_mu);
     pthread_mutex_destroy(&t->touch_mu);
@@ -1084,6 +1093,20 @@ static void set_pair_bit(ShdTopology* t, int i, int j) {
 /* _topology_getPathEntry (topology.c:1900-1981) for slots (si, di): applies
  * the side effects and returns the slot pair whose entry answers.  Lock-free
  * on a hit; safe to call from any number of threads. */
+/* Whether shd_resolve(si, di) could have a side effect (a row touch, a self
+ * or direct-pair release) -- false once the pair's entry is cached, the
+ * steady state of a long simulation.  Read-only and lock-free; a concurrent
+ * release can only turn a true into a false, never the reverse. */
+int shd_resolve_pending(ShdTopology* t, int si, int di) {
+    if (t->use_sp) {
+        if (si == di) return !__atomic_load_n(&t->self_released[si], __ATOMIC_ACQUIRE);
+        const uint32_t ts = touch_of(t, si);
+        if (ts != SHD_UNTOUCHED) return 0;
+        return t->directed ? 1 : touch_of(t, di) == SHD_UNTOUCHED;
+    }
+    return !pair_bit(t, si, di) && !pair_bit(t, di, si);
+}
+
 int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj) {
     size_t A = (size_t)t->A;
     int rc = 0;
@@ -1278,6 +1301,26 @@ int shd_topology_increment_path_packet_counter(ShdTopology* t, uint32_t s, uint3
     return shd_count_packet(t, oi, oj, 1);
 }
 
+static uint64_t pkt_count_of(ShdTopology* t, int i, int j);
+
+int shd_topology_copy_path_packet_counts(ShdTopology* t, int lo, int hi, uint64_t* out) {
+    if (!t || (!out && hi > lo)) return -EINVAL;
+    if (!__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return shd_fail(-EAGAIN, "no table yet");
+    if (lo < 0 || hi > t->A || lo > hi) return shd_fail(-EINVAL, "row range out of bounds");
+    const size_t A = (size_t)t->A;
+    memset(out, 0, sizeof(uint64_t) * (size_t)(hi - lo) * A);
+    int rc = shd_pcnt_sync(t); /* the rounds' logged counts folded in first */
+    if (!rc) rc = shd_pcnt_read_rows(t, lo, hi, out);
+    pthread_mutex_lock(&t->pkt_mu);
+    for (uint64_t h = 0; !rc && h < t->pkt_cap; h++)
+        if (t->pkt_keys[h] != UINT64_MAX) {
+            const int i = (int)(t->pkt_keys[h] >> 32), j = (int)(uint32_t)t->pkt_keys[h];
+            if (i >= lo && i < hi) out[(size_t)(i - lo) * A + (size_t)j] += t->pkt_vals[h];
+        }
+    pthread_mutex_unlock(&t->pkt_mu);
+    return rc;
+}
+
 int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, uint64_t* out) {
     if (!t || !out) return -EINVAL;
     *out = 0;
@@ -1285,21 +1328,22 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
     IpSlot* b = ipmap_find(&t->ipmap, d);
     if (!a || !b || !__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return 0;
     int si = t->vertex_slot[a->vertex], di = t->vertex_slot[b->vertex];
-    pthread_mutex_lock(&t->pkt_mu);
-    for (int pass = 0; pass < 2 && t->pkt_cap; pass++) {
-        uint64_t key = pass ? (((uint64_t)(uint32_t)di << 32) | (uint32_t)si) : (((uint64_t)(uint32_t)si << 32) | (uint32_t)di);
-        uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> 20 & (t->pkt_cap - 1);
-        while (t->pkt_keys[h] != UINT64_MAX) {
-            if (t->pkt_keys[h] == key) {
-                *out = t->pkt_vals[h];
-                pass = 2;
-                break;
-            }
-            h = (h + 1) & (t->pkt_cap - 1);
-        }
+    /* the cached path of the pair is (si, di) or (di, si), never both
+     * (topology.c:1189-1215), and only it is ever counted: the sum of the two
+     * keys is its count -- host map (explicit increments, spilled counters)
+     * plus the rounds' device counters */
+    uint64_t dv = 0, tot = 0;
+    int rc = shd_pcnt_sync(t); /* the rounds' logged counts folded in first */
+    for (int pass = 0; pass < (si == di ? 1 : 2) && !rc; pass++) {
+        const int i = pass ? di : si, j = pass ? si : di;
+        if (!(rc = shd_pcnt_read(t, i, j, &dv))) tot += dv;
     }
+    pthread_mutex_lock(&t->pkt_mu);
+    tot += pkt_count_of(t, si, di);
+    if (si != di) tot += pkt_count_of(t, di, si);
     pthread_mutex_unlock(&t->pkt_mu);
-    return 0;
+    *out = tot;
+    return rc;
 }
 
 /* ------------------------------------------------------------------ */
@@ -1335,14 +1379,15 @@ static int self_is_direct(const ShdTopology* t, int v) {
     return direct;
 }
 
-static void log_line(ShdTopology* t, ShdPathLogFn fn, void* user, int i, int j, ShdEntry e, int direct) {
+/* dev: the rounds' device count of (i, j), added to the host map's */
+static void log_line(ShdTopology* t, ShdPathLogFn fn, void* user, int i, int j, ShdEntry e, int direct, uint64_t dev) {
     char line[512];
     const int si = t->slot_vertex[i], di = t->slot_vertex[j];
     snprintf(line, sizeof line,
              "Found path %li%s%li in cache: SourceIndex=%ld DestinationIndex=%ld Latency=%f Reliability=%f "
              "PacketCount=%lu isDirect=%s",
              (long)t->v_id[si], t->directed ? "->" : "<->", (long)t->v_id[di], (long)si, (long)di, e.lat, e.rel,
-             (unsigned long)pkt_count_of(t, i, j), direct ? "True" : "False");
+             (unsigned long)(pkt_count_of(t, i, j) + dev), direct ? "True" : "False");
     fn(line, user);
 }
 
@@ -1359,12 +1404,18 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
     if (nlines) *nlines = 0;
     if (!__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return 0;
     int rc = shd_release_sync(t, 1); /* (topology_free's log follows every release) */
+    if (!rc) rc = shd_pcnt_sync(t); /* and every round's path packet counts */
     if (rc) return rc;
     const int A = t->A;
     ShdEntry* row = NULL;
     if (!t->h_tab) {
         row = (ShdEntry*)malloc(sizeof(ShdEntry) * (size_t)A);
         if (!row) return -ENOMEM;
+    }
+    uint64_t* prow = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(A ? A : 1)); /* the row's device counts */
+    if (!prow) {
+        free(row);
+        return -ENOMEM;
     }
     pthread_mutex_lock(&t->pkt_mu);
     for (int i = 0; i < A && !rc; i++) {
@@ -1386,20 +1437,23 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
                 (rc = shd_dev_d2h(row, s->base + (size_t)i * (size_t)A, sizeof(ShdEntry) * (size_t)A)))
                 break;
         }
+        memset(prow, 0, sizeof(uint64_t) * (size_t)A);
+        if ((rc = shd_pcnt_read_row(t, i, prow))) break;
         for (int j = 0; j < A; j++) {
             if (t->use_sp) {
                 if (j == i) {
-                    if (self) log_line(t, fn, user, i, i, r[i], self_is_direct(t, t->slot_vertex[i])), n++;
+                    if (self) log_line(t, fn, user, i, i, r[i], self_is_direct(t, t->slot_vertex[i]), prow[i]), n++;
                 } else if (si != SHD_UNTOUCHED && touch_of(t, j) > si && r[j].lat >= 0) {
-                    log_line(t, fn, user, i, j, r[j], 0), n++;
+                    log_line(t, fn, user, i, j, r[j], 0, prow[j]), n++;
                 }
             } else if (pair_bit(t, i, j)) {
-                log_line(t, fn, user, i, j, r[j], 1), n++;
+                log_line(t, fn, user, i, j, r[j], 1, prow[j]), n++;
             }
         }
     }
     pthread_mutex_unlock(&t->pkt_mu);
     free(row);
+    free(prow);
     if (nlines) *nlines = n;
     return rc;
 }
@@ -1411,6 +1465,10 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
 void shd_shards_clear(ShdTopology* t) {
     shd_ptab_drop(t); /* (every re-adoption and the teardown pass here) */
     (void)shd_release_sync(t, 0); /* nothing of the old table stays queued or in flight */
+    /* the old table's path packet counts stay, in the host map (teardown:
+     * already discarded) */
+    (void)shd_pcnt_drop(t, &t->pcnt);
+    for (int k = 0; k < t->nshards; k++) (void)shd_pcnt_drop(t, &t->shards[k].pcnt);
     shd_rel_list_free(&t->relq);
     shd_rel_list_free(&t->relself);
     for (int k = 0; k < t->nshards; k++) {

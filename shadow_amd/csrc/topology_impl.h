@@ -61,6 +61,28 @@ typedef struct {
 } ShdRelList;
 void shd_rel_list_free(ShdRelList* q);
 
+/* Device path packet counters of resident rows [lo, hi): one u32 per table
+ * entry (row r at base + r * A), the rounds' kernels add 1 per kept packet
+ * at its answering pair (worker.c:551).  A counter never wraps: before a
+ * round could take any counter past 2^32 - 1 (budget: packets counted since
+ * the last spill), the counters >= 2^31 move into the host map (u64). */
+typedef struct {
+    uint32_t* alloc;
+    uint32_t* base;
+    int lo, hi;
+    int device;
+    uint64_t budget;
+    /* the counter log (SHD_PCNT=log): log_fill records logged since the last
+     * fold, keys u32 (u64 when the table has 2^32 entries or more); cur /
+     * cur_n: the slice reserved for the round being launched */
+    void* log;
+    size_t log_cap, log_fill;
+    int log64;
+    void* cur;
+    size_t cur_n;
+    void* fold; /* shd_dev_pcnt_fold scratch */
+} ShdPcnt;
+
 /* A device-resident piece of the routing table (no host mirror): rows [lo,
  * hi) on `device`, row r at base + r * A.  One shard for a single-GPU table,
  * several for a single-process multi-GPU table (shd_topology_adopt_table_shards);
@@ -87,6 +109,7 @@ typedef struct {
     uint32_t* d_rofs; /* regroup: per source shard the rebased destination offsets + block bases */
     size_t cap_n, cap_r, cap_rofs;
     uint32_t cap_h;
+    ShdPcnt pcnt; /* path packet counters of the shard's rows (multi-shard rounds) */
 } ShdShard;
 
 
@@ -156,16 +179,30 @@ struct ShdTopology {
     ShdMinJumpFn cb;
     void* cb_user;
 
-    /* path packet counters keyed by the answering (owner) pair */
+    /* path packet counters keyed by the answering (owner) pair: the host map
+     * (explicit increments, spilled device counters) plus the device
+     * counters of the rounds (pcnt; per shard for multi-shard tables) */
     uint64_t *pkt_keys, *pkt_vals;
     uint64_t pkt_cap, pkt_n;
+    ShdPcnt pcnt;
 
-    /* round staging (host API): one buffer per worker */
+    /* round staging (host API): one pinned buffer per worker */
     uint64_t barrier, end_time, bootstrap_end;
     ShdWorkerBuf* wbuf;
     int nworkers;
-    ShdPkt* staged; /* concatenation at collect (worker order) */
+    ShdPkt* staged; /* concatenation at collect (worker order; multi-shard rounds) */
     size_t capstaged;
+    /* shd_round_collect's device buffers (grow-only), its stream and its
+     * pinned counter read-back */
+    ShdPkt* d_crecs;
+    ShdDeliv* d_cout;
+    uint8_t* d_cstat;
+    uint32_t* d_coff;
+    uint64_t* d_ccnt;
+    uint64_t* h_ccnt;
+    size_t cap_c;
+    uint32_t cap_coff;
+    void* cstream;
 
     /* device workspace of the round pipeline (packet.hip) */
     void* ws;
@@ -179,6 +216,8 @@ struct ShdTopology {
 void shd_topology_release_device(ShdTopology* t);
 void shd_shards_clear(ShdTopology* t);
 int shd_resolve(ShdTopology* t, int si, int di, int* oi, int* oj);
+/* could shd_resolve(si, di) still have a side effect (read-only) */
+int shd_resolve_pending(ShdTopology* t, int si, int di);
 /* device-resident releases (topology.c): launch the queue once it is long
  * enough (never waits); wait for everything and fold it in touch order (fold
  * = 1) or drop it (0) */
@@ -199,5 +238,27 @@ int shd_ensure_ptab(ShdTopology* t);
 void shd_ptab_drop(ShdTopology* t);
 int shd_ptab_release_for_retry(ShdTopology* t, int rc);
 int shd_ensure_routes(ShdTopology* t);
+/* device path packet counters (routes.c): allocated (zeroed) for the rows
+ * [lo, hi) on the calling thread's device at the first round, spilled ahead
+ * of a round of n records when they could wrap (caller holds round_mu);
+ * drop folds every counter into the host map and frees them */
+int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n);
+/* after the round's launch: rc == 0 adds its reserved slice to the log */
+void shd_pcnt_commit(ShdPcnt* p, int rc);
+/* the round context's counter fields for p (its reserved slice / counters) */
+void shd_pcnt_ctx(const ShdPcnt* p, ShdPktCtx* c);
+/* folds every log of the topology into its counters (takes round_mu; the
+ * readers call it before reading) */
+int shd_pcnt_sync(ShdTopology* t);
+int shd_pcnt_drop(ShdTopology* t, ShdPcnt* p);
+/* frees every device counter without folding (topology teardown) */
+void shd_pcnt_discard(ShdTopology* t);
+/* device count of the flat table entry idx (0 if the rows are not resident
+ * here or no round counted yet); waits for the device */
+int shd_pcnt_read(ShdTopology* t, int row, int col, uint64_t* v);
+/* counts of row `row`, columns [0, A), added into out (A values) */
+int shd_pcnt_read_row(ShdTopology* t, int row, uint64_t* out);
+/* rows [lo, hi), row-major, added into out ((hi - lo) * A values) */
+int shd_pcnt_read_rows(ShdTopology* t, int lo, int hi, uint64_t* out);
 
 #endif

@@ -197,6 +197,19 @@ class Topology:
         check(lib().shd_topology_get_path_packet_count(self._h, src_ip, dst_ip, C.byref(out)))
         return out.value
 
+    def path_packet_counts(self, row_lo: int = 0, row_hi: int | None = None) -> np.ndarray:
+        """Every path packet counter of table rows [row_lo, row_hi): a
+        (rows, A) u64 array, entry (i, j) = packets counted at pair (i, j)."""
+        A = self.slot_count()
+        row_hi = A if row_hi is None else row_hi
+        out = np.empty((row_hi - row_lo, A), dtype=np.uint64)
+        check(lib().shd_topology_copy_path_packet_counts(self._h, row_lo, row_hi, out.ctypes.data))
+        return out
+
+    def path_counts_sync(self):
+        """Adds the rounds' logged path packet counts into the device counters."""
+        check(lib().shd_topology_path_counts_sync(self._h))
+
     def cached_paths_log(self) -> list[str]:
         """topology_free's teardown log (shd_topology_log_cached_paths)."""
         from ._lib import PATH_LOG_FN

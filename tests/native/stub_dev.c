@@ -205,3 +205,33 @@ int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n,
     for (size_t i = 0; i < n; i++) d_out[i] = tab[d_idx[i]];
     return 0;
 }
+
+int shd_dev_h2d_async(void* d, const void* h, size_t bytes, void* stream) { return shd_dev_h2d(d, h, bytes); }
+int shd_dev_d2h_async(void* h, const void* d, size_t bytes, void* stream) { return shd_dev_d2h(h, d, bytes); }
+int shd_host_alloc(void** p, size_t bytes) {
+    *p = malloc(bytes ? bytes : 4);
+    return *p ? 0 : -ENOMEM;
+}
+void shd_host_free(void* p) { free(p); }
+int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, size_t cap, uint32_t* d_nlist,
+                       size_t* appended) {
+    size_t k = 0;
+    for (size_t i = 0; i < n && k < cap; i++)
+        if (cnt[i] && cnt[i] >= thr) {
+            d_list[2 * k] = i;
+            d_list[2 * k + 1] = cnt[i];
+            cnt[i] = 0;
+            k++;
+        }
+    *d_nlist = (uint32_t)k;
+    *appended = k;
+    return 0;
+}
+int shd_dev_pcnt_fold(const void* log, int log64, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream) {
+    for (size_t i = 0; i < L; i++) {
+        const uint64_t k = log64 ? ((const uint64_t*)log)[i] : ((const uint32_t*)log)[i];
+        if (log64 ? k != UINT64_MAX : k != UINT32_MAX) dense[k]++;
+    }
+    return 0;
+}
+void shd_dev_pcnt_scratch_free(void* scratch) { (void)scratch; }

@@ -19,6 +19,7 @@ import time
 import numpy as np
 import pytest
 
+import count_check
 import oracle_ctypes as O
 from shadow_amd import Topology, _lib, scenario, synth
 
@@ -68,6 +69,7 @@ def test_c4_three_simulated_rounds():
     d_status = torch.empty(n, dtype=torch.uint8, device=dev)
     d_cnt = torch.empty(2, dtype=torch.int64, device=dev)
     h_states, h_seqs = st[pool].astype(np.uint32), np.zeros(npool, dtype=np.uint64)
+    all_recs, all_status = [], []
     for r in range(3):
         t0, barrier = T0 + r * W, T0 + (r + 1) * W
         a, b = r % 2, (r + 1) % 2
@@ -88,7 +90,19 @@ def test_c4_three_simulated_rounds():
         assert int(cnt[1]) == omt, f"round {r}: min time"
         assert np.array_equal(out, oout), f"round {r}: events"
         assert out["time"].min() >= barrier  # (inter-host deliveries clamp to the advancing barrier)
+        all_recs.append(recs.copy())
+        all_status.append(ostatus)
         progress(t_start, f"round {r}: {len(out)} of {n} delivered, equal to the oracle")
+    # path packet counters accumulated over the three device rounds
+    # (worker.c:551): every counter of the owner rows against the
+    # restatement, every pool pair against the oracle's counters
+    hslot = count_check.slot_map(verts)
+    keys, counts = count_check.expected_keys(hslot, np.concatenate(all_recs), np.concatenate(all_status), A)
+    count_check.check_rows(top, keys, counts, A, np.unique(keys // A))
+    for x in pool:
+        for y in pool[::7]:
+            assert top.path_packet_count(int(ips[x]), int(ips[y])) == orc.packet_count(int(ips[x]), int(ips[y]))
+    progress(t_start, f"path packet counters of {len(np.unique(keys // A))} rows equal")
     assert np.array_equal(d_st[1].cpu().numpy().view(np.uint32), h_states)  # (3 rounds: the carry ends in [1])
     assert np.array_equal(d_sq[1].cpu().numpy().view(np.uint64), h_seqs)
     top.close()

@@ -15,6 +15,7 @@ span all 200k hosts, decided against rows the oracle holds
 import numpy as np
 import pytest
 
+import count_check
 import oracle_ctypes as O
 from shadow_amd import Topology, scenario, synth
 
@@ -136,11 +137,24 @@ def test_c3_uniform_unrestricted_round_bit_exact(monkeypatch):
     ips_o, _, verts_o = scenario.register_hosts(orc, H, seed=1)
     assert (verts == verts_o).all()
     tab = full.view(A, A, 2).cpu().numpy()
+    # this H = 100k table itself, every one of its 19,870 rows, against the
+    # oracle's Dijkstra (topology.c:1578-1814) before it is preloaded
+    import time
+    t0 = time.perf_counter()
+    bad = []
+    for b in range(0, A, 2048):
+        rows = np.arange(b, min(A, b + 2048))
+        olat, orel = orc.rows_parallel(sv[rows], sv, 16)
+        diff = (bits(tab[rows, :, 0]) != bits(olat)).any(1) | (bits(tab[rows, :, 1]) != bits(orel)).any(1)
+        bad += [int(x) for x in rows[diff]]
+        print(f"[c3] table rows {b}..{b + len(rows)} of {A} compared ({time.perf_counter() - t0:.1f}s)", flush=True)
+    assert not bad, f"{len(bad)} rows differ, first {bad[:8]}"
     orc.preload(sv, tab[:, :, 0], tab[:, :, 1])
     del tab
     pk = synth.packet_batch(10_000_000, H, 0x5EED0003, 100_000_000, 10_000_000, st)  # the bench's batch
     oout, ostatus, omt = orc.round(ips_o, pk, BARRIER, END)
-    for pipe in ("slab", "part"):
+    pipes = ("slab", "part")
+    for pipe in pipes:
         monkeypatch.setenv("SHD_PACKET_PIPELINE", pipe)
         out, offs, status, mt = device_round(top, pk, H)
         assert np.array_equal(status, ostatus), pipe
@@ -150,6 +164,18 @@ def test_c3_uniform_unrestricted_round_bit_exact(monkeypatch):
         assert np.array_equal(out, oout), pipe
         assert np.diff(offs).max() < 256  # uniform: every segment on the register-sort path
         del out
+    # path packet counters, counted by the device rounds (worker.c:551): all
+    # 19,870^2 counters against the numpy restatement (both rounds counted),
+    # and 20k host pairs against the oracle's own counters
+    hslot = count_check.slot_map(verts)
+    C = top.path_packet_counts()
+    want = count_check.expected_counts(hslot, pk, ostatus, A)
+    assert int(want.sum()) == int(np.isin(ostatus, count_check.KEPT).sum())
+    assert np.array_equal(C, want * len(pipes))
+    del want
+    rng = np.random.default_rng(5)
+    k = rng.integers(0, len(pk), 20_000)
+    count_check.check_against_oracle(C // len(pipes), hslot, orc, ips_o, pk["src_host"][k], pk["dst_host"][k])
 
 
 @pytest.fixture(scope="module")
@@ -248,3 +274,13 @@ def test_c4_round_all_hosts_bit_exact(c4):
     assert mt == omt
     assert offs[-1] == len(out) and np.array_equal(np.diff(offs), np.bincount(oout["dst_host"], minlength=H))
     assert np.array_equal(out, oout)
+    # path packet counters of the round (worker.c:551): every counter of the
+    # 1,027 owner rows against the restatement, 20k pairs against the oracle
+    A = c4["A"]
+    keys, counts = count_check.expected_keys(hslot, pk, ostatus, A)
+    assert (keys // A >= 0).all() and np.isin(keys // A, rows).all()
+    count_check.check_rows(top, keys, counts, A, rows)
+    k = rng.integers(0, len(pk), 20_000)
+    for x, y in zip(pk["src_host"][k], pk["dst_host"][k]):
+        assert top.path_packet_count(int(c4["ips"][x]), int(c4["ips"][y])) == orc.packet_count(int(c4["ips"][x]),
+                                                                                                  int(c4["ips"][y]))

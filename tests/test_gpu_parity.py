@@ -10,6 +10,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
+import count_check
 import oracle_ctypes as O
 from shadow_amd import Topology, scenario, synth
 
@@ -28,6 +29,7 @@ def make_pair(gml, H, use_sp=True, seed=1):
     orc = O.OracleTopology(gml, use_sp)
     ips2, st2, verts2 = scenario.register_hosts(orc, H, seed)
     assert (verts == verts2).all() and (st == st2).all()
+    top.verts = verts
     return top, orc, ips, st
 
 
@@ -234,10 +236,13 @@ def test_packet_round_host_api_bit_exact(case, pipeline):
     for h in range(H):
         assert (out["dst_host"][offs[h]:offs[h + 1]] == h).all()
     assert offs[-1] == len(out)
-    # path packet counters (topology_incrementPathPacketCounter per kept packet)
+    # path packet counters (topology_incrementPathPacketCounter per kept packet,
+    # counted on the device inside the round): single pairs, and every cached
+    # path's count in the teardown log
     for a in range(0, H, max(1, H // 7)):
         for b in range(0, H, max(1, H // 5)):
             assert top.path_packet_count(int(ips[a]), int(ips[b])) == orc.packet_count(int(ips[a]), int(ips[b]))
+    assert top.cached_paths_log() == orc.cached_paths_log()
 
 
 def test_multi_round_state_carries():
@@ -310,6 +315,56 @@ def test_device_api_matches_oracle_after_touch_all(pipeline):
     assert np.array_equal(d_status.cpu().numpy(), ostatus)
     assert cnt[1] == omt
     assert np.array_equal(out, oout)
+    # the device round counted every kept packet at its answering pair
+    # (worker.c:551): every host pair's path count against the oracle's (the
+    # device API applies no lookup side effect, so the oracle's round has
+    # released self paths the product's has not: no log compare here)
+    a, b = np.meshgrid(np.arange(H), np.arange(H), indexing="ij")
+    count_check.check_against_oracle(top.path_packet_counts(), count_check.slot_map(top.verts), orc, ips,
+                                     a.ravel(), b.ravel())
+
+
+@pytest.mark.parametrize("mode", ["log", "log_small", "atomic"])
+@pytest.mark.parametrize("api", ["host", "device"])
+def test_path_counters_spill_to_host(api, mode, monkeypatch):
+    """The device counters move to the host map before any could wrap
+    (SHD_PCNT_SPILL_AT lowers the 2^31 threshold to 3): five rounds, every
+    cached path's count equal to the oracle's after each.  Modes: the log
+    (folded at each read), a log of 4,000 records (each round but the first
+    folds the previous one first: SHD_PCNT_LOG) and the per-packet atomic."""
+    import torch
+    monkeypatch.setenv("SHD_PCNT_SPILL_AT", "3")
+    monkeypatch.setenv("SHD_PCNT", "atomic" if mode == "atomic" else "log")
+    if mode == "log_small":
+        monkeypatch.setenv("SHD_PCNT_LOG", "4000")
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    if api == "device":
+        top.touch_all()
+        lat, rel, sv = top.table()
+        orc.preload(sv, lat, rel)
+    for r in range(5):
+        pk = synth.packet_batch(3000, H, 0x5EED0310 + r, 100_000_000, 10_000_000, st)
+        if api == "host":
+            top.round(pk, 110_000_000, 10**15)
+        else:
+            n = len(pk)
+            d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+            d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+            d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+            d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+            d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                               d_status.data_ptr(), d_cnt.data_ptr(), 0)
+        orc.round(ips, pk, 110_000_000, 10**15)
+        if api == "host":
+            assert top.cached_paths_log() == orc.cached_paths_log(), f"round {r}"
+        else:
+            a, b = np.meshgrid(np.arange(H), np.arange(H), indexing="ij")
+            count_check.check_against_oracle(top.path_packet_counts(), count_check.slot_map(top.verts), orc, ips,
+                                             a.ravel(), b.ravel())
+    assert max(int(x.split("PacketCount=")[1].split()[0]) for x in orc.cached_paths_log()) > 3  # spilled
 
 
 def test_deliv_sort_device_against_lexsort(pipeline):

@@ -144,7 +144,19 @@ def _oracle_round(gml, world, hot=0):
     orc.preload(sv, lat, rel)
     allpk = np.concatenate([_packets(r, world, st, hot) for r in range(world)])
     ref, status, mt = orc.round(ips, allpk, BARRIER, END)
+    _oracle_round.last = (orc, ips, verts)
     return want_tab, ref, mt
+
+
+def _check_counts(tops):
+    """The path packet counters summed over the ranks (each counts the
+    packets it decided, worker.c:551) against the oracle's single round, for
+    every host pair."""
+    from count_check import check_against_oracle, slot_map
+    orc, ips, verts = _oracle_round.last
+    C = sum(top.path_packet_counts() for top, _ in tops)
+    a, b = np.meshgrid(np.arange(H), np.arange(H), indexing="ij")
+    check_against_oracle(C, slot_map(verts), orc, ips, a.ravel(), b.ravel())
 
 
 def _check_union(bufs, res, world, host_bounds, ref, mt, nrec=None):
@@ -197,6 +209,7 @@ def test_threads_as_ranks(kind, world, fused):
     for b in bufs:  # every rank's all-gathered table
         assert b["tab"].cpu().numpy().tobytes() == want_tab
     _check_union(bufs, res, world, host_bounds, ref, mt)
+    _check_counts(tops)
 
 
 @pytest.mark.timeout(300)
@@ -230,6 +243,7 @@ def test_exchange_long_segments(world, hot, wire_sorted, monkeypatch):
         xps.close()
     _, ref, mt = _oracle_round(gml, world, hot)
     _check_union(bufs, res, world, host_bounds, ref, mt)
+    _check_counts(tops)
 
 
 @pytest.mark.timeout(300)
@@ -266,6 +280,7 @@ def test_row_sharded_route_decide_exchange(kind, world):
         xps.close()
     _, ref, mt = _oracle_round(gml, world)
     _check_union(bufs, res, world, host_bounds, ref, mt)
+    _check_counts(tops)  # (each record counted on the rank holding its answering row)
 
 
 @pytest.mark.timeout(300)
