@@ -34,6 +34,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec (6.29 mea
 # writes the 32 B event; place/segsort move the 32 B event in and out.
 BYTES_SCATTER_PER_PKT = 32 + 2 * 4 + 16 + 32
 BYTES_MOVE_PER_EVENT = 32 + 32
+# path packet counters (worker.c:551): the scatter logs one u32 pair key per
+# record (tables below 2^32 entries); the fold reads it back, partitions it
+# and adds it into the u32 counters (PCNT_FOLD_BYTES per kept packet + the
+# counter lines it touches)
+PCNT_LOG_BYTES = 4
 STAGES = ["packet_scatter", "scan", "place", "segment_sort"]
 
 
@@ -295,6 +300,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    top.path_counts_sync()  # (the warm-up rounds' path packet counts: outside the timed region)
     state_before = gpu_state(local) if rank == 0 else None
     lib = _lib.lib()
     _lib.check(lib.shd_round_timing_enable(1))
@@ -304,8 +310,15 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
+    # topology_incrementPathPacketCounter of every kept packet (worker.c:551):
+    # the rounds logged their packets' pairs; the fold that adds the K
+    # rounds' logs into the counters is part of the timed work
+    t_rounds = time.perf_counter()
+    top.path_counts_sync()
+    t_fold = time.perf_counter() - t_rounds
     barrier()
     dt = max_over_ranks(time.perf_counter() - t0)
+    kept = int((d_status != 0).sum().item())  # delivered + dropped at the end time: the counted packets
     stage_ms = (C.c_double * 4)()
     nl = C.c_int()
     _lib.check(lib.shd_round_timing_read(stage_ms, 4, C.byref(nl)))
@@ -329,13 +342,14 @@ def main():
         # k_part_sort (+ listed segments): the staged event in, the 32-B event
         # and the offsets out
         kernels = ["k_part_scatter", "-", "-", "k_part_sort (+ k_segsort_mid/merge for listed segments)"]
-        alg_bytes = [(32 + 2 * 4 + 16 + 1) * P + 16.0 * delivered, 0.0, 0.0, (16 + 32) * delivered + 4.0 * (H + 1)]
+        alg_bytes = [(32 + 2 * 4 + 16 + 1 + PCNT_LOG_BYTES) * P + 16.0 * delivered, 0.0, 0.0,
+                     (16 + 32) * delivered + 4.0 * (H + 1)]
     else:
         # scan: counts in, offsets out; place: only the overflow events move
         # (k_place_ovf; 0 B when no segment outgrew its slab); sort: every
         # delivered event in and out
         kernels = ["k_pkt_scatter", "k_scan_*", "k_place_ovf", "k_segsort_dst (+ mid/merge)"]
-        alg_bytes = [BYTES_SCATTER_PER_PKT * P, 4.0 * 2 * H, BYTES_MOVE_PER_EVENT * overflow,
+        alg_bytes = [(BYTES_SCATTER_PER_PKT + PCNT_LOG_BYTES) * P, 4.0 * 2 * H, BYTES_MOVE_PER_EVENT * overflow,
                      BYTES_MOVE_PER_EVENT * delivered]
     achieved = [alg_bytes[k] / (per_launch_ms[k] * 1e-3) / 1e9 if per_launch_ms[k] > 0 else 0.0 for k in range(4)]
     total_pkts = P * world * args.steps
@@ -404,6 +418,15 @@ def main():
             "pipeline": pipe_name,
         },
         "gpu_state": {"before_timed": state_before, "after_timed": gpu_state(local) if rank == 0 else None},
+        "path_counts": {
+            "what": "topology_incrementPathPacketCounter of every kept packet (worker.c:551) inside the timed "
+                    "region: k_part_scatter logs each record's answering pair (4 B, coalesced); at the end of "
+                    "the K timed rounds shd_topology_path_counts_sync adds the K logs into the u32 counters "
+                    "(bucket partition + LDS accumulation, shd_dev_pcnt_fold)",
+            "mode": os.environ.get("SHD_PCNT", "log"), "counted_per_round_rank0": kept,
+            "fold_ms_total": t_fold * 1e3, "fold_ms_per_round": t_fold * 1e3 / args.steps,
+            "rounds_per_fold": args.steps,
+        },
     }
 
     # ------------------------------------------- receive side (§8f-2 / -4)
@@ -674,12 +697,16 @@ def main():
             for _ in range(3):
                 round4()
             torch.cuda.synchronize(dev)
+            t4.path_counts_sync()
             barrier()
             _lib.check(lib4.shd_round_timing_enable(1))
             s0 = time.perf_counter()
             for _ in range(args.c4_rounds):
                 round4()
             torch.cuda.synchronize(dev)
+            s1 = time.perf_counter()
+            t4.path_counts_sync()  # the rounds' path packet counts (worker.c:551), in the timed region
+            fold4 = time.perf_counter() - s1
             barrier()
             tp4 = max_over_ranks(time.perf_counter() - s0)
             # the carry reached every round: each sender's event counter advanced
@@ -700,7 +727,7 @@ def main():
                 "packets_per_s": n4 * world * args.c4_rounds / tp4, "ms_per_round": tp4 / args.c4_rounds * 1e3,
                 "handoff_ms_per_round_rank0": sum(st4ms[k] for k in range(4)) / max(nl4.value, 1),
                 "delivered_last_round_rank0": int(r_cnt.cpu().numpy().view(np.uint64)[0]),
-                "carry_checked": carry_ok,
+                "carry_checked": carry_ok, "path_counts_fold_s": fold4,
                 "per_round_advance": "barrier += 10 ms; every sender's rand_r state and event counter carried on the "
                                      "device; new destinations each round (shd_synth_sends_device, in the timed "
                                      "loop; handoff_ms = the decide/group/sort stages alone)",

@@ -195,9 +195,9 @@ int shd_topology_latency_table_fw(ShdTopology* top, void* d_lat, void* stream);
  * max-latency + 1 distance buckets, each settled bucket's edges relaxed
  * edge-parallel by one wave; csrc/frontier.hip).  Same entries as the
  * table's latency column (tie-independent, as for the min-plus entry above),
- * no lookup side effects; graphs whose edge latencies are all whole ms (at
- * most 65,535) -- -ENOTSUP otherwise.  Synchronous on stream (hipStream_t,
- * NULL: the null stream). */
+ * no lookup side effects; graphs whose edge latencies are all whole ms and at
+ * most 3,348 ms (the per-wave bucket ring lives in LDS) -- -ENOTSUP
+ * otherwise.  Synchronous on stream (hipStream_t, NULL: the null stream). */
 int shd_topology_latency_rows_frontier(ShdTopology* top, int row_lo, int row_hi, void* d_lat, void* stream);
 int shd_topology_adopt_table_device(ShdTopology* top, void* d_table);
 /* Adopts a device table WITHOUT a host mirror (tables larger than host RAM
@@ -335,8 +335,11 @@ int shd_topology_path_counts_sync(ShdTopology* top);
  * a metadata overflow, an out-of-range overflow event) has SHD_ROUND_FAULT
  * set in counters[0] -- in that same round, so an asynchronous caller sees
  * it with the count -- and its outputs must not be used; the call returns
- * -EIO itself when stream is NULL (synchronous), else the next call on the
- * topology does (once). */
+ * -EIO itself when stream is NULL (synchronous).  With a stream, counters[0]
+ * bit 63 is the authoritative per-round signal; the sticky fault word is
+ * also reported (-EIO, once) by some later call on the topology after the
+ * faulted round has completed -- not necessarily the next call, which may
+ * start while that round still runs. */
 #define SHD_ROUND_FAULT (1ull << 63)
 int shd_round_process_device(ShdTopology* top, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                              uint64_t end_time, uint64_t bootstrap_end, ShdDeliv* d_out,

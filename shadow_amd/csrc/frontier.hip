@@ -55,6 +55,10 @@ __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin
 
 // per-wave LDS: head[nbk] | tail[nbk] | fill[nbk] | offs[64] | starts[64] | htab[64]
 __host__ __device__ constexpr size_t dial_lds_words(int nbk) { return 3 * (size_t)nbk + 192; }
+// the largest edge latency (ms) whose bucket ring fits the 160 KiB LDS (checked below)
+constexpr int kFrontierMaxWms = 3348;
+static_assert(dial_lds_words(kFrontierMaxWms + 1) * 4 * kWaves <= 160 * 1024, "ring fits the LDS");
+static_assert(dial_lds_words(kFrontierMaxWms + 2) * 4 * kWaves > 160 * 1024, "the limit is the largest that fits");
 
 // rows: rowlist[0 .. nrows) (or row_lo + i when rowlist is null); a row whose
 // chunk pool ran out is appended to redo (for a second launch with the
@@ -281,7 +285,11 @@ extern "C" int shd_dev_frontier_latency(const ShdGraphDev* gp, int row_lo, int r
                                         void* stream) {
     const ShdGraphDev g = *gp;
     if (!g.sl) return shd_fail(-ENOTSUP, "frontier latencies need whole-ms edge latencies");
-    if (wmax < 1 || wmax > 65535) return shd_fail(-ENOTSUP, "frontier latencies: largest edge latency %d ms", wmax);
+    // the ring's head / tail / fill words of the 4 waves live in LDS: at most
+    // 3,349 buckets, i.e. edge latencies up to kFrontierMaxWms = 3,348 ms
+    if (wmax < 1 || wmax > kFrontierMaxWms)
+        return shd_fail(-ENOTSUP, "frontier latencies: largest edge latency %d ms (the limit is %d ms)", wmax,
+                        kFrontierMaxWms);
     const int nrows = row_hi - row_lo;
     if (nrows <= 0) return 0;
     hipStream_t s = (hipStream_t)stream;

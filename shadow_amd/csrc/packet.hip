@@ -2665,6 +2665,100 @@ __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* 
 // kWire: the sorted segments go out as the exchange's 24-B wire records
 // (`out` is then a Wire array; listed segments are staged and listed as
 // always -- their sorted ShdDeliv form is converted by k_listed_wire)
+// Segments of kTinySeg < n <= 128 events (the C3 round: ~92 per destination)
+// ranked by TIME BUCKET instead of all pairs: the wave spreads the segment's
+// time offsets over 64 buckets ((t - tmin) >> sh), counts them in LDS, scans
+// the counts (each bucket's first rank) and lists each bucket's events; an
+// event's rank is its bucket's first rank plus the events of its own bucket
+// before it in event_compare order (time offset, src, srcHostEventID: the
+// stage record's fields order as the full values do).  O(n) LDS work and a
+// few compares per event instead of the all-pairs rank's 2n 64-bit compares
+// per lane (k_part_sort was VALU-bound on those).  Returns
+// false (wave-uniform, before any output) when a bucket holds more than
+// kBucketRankMax events -- e.g. many events clamped to the barrier, which all
+// share one time -- and the caller takes the all-pairs rank.
+constexpr uint32_t kBucketRankMax = 8;
+constexpr uint32_t kBucketRankSeg = 128;
+// per wave, in the wave's LDS key array (the two paths never overlap in time)
+struct BucketRankLds {
+    uint32_t h[2 * 64]; // [0, 64): counts, then first ranks; [64, 128): fill cursors, then counts
+    uint8_t m[128];     // the events of each bucket, at its first rank
+};
+static_assert(sizeof(BucketRankLds) <= 8 * (64 * 2 + 8), "fits a wave's LDS key array (kKeyE >= 2)");
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
+}
+// rank[e] of element e * 64 + lane (< n) of the segment lev[o, o + n)
+__device__ __forceinline__ bool wave_bucket_rank(const uint4* lev, uint32_t o, uint32_t n, uint32_t shift,
+                                                 BucketRankLds& w, int lane, uint32_t (&rank)[2]) {
+    uint32_t tmin = ~0u, tmax = 0u, tv[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        if (i < n) {
+            tv[e] = lev[o + i].x;
+            tmin = min(tmin, tv[e]);
+            tmax = max(tmax, tv[e]);
+        }
+    }
+    tmin = wave_min_u32(tmin);
+    const uint32_t span = wave_max_u32(tmax) - tmin;
+    const uint32_t sh = span < 64u ? 0u : 26u - (uint32_t)__clz((int)span); // (span >> sh) < 64
+    w.h[lane] = w.h[lane + 64] = 0u;
+    wave_lds_sync();
+    uint32_t bk[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 2; e++)
+        if ((uint32_t)(e * 64 + lane) < n) {
+            bk[e] = (tv[e] - tmin) >> sh;
+            atomicAdd(&w.h[bk[e]], 1u);
+        }
+    wave_lds_sync();
+    const uint32_t h0 = w.h[lane];
+    if (__ballot(h0 > kBucketRankMax)) return false;
+    const uint32_t ex = wave_incl_scan(h0, lane) - h0;
+    wave_lds_sync(); // (every lane has read its count)
+    w.h[lane] = ex;
+    wave_lds_sync();
+    uint32_t first[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        if (i < n) {
+            first[e] = w.h[bk[e]];
+            w.m[first[e] + atomicAdd(&w.h[64 + bk[e]], 1u)] = (uint8_t)i;
+        }
+    }
+    wave_lds_sync();
+    for (int e = 0; e < 2; e++) { // (not unrolled: one element's compares at a time)
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        const uint32_t f = e ? first[1] : first[0], b = e ? bk[1] : bk[0];
+        uint32_t rk = f;
+        if (i < n) {
+            const uint4 me = lev[o + i];
+            const uint32_t cb = w.h[64 + b], sr = me.w >> shift;
+            for (uint32_t k = 0; k < cb; k++) {
+                const uint4 x = lev[o + w.m[f + k]];
+                const uint32_t sx = x.w >> shift;
+                rk += (uint32_t)(x.x < me.x || (x.x == me.x && (sx < sr || (sx == sr && x.y < me.y))));
+            }
+        }
+        if (e) rank[1] = rk;
+        else rank[0] = rk;
+    }
+    return true;
+}
+
 template <int kWG, int kCap, int kKeyE, bool kWire>
 __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
@@ -2687,6 +2781,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     const bool perm = kPermOk && (lds_keys & 2u);
     __shared__ unsigned long long keys[kWG / 64][kKeyE ? 64 * kKeyE + 8 : 1];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
+    const bool brank = kKeyE >= 2 && (lds_keys & 4u);
     const uint32_t b = blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t d0 = b << g.shift;
@@ -2791,6 +2886,33 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
             };
             constexpr int kOut = kWire ? 2 : 1;
             ShdDeliv* const wo = reinterpret_cast<ShdDeliv*>(inv);
+            if (brank && nj <= kBucketRankSeg) {
+                uint32_t rk[2];
+                if (wave_bucket_rank(lev, o, nj, g.shift, *reinterpret_cast<BucketRankLds*>(keys[wv]), lane, rk)) {
+#pragma unroll
+                    for (int e = 0; e < 2; e++) {
+                        const uint32_t i = (uint32_t)(e * 64 + lane);
+                        if (i >= nj) continue;
+                        if (perm) {
+                            inv[o + rk[e]] = (uint16_t)(o + i);
+                            continue;
+                        }
+                        const uint4 r = lev[o + i];
+                        const unsigned long long t = g.tbase + r.x;
+                        const uint32_t sr = r.w >> g.shift;
+                        if (kWire) {
+                            st_wire(reinterpret_cast<Wire*>(out) + obase + o + rk[e], t, (unsigned long long)r.y, sr, r.z);
+                        } else {
+                            shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[obase + o + rk[e]]);
+                            const shd_v4u a = {(uint32_t)t, (uint32_t)(t >> 32), r.y, 0u};
+                            const shd_v4u c2 = {sr, dh, r.z, 0u};
+                            __builtin_nontemporal_store(a, q);
+                            __builtin_nontemporal_store(c2, q + 1);
+                        }
+                    }
+                    continue;
+                }
+            }
             if (nj <= 64) {
                 if (perm) wave_rank_segment<1, 3>(load, nj, dh, wo, o, lane, lk);
                 else wave_rank_segment<1, kOut>(load, nj, dh, out, obase + o, lane, lk);
@@ -2868,8 +2990,10 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
 
 // the kernels: the compiler's register choice, or sized for kOcc waves per
 // SIMD (SHD_PART_SORT=4: no LDS keys, 63 VGPRs, four workgroups per CU)
-template <int kWG, int kCap, int kKeyE = 4, bool kWire = false>
-__global__ __launch_bounds__(kWG) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
+// kMinW: waves per SIMD the registers are held to (instance 3: 6, three
+// 512-thread workgroups per CU -- the LDS allows it, the registers must too)
+template <int kWG, int kCap, int kKeyE = 4, bool kWire = false, int kMinW = 1>
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kMinW, 8))) void k_part_sort(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
                                                           const uint32_t* __restrict__ wcnt,
                                                           const ShdDeliv* __restrict__ wide,
@@ -3342,9 +3466,14 @@ uint32_t lds_keys() {
 // written in order through the LDS permutation -- measured 3-4 us slower per
 // round than every event stored at its rank (profiles/r04af_part_perm_probe.log:
 // the L2 merges the scattered halves; the extra pass and barrier cost more)
+// bit 2 (SHD_SORT_BUCKET=1 sets it): segments of 17..128 events ranked by
+// time bucket (wave_bucket_rank) instead of all pairs -- measured slower on
+// C3 (sort 0.193-0.195 vs 0.149-0.150 ms in one process,
+// profiles/r05c_sort_bucket_rank_probe.log), kept as the A/B form
 uint32_t part_sort_flags() {
     const char* v = getenv("SHD_PART_PERM");
-    return lds_keys() | (v && strcmp(v, "1") == 0 ? 2u : 0u);
+    const char* bk = getenv("SHD_SORT_BUCKET");
+    return lds_keys() | (v && strcmp(v, "1") == 0 ? 2u : 0u) | (bk && strcmp(bk, "1") == 0 ? 4u : 0u);
 }
 // Compact 16-B slab records (CSlab) with the rank sort; SHD_SLAB_COMPACT=0
 // (or the bitonic segment sort) keeps the 32-B slab
@@ -3735,181 +3864,329 @@ __global__ __launch_bounds__(256) void k_pcnt_spill(uint32_t* __restrict__ cnt, 
 }
 
 // ---- the counter log's fold (shd_dev_pcnt_fold) ----
-// Key space [0, N) in buckets of 2^S counters (at most kFoldBuckets of
-// them); the log in W chunks, one 1,024-thread workgroup each.
-// 1. k_fold_hist: each chunk's histogram over the buckets (LDS) -> column w
-//    of the bucket-major matrix M[b * W + w];
-// 2. the exclusive scan of M (scan_counts): every (bucket, chunk) run's start;
-// 3. k_fold_scatter: each chunk's keys to their runs (LDS cursors);
-// 4. k_fold_add: one workgroup per bucket adds its keys into LDS counters
-//    (sub-regions of 2^kFoldLds counters: 128 KB) and then each nonzero LDS
-//    counter into the dense table -- the bucket's counters belong to this
-//    workgroup alone, so plain loads and stores, and only the lines with a
-//    nonzero counter move (a dense bucket streams, a sparse one touches few).
-constexpr uint32_t kFoldBuckets = 16384;
-constexpr uint32_t kFoldLds = 15; // log2 of the LDS counters per pass (32K x 4 B)
+// The logged keys (u32 flat entry indices < N <= kFoldMaxN, all-ones = not
+// kept) are added into the dense counters by a two-level partition and one
+// LDS accumulation per 32K-counter region:
+//   key -> region r = key >> 15 (at most 16,384), coarse c = r >> 7 (<= 128),
+//   fine f = r & 127.
+// 1. k_fold_hist1: per tile of kFoldT log entries, the count per coarse
+//    bucket -> M1[c * nt1 + t]; scan -> every (c, t) run's start;
+// 2. k_fold_part1: each tile's kept keys counting-sorted by coarse bucket in
+//    LDS and written in that order (a run per coarse bucket: consecutive
+//    lanes, consecutive addresses) -> part;
+// 3. k_fold_hist2 / k_fold_part2: the same within each coarse bucket's
+//    contiguous range of part, by fine bucket, over tiles of that range
+//    alone; M2 is laid out (c, f, t), so its scan is the global order of the
+//    regions -> back into the log's buffer;
+// 4. k_fold_add: one workgroup per region adds its keys into LDS counters and
+//    each nonzero one into the dense table (the region's counters belong to
+//    this workgroup alone: plain read-modify-write, only the lines that hold a
+//    nonzero counter move).
+// Every pass streams the keys with whole-line writes; the single-level
+// partition over 12k regions (runs of < 1 key per tile) wrote every key as
+// its own store: 2.1 ms of a 3.1 ms fold of 184M keys (profiles/r05d_fold_kernel_stats.csv).
+constexpr uint32_t kFoldRegionBits = 15;          // 32K u32 counters = 128 KB of LDS
+constexpr uint32_t kFoldFineBits = 7;              // 128 regions per coarse bucket
+constexpr uint32_t kFoldCoarse = 128;              // at most
+constexpr unsigned long long kFoldMaxN = 1ull << (kFoldRegionBits + kFoldFineBits + 7); // 2^29 counters
 constexpr int kFoldWG = 1024;
-constexpr int kFoldUnroll = 4;
+constexpr int kFoldPer = 8;                        // keys per thread per tile
+constexpr uint32_t kFoldT = kFoldWG * kFoldPer;    // 8,192 keys per tile
+constexpr uint32_t kFoldSent = 0xFFFFFFFFu;
 
-template <typename K>
-__global__ __launch_bounds__(kFoldWG) void k_fold_hist(const K* __restrict__ keys, size_t L, uint32_t S, uint32_t B,
-                                                       size_t chunk, uint32_t W, uint32_t* __restrict__ M) {
-    extern __shared__ uint32_t fh[];
-    for (uint32_t b = threadIdx.x; b < B; b += kFoldWG) fh[b] = 0;
-    __syncthreads();
-    const size_t beg = (size_t)blockIdx.x * chunk, end = beg + chunk < L ? beg + chunk : L;
-    for (size_t i0 = beg + threadIdx.x; i0 < end; i0 += (size_t)kFoldWG * kFoldUnroll) {
-        K k[kFoldUnroll];
-#pragma unroll
-        for (int u = 0; u < kFoldUnroll; u++) {
-            const size_t i = i0 + (size_t)u * kFoldWG;
-            k[u] = i < end ? __builtin_nontemporal_load(keys + i) : (K)~(K)0;
-        }
-#pragma unroll
-        for (int u = 0; u < kFoldUnroll; u++)
-            if (k[u] != (K)~(K)0) atomicAdd(&fh[(uint32_t)(k[u] >> S)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < B; b += kFoldWG) M[(size_t)b * W + blockIdx.x] = fh[b];
-}
+__device__ __forceinline__ uint32_t fold_coarse(uint32_t k) { return k >> (kFoldRegionBits + kFoldFineBits); }
+__device__ __forceinline__ uint32_t fold_fine(uint32_t k) { return (k >> kFoldRegionBits) & ((1u << kFoldFineBits) - 1u); }
 
-template <typename K>
-__global__ __launch_bounds__(kFoldWG) void k_fold_scatter(const K* __restrict__ keys, size_t L, uint32_t S, uint32_t B,
-                                                          size_t chunk, uint32_t W, const uint32_t* __restrict__ off,
-                                                          K* __restrict__ part) {
-    extern __shared__ uint32_t fo[];
-    for (uint32_t b = threadIdx.x; b < B; b += kFoldWG) fo[b] = off[(size_t)b * W + blockIdx.x];
-    __syncthreads();
-    const size_t beg = (size_t)blockIdx.x * chunk, end = beg + chunk < L ? beg + chunk : L;
-    for (size_t i0 = beg + threadIdx.x; i0 < end; i0 += (size_t)kFoldWG * kFoldUnroll) {
-        K k[kFoldUnroll];
+// one tile's keys into registers (sentinel past the end)
+__device__ __forceinline__ void fold_load(const uint32_t* __restrict__ keys, size_t beg, size_t end,
+                                          uint32_t (&k)[kFoldPer]) {
 #pragma unroll
-        for (int u = 0; u < kFoldUnroll; u++) {
-            const size_t i = i0 + (size_t)u * kFoldWG;
-            k[u] = i < end ? __builtin_nontemporal_load(keys + i) : (K)~(K)0;
-        }
-#pragma unroll
-        for (int u = 0; u < kFoldUnroll; u++)
-            if (k[u] != (K)~(K)0) part[atomicAdd(&fo[(uint32_t)(k[u] >> S)], 1u)] = k[u];
+    for (int u = 0; u < kFoldPer; u++) {
+        const size_t i = beg + (size_t)u * kFoldWG + threadIdx.x;
+        k[u] = i < end ? __builtin_nontemporal_load(keys + i) : kFoldSent;
     }
 }
 
-template <typename K>
-__global__ __launch_bounds__(kFoldWG) void k_fold_add(const K* __restrict__ part, const uint32_t* __restrict__ off,
-                                                      uint32_t W, uint32_t S, uint32_t* __restrict__ dense,
-                                                      unsigned long long N) {
+// the digit counts of a tile in LDS h[128] (zeroed by the caller, synced after)
+template <bool kCoarse>
+__device__ __forceinline__ void fold_count(const uint32_t (&k)[kFoldPer], uint32_t* h) {
+#pragma unroll
+    for (int u = 0; u < kFoldPer; u++)
+        if (k[u] != kFoldSent) atomicAdd(&h[kCoarse ? fold_coarse(k[u]) : fold_fine(k[u])], 1u);
+}
+
+__global__ __launch_bounds__(kFoldWG) void k_fold_hist1(const uint32_t* __restrict__ log, size_t L, uint32_t C,
+                                                        uint32_t nt1, uint32_t* __restrict__ M1) {
+    __shared__ uint32_t h[kFoldCoarse];
+    if (threadIdx.x < kFoldCoarse) h[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t k[kFoldPer];
+    const size_t beg = (size_t)blockIdx.x * kFoldT;
+    fold_load(log, beg, beg + kFoldT < L ? beg + kFoldT : L, k);
+    fold_count<true>(k, h);
+    __syncthreads();
+    if (threadIdx.x < C) M1[(size_t)threadIdx.x * nt1 + blockIdx.x] = h[threadIdx.x];
+}
+
+// counting sort of the tile's keys by digit in LDS, then written in that
+// order: element j of the sorted tile (digit d, the d-run's j - start[d]-th)
+// goes to base[d] + j - start[d] (base: this tile's run starts, LDS)
+template <bool kCoarse>
+__device__ __forceinline__ void fold_part_tile(const uint32_t (&k)[kFoldPer], uint32_t* h, uint32_t* start,
+                                               const uint32_t* base, uint32_t* stage, uint32_t* __restrict__ out) {
+    uint32_t rk[kFoldPer];
+#pragma unroll
+    for (int u = 0; u < kFoldPer; u++)
+        rk[u] = k[u] != kFoldSent ? atomicAdd(&h[kCoarse ? fold_coarse(k[u]) : fold_fine(k[u])], 1u) : 0u;
+    __syncthreads();
+    __shared__ uint32_t tot;
+    if (threadIdx.x < 64) { // exclusive scan of the 128 counts (two per lane)
+        const uint32_t a = h[2 * threadIdx.x], b = h[2 * threadIdx.x + 1];
+        const uint32_t inc = wave_incl_scan(a + b, (int)threadIdx.x);
+        start[2 * threadIdx.x] = inc - a - b;
+        start[2 * threadIdx.x + 1] = inc - b;
+        if (threadIdx.x == 63) tot = inc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kFoldPer; u++)
+        if (k[u] != kFoldSent) stage[start[kCoarse ? fold_coarse(k[u]) : fold_fine(k[u])] + rk[u]] = k[u];
+    __syncthreads();
+    const uint32_t n = tot;
+    for (uint32_t j = threadIdx.x; j < n; j += kFoldWG) {
+        const uint32_t key = stage[j], d = kCoarse ? fold_coarse(key) : fold_fine(key);
+        out[base[d] + (j - start[d])] = key;
+    }
+}
+
+__global__ __launch_bounds__(kFoldWG) void k_fold_part1(const uint32_t* __restrict__ log, size_t L, uint32_t C,
+                                                        uint32_t nt1, const uint32_t* __restrict__ M1,
+                                                        uint32_t* __restrict__ part) {
+    __shared__ uint32_t h[kFoldCoarse], start[kFoldCoarse], base[kFoldCoarse];
+    __shared__ uint32_t stage[kFoldT];
+    if (threadIdx.x < kFoldCoarse) {
+        h[threadIdx.x] = 0u;
+        base[threadIdx.x] = threadIdx.x < C ? M1[(size_t)threadIdx.x * nt1 + blockIdx.x] : 0u;
+    }
+    __syncthreads();
+    uint32_t k[kFoldPer];
+    const size_t beg = (size_t)blockIdx.x * kFoldT;
+    fold_load(log, beg, beg + kFoldT < L ? beg + kFoldT : L, k);
+    fold_part_tile<true>(k, h, start, base, stage, part);
+}
+
+// the level-2 tiles: coarse bucket c's range of part is [M1[c * nt1],
+// M1[(c + 1) * nt1]) and holds tiles_c = ceil(size / kFoldT) tiles; tbase[c]
+// = the tiles before c.  Every workgroup derives them from M1 (LDS).
+struct FoldL2 {
+    uint32_t lo[kFoldCoarse + 1]; // range starts (lo[C] = total)
+    uint32_t tb[kFoldCoarse + 1]; // tile bases (tb[C] = all tiles)
+};
+__device__ __forceinline__ void fold_l2_geometry(const uint32_t* __restrict__ M1, uint32_t C, uint32_t nt1, FoldL2& g) {
+    if (threadIdx.x < 64) {
+        uint32_t lo[2], nt[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const uint32_t c = 2 * threadIdx.x + e;
+            lo[e] = c <= C ? M1[(size_t)c * nt1] : 0u;
+        }
+        // (tile counts need the next range start: lo of c + 1)
+        const uint32_t next1 = (2 * threadIdx.x + 2 <= C) ? M1[(size_t)(2 * threadIdx.x + 2) * nt1] : 0u;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const uint32_t c = 2 * threadIdx.x + e;
+            const uint32_t hi = e == 0 ? lo[1] : next1;
+            nt[e] = c < C ? (hi - lo[e] + kFoldT - 1) / kFoldT : 0u;
+            if (c <= C) g.lo[c] = lo[e];
+        }
+        const uint32_t inc = wave_incl_scan(nt[0] + nt[1], (int)threadIdx.x);
+        if (2 * threadIdx.x <= C) g.tb[2 * threadIdx.x] = inc - nt[0] - nt[1];
+        if (2 * threadIdx.x + 1 <= C) g.tb[2 * threadIdx.x + 1] = inc - nt[1];
+        if (threadIdx.x == 63) { // (C = 128: entry C lies past the 64 lanes' pairs)
+            g.tb[C] = inc;
+            g.lo[C] = M1[(size_t)C * nt1];
+        }
+    }
+    __syncthreads();
+}
+// the (coarse, tile) of level-2 tile number `gt` (false: past the last tile)
+__device__ __forceinline__ bool fold_l2_tile(const FoldL2& g, uint32_t C, uint32_t gt, uint32_t* c, uint32_t* t) {
+    if (gt >= g.tb[C]) return false;
+    uint32_t a = 0, b = C; // largest c with tb[c] <= gt and a tile of its own
+    while (b - a > 1) {
+        const uint32_t m = (a + b) >> 1;
+        if (g.tb[m] <= gt) a = m;
+        else b = m;
+    }
+    while (g.tb[a + 1] <= gt) a++; // (skips empty buckets: tb[a + 1] == tb[a])
+    *c = a;
+    *t = gt - g.tb[a];
+    return true;
+}
+
+__global__ __launch_bounds__(kFoldWG) void k_fold_hist2(const uint32_t* __restrict__ part, const uint32_t* __restrict__ M1,
+                                                        uint32_t C, uint32_t nt1, uint32_t* __restrict__ M2) {
+    __shared__ FoldL2 g;
+    __shared__ uint32_t h[1u << kFoldFineBits];
+    fold_l2_geometry(M1, C, nt1, g);
+    uint32_t c, t;
+    if (!fold_l2_tile(g, C, blockIdx.x, &c, &t)) return; // (block-uniform)
+    if (threadIdx.x < (1u << kFoldFineBits)) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t ntc = g.tb[c + 1] - g.tb[c];
+    const size_t beg = (size_t)g.lo[c] + (size_t)t * kFoldT, end = beg + kFoldT < g.lo[c + 1] ? beg + kFoldT : g.lo[c + 1];
+    uint32_t k[kFoldPer];
+    fold_load(part, beg, end, k);
+    fold_count<false>(k, h);
+    __syncthreads();
+    if (threadIdx.x < (1u << kFoldFineBits))
+        M2[((size_t)g.tb[c] << kFoldFineBits) + (size_t)threadIdx.x * ntc + t] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kFoldWG) void k_fold_part2(const uint32_t* __restrict__ part, const uint32_t* __restrict__ M1,
+                                                        uint32_t C, uint32_t nt1, const uint32_t* __restrict__ M2,
+                                                        uint32_t* __restrict__ out) {
+    __shared__ FoldL2 g;
+    __shared__ uint32_t h[1u << kFoldFineBits], start[1u << kFoldFineBits], base[1u << kFoldFineBits];
+    __shared__ uint32_t stage[kFoldT];
+    fold_l2_geometry(M1, C, nt1, g);
+    uint32_t c, t;
+    if (!fold_l2_tile(g, C, blockIdx.x, &c, &t)) return;
+    const uint32_t ntc = g.tb[c + 1] - g.tb[c];
+    if (threadIdx.x < (1u << kFoldFineBits)) {
+        h[threadIdx.x] = 0u;
+        base[threadIdx.x] = M2[((size_t)g.tb[c] << kFoldFineBits) + (size_t)threadIdx.x * ntc + t];
+    }
+    __syncthreads();
+    const size_t beg = (size_t)g.lo[c] + (size_t)t * kFoldT, end = beg + kFoldT < g.lo[c + 1] ? beg + kFoldT : g.lo[c + 1];
+    uint32_t k[kFoldPer];
+    fold_load(part, beg, end, k);
+    fold_part_tile<false>(k, h, start, base, stage, out);
+}
+
+// region r = c * 128 + f: its keys are [M2 index (c, f, 0), (c, f + 1, 0))
+__global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ M1,
+                                                      uint32_t C, uint32_t nt1, const uint32_t* __restrict__ M2,
+                                                      uint32_t* __restrict__ dense, unsigned long long N) {
     extern __shared__ uint32_t fc[];
-    const uint32_t b = blockIdx.x;
-    const size_t beg = off[(size_t)b * W], end = off[(size_t)(b + 1) * W];
-    if (beg == end) return; // (block-uniform)
-    const uint32_t R = S < kFoldLds ? S : kFoldLds;
-    const uint32_t nsub = 1u << (S - R);
-    const unsigned long long bbase = (unsigned long long)b << S;
-    for (uint32_t sub = 0; sub < nsub; sub++) {
-        const unsigned long long sbase = bbase + ((unsigned long long)sub << R);
-        if (sbase >= N) break;
-        for (uint32_t j = threadIdx.x; j < (1u << R); j += kFoldWG) fc[j] = 0;
-        __syncthreads();
-        for (size_t i0 = beg + threadIdx.x; i0 < end; i0 += (size_t)kFoldWG * kFoldUnroll) {
-            K k[kFoldUnroll];
+    __shared__ FoldL2 g;
+    fold_l2_geometry(M1, C, nt1, g);
+    const uint32_t r = blockIdx.x, c = r >> kFoldFineBits, f = r & ((1u << kFoldFineBits) - 1u);
+    const uint32_t ntc = g.tb[c + 1] - g.tb[c];
+    if (!ntc) return; // (block-uniform: the coarse bucket is empty)
+    const size_t mb = (size_t)g.tb[c] << kFoldFineBits;
+    const uint32_t beg = M2[mb + (size_t)f * ntc], end = M2[mb + (size_t)(f + 1) * ntc];
+    if (beg == end) return;
+    constexpr uint32_t R = 1u << kFoldRegionBits;
+    for (uint32_t j = threadIdx.x; j < R; j += kFoldWG) fc[j] = 0u;
+    __syncthreads();
+    for (uint32_t i0 = beg + threadIdx.x; i0 < end; i0 += kFoldWG * 4) {
+        uint32_t k[4];
 #pragma unroll
-            for (int u = 0; u < kFoldUnroll; u++) {
-                const size_t i = i0 + (size_t)u * kFoldWG;
-                k[u] = i < end ? part[i] : (K)~(K)0;
-            }
+        for (int u = 0; u < 4; u++) k[u] = i0 + u * kFoldWG < end ? keys[i0 + u * kFoldWG] : kFoldSent;
 #pragma unroll
-            for (int u = 0; u < kFoldUnroll; u++) {
-                const unsigned long long rel = (unsigned long long)k[u] - sbase;
-                if (k[u] != (K)~(K)0 && rel < (1ull << R)) atomicAdd(&fc[(uint32_t)rel], 1u);
-            }
-        }
-        __syncthreads();
-        const unsigned long long rem = N - sbase;
-        const uint32_t lim = rem < (1ull << R) ? (uint32_t)rem : (1u << R);
-        for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
-            const uint32_t v = fc[j];
-            if (v) dense[sbase + j] += v;
-        }
-        __syncthreads();
+        for (int u = 0; u < 4; u++)
+            if (k[u] != kFoldSent) atomicAdd(&fc[k[u] & (R - 1u)], 1u);
+    }
+    __syncthreads();
+    const unsigned long long rb = (unsigned long long)r << kFoldRegionBits;
+    const uint32_t lim = N - rb < R ? (uint32_t)(N - rb) : R;
+    for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
+        const uint32_t v = fc[j];
+        if (v) dense[rb + j] += v;
     }
 }
 
 struct FoldScratch {
-    void* part = nullptr;
-    size_t cap_part = 0; // bytes
-    uint32_t* M = nullptr;
-    size_t cap_M = 0; // words
+    uint32_t* part = nullptr;
+    size_t cap_part = 0; // keys
+    uint32_t* M1 = nullptr;
+    size_t cap_M1 = 0; // words
+    uint32_t* M2 = nullptr;
+    size_t cap_M2 = 0;
     uint32_t* bsum = nullptr;
     size_t cap_bsum = 0;
 };
 
-template <typename K>
-int pcnt_fold(const K* log, size_t L, uint32_t* dense, unsigned long long N, FoldScratch& f, hipStream_t s) {
-    uint32_t S = kFoldLds;
-    while ((N - 1) >> S >= kFoldBuckets) S++;
-    const uint32_t B = (uint32_t)(((N - 1) >> S) + 1);
-    size_t chunk = (L + 1023) / 1024;
-    if (chunk < (1u << 16)) chunk = 1u << 16;
-    const uint32_t W = (uint32_t)((L + chunk - 1) / chunk);
-    const size_t m = (size_t)B * W;
-    int rc = 0;
-    auto grow = [&](void** p, size_t* cap, size_t need, const char* what) {
-        if (need <= *cap) return 0;
-        (void)hipFree(*p);
-        *p = nullptr;
-        *cap = 0;
-        const size_t c = need + need / 8;
-        if (int r = hip_status(hipMalloc(p, c), what)) return r;
-        *cap = c;
-        return 0;
-    };
-    size_t cm = f.cap_M * 4, cb = f.cap_bsum * 4;
-    if ((rc = grow(&f.part, &f.cap_part, L * sizeof(K), "hipMalloc fold part")) ||
-        (rc = grow((void**)&f.M, &cm, 4 * (m + 1), "hipMalloc fold matrix")) ||
-        (rc = grow((void**)&f.bsum, &cb, 4 * (m / kScanTile + 2), "hipMalloc fold scan")))
+int fold_grow(uint32_t** p, size_t* cap, size_t need, const char* what) {
+    if (need <= *cap) return 0;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (int r = hip_status(hipMalloc((void**)p, 4 * need), what)) return r;
+    *cap = need;
+    return 0;
+}
+
+// buffers for folds of up to L keys (grow-only; reserved with the log so that
+// a fold inside a timed region allocates nothing)
+int fold_reserve(FoldScratch& f, size_t L) {
+    const size_t nt1 = (L + kFoldT - 1) / kFoldT;
+    const size_t m1 = kFoldCoarse * nt1 + 1, m2 = ((nt1 + kFoldCoarse) << kFoldFineBits) + 1;
+    const size_t mb = (m1 > m2 ? m1 : m2) / kScanTile + 2;
+    int rc;
+    if ((rc = fold_grow(&f.part, &f.cap_part, L ? L : 1, "hipMalloc fold part")) ||
+        (rc = fold_grow(&f.M1, &f.cap_M1, m1, "hipMalloc fold M1")) ||
+        (rc = fold_grow(&f.M2, &f.cap_M2, m2, "hipMalloc fold M2")) ||
+        (rc = fold_grow(&f.bsum, &f.cap_bsum, mb, "hipMalloc fold scan")))
         return rc;
-    f.cap_M = cm / 4;
-    f.cap_bsum = cb / 4;
+    return 0;
+}
+
+// (log: both the input and, after the level-1 pass has read it, the level-2
+// output -- one scratch array of L keys besides it)
+int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, unsigned long long N, FoldScratch& f, hipStream_t s) {
+    if (N > kFoldMaxN) return shd_fail(-EINVAL, "fold: %llu counters exceed the fold's %llu", N, kFoldMaxN);
+    if (int rc = fold_reserve(f, L)) return rc;
     static bool attr = false;
     if (!attr) {
-        if ((rc = hip_status(hipFuncSetAttribute((const void*)k_fold_add<uint32_t>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 << kFoldLds),
-                             "hipFuncSetAttribute k_fold_add")) ||
-            (rc = hip_status(hipFuncSetAttribute((const void*)k_fold_add<unsigned long long>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 4 << kFoldLds),
-                             "hipFuncSetAttribute k_fold_add")))
+        if (int rc = hip_status(hipFuncSetAttribute((const void*)k_fold_add, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    4 << kFoldRegionBits),
+                                "hipFuncSetAttribute k_fold_add"))
             return rc;
         attr = true;
     }
-    K* part = static_cast<K*>(f.part);
-    hipLaunchKernelGGL(k_fold_hist<K>, dim3(W), dim3(kFoldWG), 4 * (size_t)B, s, log, L, S, B, chunk, W, f.M);
-    scan_counts(f.M, m, f.M, f.bsum, nullptr, s);
-    hipLaunchKernelGGL(k_fold_scatter<K>, dim3(W), dim3(kFoldWG), 4 * (size_t)B, s, log, L, S, B, chunk, W, f.M,
-                       part);
-    // (the scatter's cursors live in LDS: M still holds every run's start, so
-    // bucket b spans [M[b * W], M[(b + 1) * W]))
-    hipLaunchKernelGGL(k_fold_add<K>, dim3(B), dim3(kFoldWG), (size_t)4 << (S < kFoldLds ? S : kFoldLds), s, part,
-                       f.M, W, S, dense, N);
+    const uint32_t R = (uint32_t)(((N - 1) >> kFoldRegionBits) + 1);
+    const uint32_t C = ((R - 1) >> kFoldFineBits) + 1;
+    const uint32_t nt1 = (uint32_t)((L + kFoldT - 1) / kFoldT);
+    const size_t m1 = (size_t)C * nt1;
+    hipLaunchKernelGGL(k_fold_hist1, dim3(nt1), dim3(kFoldWG), 0, s, log, L, C, nt1, f.M1);
+    scan_counts(f.M1, m1, f.M1, f.bsum, nullptr, s);
+    hipLaunchKernelGGL(k_fold_part1, dim3(nt1), dim3(kFoldWG), 0, s, log, L, C, nt1, f.M1, f.part);
+    const uint32_t nt2 = nt1 + C; // level-2 tiles: at most one partial tile per coarse bucket more
+    const size_t m2 = (size_t)nt2 << kFoldFineBits;
+    // (M2 past the last tile stays unused; its scan covers the whole
+    // reservation's head: entries never written are read as left by the
+    // previous fold, so zero them)
+    if (int rc = hip_status(hipMemsetAsync(f.M2, 0, 4 * m2, s), "memset fold M2")) return rc;
+    hipLaunchKernelGGL(k_fold_hist2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2);
+    scan_counts(f.M2, m2, f.M2, f.bsum, nullptr, s);
+    hipLaunchKernelGGL(k_fold_part2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2, log);
+    hipLaunchKernelGGL(k_fold_add, dim3(R), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, f.M1, C, nt1, f.M2,
+                       dense, N);
     return hip_status(hipGetLastError(), "pcnt fold launch");
 }
 
 } // namespace
 
-extern "C" int shd_dev_pcnt_fold(const void* log, int log64, size_t L, uint32_t* dense, uint64_t N, void** scratch,
-                                 void* stream) {
+extern "C" int shd_dev_pcnt_fold_reserve(size_t L, void** scratch) {
+    if (!*scratch && !(*scratch = new (std::nothrow) FoldScratch())) return shd_fail(-ENOMEM, "fold scratch");
+    return fold_reserve(*static_cast<FoldScratch*>(*scratch), L);
+}
+
+extern "C" int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream) {
     if (!L || !N) return 0;
     if (!*scratch && !(*scratch = new (std::nothrow) FoldScratch())) return shd_fail(-ENOMEM, "fold scratch");
-    FoldScratch& f = *static_cast<FoldScratch*>(*scratch);
-    hipStream_t s = (hipStream_t)stream;
-    return log64 ? pcnt_fold(static_cast<const unsigned long long*>(log), L, dense, N, f, s)
-                 : pcnt_fold(static_cast<const uint32_t*>(log), L, dense, N, f, s);
+    return pcnt_fold(static_cast<uint32_t*>(log), L, dense, N, *static_cast<FoldScratch*>(*scratch),
+                     (hipStream_t)stream);
 }
 
 extern "C" void shd_dev_pcnt_scratch_free(void* scratch) {
     if (!scratch) return;
     FoldScratch* f = static_cast<FoldScratch*>(scratch);
     (void)hipFree(f->part);
-    (void)hipFree(f->M);
+    (void)hipFree(f->M1);
+    (void)hipFree(f->M2);
     (void)hipFree(f->bsum);
     delete f;
 }
@@ -4122,7 +4399,7 @@ int part_round(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
                        (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters, part_sort_flags())
         if (sc == 1) SHD_PART_SORT_LAUNCH(512, 3584);
         else if (sc == 2) SHD_PART_SORT_LAUNCH(256, 1792);
-        else if (sc == 3) SHD_PART_SORT_LAUNCH(512, 2304, 2);
+        else if (sc == 3) SHD_PART_SORT_LAUNCH(512, 2304, 2, false, 6);
         else if (sc == 4)
             hipLaunchKernelGGL((k_part_sort_occ<512, 2304, 0, 8>), dim3(g.nb), dim3(512), 0, s, g, w.pstage, gcnt, wcnt,
                                w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_dst_offsets, d_out, w.st1, w.big, w.nbig, counters,
@@ -4406,14 +4683,14 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
         if (wsorted) {
             ShdDeliv* wout = static_cast<ShdDeliv*>(d_wire); // (a Wire array: kWire)
             const int sc = part_sort_cfg();
-#define SHD_WIRE_SORT_LAUNCH(WG, CAP, KE)                                                                             \
-    hipLaunchKernelGGL((k_part_sort<WG, CAP, KE, true>), dim3(pg.nb), dim3(WG), 0, s, pg, w.pstage, w.cnt1,            \
+#define SHD_WIRE_SORT_LAUNCH(WG, CAP, KE, ...)                                                                        \
+    hipLaunchKernelGGL((k_part_sort<WG, CAP, KE, true, ##__VA_ARGS__>), dim3(pg.nb), dim3(WG), 0, s, pg, w.pstage, w.cnt1,            \
                        w.cnt1 + pg.nb, w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_off, wout, w.st1, w.big, w.nbig, counters, \
                        part_sort_flags())
             if (sc == 0) SHD_WIRE_SORT_LAUNCH(1024, 7168, 4);
             else if (sc == 1) SHD_WIRE_SORT_LAUNCH(512, 3584, 4);
             else if (sc == 2) SHD_WIRE_SORT_LAUNCH(256, 1792, 4);
-            else SHD_WIRE_SORT_LAUNCH(512, 2304, 2);
+            else SHD_WIRE_SORT_LAUNCH(512, 2304, 2, 6);
 #undef SHD_WIRE_SORT_LAUNCH
             if ((rc = hip_status(hipGetLastError(), "k_part_sort (wire) launch")) ||
                 (rc = sort_listed(w, w.st1, d_off, w.st2, s, counters)))

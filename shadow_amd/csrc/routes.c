@@ -503,13 +503,16 @@ int shd_ptab_release_for_retry(ShdTopology* t, int rc) {
  * per-packet device atomic (SHD_PCNT=atomic) costs the round +0.365 ms at
  * C3. */
 
-/* SHD_PCNT: "log" (default), "atomic" (one device atomic per kept packet,
- * the A/B form), "0" (measurement only: counts are not kept). */
-static int pcnt_mode(void) {
+/* SHD_PCNT: "log" (the default where the fold applies: tables of at most
+ * SHD_PCNT_FOLD_MAX_N = 2^29 entries, C1-C3), "atomic" (one device atomic
+ * per kept packet: the default above, C4's 7.5e9-entry table, whose 1M-packet
+ * rounds spend ~0.04 ms on them), "0" (measurement only: counts are not
+ * kept). */
+static int pcnt_mode_of(const ShdTopology* t, const ShdPcnt* p) {
     const char* v = getenv("SHD_PCNT");
     if (v && strcmp(v, "0") == 0) return 0;
     if (v && strcmp(v, "atomic") == 0) return 2;
-    return 1;
+    return (uint64_t)p->hi * (uint64_t)t->A <= SHD_PCNT_FOLD_MAX_N ? 1 : 2;
 }
 
 /* Spill threshold: counters >= T move to the host map once the packets
@@ -543,8 +546,7 @@ static int pcnt_fold(ShdTopology* t, ShdPcnt* p) {
     int rc = shd_dev_init(p->device);
     if (!rc) rc = shd_dev_sync();
     if (!rc)
-        rc = shd_dev_pcnt_fold(p->log, p->log64, p->log_fill, p->base, (uint64_t)(p->hi) * (uint64_t)t->A, &p->fold,
-                               NULL);
+        rc = shd_dev_pcnt_fold(p->log, p->log_fill, p->base, (uint64_t)(p->hi) * (uint64_t)t->A, &p->fold, NULL);
     if (!rc) rc = shd_dev_sync();
     if (!rc) p->log_fill = 0;
     shd_dev_init(t->device);
@@ -583,7 +585,11 @@ static int pcnt_spill(ShdTopology* t, ShdPcnt* p, uint32_t thr) {
 
 int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
     p->cur = NULL;
-    const int mode = pcnt_mode();
+    p->mode = 0;
+    ShdPcnt want = *p;
+    want.lo = lo;
+    want.hi = hi;
+    const int mode = pcnt_mode_of(t, &want);
     if (!mode || hi <= lo) return 0;
     int rc = 0;
     if (p->alloc && (p->lo != lo || p->hi != hi) && (rc = shd_pcnt_drop(t, p))) return rc;
@@ -605,7 +611,6 @@ int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
         p->hi = hi;
         p->device = dev;
         p->budget = 0;
-        p->log64 = (uint64_t)hi * (uint64_t)t->A >= 0xFFFFFFFFull; /* keys are flat entry indices */
     }
     const uint64_t T = pcnt_spill_at();
     if (p->budget + n >= T) { /* a counter below T could otherwise pass 2^32 - 1 */
@@ -613,8 +618,9 @@ int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
         p->budget = 0;
     }
     p->budget += n;
+    p->mode = mode;
     if (mode == 2) return shd_dev_init(dev);
-    const size_t ksz = p->log64 ? 8 : 4;
+    const size_t ksz = 4; /* (log mode: u32 keys, the table is below 2^29 entries) */
     if (p->log_fill + n > p->log_cap) {
         if ((rc = pcnt_fold(t, p))) return rc;
         if (n > p->log_cap || !p->log) {
@@ -623,7 +629,9 @@ int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
             p->log = NULL;
             p->log_cap = 0;
             const size_t cap = pcnt_log_cap(n);
-            if ((rc = shd_dev_malloc(&p->log, cap * ksz))) return rc;
+            /* the log and the fold's buffers for a full log: a fold inside a
+             * timed region allocates nothing */
+            if ((rc = shd_dev_malloc(&p->log, cap * ksz)) || (rc = shd_dev_pcnt_fold_reserve(cap, &p->fold))) return rc;
             p->log_cap = cap;
         }
     }
@@ -636,8 +644,8 @@ int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
 
 void shd_pcnt_ctx(const ShdPcnt* p, ShdPktCtx* c) {
     c->plog = p->cur;
-    c->plog64 = (uint32_t)p->log64;
-    c->pcnt = pcnt_mode() == 2 ? p->base : NULL;
+    c->plog64 = 0;
+    c->pcnt = p->mode == 2 ? p->base : NULL;
 }
 
 void shd_pcnt_commit(ShdPcnt* p, int rc) {

@@ -177,14 +177,17 @@ typedef struct {
  * the number of entries appended in *appended (host). */
 int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, size_t cap, uint32_t* d_nlist,
                        size_t* appended);
-/* Adds the L logged keys of `log` (u32 or u64 flat entry indices below N,
- * all-ones = nothing) into the dense counters (N u32): a bucket partition
- * of the keys (histogram, scan, scatter) and one workgroup per bucket that
- * accumulates its keys in LDS and adds its counters to the dense table
- * (exclusive owner: plain read-modify-write of the touched lines).  Enqueued
- * on stream; *scratch: grow-only buffers (NULL the first time), freed with
- * shd_dev_pcnt_scratch_free. */
-int shd_dev_pcnt_fold(const void* log, int log64, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream);
+/* Adds the L logged keys of `log` (u32 flat entry indices below N <=
+ * SHD_PCNT_FOLD_MAX_N, all-ones = nothing) into the dense counters (N u32):
+ * a two-level partition of the keys into 32K-counter regions and one
+ * workgroup per region that accumulates its keys in LDS and adds its
+ * counters to the dense table.  The log's buffer is overwritten (it holds
+ * the second level's output).  Enqueued on stream; *scratch: grow-only
+ * buffers (NULL the first time; shd_dev_pcnt_fold_reserve sizes them for L
+ * keys ahead), freed with shd_dev_pcnt_scratch_free. */
+#define SHD_PCNT_FOLD_MAX_N (1ull << 29)
+int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream);
+int shd_dev_pcnt_fold_reserve(size_t L, void** scratch);
 void shd_dev_pcnt_scratch_free(void* scratch);
 
 /* The 8-B packet-path table of nent entries of tab ({u32 delay_ns =

@@ -77,8 +77,16 @@ extern "C" int shd_synth_sends_device(const uint32_t* d_pool, uint32_t npool, ui
                                       uint32_t ndst, const uint32_t* d_state_in, uint32_t* d_state_out,
                                       const uint64_t* d_seq_in, uint64_t* d_seq_out, ShdPkt* d_recs, void* stream) {
     if (!npool || !m) return 0;
-    if (!d_pool || !ndst || !d_state_in || !d_state_out || !d_seq_in || !d_seq_out || !d_recs || d_state_in == d_state_out)
+    if (!d_pool || !ndst || !d_state_in || !d_state_out || !d_seq_in || !d_seq_out || !d_recs)
         return shd_fail(-EINVAL, "bad synthetic-send arguments");
+    // the carried states are read by every packet's thread while the last one
+    // of each sender writes them: input and output arrays must not overlap
+    auto overlap = [npool](const void* a, const void* b, size_t elem) {
+        const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b, len = (uintptr_t)npool * elem;
+        return x < y + len && y < x + len;
+    };
+    if (overlap(d_state_in, d_state_out, 4) || overlap(d_seq_in, d_seq_out, 8))
+        return shd_fail(-EINVAL, "synthetic sends: the carried state arrays in and out overlap");
     const size_t n = (size_t)npool * m;
     const size_t g = (n + 255) / 256;
     // the round's hash key: seed and round index spread apart (splitmix64 of both)

@@ -77,7 +77,8 @@ typedef struct {
      * cur_n: the slice reserved for the round being launched */
     void* log;
     size_t log_cap, log_fill;
-    int log64;
+    int log64; /* (always 0: the fold takes u32 keys) */
+    int mode;  /* this round's: 0 none, 1 log, 2 atomic */
     void* cur;
     size_t cur_n;
     void* fold; /* shd_dev_pcnt_fold scratch */

@@ -404,6 +404,10 @@ extern "C" int shd_dev_event_cuts(void* ws, const uint32_t* d_dst_offsets, const
 // destination slabs again.  Scratch (device, caller-sized, see
 // xchg_scratch_words): [cuts | H + W slices | W x (H_me + 1) received offsets
 // | W + 1 block bases]; host (pinned): [cuts | block bases].
+// the count matrix of a rank whose workspace could not allocate its own
+// (exchange_runs_core): a static device array, so that rank can still join the
+// matrix all-gather and report its failure through it
+__device__ uint64_t g_xmat_fallback[64 * 66];
 namespace {
 int local_allgatherv(void* user, void* d_buf, const uint64_t* off, void* stream);
 int local_alltoallv_off(void* user, const void* d_send, const uint64_t* send_bytes, const uint64_t* send_off,
@@ -435,9 +439,25 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
     // so all of them fail together.
     uint64_t *d_mat = nullptr, *h_mat = nullptr;
     // (the library's own transports: their all-gather takes any device
-    // buffer; a caller's transport may only know the buffers it registered)
+    // buffer; a caller's transport may only know the buffers it registered).
+    // The form depends on the transport alone, so every rank takes the same
+    // collectives: a rank whose matrix allocation failed still joins the
+    // all-gather, with the static fallback matrix, and reports the failure in
+    // its row's flag -- every rank then returns an error together.
     const bool own = x->allgatherv == rccl_allgatherv || x->allgatherv == local_allgatherv;
-    const bool one_trip = own && shd_dev_ws_xmat(ws, (size_t)W * (W + 2), &d_mat, &h_mat) == 0;
+    const bool one_trip = own;
+    std::vector<uint64_t> h_fallback;
+    if (one_trip) {
+        const int xrc = shd_dev_ws_xmat(ws, (size_t)W * (W + 2), &d_mat, &h_mat);
+        if (xrc) {
+            if (!local_rc) local_rc = xrc;
+            if ((rc = hip_status(hipGetSymbolAddress((void**)&d_mat, HIP_SYMBOL(g_xmat_fallback)),
+                                 "fallback count matrix")))
+                return rc;
+            h_fallback.assign((size_t)W * (W + 2), 0);
+            h_mat = h_fallback.data();
+        }
+    }
     if (local_rc && !one_trip) { // only the count all-to-all that tells the peers
         std::vector<uint64_t> none(W, 0);
         size_t nr = 0;

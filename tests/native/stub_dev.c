@@ -227,11 +227,12 @@ int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, 
     *appended = k;
     return 0;
 }
-int shd_dev_pcnt_fold(const void* log, int log64, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream) {
+int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream) {
     for (size_t i = 0; i < L; i++) {
-        const uint64_t k = log64 ? ((const uint64_t*)log)[i] : ((const uint32_t*)log)[i];
-        if (log64 ? k != UINT64_MAX : k != UINT32_MAX) dense[k]++;
+        const uint32_t k = ((const uint32_t*)log)[i];
+        if (k != UINT32_MAX) dense[k]++;
     }
     return 0;
 }
+int shd_dev_pcnt_fold_reserve(size_t L, void** scratch) { return 0; }
 void shd_dev_pcnt_scratch_free(void* scratch) { (void)scratch; }

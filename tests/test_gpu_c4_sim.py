@@ -109,3 +109,26 @@ def test_c4_three_simulated_rounds():
     orc.close()
     del table
     torch.cuda.empty_cache()
+
+
+def test_synth_sends_rejects_overlapping_carry():
+    """The load generator's carried states: in and out arrays that overlap
+    (for the rand_r states or the event counters) are refused (-EINVAL)."""
+    import torch
+    lib = _lib.lib()
+    dev = torch.device("cuda")
+    npool, m = 64, 4
+    pool = torch.arange(npool, dtype=torch.int32, device=dev)
+    st = torch.zeros(2 * npool, dtype=torch.int32, device=dev)
+    sq = torch.zeros(2 * npool, dtype=torch.int64, device=dev)
+    recs = torch.empty(npool * m * 32, dtype=torch.uint8, device=dev)
+    P = lambda t, off=0: C.c_void_p(t.data_ptr() + off * t.element_size())  # noqa: E731
+
+    def call(st_in, st_out, sq_in, sq_out):
+        return lib.shd_synth_sends_device(P(pool), npool, m, 0, 1, 0, 1000, None, 1000, st_in, st_out, sq_in, sq_out,
+                                          P(recs), None)
+    assert call(P(st), P(st, npool), P(sq), P(sq, npool)) == 0
+    torch.cuda.synchronize()
+    assert call(P(st), P(st, npool), P(sq), P(sq)) == -22           # the same counters
+    assert call(P(st), P(st, npool), P(sq), P(sq, npool // 2)) == -22  # overlapping counters
+    assert call(P(st), P(st, 1), P(sq), P(sq, npool)) == -22           # overlapping states

@@ -216,6 +216,34 @@ def test_c4_sampled_rows_bit_exact(c4):
     assert not bad, f"rows differ: {bad[:8]}"
 
 
+@pytest.mark.timeout(900)
+def test_c4_all_rows_bit_exact(c4):
+    """Every one of the 86,603 rows of the C4 table -- latencies AND
+    reliabilities (the tie-dependent half, topology.c:1578-1814) -- against the
+    oracle's igraph-0.8 Dijkstra, in blocks of 2,048 rows (one D2H each), the
+    oracle's rows on the job's CPU share."""
+    import os
+    import time
+
+    import torch
+    sv, A, full = c4["sv"], c4["A"], c4["full"]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    t0 = time.perf_counter()
+    bad = []
+    blk = 2048
+    for b in range(0, A, blk):
+        rows = np.arange(b, min(A, b + blk))
+        got = full.view(A, A, 2)[b:b + len(rows)].cpu().numpy()
+        olat, orel = c4["orc"].rows_parallel(sv[rows], sv, threads)
+        diff = (bits(got[:, :, 0]) != bits(olat)).any(1) | (bits(got[:, :, 1]) != bits(orel)).any(1)
+        bad += [int(x) for x in rows[diff]]
+        del got, olat, orel
+        print(f"[c4] rows {b}..{b + len(rows)} of {A} compared ({time.perf_counter() - t0:.1f}s, {threads} threads)",
+              flush=True)
+    assert not bad, f"{len(bad)} rows differ, first {bad[:8]}"
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.timeout(600)
 def test_c4_frontier_latencies_all_rows(c4):
     """The frontier SSSP's latencies for all 86,603 rows of C4 against the

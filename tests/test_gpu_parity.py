@@ -367,6 +367,46 @@ def test_path_counters_spill_to_host(api, mode, monkeypatch):
     assert max(int(x.split("PacketCount=")[1].split()[0]) for x in orc.cached_paths_log()) > 3  # spilled
 
 
+@pytest.mark.parametrize("log", ["250000", "-"])
+def test_path_counter_fold_multi_region(log, monkeypatch):
+    """The counter log's fold over several coarse buckets and hundreds of
+    32K-counter regions (A ~ 5,600 slots: 31M counters), three device rounds
+    of 200k packets: every counter against the numpy restatement after each
+    round.  SHD_PCNT_LOG=250000 makes the second and third round fold the
+    logs before them first; "-" folds only at each read."""
+    import torch
+    if log != "-":
+        monkeypatch.setenv("SHD_PCNT_LOG", log)
+    monkeypatch.setenv("SHD_PCNT", "log")
+    gml = synth.sparse_graph_gml(7000, 0x5EED0F11)
+    H = 14_000
+    top = Topology(gml)
+    ips, st, verts = scenario.register_hosts(top, H, seed=1)
+    A = top.slot_count()
+    assert A * A > (1 << 24)  # several coarse buckets (2^22 counters each)
+    top.touch_all()
+    hslot = count_check.slot_map(verts)
+    want = np.zeros((A, A), dtype=np.uint64)
+    n = 200_000
+    for r in range(3):
+        pk = synth.packet_batch(n, H, 0x5EED0F12 + r, 100_000_000, 10_000_000, st)
+        if r == 1:  # a hot pair: many counts on one counter
+            pk["src_host"][:5000], pk["dst_host"][:5000] = 3, 7
+        d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+        d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+        d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+        d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+        d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                           d_status.data_ptr(), d_cnt.data_ptr(), 0)
+        torch.cuda.synchronize()
+        want += count_check.expected_counts(hslot, pk, d_status.cpu().numpy(), A)
+        got = top.path_packet_counts()
+        bad = np.argwhere(got != want)
+        assert len(bad) == 0, f"round {r}: {len(bad)} counters differ, first {bad[:4].tolist()}"
+
+
 def test_deliv_sort_device_against_lexsort(pipeline):
     import torch
     top, _, _, _ = make_pair(synth.complete_graph_gml(5, 3), 5)
@@ -835,6 +875,29 @@ def test_frontier_latencies_equal_table(name):
     d2 = torch.full(((hi - lo) * A,), 7.0, dtype=torch.float64, device="cuda")
     top.latency_rows_frontier(lo, hi, d2.data_ptr())
     assert np.array_equal(bits(d2.cpu().numpy().reshape(hi - lo, A)), bits(lat[lo:hi])), name
+
+
+@pytest.mark.parametrize("wmax", [3348, 3349])
+def test_frontier_largest_edge_latency(wmax):
+    """The frontier kernel's bucket ring lives in LDS: edge latencies up to
+    3,348 ms (every row equal to the table's latencies), one more declines
+    with -ENOTSUP (shdnet.h)."""
+    import torch
+    gml = synth.sparse_graph_gml(300, 0x5EED0F01, max_ms=wmax - 1)
+    gml = gml.replace('latency "1 ms"', f'latency "{wmax} ms"', 1)
+    assert f'"{wmax} ms"' in gml
+    top, orc, _, _ = make_pair(gml, 400)
+    lat, rel, sv = top.table()
+    A = len(sv)
+    d = torch.full((A * A,), 7.0, dtype=torch.float64, device="cuda")
+    if wmax <= 3348:
+        top.latency_rows_frontier(0, A, d.data_ptr())
+        assert np.array_equal(bits(d.cpu().numpy().reshape(A, A)), bits(lat))
+    else:
+        from shadow_amd._lib import ShdError
+        with pytest.raises(ShdError) as ei:
+            top.latency_rows_frontier(0, A, d.data_ptr())
+        assert ei.value.code == -95  # ENOTSUP
 
 
 def test_frontier_needs_whole_ms():
