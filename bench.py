@@ -126,6 +126,23 @@ def request_roofline(requests, seconds, key, what):
             "frac": ach / ceiling if ceiling else None}
 
 
+def attainable(P, delivered, scatter_ms):
+    """The scatter's attainable time: its P random 8-B table gathers at the
+    measured gather ceiling, plus its streamed bytes (record 32 B + status
+    1 B + counter-log key 4 B per packet, the 16-B staged event per delivered
+    packet) at the HBM peak -- the two costs added, as if nothing overlapped
+    them (a floor any overlap only lowers)."""
+    ceiling, src = request_ceiling("gath8_3160MB")
+    if not ceiling:
+        return None
+    g_ms = P / (ceiling * 1e9) * 1e3
+    streamed = (32 + 1 + PCNT_LOG_BYTES) * P + 16.0 * delivered
+    s_ms = streamed / (HBM_PEAK_GBS * 1e9) * 1e3
+    return {"kernel": "k_part_scatter", "gathers": P, "gather_ceiling_G_per_s": ceiling, "gathers_ms": g_ms,
+            "streamed_bytes": streamed, "streamed_ms": s_ms, "ms": g_ms + s_ms, "measured_ms": scatter_ms,
+            "frac": (g_ms + s_ms) / scatter_ms, "source": src}
+
+
 # The C1 kernel (k_sssp_ilds) keeps a row's whole state in LDS; its SQ
 # counters (profiles/r03h_sq_c1: 640 SALU + 492 VALU + 71 LDS instructions
 # per pop, one wave per SIMD, 44 % of wave cycles waiting) put it on the
@@ -411,6 +428,8 @@ def main():
                                                     if pipe_name == "part" else
                                                     "plus one slot atomic and one 16-B slab store per event") + ")")
             if per_launch_ms[0] > 0 else None,
+            "attainable": attainable(P, delivered, per_launch_ms[0]) if pipe_name == "part" and per_launch_ms[0] > 0
+            else None,
             # the whole hand-off at SURVEY.md §8d's 88 B per packet over every stage
             "handoff": {"alg_bytes_per_packet": BYTES_SCATTER_PER_PKT, "ms": sum(per_launch_ms),
                         "achieved": BYTES_SCATTER_PER_PKT * P / (sum(per_launch_ms) * 1e-3) / 1e9,

@@ -2354,9 +2354,9 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* tota
 // (consecutive lanes, consecutive records of a run); else each thread keeps
 // its events in registers and stores them at their run positions itself (LDS
 // holds only the bucket counts: more workgroups per CU).
-// kProbe (SHD_PART_PROBE, measurement only -- outputs deliberately wrong):
-// 1 no table gather, 2 no run-reservation atomics, 3 no stage stores, 4 no
-// host->slot gathers
+// kProbe (SHD_PART_PROBE, measurement only -- outputs deliberately wrong), a
+// bit set: 1 no table gather, 2 no run-reservation atomics, 4 no stage
+// stores, 8 no host->slot gathers
 // kOcc: waves per SIMD the registers are sized for (0: the compiler's
 // choice -- 71 VGPRs, one 1,024-thread workgroup per CU; 8: two per CU, with
 // spills)
@@ -2408,7 +2408,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
         for (int k = 0; k < kB; k++) {
             const bool known = live[k] && p[k].src_host < c.nhosts && p[k].dst_host < c.nhosts;
             uint2 hs = make_uint2(~0u, ~0u), hd = make_uint2(~0u, ~0u);
-            if (known && kProbe == 4) {
+            if (known && (kProbe & 8)) {
                 hs = make_uint2(p[k].src_host % (uint32_t)A, 0u);
                 hd = make_uint2(p[k].dst_host % (uint32_t)A, 1u);
             } else if (known) {
@@ -2439,8 +2439,8 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
         uint2 q[kB];
 #pragma unroll
         for (int k = 0; k < kB; k++) {
-            q[k] = make_uint2(kProbe == 1 ? 1000000u : kPtabFallback, kProbe == 1 ? 0xFFFFFFFFu : 0u);
-            if (kProbe != 1 && ptab && si[k] >= 0 && di[k] >= 0) {
+            q[k] = make_uint2((kProbe & 1) ? 1000000u : kPtabFallback, (kProbe & 1) ? 0xFFFFFFFFu : 0u);
+            if (!(kProbe & 1) && ptab && si[k] >= 0 && di[k] >= 0) {
                 const unsigned long long v =
                     __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ptab) + ei[k]);
                 q[k] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
@@ -2524,7 +2524,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
     } else {
         for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) {
             const uint32_t h = hist[b];
-            if (kProbe == 2) gb[b] = (blockIdx.x * 37u + b) % (g.cap > 64 ? g.cap - 64 : 1u);
+            if ((kProbe & 2)) gb[b] = (blockIdx.x * 37u + b) % (g.cap > 64 ? g.cap - 64 : 1u);
             else gb[b] = h ? atomicAdd(&gcnt[b], h) : 0u;
         }
     }
@@ -2532,7 +2532,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
     auto put = [&](bool valid, const uint4& e, uint32_t li, size_t j) { // (every lane: ballot inside)
         const uint32_t b = valid ? (e.w - g.host_lo) >> g.shift : 0u;
         const bool in = valid && j < g.cap;
-        if (in && kProbe != 3) // runs of a bucket, consecutive records
+        if (in && !(kProbe & 4)) // runs of a bucket, consecutive records
             stage[(size_t)b * g.cap + j] =
                 make_uint4(e.x, e.y, (uint32_t)(base + li) + c.idx_base, (e.z << g.shift) | ((e.w - g.host_lo) & mask));
         const bool full = valid && !in; // the bucket's region is full: whole event to the wide list
@@ -4282,8 +4282,8 @@ struct PartCfg {
 };
 int part_probe() {
     const char* v = getenv("SHD_PART_PROBE");
-    const int k = v ? atoi(v) : 0;
-    return k >= 1 && k <= 4 ? k : 0;
+    const int k = v ? atoi(v) : 0; // (the instantiated bit sets)
+    return k == 1 || k == 2 || k == 4 || k == 8 || k == 6 || k == 5 || k == 7 || k == 15 ? k : 0;
 }
 PartCfg part_cfg(uint32_t nb) {
     const char* v = getenv("SHD_PART_SCATTER");
@@ -4312,8 +4312,12 @@ int part_attr() {
                             {(const void*)k_part_scatter<1024, 8192, false>, 1024, 8192, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 1>, 1024, 4096, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 2>, 1024, 4096, false},
-                            {(const void*)k_part_scatter<1024, 4096, false, 3>, 1024, 4096, false},
-                            {(const void*)k_part_scatter<1024, 4096, false, 4>, 1024, 4096, false}};
+                            {(const void*)k_part_scatter<1024, 4096, false, 4>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 8>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 6>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 5>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 7>, 1024, 4096, false},
+                            {(const void*)k_part_scatter<1024, 4096, false, 15>, 1024, 4096, false}};
     if (int rc = hip_status(hipFuncSetAttribute((const void*)k_wide_group, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                 (int)(4 * kPartMaxBuckets)),
                             "hipFuncSetAttribute k_wide_group"))
@@ -4357,8 +4361,12 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         if (pr && !f.lds && f.wg == 1024) {
             if (pr == 1) SHD_PART_LAUNCH(1024, 4096, false, 1);
             else if (pr == 2) SHD_PART_LAUNCH(1024, 4096, false, 2);
-            else if (pr == 3) SHD_PART_LAUNCH(1024, 4096, false, 3);
-            else SHD_PART_LAUNCH(1024, 4096, false, 4);
+            else if (pr == 4) SHD_PART_LAUNCH(1024, 4096, false, 4);
+            else if (pr == 8) SHD_PART_LAUNCH(1024, 4096, false, 8);
+            else if (pr == 6) SHD_PART_LAUNCH(1024, 4096, false, 6);
+            else if (pr == 5) SHD_PART_LAUNCH(1024, 4096, false, 5);
+            else if (pr == 7) SHD_PART_LAUNCH(1024, 4096, false, 7);
+            else SHD_PART_LAUNCH(1024, 4096, false, 15);
         } else if (f.lds) SHD_PART_LAUNCH(1024, 4096, true);
         else if (f.fn == (const void*)k_part_scatter<1024, 4096, false, 0, 8>) SHD_PART_LAUNCH(1024, 4096, false, 0, 8);
         else if (f.wg == 1024 && f.ch == 8192) SHD_PART_LAUNCH(1024, 8192, false);
