@@ -2582,6 +2582,235 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
     }
 }
 
+// The software-pipelined scatter (SHD_PART_SCATTER=7): the same decisions,
+// runs and outputs as k_part_scatter, but one persistent workgroup per CU
+// walks its chunks with the NEXT chunk's table gathers in flight while the
+// current chunk is decided, reserved and stored.  Why: the measurement-only
+// probes (profiles/r05g_part_scatter_probe_bits.log) show the forms' costs
+// adding up -- floor 0.16 ms + table gather 0.22 ms (its whole ceiling time,
+// 10M gathers at 46.2 G/s) + stage stores 0.08 ms -- i.e. every CU waits for
+// its gathers and then does everything else, so the gathers (the one
+// irreducible random request) overlap nothing.  Here they overlap the
+// decide, the run reservation and the stores of the chunk before.
+//
+// Per iteration (a chunk of ch <= kCH records; chunk = blockIdx.x + it *
+// gridDim.x, every workgroup the same number of chunks):
+//   decide(cur)  -- waits for cur's gathers, issued one iteration earlier;
+//                   status, counter log, LDS ranks, the wide list
+//   load(next)   -- next chunk's records
+//   barrier; run reservation (one atomic per nonempty bucket, results kept
+//                   in registers); gather(next) -- host->slot + table
+//                   gathers issued; the reservations into LDS
+//   barrier; stores of cur's events at their runs
+// Vector memory returns count in issue order: reading the reservation
+// results waits for the record loads (older) but not for next's table
+// gathers (younger), which stay in flight across the barrier and the stores.
+// A workgroup barrier ordering LDS only: __syncthreads()'s workgroup fence
+// also covers global memory and so waits for every outstanding vector memory
+// operation (s_waitcnt vmcnt(0)) -- in-flight table gathers included.  The
+// pipelined scatter shares only LDS across its barriers.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+constexpr uint32_t kPartPipeMaxBuckets = 8192; // (the reservations held in registers: 8 per thread)
+
+template <int kR>
+struct PartFront {
+    ShdPkt p[kR];
+    int si[kR], di[kR];
+    size_t ei[kR];
+    uint2 q[kR];
+    bool live[kR];
+};
+
+// (No divergent branch around a load whose result waits for a later use: a
+// value merged at a branch join is copied there, and the copy waits for the
+// load -- dead lanes load a valid address and are masked afterwards.)
+template <int kWG, int kR>
+__device__ __forceinline__ void part_load(PartFront<kR>& f, const ShdPkt* __restrict__ recs, size_t base,
+                                          uint32_t ch, size_t n) {
+#pragma unroll
+    for (int k = 0; k < kR; k++) {
+        const uint32_t li = (uint32_t)(k * kWG + threadIdx.x);
+        const size_t i = base + li;
+        f.live[k] = li < ch && i < n;
+        f.p[k] = ld_pkt(&recs[f.live[k] ? i : n - 1]); // (n >= 1)
+    }
+}
+
+__device__ unsigned long long g_ptab_none = ((unsigned long long)0u << 32) | kPtabFallback;
+
+template <int kR>
+__device__ __forceinline__ void part_gather(PartFront<kR>& f, const ShdPktCtx& c) {
+    const size_t A = (size_t)c.A;
+    const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
+    uint32_t ts[kR], td[kR];
+#pragma unroll
+    for (int k = 0; k < kR; k++) {
+        const bool known = f.live[k] && f.p[k].src_host < c.nhosts && f.p[k].dst_host < c.nhosts;
+        uint2 hs = host_info[known ? f.p[k].src_host : 0u], hd = host_info[known ? f.p[k].dst_host : 0u];
+        if (!known) hs = hd = make_uint2(~0u, ~0u);
+        f.si[k] = hs.x == ~0u ? -1 : (int)hs.x;
+        f.di[k] = hd.x == ~0u ? -1 : (int)hd.x;
+        ts[k] = hs.y;
+        td[k] = hd.y;
+    }
+#pragma unroll
+    for (int k = 0; k < kR; k++) {
+        int oi = f.si[k], oj = f.di[k];
+        if (oi >= 0 && oj >= 0) {
+            if (c.mode == 0) {
+                if (oi != oj && td[k] < ts[k]) oi = f.di[k], oj = f.si[k]; // owner: row touched first
+            } else if (c.mode == 2) {
+                const size_t b = (size_t)oi * A + (size_t)oj;
+                if (!((c.pair_bits[b >> 5] >> (b & 31)) & 1u)) oi = f.di[k], oj = f.si[k];
+            }
+        }
+        if (oi < c.row_lo || oi >= c.row_hi) f.si[k] = -1; // another rank's row: not decided here
+        f.ei[k] = (size_t)(oi < 0 ? 0 : oi) * A + (size_t)(oj < 0 ? 0 : oj);
+    }
+    // the table gathers, left in flight: read only by the decision (a pair
+    // not decided here, or no ptab, reads the fallback marker)
+    const unsigned long long* __restrict__ pt =
+        c.ptab ? reinterpret_cast<const unsigned long long*>(c.ptab) : &g_ptab_none;
+#pragma unroll
+    for (int k = 0; k < kR; k++) {
+        const bool ok = c.ptab && f.si[k] >= 0 && f.di[k] >= 0;
+        const unsigned long long v = __builtin_nontemporal_load(pt + (ok ? f.ei[k] : 0));
+        f.q[k] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+    }
+}
+
+template <int kWG, int kCH>
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_part_scatter_pipe(
+    ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n, uint64_t barrier, uint64_t end_time, uint64_t boot_end,
+    PartGeo g, uint4* __restrict__ stage, uint32_t* __restrict__ gcnt, uint32_t* __restrict__ wcnt,
+    uint8_t* __restrict__ status, unsigned long long* counters, ShdDeliv* __restrict__ wide,
+    uint32_t* __restrict__ nwide, uint32_t ch, uint32_t nchunks) {
+    constexpr int kR = kCH / kWG;
+    static_assert(kCH % kWG == 0, "chunk");
+    extern __shared__ uint4 part_smem[];
+    uint32_t* hist = reinterpret_cast<uint32_t*>(part_smem); // hist[nb] | gb[nb]
+    uint32_t* gb = hist + g.nb;
+    __shared__ unsigned long long wmin[kWG / 64];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) hist[b] = 0;
+    __syncthreads();
+    const uint32_t smax = g.shift ? (0xFFFFFFFFu >> g.shift) : 0xFFFFFFFFu;
+    const uint32_t mask = (1u << g.shift) - 1u;
+    unsigned long long mn = ~0ull;
+    PartFront<kR> f;
+    uint32_t chunk = blockIdx.x; // (< nchunks: the grid is at most the chunk count)
+    part_load<kWG>(f, recs, (size_t)chunk * ch, ch, n);
+    part_gather(f, c);
+    for (; chunk < nchunks; chunk += gridDim.x) {
+        const size_t base = (size_t)chunk * ch;
+        const uint32_t nxt = chunk + gridDim.x;
+        const size_t nbase = (size_t)(nxt < nchunks ? nxt : chunk) * ch; // (the last: a harmless reload)
+        uint4 rv[kR];                    // {time - tbase, seq, src, dst}, w = ~0: none
+        uint32_t rr[kR];
+#pragma unroll
+        for (int k = 0; k < kR; k++) {
+            const ShdPkt& p = f.p[k];
+            const uint32_t li = (uint32_t)(k * kWG + threadIdx.x);
+            uint8_t st = 0xff; // unregistered host: not delivered
+            uint64_t t = 0;
+            if (f.live[k] && f.si[k] >= 0 && f.di[k] >= 0) {
+                uint32_t rs = p.rng_state;
+                const uint32_t r = (uint32_t)glibc_rand_r(&rs);
+                bool keep;
+                uint64_t delay;
+                if (f.q[k].x != kPtabFallback) {
+                    keep = r <= f.q[k].y; // == (chance <= rel), see kPtabFallback
+                    delay = f.q[k].x;
+                } else {
+                    const ShdEntry e = c.tab[f.ei[k]];
+                    keep = (double)r / 2147483647.0 <= e.rel; // random_nextDouble, worker.c:545
+                    delay = (uint64_t)ceil(e.lat * 1000000.0);
+                }
+                st = SHD_DROPPED_LOSS;
+                if (p.now < boot_end || keep || p.payload_len == 0) {
+                    t = p.now + delay;                    // worker.c:548-549
+                    if (t >= end_time) st = SHD_DROPPED_END; // scheduler.c:236-239
+                    else {
+                        if (p.src_host != p.dst_host && t < barrier) t = barrier; // host_single.c:187-192
+                        st = SHD_DELIVERED;
+                    }
+                    if (c.pcnt) atomicAdd(c.pcnt + f.ei[k], 1u); // (SHD_PCNT=atomic) worker.c:551
+                }
+            }
+            if (f.live[k]) pcnt_log(c, base + li, st == SHD_DELIVERED || st == SHD_DROPPED_END, f.ei[k]);
+            const bool dl = st == SHD_DELIVERED;
+            const uint32_t dr = p.dst_host - g.host_lo;
+            const bool fits = dl && c_fits(t, g.tbase, p.seq) && p.src_host <= smax && dr < g.H;
+            rv[k] = make_uint4(0u, 0u, 0u, ~0u);
+            rr[k] = 0;
+            if (fits) {
+                rr[k] = atomicAdd(&hist[dr >> g.shift], 1u); // LDS
+                rv[k] = make_uint4((uint32_t)(t - g.tbase), (uint32_t)p.seq, p.src_host, p.dst_host);
+            }
+            const uint32_t ws = wave_alloc(dl && !fits, nwide, lane); // (every lane: ballot)
+            if (dl && !fits) {
+                st_ev(&wide[ws], ShdDeliv{t, p.seq, p.src_host, p.dst_host, (uint32_t)(base + li) + c.idx_base, 0u});
+                if (dr < g.H) atomicAdd(&wcnt[dr >> g.shift], 1u);
+            }
+            if (dl && t >= barrier && t < mn) mn = t; // worker.c:350-363
+            if (f.live[k]) status[base + li] = st;
+        }
+        part_load<kWG>(f, recs, nbase, ch, n);
+        lds_barrier(); // the chunk's ranks are all taken
+        // every reservation in flight at once (a loop that stored each result
+        // before the next atomic waited for each round trip in turn)
+        constexpr int kPer = (int)((kPartPipeMaxBuckets + kWG - 1) / kWG);
+        uint32_t res[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t b = threadIdx.x + (uint32_t)k * kWG;
+            const uint32_t h = b < g.nb ? hist[b] : 0u;
+            res[k] = 0u;
+            if (h) res[k] = atomicAdd(&gcnt[b], h);
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t b = threadIdx.x + (uint32_t)k * kWG;
+            if (b < g.nb) gb[b] = res[k], hist[b] = 0; // (hist reused after the next barrier)
+        }
+        part_gather(f, c);
+        lds_barrier(); // the runs' bases are published
+#pragma unroll
+        for (int k = 0; k < kR; k++) {
+            const uint32_t li = (uint32_t)(k * kWG + threadIdx.x);
+            const bool valid = rv[k].w != ~0u;
+            const uint32_t b = valid ? (rv[k].w - g.host_lo) >> g.shift : 0u;
+            const size_t j = valid ? (size_t)gb[b] + rr[k] : 0;
+            const bool in = valid && j < g.cap;
+            if (in)
+                stage[(size_t)b * g.cap + j] = make_uint4(rv[k].x, rv[k].y, (uint32_t)(base + li) + c.idx_base,
+                                                          (rv[k].z << g.shift) | ((rv[k].w - g.host_lo) & mask));
+            const bool full = valid && !in; // the bucket's region is full: whole event to the wide list
+            const uint32_t ws = wave_alloc(full, nwide, lane);
+            if (full) {
+                st_ev(&wide[ws], ShdDeliv{g.tbase + rv[k].x, (unsigned long long)rv[k].y, rv[k].z, rv[k].w,
+                                          (uint32_t)(base + li) + c.idx_base, 0u});
+                atomicAdd(&wcnt[b], 1u);
+            }
+        }
+        // (gb is next written after the next iteration's first barrier, when
+        // every thread has left these stores)
+    }
+    mn = wave_min_u64(mn);
+    if (lane == 0) wmin[threadIdx.x >> 6] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = wmin[0];
+        for (int k = 1; k < kWG / 64; k++) m = wmin[k] < m ? wmin[k] : m;
+        if (m != ~0ull) atomicMin(&counters[1], m);
+    }
+}
+
 // The part round's per-bucket counters (w.cnt1): gcnt[nb] (staged events) |
 // wcnt[nb] (wide events) | wcur[nb] (k_wide_group's cursors) | bpre[nb + 1]
 // (each bucket's output base: the earlier buckets' totals) | wpre[nb] (its
@@ -4279,6 +4508,7 @@ struct PartCfg {
     const void* fn;
     int wg, ch;
     bool lds;
+    int pipe = 0; // k_part_scatter_pipe: persistent workgroups per CU
 };
 int part_probe() {
     const char* v = getenv("SHD_PART_PROBE");
@@ -4295,6 +4525,10 @@ PartCfg part_cfg(uint32_t nb) {
     if (k == 4) return {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false};
     if (k == 5) return {(const void*)k_part_scatter<512, 4096, false>, 512, 4096, false};
     if (k == 6) return {(const void*)k_part_scatter<1024, 8192, false>, 1024, 8192, false};
+    if ((k == 7 || k == 8 || k == 9) && nb > kPartPipeMaxBuckets) k = 1;
+    if (k == 7) return {(const void*)k_part_scatter_pipe<1024, 2048>, 1024, 2048, false, 1};
+    if (k == 8) return {(const void*)k_part_scatter_pipe<512, 1024>, 512, 1024, false, 2};
+    if (k == 9) return {(const void*)k_part_scatter_pipe<256, 512>, 256, 512, false, 3};
     return {(const void*)k_part_scatter<1024, 4096, true>, 1024, 4096, true};
 }
 size_t part_lds(const PartCfg& f, uint32_t nb) {
@@ -4317,7 +4551,10 @@ int part_attr() {
                             {(const void*)k_part_scatter<1024, 4096, false, 6>, 1024, 4096, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 5>, 1024, 4096, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 7>, 1024, 4096, false},
-                            {(const void*)k_part_scatter<1024, 4096, false, 15>, 1024, 4096, false}};
+                            {(const void*)k_part_scatter<1024, 4096, false, 15>, 1024, 4096, false},
+                            {(const void*)k_part_scatter_pipe<1024, 2048>, 1024, 2048, false},
+                            {(const void*)k_part_scatter_pipe<512, 1024>, 512, 1024, false},
+                            {(const void*)k_part_scatter_pipe<256, 512>, 256, 512, false}};
     if (int rc = hip_status(hipFuncSetAttribute((const void*)k_wide_group, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                 (int)(4 * kPartMaxBuckets)),
                             "hipFuncSetAttribute k_wide_group"))
@@ -4348,12 +4585,35 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         // 2,442 x 4,096 on 256 CUs); SHD_PART_EVEN=0: f.ch each
         uint32_t ch = (uint32_t)f.ch;
         const char* ev = getenv("SHD_PART_EVEN");
-        if (!(ev && strcmp(ev, "0") == 0)) {
-            const size_t ncu = (size_t)dev_cus(), waves = (n + ncu * f.ch - 1) / (ncu * f.ch);
+        const size_t ncu = (size_t)dev_cus();
+        if (f.pipe) {
+            // persistent: f.pipe workgroups per CU, each the same number of
+            // chunks of at most f.ch records
+            // (SHD_PART_PIPE_GRID: another workgroup count -- tests walk many
+            // chunks per workgroup on small batches with it)
+            const char* pg = getenv("SHD_PART_PIPE_GRID");
+            const size_t nwg = pg && atoi(pg) > 0 ? (size_t)atoi(pg) : ncu * (size_t)f.pipe,
+                         iters = (n + nwg * f.ch - 1) / (nwg * f.ch);
+            ch = (uint32_t)((n + nwg * iters - 1) / (nwg * iters));
+        } else if (!(ev && strcmp(ev, "0") == 0)) {
+            const size_t waves = (n + ncu * f.ch - 1) / (ncu * f.ch);
             ch = (uint32_t)((n + ncu * waves - 1) / (ncu * waves));
         }
         const dim3 grid((unsigned)((n + ch - 1) / ch)), blk(f.wg);
         const size_t lds = part_lds(f, g.nb);
+        if (f.pipe) {
+            const char* pg = getenv("SHD_PART_PIPE_GRID");
+            const unsigned nch = grid.x,
+                           nwg = pg && atoi(pg) > 0 ? (unsigned)atoi(pg) : (unsigned)ncu * (unsigned)f.pipe,
+                           ng = nch < nwg ? nch : nwg;
+#define SHD_PIPE_LAUNCH(WG, CH)                                                                                       \
+    hipLaunchKernelGGL((k_part_scatter_pipe<WG, CH>), dim3(ng), blk, lds, s, *c, d_recs, n, barrier, end_time,         \
+                       bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters, w.st2, w.nbig + 1, ch, nch)
+            if (f.wg == 1024) SHD_PIPE_LAUNCH(1024, 2048);
+            else if (f.wg == 512) SHD_PIPE_LAUNCH(512, 1024);
+            else SHD_PIPE_LAUNCH(256, 512);
+#undef SHD_PIPE_LAUNCH
+        } else {
 #define SHD_PART_LAUNCH(WG, CH, L, ...)                                                                             \
     hipLaunchKernelGGL((k_part_scatter<WG, CH, L, ##__VA_ARGS__>), grid, blk, lds, s, *c, d_recs, n, barrier, end_time, \
                        bootstrap_end, g, w.pstage, gcnt, wcnt, d_status, counters, w.st2, w.nbig + 1, ch)
@@ -4374,6 +4634,7 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         else if (f.wg == 512 && f.ch == 4096) SHD_PART_LAUNCH(512, 4096, false);
         else if (f.wg == 512) SHD_PART_LAUNCH(512, 2048, false);
         else SHD_PART_LAUNCH(256, 2048, false);
+        }
 #undef SHD_PART_LAUNCH
         // the wide list by bucket (w.tmp: unused by this pipeline), for the
         // second pass to read its buckets' own
