@@ -299,12 +299,23 @@ def main():
         d_final_off = torch.empty(my_hi - my_lo + 1, dtype=torch.int32, device=dev)
         xport.register(d_out, d_recv, d_send)
 
+    # N>1: the exchange's phase times of every timed step (HIP events,
+    # shd_round_exchange_phases: decide, counts, group 1, group 2, merge,
+    # call, transfer beside the decide)
+    xph = {"on": False, "sum": [0.0] * 7, "n": 0}
+    ph_buf, ph_ok = (C.c_double * 7)(), C.c_int()
+
     def step():
         if world > 1 and not split:
             last["nrecv"] = top.process_exchange(xport, d_recs.data_ptr(), P, barrier_t, end_t, 0, own_lo,
                                                  d_send.data_ptr(), d_status.data_ptr(), d_cnt.data_ptr(),
                                                  d_recv.data_ptr(), 2 * P, d_final.data_ptr(),
                                                  d_final_off.data_ptr(), sptr)
+            if xph["on"]:
+                _lib.check(_lib.lib().shd_round_exchange_phases(ph_buf, 7, C.byref(ph_ok)))
+                if ph_ok.value:
+                    xph["sum"] = [a + b for a, b in zip(xph["sum"], ph_buf)]
+                    xph["n"] += 1
             return
         top.process_device(d_recs.data_ptr(), P, barrier_t, end_t, 0, d_out.data_ptr(), d_off.data_ptr(),
                            d_status.data_ptr(), d_cnt.data_ptr(), sptr)
@@ -324,8 +335,10 @@ def main():
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    xph["on"] = True
     for _ in range(args.steps):
         step()
+    xph["on"] = False
     torch.cuda.synchronize(dev)
     # topology_incrementPathPacketCounter of every kept packet (worker.c:551):
     # the rounds logged their packets' pairs; the fold that adds the K
@@ -447,6 +460,21 @@ def main():
             "rounds_per_fold": args.steps,
         },
     }
+
+    if world > 1:
+        names = ["decide", "counts", "group1", "group2", "merge", "call", "transfer_beside_decide"]
+        mine = [v / xph["n"] for v in xph["sum"]] if xph["n"] else None
+        result["exchange_phases"] = {
+            "what": "per timed step, HIP events on the launch and transfer streams "
+                    "(shd_round_exchange_phases): decide = the sender's kernels; counts = the count-matrix "
+                    "all-gather; group1 / group2 = the payload send/recv groups of owners [0, W/2) and "
+                    "[W/2, W) on the transfer stream; merge = the owner merge; call = the whole "
+                    "shd_round_process_exchange; transfer_beside_decide = group 1's start to the end of the "
+                    "sender's kernels (the overlap)",
+            "split": mine is not None,
+            "rank0_ms": dict(zip(names, mine)) if mine else None,
+            "max_over_ranks_ms": dict(zip(names, [max_over_ranks(v) for v in mine])) if mine else None,
+        }
 
     # ------------------------------------------- receive side (§8f-2 / -4)
     if not args.no_nic and world == 1:

@@ -416,7 +416,10 @@ int shd_round_exchange(ShdTopology* top, const ShdTransport* xport, const ShdDel
  * shd_round_exchange's.  d_send: >= 24 * n bytes; d_recv: recv_cap wire
  * records (24 * recv_cap bytes); d_status / d_counters as
  * shd_round_process_device (counters[0]: events this rank decided,
- * counters[1]: its min delivered time).  Needs the slab pipeline (default).
+ * counters[1]: its min delivered time).  On the library's own transports
+ * with two ranks or more the payload goes out in two send/recv groups --
+ * the owners below rank W/2 first, while the sender sorts the rest, then the
+ * others while the first owners merge (shd_round_exchange_phases).
  * Synchronous. */
 int shd_round_process_exchange(ShdTopology* top, const ShdTransport* xport, const ShdPkt* d_recs, size_t n,
                                uint64_t barrier, uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds,
@@ -576,6 +579,14 @@ int shd_round_timing_enable(int enable);
  * (SHD_PACKET_PIPELINE or the default): 0 bucket, 1 rank, 2 slab, 3 part. */
 int shd_round_pipeline_of(uint32_t nhosts, size_t n, int* pipe);
 int shd_round_timing_read(double* stage_ms, int nstages, int* launches);
+/* Phase times (ms, HIP events) of this thread's last shd_round_process_exchange
+ * that sent in two groups (the split exchange: the library's own transports,
+ * two ranks or more, SHD_XCHG_SPLIT != 0): [0] decide (the sender's
+ * kernels), [1] counts (the count-matrix all-gather), [2] group 1 (owners
+ * [0, W/2)), [3] group 2, [4] owner merge, [5] the whole call, [6] the
+ * transfer time that ran beside the sender's kernels.  *valid = 0 when the
+ * last call did not complete a split exchange. */
+int shd_round_exchange_phases(double* ms, int n, int* valid);
 
 /* Unit strings as the GML loader reads them (replace parse_time_nanosec /
  * parse_bandwidth, bindings.h:279,282, core/support/units.rs:777-837):

@@ -11,7 +11,9 @@ transport, 10M packets per rank (senders: the rank's own hosts) over the
 same 100k hosts -- the owner's segments of ~92 N events from N runs of a
 weak-scaled exchange; ms per exchanged round (all N ranks, serialised on the
 one GPU) with SHD_WIRE_SORTED unset (the default rule), 1 and 0, and the
-unions checked equal."""
+unions checked equal; each rank's phase times of its last split exchange
+(shd_round_exchange_phases).  XCHG_PROBE_KNOB=SHD_XCHG_SPLIT=1/0: the split
+exchange against one group after the whole round."""
 import os
 import sys
 import time
@@ -58,6 +60,10 @@ def local_ranks(N):
     xps = InProcessTransports(N, "local")
     nres = [0] * N
     errs = []
+    phases = [None] * N
+    import ctypes as C
+
+    from shadow_amd import _lib
 
     def one(r, k):
         try:
@@ -67,6 +73,12 @@ def local_ranks(N):
                                                    bounds, b["send"].data_ptr(), b["status"].data_ptr(),
                                                    b["cnt"].data_ptr(), b["recv"].data_ptr(), 2 * P,
                                                    b["fin"].data_ptr(), b["fin_off"].data_ptr())
+            # this thread's last split exchange (HIP events): decide, counts,
+            # group 1, group 2, merge, whole call, transfer beside the decide
+            ph = (C.c_double * 7)()
+            ok = C.c_int()
+            _lib.check(_lib.lib().shd_round_exchange_phases(ph, 7, C.byref(ok)))
+            phases[r] = list(ph) if ok.value else None
         except BaseException as e:
             errs.append(e)
 
@@ -103,6 +115,11 @@ def local_ranks(N):
             print(f"N={N} {knob.split('=')[0] if knob else 'SHD_WIRE_SORTED'}={v}: {dt:.3f} ms per exchanged round "
                   "(all ranks on one GPU), "
                   f"{sum(nres)} events", flush=True)
+            for r in range(N):
+                if phases[r]:
+                    p = phases[r]
+                    print(f"  rank {r}: decide {p[0]:.3f} counts {p[1]:.3f} group1 {p[2]:.3f} group2 {p[3]:.3f} "
+                          f"merge {p[4]:.3f} call {p[5]:.3f} transfer beside decide {p[6]:.3f} ms", flush=True)
             outs[v] = union()
         if not knob:
             print("sorted and unsorted wire unions identical:",

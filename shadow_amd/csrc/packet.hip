@@ -2332,6 +2332,7 @@ struct PartGeo {
     uint32_t shift, nb;  // bucket = (dst - host_lo) >> shift
     uint32_t cap;        // stage records per bucket
     unsigned long long tbase;
+    uint32_t b0 = 0;     // the sorts: first bucket of the launch (blockIdx.x + b0)
 };
 
 __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* total, uint32_t* ws) {
@@ -3011,7 +3012,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     __shared__ unsigned long long keys[kWG / 64][kKeyE ? 64 * kKeyE + 8 : 1];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
     const bool brank = kKeyE >= 2 && (lds_keys & 4u);
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = g.b0 + blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t d0 = b << g.shift;
     const uint32_t nd = min(1u << g.shift, g.H - d0);
@@ -3061,7 +3062,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
         }
         if (threadIdx.x == 63) loc[nd] = inc;
     }
-    if (b == gridDim.x - 1 && threadIdx.x == 0) {
+    if (b == g.nb - 1 && threadIdx.x == 0) {
         offsets[g.H] = obase + tot;
         counters[0] = obase + tot; // the round's delivered count
     }
@@ -3280,7 +3281,7 @@ __global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __res
                                                    Wire* __restrict__ wire, unsigned long long* __restrict__ counters,
                                                    uint32_t* __restrict__ fault) {
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = g.b0 + blockIdx.x;
     const uint32_t d0 = b << g.shift;
     const uint32_t nd = min(1u << g.shift, g.H - d0);
     const uint32_t mask = (1u << g.shift) - 1u;
@@ -3326,7 +3327,7 @@ __global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __res
             offsets[d0 + threadIdx.x] = obase + inc - v;
         }
     }
-    if (b == gridDim.x - 1 && threadIdx.x == 0) {
+    if (b == g.nb - 1 && threadIdx.x == 0) {
         offsets[g.H] = obase + tot;
         counters[0] = obase + tot;
     }
@@ -3351,6 +3352,49 @@ __global__ __launch_bounds__(kWG) void k_part_wire(PartGeo g, const uint4* __res
         }
 }
 
+// The split exchange's per-owner cuts straight from the partition, before
+// any bucket is sorted: cuts[r] = the grouped output's offset of host
+// bounds[r] -- the earlier buckets' totals (k_wide_group's bpre) plus the
+// events of bounds[r]'s bucket below it, staged and wide; what the sorts'
+// destination offsets say at that host.  One workgroup per cut.
+struct CutArgs {
+    uint32_t b[65];
+    int W;
+};
+__global__ __launch_bounds__(256) void k_part_cuts(PartGeo g, const uint4* __restrict__ stage,
+                                                   const uint32_t* __restrict__ gcnt, const uint32_t* __restrict__ wcnt,
+                                                   const ShdDeliv* __restrict__ wide, const uint32_t* __restrict__ nwide,
+                                                   uint32_t wide_cap, CutArgs a, uint32_t* __restrict__ cuts) {
+    __shared__ uint32_t ws[4];
+    const uint32_t hb = a.b[blockIdx.x];
+    const uint32_t* bpre = gcnt + 3 * (size_t)g.nb; // (part_cnt_words)
+    if (hb >= g.H) {
+        if (threadIdx.x == 0) cuts[blockIdx.x] = bpre[g.nb];
+        return;
+    }
+    const uint32_t mask = (1u << g.shift) - 1u, b = hb >> g.shift, d = hb & mask;
+    uint32_t c = 0;
+    if (d) {
+        const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b];
+        const uint4* sb = stage + (size_t)b * g.cap;
+        for (uint32_t i = threadIdx.x; i < ns; i += 256) c += (sb[i].w & mask) < d ? 1u : 0u;
+        if (nw && *nwide <= wide_cap) {
+            const ShdDeliv* wb = wide + bpre[g.nb + 1 + b];
+            for (uint32_t i = threadIdx.x; i < nw; i += 256)
+                c += ((wb[i].dst_host - g.host_lo) & mask) < d ? 1u : 0u;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cuts[blockIdx.x] = bpre[b] + ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// cuts[r] = offsets[bounds[r]] (a sender whose offsets are all written)
+__global__ void k_gather_cuts(const uint32_t* __restrict__ offsets, CutArgs a, uint32_t* __restrict__ cuts) {
+    if ((int)threadIdx.x <= a.W) cuts[threadIdx.x] = offsets[a.b[threadIdx.x]];
+}
+
 // the round's fault word when no merge kernel runs: the stage guards only
 __global__ void k_fault_word(const uint32_t* __restrict__ nbig, MergeMeta mm) {
     if (threadIdx.x == 0) {
@@ -3361,6 +3405,7 @@ __global__ void k_fault_word(const uint32_t* __restrict__ nbig, MergeMeta mm) {
 
 // ---- workspace (grow-only, one per topology; see shd_dev_ws_new) ----
 constexpr size_t kXmatWords = 64 * 66; // the exchange's count matrix at the largest world (xchg.hip kMaxWorld)
+constexpr int kXchgEvents = 16;
 struct Ws {
     int device = -1;           // device the buffers live on
     hipEvent_t done = nullptr; // recorded after the last launch that used the buffers
@@ -3398,6 +3443,8 @@ struct Ws {
     size_t cap_xhost = 0;
     uint64_t* xmat = nullptr;  // the exchange's count matrix (kXmatWords u64), device and pinned host
     uint64_t* hxmat = nullptr;
+    hipStream_t xs = nullptr;  // the split exchange's transfer stream (non-blocking) and its events
+    hipEvent_t xev[kXchgEvents] = {};
 };
 
 int hip_status(hipError_t e, const char* what) {
@@ -4048,6 +4095,9 @@ extern "C" void shd_dev_ws_free(void* p) {
     if (w->hxmat) (void)hipHostFree(w->hxmat);
     if (w->done) (void)hipEventDestroy(w->done);
     if (w->fin) (void)hipEventDestroy(w->fin);
+    if (w->xs) (void)hipStreamDestroy(w->xs);
+    for (hipEvent_t e : w->xev)
+        if (e) (void)hipEventDestroy(e);
     delete w;
 }
 
@@ -4466,6 +4516,21 @@ extern "C" int shd_dev_ws_xmat(void* ws, size_t words, uint64_t** d, uint64_t** 
     }
     *d = w.xmat;
     *h = w.hxmat;
+    return 0;
+}
+
+extern "C" int shd_dev_ws_xchg_sync_objs(void* ws, void** xfer_stream, void** events, int nevents) {
+    if (!ws) return shd_fail(-ENOMEM, "no round workspace");
+    Ws& w = *static_cast<Ws*>(ws);
+    if (nevents > kXchgEvents) return shd_fail(-EINVAL, "%d exchange events > %d", nevents, kXchgEvents);
+    int rc = 0;
+    if (!w.xs && (rc = hip_status(hipStreamCreateWithFlags(&w.xs, hipStreamNonBlocking), "hipStreamCreate exchange")))
+        return rc;
+    for (int k = 0; k < nevents; k++) {
+        if (!w.xev[k] && (rc = hip_status(hipEventCreate(&w.xev[k]), "hipEventCreate exchange"))) return rc;
+        events[k] = w.xev[k];
+    }
+    *xfer_stream = w.xs;
     return 0;
 }
 
@@ -4919,6 +4984,54 @@ extern "C" int shd_dev_deliv_merge_runs(void* ws, const void* d_in, int wire, in
                                          host_hi, d_out, d_dst_offsets, stream);
 }
 
+// The part sender's bucket sorts for buckets [b_lo, b_hi): sort_wire -- every
+// destination's run goes out sorted (the part sort writing wire records;
+// listed segments sorted later by the listed kernels, grouped_finish), so
+// the owners merge sorted runs; else unsorted runs (k_part_wire), the owners
+// sort their union.
+int grouped_sorts(Ws& w, PartGeo pg, void* d_wire, uint32_t* d_off, unsigned long long* counters, hipStream_t s,
+                  bool wsorted, uint32_t b_lo, uint32_t b_hi) {
+    if (b_hi <= b_lo) return 0;
+    pg.b0 = b_lo;
+    const dim3 grid(b_hi - b_lo);
+    if (wsorted) {
+        ShdDeliv* wout = static_cast<ShdDeliv*>(d_wire); // (a Wire array: kWire)
+        const int sc = part_sort_cfg();
+#define SHD_WIRE_SORT_LAUNCH(WG, CAP, KE, ...)                                                                        \
+    hipLaunchKernelGGL((k_part_sort<WG, CAP, KE, true, ##__VA_ARGS__>), grid, dim3(WG), 0, s, pg, w.pstage, w.cnt1,   \
+                       w.cnt1 + pg.nb, w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_off, wout, w.st1, w.big, w.nbig, counters, \
+                       part_sort_flags())
+        if (sc == 0) SHD_WIRE_SORT_LAUNCH(1024, 7168, 4);
+        else if (sc == 1) SHD_WIRE_SORT_LAUNCH(512, 3584, 4);
+        else if (sc == 2) SHD_WIRE_SORT_LAUNCH(256, 1792, 4);
+        else SHD_WIRE_SORT_LAUNCH(512, 2304, 2, 6);
+#undef SHD_WIRE_SORT_LAUNCH
+        return hip_status(hipGetLastError(), "k_part_sort (wire) launch");
+    }
+    hipLaunchKernelGGL((k_part_wire<512, 5>), grid, dim3(512), 0, s, pg, w.pstage, w.cnt1, w.cnt1 + pg.nb, w.tmp,
+                       w.nbig + 1, (uint32_t)w.cap_n, d_off, static_cast<Wire*>(d_wire), counters, w.nbig + 2);
+    return hip_status(hipGetLastError(), "k_part_wire launch");
+}
+
+// ... and what follows the sorts: the listed segments (sorted into w.st2 --
+// the wide list's first copy, free by then -- and converted to wire records)
+// and the round's fault word.  (ws_end is the caller's.)
+int grouped_finish(Ws& w, const PartGeo& pg, void* d_wire, uint32_t* d_off, unsigned long long* counters,
+                   hipStream_t s, bool wsorted) {
+    int rc;
+    if (wsorted) {
+        if ((rc = sort_listed(w, w.st1, d_off, w.st2, s, counters))) return rc;
+        hipLaunchKernelGGL(k_listed_wire, dim3(1024), dim3(256), 0, s, w.st2, d_off, w.big, w.nbig,
+                           merge_meta(w, counters).cap_big, static_cast<Wire*>(d_wire));
+        if ((rc = hip_status(hipGetLastError(), "k_listed_wire launch"))) return rc;
+    }
+    mark(4, s);
+    if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
+    if ((rc = dbg_sync(s, "grouped part round"))) return rc;
+    hipLaunchKernelGGL(k_fault_word, dim3(1), dim3(64), 0, s, w.nbig, merge_meta(w, counters));
+    return copy_faults(w, s);
+}
+
 // The sender's side of shd_round_process_exchange: the slab round up to the
 // per-destination offsets (d_off, H + 1), then the grouped, unsorted wire
 // records (k_group_wire) instead of the segment sort.  Slab pipeline only.
@@ -4943,42 +5056,11 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
             (rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, pg, d_status, counters, s)))
             return rc;
         mark_same(3, 2);
-        // sort_wire: every destination's run goes out sorted (the part sort
-        // writing wire records; listed segments sorted by the listed kernels
-        // into w.st2 -- the wide list's first copy, free by then -- and
-        // converted), so the owners merge sorted runs; else unsorted runs
-        // (k_part_wire), the owners sort their union
         const bool wsorted = sort_wire != 0;
-        if (wsorted) {
-            ShdDeliv* wout = static_cast<ShdDeliv*>(d_wire); // (a Wire array: kWire)
-            const int sc = part_sort_cfg();
-#define SHD_WIRE_SORT_LAUNCH(WG, CAP, KE, ...)                                                                        \
-    hipLaunchKernelGGL((k_part_sort<WG, CAP, KE, true, ##__VA_ARGS__>), dim3(pg.nb), dim3(WG), 0, s, pg, w.pstage, w.cnt1,            \
-                       w.cnt1 + pg.nb, w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_off, wout, w.st1, w.big, w.nbig, counters, \
-                       part_sort_flags())
-            if (sc == 0) SHD_WIRE_SORT_LAUNCH(1024, 7168, 4);
-            else if (sc == 1) SHD_WIRE_SORT_LAUNCH(512, 3584, 4);
-            else if (sc == 2) SHD_WIRE_SORT_LAUNCH(256, 1792, 4);
-            else SHD_WIRE_SORT_LAUNCH(512, 2304, 2, 6);
-#undef SHD_WIRE_SORT_LAUNCH
-            if ((rc = hip_status(hipGetLastError(), "k_part_sort (wire) launch")) ||
-                (rc = sort_listed(w, w.st1, d_off, w.st2, s, counters)))
-                return rc;
-            hipLaunchKernelGGL(k_listed_wire, dim3(1024), dim3(256), 0, s, w.st2, d_off, w.big, w.nbig,
-                               merge_meta(w, counters).cap_big, static_cast<Wire*>(d_wire));
-            if ((rc = hip_status(hipGetLastError(), "k_listed_wire launch"))) return rc;
-        } else {
-            hipLaunchKernelGGL((k_part_wire<512, 5>), dim3(pg.nb), dim3(512), 0, s, pg, w.pstage, w.cnt1,
-                               w.cnt1 + pg.nb, w.tmp, w.nbig + 1, (uint32_t)w.cap_n, d_off, static_cast<Wire*>(d_wire),
-                               counters, w.nbig + 2);
-            if ((rc = hip_status(hipGetLastError(), "k_part_wire launch"))) return rc;
-        }
+        if ((rc = grouped_sorts(w, pg, d_wire, d_off, counters, s, wsorted, 0, pg.nb)) ||
+            (rc = grouped_finish(w, pg, d_wire, d_off, counters, s, wsorted)))
+            return rc;
         if (sorted_out) *sorted_out = wsorted ? 1 : 0;
-        mark(4, s);
-        if (g_tm.on && g_tm.n < kMaxTimed) g_tm.n++;
-        if ((rc = dbg_sync(s, "grouped part round"))) return rc;
-        hipLaunchKernelGGL(k_fault_word, dim3(1), dim3(64), 0, s, w.nbig, merge_meta(w, counters));
-        if ((rc = copy_faults(w, s))) return rc;
         return ws_end(w, s);
     }
     const int pipe = pipeline_for(H, true);
@@ -5016,5 +5098,63 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
     // reads back (no merge kernel runs on the sender's side)
     hipLaunchKernelGGL(k_fault_word, dim3(1), dim3(64), 0, s, w.nbig, merge_meta(w, counters));
     if ((rc = copy_faults(w, s))) return rc;
+    return ws_end(w, s);
+}
+
+// shd_dev_packet_round_grouped in two halves (see ShdSplitHooks): the cuts
+// from the partition, the front hook, the buckets of the owners below
+// bounds[half] (through the bucket holding bounds[half]: the cut there is
+// then written by this half too), the listed-segment count so far, the mid
+// hook, the other buckets and the listed segments.
+extern "C" int shd_dev_packet_round_grouped_split(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n,
+                                                  uint64_t barrier, uint64_t end_time, uint64_t bootstrap_end,
+                                                  void* d_wire, uint32_t* d_off, uint8_t* d_status,
+                                                  uint64_t* d_counters, void* stream, int sort_wire,
+                                                  const uint32_t* bounds, int W, int half, uint32_t* d_cuts,
+                                                  uint32_t* d_listed_a, const ShdSplitHooks* hooks) {
+    hipStream_t s = (hipStream_t)stream;
+    if (!c->ws) return shd_fail(-ENOMEM, "no round workspace");
+    if (W < 1 || W > 64 || half < 0 || half > W) return shd_fail(-EINVAL, "bad split");
+    Ws& w = *static_cast<Ws*>(c->ws);
+    const uint32_t H = c->nhosts;
+    const unsigned long long tb = barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull;
+    CutArgs ca;
+    ca.W = W;
+    for (int r = 0; r <= W; r++) ca.b[r] = bounds[r];
+    int rc;
+    PartGeo pg;
+    if (!(pipeline_for(H, true, true) == kPartPipe && part_geometry(0, H, n, tb, &pg))) {
+        // the slab sender: the whole round, then its cuts and both hooks
+        int sorted = 0;
+        if ((rc = shd_dev_packet_round_grouped(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire, d_off, d_status,
+                                               d_counters, stream, sort_wire, &sorted)))
+            return rc;
+        hipLaunchKernelGGL(k_gather_cuts, dim3(1), dim3(128), 0, s, d_off, ca, d_cuts);
+        if ((rc = hip_status(hipGetLastError(), "cuts launch")) ||
+            (rc = hip_status(hipMemsetAsync(d_listed_a, 0, 4, s), "memset listed")) ||
+            (rc = hooks->front(hooks->user, d_cuts, sorted)))
+            return rc;
+        return hooks->mid(hooks->user);
+    }
+    unsigned long long* counters = (unsigned long long*)d_counters;
+    if ((rc = part_attr()) || (rc = ws_begin(w, s)) || (rc = ws_reserve(w, n, part_cnt_words(pg.nb), H)) ||
+        (rc = pstage_reserve(w, (size_t)pg.nb * pg.cap)) ||
+        (rc = part_front(w, c, d_recs, n, barrier, end_time, bootstrap_end, pg, d_status, counters, s)))
+        return rc;
+    mark_same(3, 2);
+    const bool wsorted = sort_wire != 0;
+    hipLaunchKernelGGL(k_part_cuts, dim3(W + 1), dim3(256), 0, s, pg, w.pstage, w.cnt1, w.cnt1 + pg.nb, w.tmp,
+                       w.nbig + 1, (uint32_t)w.cap_n, ca, d_cuts);
+    if ((rc = hip_status(hipGetLastError(), "k_part_cuts launch")) ||
+        (rc = hooks->front(hooks->user, d_cuts, wsorted ? 1 : 0)))
+        return rc;
+    const uint32_t hb = bounds[half];
+    const uint32_t b_a = hb >= H ? pg.nb : ((hb >> pg.shift) + 1 < pg.nb ? (hb >> pg.shift) + 1 : pg.nb);
+    if ((rc = grouped_sorts(w, pg, d_wire, d_off, counters, s, wsorted, 0, b_a)) ||
+        (rc = hip_status(hipMemcpyAsync(d_listed_a, w.nbig, 4, hipMemcpyDeviceToDevice, s), "listed count")) ||
+        (rc = hooks->mid(hooks->user)) ||
+        (rc = grouped_sorts(w, pg, d_wire, d_off, counters, s, wsorted, b_a, pg.nb)) ||
+        (rc = grouped_finish(w, pg, d_wire, d_off, counters, s, wsorted)))
+        return rc;
     return ws_end(w, s);
 }

@@ -241,6 +241,29 @@ int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_recs, size_
                                  uint64_t end_time, uint64_t bootstrap_end, void* d_wire, uint32_t* d_off,
                                  uint8_t* d_status, uint64_t* d_counters, void* stream, int sort_wire,
                                  int* sorted_out);
+/* The same sender round in two halves for an exchange that sends in two
+ * groups (xchg.hip): the per-owner cuts of the grouped output (d_cuts,
+ * W + 1 words) come from the partition before any bucket is sorted and
+ * front(user, d_cuts, sorted) is called (the exchange's count matrix goes
+ * out on the stream behind them); then the buckets of the owners below
+ * bounds[half] are sorted, the listed-segment count so far is copied to
+ * d_listed_a and mid(user) is called (the exchange's host read-back);
+ * then the rest.  With no part geometry (the slab pipeline) the whole round
+ * runs first and both hooks follow it.  A hook's nonzero return stops
+ * the round and is returned. */
+typedef struct {
+    int (*front)(void* user, const uint32_t* d_cuts, int sorted);
+    int (*mid)(void* user);
+    void* user;
+} ShdSplitHooks;
+int shd_dev_packet_round_grouped_split(const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                                       uint64_t end_time, uint64_t bootstrap_end, void* d_wire, uint32_t* d_off,
+                                       uint8_t* d_status, uint64_t* d_counters, void* stream, int sort_wire,
+                                       const uint32_t* bounds, int W, int half, uint32_t* d_cuts,
+                                       uint32_t* d_listed_a, const ShdSplitHooks* hooks);
+/* streams and events of the split exchange (created on first use, kept
+ * with the workspace): the transfer stream and four events */
+int shd_dev_ws_xchg_sync_objs(void* ws, void** xfer_stream, void** events, int nevents);
 /* decide + group + exchange + merge in one call (shd_round_process_exchange) */
 int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n, uint64_t barrier,
                            uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds, void* d_wire_send,

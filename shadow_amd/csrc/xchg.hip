@@ -146,6 +146,15 @@ __global__ void k_count_row(const uint32_t* __restrict__ offsets, RouteArgs ra, 
     if (r == 0) row[W] = cap, row[W + 1] = sorted ? 2ull : 0ull;
 }
 
+// the same row from cuts computed by the sender (the split exchange's
+// shd_dev_packet_round_grouped_split)
+__global__ void k_count_row_cuts(const uint32_t* __restrict__ cuts, int W, uint64_t* __restrict__ row, uint64_t cap,
+                                 int failed, int sorted) {
+    const int r = threadIdx.x;
+    if (r < W) row[r] = failed ? 0ull : (uint64_t)(cuts[r + 1] - cuts[r]);
+    if (r == 0) row[W] = cap, row[W + 1] = failed ? 1ull : sorted ? 2ull : 0ull;
+}
+
 int make_args(const uint32_t* bounds, int world, RouteArgs* ra) {
     if (world < 1 || world > kMaxWorld) return shd_fail(-EINVAL, "world %d outside 1..%d", world, kMaxWorld);
     ra->world = world;
@@ -204,11 +213,13 @@ int exchange_blocks(const ShdTransport* x, const void* d_send, const uint64_t* s
 // Peer r's slice of this rank's destination offsets, rebased to its block:
 // out[lo_r + r + j] = off[lo_r + j] - off[lo_r], j = 0 .. H_r (the slices of
 // all peers back to back: sum of (H_r + 1) = H + W entries).
+// (r0, r1: only the slices of owners [r0, r1) -- the split exchange's groups)
 __global__ __launch_bounds__(256) void k_offset_slices(const uint32_t* __restrict__ off, RouteArgs ra,
-                                                       uint32_t* __restrict__ out) {
-    const uint32_t total = ra.bounds[ra.world] + (uint32_t)ra.world;
-    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
-        int r = 0;
+                                                       uint32_t* __restrict__ out, int r0 = 0, int r1 = -1) {
+    if (r1 < 0) r1 = ra.world;
+    const uint32_t first = ra.bounds[r0] + (uint32_t)r0, total = ra.bounds[r1] + (uint32_t)r1;
+    for (uint32_t p = first + blockIdx.x * blockDim.x + threadIdx.x; p < total; p += gridDim.x * blockDim.x) {
+        int r = r0;
         while (r + 1 < ra.world && p >= ra.bounds[r + 1] + (uint32_t)(r + 1)) r++;
         const uint32_t lo = ra.bounds[r], j = p - lo - (uint32_t)r;
         out[p] = off[lo + j] - off[lo];
@@ -289,7 +300,7 @@ int rccl_alltoallv(void* user, const void* d_send, const uint64_t* send_bytes, v
 // RCCL launch per round instead of two back to back on the stream.
 int rccl_alltoallv2(void* user, const void* d_send, const uint64_t* send_bytes, const uint64_t* send_off,
                     void* d_recv, const uint64_t* recv_bytes, const void* d_send2, const uint64_t* send2_bytes,
-                    void* d_recv2, const uint64_t* recv2_bytes, void* stream) {
+                    void* d_recv2, const uint64_t* recv2_bytes, void* stream, const uint64_t* send2_off = nullptr) {
     Rccl* t = static_cast<Rccl*>(user);
     const int W = t->x.world;
     hipStream_t s = (hipStream_t)stream;
@@ -303,7 +314,8 @@ int rccl_alltoallv2(void* user, const void* d_send, const uint64_t* send_bytes, 
         if (!rc && recv_bytes[r])
             rc = nccl_status(ncclRecv((char*)d_recv + ro, recv_bytes[r], ncclChar, r, t->comm, s), "ncclRecv");
         if (!rc && send2_bytes[r])
-            rc = nccl_status(ncclSend((const char*)d_send2 + so2, send2_bytes[r], ncclChar, r, t->comm, s),
+            rc = nccl_status(ncclSend((const char*)d_send2 + (send2_off ? send2_off[r] : so2), send2_bytes[r],
+                                      ncclChar, r, t->comm, s),
                              "ncclSend");
         if (!rc && recv2_bytes[r])
             rc = nccl_status(ncclRecv((char*)d_recv2 + ro2, recv2_bytes[r], ncclChar, r, t->comm, s), "ncclRecv");
@@ -589,7 +601,263 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
     return 0;
 }
 
+// ---- the split exchange (shd_round_process_exchange on the library's own
+// transports, SHD_XCHG_SPLIT != 0) ----
+//
+// The owners are split in two halves, A = ranks [0, W/2) and B = [W/2, W),
+// and the payload goes out in two send/recv groups on a transfer stream of
+// its own: A's blocks as soon as the sender has sorted A's buckets, while it
+// sorts B's; B's blocks after that, while the A owners merge.  The count
+// matrix does not wait for any sort: the per-owner cuts come straight from
+// the partition (k_part_cuts), so the matrix all-gather and the host's read
+// of it run beside the first half's sort.  Per rank and round (stream s =
+// the caller's, x = the transfer stream):
+//   s: scatter | cuts | count row | matrix all-gather | sort A | read-back (E)
+//      | sort B, listed | (B) ............ | merge (own half's group) | wait G2
+//   x:                  wait E (B if A had listed segments) | slices A,
+//      group 1 (G1) | wait B | slices B, group 2 (G2)
+// Phase times of the last split round of this thread, from HIP events
+// (shd_round_exchange_phases): decide (the sender's kernels), counts (the
+// matrix all-gather), group 1, group 2, merge, whole call, and the time the
+// transfers ran beside the sender's sort (group 1's start to the end of
+// the sender's kernels).
+constexpr int kPhases = 7;
+thread_local double t_phase[kPhases];
+thread_local int t_phase_valid = 0;
+
+enum { kEvE, kEvB, kEvG1, kEvG2, kEv0, kEvFront, kEvCounts, kEvG1s, kEvG2s, kEvMs, kEvMe, kEvEnd, kEvCount };
+
+struct SplitCtx {
+    const ShdTransport* x;
+    hipStream_t s;
+    int W, me;
+    uint64_t *d_mat, *h_mat;
+    uint32_t *d_cuts, *h_cuts, *d_listed, *h_listed;
+    uint64_t recv_cap;
+    hipEvent_t* ev;
+    bool front_done, mid_done;
+};
+
+int split_front(void* u, const uint32_t* d_cuts, int sorted) {
+    SplitCtx* k = static_cast<SplitCtx*>(u);
+    const size_t rw = (size_t)k->W + 2;
+    (void)hipEventRecord(k->ev[kEvFront], k->s);
+    hipLaunchKernelGGL(k_count_row_cuts, dim3(1), dim3(kMaxWorld + 1), 0, k->s, d_cuts, k->W,
+                       k->d_mat + (size_t)k->me * rw, k->recv_cap, d_cuts ? 0 : 1, sorted);
+    std::vector<uint64_t> moff(k->W + 1);
+    for (int r = 0; r <= k->W; r++) moff[r] = 8ull * rw * (uint64_t)r;
+    int rc = hip_status(hipGetLastError(), "count row launch");
+    if (!rc) rc = k->x->allgatherv(k->x->user, k->d_mat, moff.data(), (void*)k->s);
+    k->front_done = true; // (the collective was entered)
+    (void)hipEventRecord(k->ev[kEvCounts], k->s);
+    return rc ? (rc < 0 ? rc : -EIO) : 0;
+}
+
+int split_mid(void* u) {
+    SplitCtx* k = static_cast<SplitCtx*>(u);
+    k->mid_done = true;
+    const size_t rw = (size_t)k->W + 2;
+    int rc;
+    if ((rc = hip_status(hipMemcpyAsync(k->h_mat, k->d_mat, 8 * rw * (size_t)k->W, hipMemcpyDeviceToHost, k->s),
+                         "counts D2H")) ||
+        (rc = hip_status(hipMemcpyAsync(k->h_cuts, k->d_cuts, 4 * (size_t)(k->W + 1), hipMemcpyDeviceToHost, k->s),
+                         "cuts D2H")) ||
+        (rc = hip_status(hipMemcpyAsync(k->h_listed, k->d_listed, 4, hipMemcpyDeviceToHost, k->s), "listed D2H")))
+        return rc;
+    return hip_status(hipEventRecord(k->ev[kEvE], k->s), "event E");
+}
+
+// one group: this rank's blocks for owners [r0, r1) and, when it is one of
+// them, its receives (every peer's block and offset slice)
+int split_group(const ShdTransport* x, int r0, int r1, int me, const void* d_events, const uint64_t* sbytes,
+                const uint64_t* soff, void* d_recv, const uint64_t* rbytes, const uint32_t* d_sl,
+                const uint64_t* sl_bytes, const uint64_t* sl_off, uint32_t* d_ro, const uint64_t* ro_bytes,
+                hipStream_t xs) {
+    const int W = x->world;
+    const bool mine = me >= r0 && me < r1;
+    std::vector<uint64_t> sb(W, 0), rb(W, 0), s2(W, 0), r2(W, 0);
+    for (int r = r0; r < r1; r++) sb[r] = sbytes[r], s2[r] = sl_bytes[r];
+    if (mine)
+        for (int r = 0; r < W; r++) rb[r] = rbytes[r], r2[r] = ro_bytes[r];
+    int rc;
+    if (x->allgatherv == rccl_allgatherv)
+        rc = rccl_alltoallv2(x->user, d_events, sb.data(), soff, d_recv, rb.data(), d_sl, s2.data(), d_ro, r2.data(),
+                             (void*)xs, sl_off);
+    else if (!(rc = local_alltoallv_off(x->user, d_events, sb.data(), soff, d_recv, rb.data(), (void*)xs)))
+        rc = local_alltoallv_off(x->user, d_sl, s2.data(), sl_off, d_ro, r2.data(), (void*)xs);
+    return rc ? (rc < 0 ? rc : -EIO) : 0;
+}
+
+float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : -1.f;
+}
+
+int exchange_split(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_recs, size_t n, uint64_t barrier,
+                   uint64_t end_time, uint64_t bootstrap_end, const uint32_t* host_bounds, void* d_wire_send,
+                   uint8_t* d_status, uint64_t* d_counters, void* d_wire_recv, size_t recv_cap, ShdDeliv* d_out,
+                   uint32_t* d_out_offsets, size_t* n_out, hipStream_t s, int sort_wire) {
+    const int W = x->world, me = x->rank, half = W / 2;
+    const uint32_t H = c->nhosts, lo = host_bounds[me], hi = host_bounds[me + 1], Hm = hi - lo;
+    constexpr size_t elem = 24; // the wire record
+    t_phase_valid = 0;
+    RouteArgs ra;
+    int rc = make_args(host_bounds, W, &ra);
+    if (rc) return rc;
+    // scratch: device [d_off H+1 | cuts | slices H+W | received slices W(Hm+1) | bases W+1 | listed]
+    //          host   [cuts | bases | listed]
+    const size_t dwords = ((size_t)H + 1) + xchg_scratch_words(H, W, Hm) + 1;
+    void *dscr = nullptr, *hscr = nullptr, *xsv = nullptr;
+    void* evv[kEvCount] = {};
+    int local_rc = shd_dev_ws_scratch(c->ws, 4 * dwords, 4 * (2 * kMaxWorld + 4), &dscr, &hscr);
+    if (!local_rc) local_rc = shd_dev_ws_xchg_sync_objs(c->ws, &xsv, evv, kEvCount);
+    uint64_t *d_mat = nullptr, *h_mat = nullptr;
+    std::vector<uint64_t> h_fallback;
+    const int xrc = shd_dev_ws_xmat(c->ws, (size_t)W * (W + 2), &d_mat, &h_mat);
+    if (xrc) { // (still joins the matrix all-gather, with the static fallback: see exchange_runs_core)
+        if (!local_rc) local_rc = xrc;
+        if ((rc = hip_status(hipGetSymbolAddress((void**)&d_mat, HIP_SYMBOL(g_xmat_fallback)), "fallback count matrix")))
+            return rc;
+        h_fallback.assign((size_t)W * (W + 2), 0);
+        h_mat = h_fallback.data();
+    }
+    if (!local_rc) { // SHD_DEBUG_FAIL_RANK=r: rank r fails before the exchange (test of the agreement)
+        const char* f = getenv("SHD_DEBUG_FAIL_RANK");
+        if (f && atoi(f) == me) local_rc = shd_fail(-EIO, "debug: injected failure of rank %d", me);
+    }
+    hipEvent_t* ev = reinterpret_cast<hipEvent_t*>(evv);
+    const hipStream_t xs = static_cast<hipStream_t>(xsv);
+    uint32_t* d_off = static_cast<uint32_t*>(dscr);
+    uint32_t* d_cuts = d_off ? d_off + (H + 1) : nullptr;
+    uint32_t* d_sl = d_cuts ? d_cuts + (kMaxWorld + 1) : nullptr;
+    uint32_t* d_ro = d_sl ? d_sl + ((size_t)H + W) : nullptr;
+    uint32_t* d_bb = d_ro ? d_ro + (size_t)W * (Hm + 1) : nullptr;
+    uint32_t* d_listed = d_bb ? d_bb + (W + 1) : nullptr;
+    uint32_t* h_cuts = static_cast<uint32_t*>(hscr);
+    uint32_t* h_bb = h_cuts ? h_cuts + (kMaxWorld + 1) : nullptr;
+    uint32_t* h_listed = h_bb ? h_bb + (kMaxWorld + 1) : nullptr;
+    SplitCtx k{x, s, W, me, d_mat, h_mat, d_cuts, h_cuts, d_listed, h_listed, (uint64_t)recv_cap, ev, false, false};
+    const ShdSplitHooks hooks{split_front, split_mid, &k};
+    if (!local_rc) {
+        (void)hipEventRecord(ev[kEv0], s);
+        local_rc = shd_dev_packet_round_grouped_split(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire_send, d_off,
+                                                      d_status, d_counters, (void*)s, sort_wire, host_bounds, W, half,
+                                                      d_cuts, d_listed, &hooks);
+    }
+    if (!k.front_done) { // failed before the matrix went out: tell every peer through it
+        std::vector<uint64_t> moff(W + 1);
+        const size_t rw = (size_t)W + 2;
+        for (int r = 0; r <= W; r++) moff[r] = 8ull * rw * (uint64_t)r;
+        hipLaunchKernelGGL(k_count_row_cuts, dim3(1), dim3(kMaxWorld + 1), 0, s, nullptr, W, d_mat + (size_t)me * rw,
+                           (uint64_t)recv_cap, 1, 0);
+        int rc2 = hip_status(hipGetLastError(), "count row launch");
+        if (!rc2) rc2 = x->allgatherv(x->user, d_mat, moff.data(), (void*)s);
+        if (!rc2) rc2 = hip_status(hipStreamSynchronize(s), "counts sync");
+        return local_rc ? local_rc : rc2;
+    }
+    // (the matrix went out saying this rank is fine: a later failure still
+    // takes part in both groups below, then reports)
+    if (!k.mid_done && (rc = split_mid(&k))) return rc;
+    (void)hipEventRecord(ev[kEvB], s);
+    if ((rc = hip_status(hipEventSynchronize(ev[kEvE]), "exchange counts"))) return rc;
+    const size_t rw = (size_t)W + 2;
+    int all_sorted = 1;
+    for (int r = 0; r < W; r++) {
+        if (h_mat[(size_t)r * rw + W + 1] & 1ull) {
+            (void)hipStreamSynchronize(s);
+            return local_rc ? local_rc : shd_fail(-EIO, "rank %d failed before the exchange", r);
+        }
+        if (!(h_mat[(size_t)r * rw + W + 1] & 2ull)) all_sorted = 0;
+    }
+    bool over = false;
+    for (int t = 0; t < W; t++) {
+        uint64_t tot = 0;
+        for (int r = 0; r < W; r++) tot += h_mat[(size_t)r * rw + t];
+        if (tot > h_mat[(size_t)t * rw + W]) over = true;
+    }
+    if (over) {
+        (void)hipStreamSynchronize(s);
+        return shd_fail(-ENOSPC, "a receive capacity is too small for this exchange");
+    }
+    std::vector<uint64_t> sbytes(W), rbytes(W), recv(W), soff(W), slb(W), sloff(W), rob(W);
+    uint64_t nrecv = 0;
+    for (int r = 0; r < W; r++) {
+        sbytes[r] = r == me ? 0 : h_mat[(size_t)me * rw + r] * elem;
+        recv[r] = h_mat[(size_t)r * rw + me];
+        rbytes[r] = r == me ? 0 : recv[r] * elem;
+        nrecv += recv[r];
+        soff[r] = (uint64_t)h_cuts[r] * elem; // (own block skipped: merged in place)
+        slb[r] = 4ull * (host_bounds[r + 1] - host_bounds[r] + 1);
+        sloff[r] = 4ull * (host_bounds[r] + (uint64_t)r);
+        rob[r] = 4ull * (Hm + 1);
+    }
+    h_bb[0] = 0;
+    for (int r = 0; r < W; r++) h_bb[r + 1] = h_bb[r] + (r == me ? 0u : (uint32_t)recv[r]);
+    const uint32_t listed_a = *h_listed;
+    const void* self_block = static_cast<const char*>(d_wire_send) + (size_t)h_cuts[me] * elem;
+    auto merge = [&]() {
+        int m;
+        (void)hipEventRecord(ev[kEvMs], s);
+        if ((m = hip_status(hipMemcpyAsync(d_bb, h_bb, 4 * (size_t)(W + 1), hipMemcpyHostToDevice, s), "bases H2D")) ||
+            (m = shd_dev_deliv_merge_runs_self(c->ws, d_wire_recv, self_block, (uint32_t)me, 1, all_sorted, nrecv, d_ro,
+                                               d_bb, (uint32_t)W, lo, hi, d_out, d_out_offsets, s)))
+            return m;
+        return hip_status(hipEventRecord(ev[kEvMe], s), "merge event");
+    };
+    auto slices = [&](int r0, int r1) {
+        const uint32_t m = host_bounds[r1] + (uint32_t)r1 - host_bounds[r0] - (uint32_t)r0;
+        hipLaunchKernelGGL(k_offset_slices, dim3(m / 256 + 1 < 4096 ? m / 256 + 1 : 4096), dim3(256), 0, xs, d_off, ra,
+                           d_sl, r0, r1);
+        return hip_status(hipGetLastError(), "offset slices launch");
+    };
+    // group 1 (owners of A) once A's buckets are sorted -- after the listed
+    // segments too when A had any (they are written at the round's end)
+    int g1 = hip_status(hipStreamWaitEvent(xs, listed_a ? ev[kEvB] : ev[kEvE], 0), "wait A");
+    (void)hipEventRecord(ev[kEvG1s], xs);
+    if (!g1) g1 = slices(0, half);
+    if (!g1) g1 = split_group(x, 0, half, me, d_wire_send, sbytes.data(), soff.data(), d_wire_recv, rbytes.data(),
+                              d_sl, slb.data(), sloff.data(), d_ro, rob.data(), xs);
+    (void)hipEventRecord(ev[kEvG1], xs);
+    int mg = 0;
+    if (me < half && !g1) mg = hip_status(hipStreamWaitEvent(s, ev[kEvG1], 0), "wait group 1") ?: merge();
+    int g2 = hip_status(hipStreamWaitEvent(xs, ev[kEvB], 0), "wait B");
+    (void)hipEventRecord(ev[kEvG2s], xs);
+    if (!g2) g2 = slices(half, W);
+    if (!g2) g2 = split_group(x, half, W, me, d_wire_send, sbytes.data(), soff.data(), d_wire_recv, rbytes.data(),
+                              d_sl, slb.data(), sloff.data(), d_ro, rob.data(), xs);
+    (void)hipEventRecord(ev[kEvG2], xs);
+    if (me >= half && !g2 && !mg) mg = hip_status(hipStreamWaitEvent(s, ev[kEvG2], 0), "wait group 2") ?: merge();
+    // the send buffer is the caller's again only when group 2 has gone out
+    (void)hipStreamWaitEvent(s, ev[kEvG2], 0);
+    (void)hipEventRecord(ev[kEvEnd], s);
+    rc = shd_dev_ws_sync(c->ws, (void*)s);
+    if (!rc) rc = hip_status(hipStreamSynchronize(xs), "transfer stream");
+    if (local_rc) return local_rc;
+    if (g1) return g1;
+    if (g2) return g2;
+    if (mg) return mg;
+    if (rc) return rc;
+    t_phase[0] = ev_ms(ev[kEv0], ev[kEvFront]) + ev_ms(ev[kEvCounts], ev[kEvB]);
+    t_phase[1] = ev_ms(ev[kEvFront], ev[kEvCounts]);
+    t_phase[2] = ev_ms(ev[kEvG1s], ev[kEvG1]);
+    t_phase[3] = ev_ms(ev[kEvG2s], ev[kEvG2]);
+    t_phase[4] = ev_ms(ev[kEvMs], ev[kEvMe]);
+    t_phase[5] = ev_ms(ev[kEv0], ev[kEvEnd]);
+    const float ov = ev_ms(ev[kEvG1s], ev[kEvB]);
+    t_phase[6] = ov > 0.f ? ov : 0.0;
+    t_phase_valid = 1;
+    *n_out = nrecv;
+    return 0;
+}
+
 } // namespace
+
+extern "C" int shd_round_exchange_phases(double* ms, int n, int* valid) {
+    if (!ms || n < 0) return -EINVAL;
+    for (int k = 0; k < n && k < kPhases; k++) ms[k] = t_phase[k];
+    if (valid) *valid = t_phase_valid;
+    return 0;
+}
 
 extern "C" int shd_dev_exchange_runs(void* ws, const ShdTransport* x, const ShdDeliv* d_events,
                                      const uint32_t* d_dst_offsets, const uint32_t* host_bounds, ShdDeliv* d_recv,
@@ -638,6 +906,16 @@ extern "C" int shd_dev_round_exchange(const ShdPktCtx* c, const ShdTransport* x,
                           : sw && strcmp(sw, "1") == 0 ? 1
                           : sw && strcmp(sw, "0") == 0 ? 0
                                                        : (double)W * (double)n > 256.0 * (double)(H ? H : 1);
+    // the split exchange (two send/recv groups overlapping the sender's second
+    // half and the first owners' merge): the library's own transports, two
+    // ranks or more; SHD_XCHG_SPLIT=0 keeps one group after the whole round.
+    // (Every rank takes the same form: it depends on the transport, W and the
+    // environment only.)
+    const char* sp = getenv("SHD_XCHG_SPLIT");
+    if (own && W >= 2 && !(sp && strcmp(sp, "0") == 0))
+        return exchange_split(c, x, d_recs, n, barrier, end_time, bootstrap_end, host_bounds, d_wire_send, d_status,
+                              d_counters, d_wire_recv, recv_cap, d_out, d_out_offsets, n_out, (hipStream_t)stream,
+                              sort_wire);
     int sorted = 0;
     if (!rc)
         rc = shd_dev_packet_round_grouped(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire_send, d_off, d_status,

@@ -177,7 +177,12 @@ def _check_union(bufs, res, world, host_bounds, ref, mt, nrec=None):
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("kind,world", [("local", 2), ("local", 3), ("rccl_all", 1), ("rccl_uid", 1)])
 @pytest.mark.parametrize("fused", [True, False], ids=["process_exchange", "device+exchange"])
-def test_threads_as_ranks(kind, world, fused):
+@pytest.mark.parametrize("split", ["1", "0"], ids=["split", "one_group"])
+def test_threads_as_ranks(kind, world, fused, split, monkeypatch):
+    """split: shd_round_process_exchange sends in two groups (owners below W/2
+    while the sender sorts the rest, then the others) -- or in one after the
+    whole round (SHD_XCHG_SPLIT=0)."""
+    monkeypatch.setenv("SHD_XCHG_SPLIT", split)
     gml, tops, A, host_bounds, bufs = _setup(world)
     row_bounds = [r * A // world for r in range(world + 1)]
     xps = _transports(kind, world)
@@ -192,9 +197,20 @@ def test_threads_as_ranks(kind, world, fused):
         top.adopt_table_device(b["tab"].data_ptr())
         top.touch_all()
         if fused:
-            return top.process_exchange(xp, b["recs"].data_ptr(), NPK, BARRIER, END, 0, host_bounds,
-                                        b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
-                                        b["recv"].data_ptr(), NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+            n = top.process_exchange(xp, b["recs"].data_ptr(), NPK, BARRIER, END, 0, host_bounds,
+                                     b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
+                                     b["recv"].data_ptr(), NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+            # this thread's phase times: a split call leaves them, one group does not
+            import ctypes as C
+
+            from shadow_amd import _lib
+            ph, ok = (C.c_double * 7)(), C.c_int()
+            _lib.check(_lib.lib().shd_round_exchange_phases(ph, 7, C.byref(ok)))
+            split_ran = split == "1" and world >= 2 and kind == "local"
+            assert ok.value == (1 if split_ran else 0)
+            if split_ran:  # decide, counts, group 1, group 2, merge, call, overlap
+                assert all(v >= 0 for v in ph) and ph[5] >= ph[0] and ph[5] >= ph[4], list(ph)
+            return n
         top.process_device(b["recs"].data_ptr(), NPK, BARRIER, END, 0, b["send"].data_ptr(), b["off"].data_ptr(),
                            b["status"].data_ptr(), b["cnt"].data_ptr(), 0)
         return top.exchange(xp, b["send"].data_ptr(), b["off"].data_ptr(), host_bounds, b["recv"].data_ptr(),
@@ -216,13 +232,15 @@ def test_threads_as_ranks(kind, world, fused):
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("hot", [1, 2, 6])
 @pytest.mark.parametrize("wire_sorted", ["1", "0"], ids=["sorted_wire", "unsorted_wire"])
-def test_exchange_long_segments(world, hot, wire_sorted, monkeypatch):
+@pytest.mark.parametrize("split", ["1", "0"], ids=["split", "one_group"])
+def test_exchange_long_segments(world, hot, wire_sorted, split, monkeypatch):
     """Packets aimed at a few hot destinations: sender segments past the
     part sort's LDS capacity (listed, sorted, converted to wire records) and
     owner segments past the run merge's LDS stage (kMergeMax: listed) or
     below it (merged from sorted runs of hundreds); SHD_WIRE_SORTED=0 sends
     unsorted runs that the owner sorts."""
     monkeypatch.setenv("SHD_WIRE_SORTED", wire_sorted)
+    monkeypatch.setenv("SHD_XCHG_SPLIT", split)
     gml, tops, A, host_bounds, bufs = _setup(world, hot)
     xps = _transports("local", world)
 
@@ -285,7 +303,8 @@ def test_row_sharded_route_decide_exchange(kind, world):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("kind,world", [("local", 2), ("local", 3)])
-def test_one_rank_failing_fails_every_rank(kind, world, monkeypatch):
+@pytest.mark.parametrize("split", ["1", "0"], ids=["split", "one_group"])
+def test_one_rank_failing_fails_every_rank(kind, world, split, monkeypatch):
     """A rank whose own stage fails before the exchange (SHD_DEBUG_FAIL_RANK)
     still joins the count all-to-all: it returns its error, every peer -EIO,
     and nobody waits in the payload collective."""
@@ -295,6 +314,7 @@ def test_one_rank_failing_fails_every_rank(kind, world, monkeypatch):
     gml, tops, A, host_bounds, bufs = _setup(world)
     xps = _transports(kind, world)
     monkeypatch.setenv("SHD_DEBUG_FAIL_RANK", "1")
+    monkeypatch.setenv("SHD_XCHG_SPLIT", split)
 
     def rank_main(r):
         top, _ = tops[r]
