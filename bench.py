@@ -301,9 +301,9 @@ def main():
 
     # N>1: the exchange's phase times of every timed step (HIP events,
     # shd_round_exchange_phases: decide, counts, group 1, group 2, merge,
-    # call, transfer beside the decide)
-    xph = {"on": False, "sum": [0.0] * 7, "n": 0}
-    ph_buf, ph_ok = (C.c_double * 7)(), C.c_int()
+    # call, transfer beside the decide, merge beside group 2)
+    xph = {"on": False, "sum": [0.0] * 8, "n": 0}
+    ph_buf, ph_ok = (C.c_double * 8)(), C.c_int()
 
     def step():
         if world > 1 and not split:
@@ -312,7 +312,7 @@ def main():
                                                  d_recv.data_ptr(), 2 * P, d_final.data_ptr(),
                                                  d_final_off.data_ptr(), sptr)
             if xph["on"]:
-                _lib.check(_lib.lib().shd_round_exchange_phases(ph_buf, 7, C.byref(ph_ok)))
+                _lib.check(_lib.lib().shd_round_exchange_phases(ph_buf, 8, C.byref(ph_ok)))
                 if ph_ok.value:
                     xph["sum"] = [a + b for a, b in zip(xph["sum"], ph_buf)]
                     xph["n"] += 1
@@ -462,7 +462,8 @@ def main():
     }
 
     if world > 1:
-        names = ["decide", "counts", "group1", "group2", "merge", "call", "transfer_beside_decide"]
+        names = ["decide", "counts", "group1", "group2", "merge", "call", "transfer_beside_decide",
+                 "merge_beside_group2"]
         mine = [v / xph["n"] for v in xph["sum"]] if xph["n"] else None
         result["exchange_phases"] = {
             "what": "per timed step, HIP events on the launch and transfer streams "
@@ -470,7 +471,7 @@ def main():
                     "all-gather; group1 / group2 = the payload send/recv groups of owners [0, W/2) and "
                     "[W/2, W) on the transfer stream; merge = the owner merge; call = the whole "
                     "shd_round_process_exchange; transfer_beside_decide = group 1's start to the end of the "
-                    "sender's kernels (the overlap)",
+                    "sender's kernels, merge_beside_group2 = the owner merge's time beside group 2 (the overlaps)",
             "split": mine is not None,
             "rank0_ms": dict(zip(names, mine)) if mine else None,
             "max_over_ranks_ms": dict(zip(names, [max_over_ranks(v) for v in mine])) if mine else None,

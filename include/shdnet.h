@@ -584,8 +584,9 @@ int shd_round_timing_read(double* stage_ms, int nstages, int* launches);
  * two ranks or more, SHD_XCHG_SPLIT != 0): [0] decide (the sender's
  * kernels), [1] counts (the count-matrix all-gather), [2] group 1 (owners
  * [0, W/2)), [3] group 2, [4] owner merge, [5] the whole call, [6] the
- * transfer time that ran beside the sender's kernels.  *valid = 0 when the
- * last call did not complete a split exchange. */
+ * transfer time that ran beside the sender's kernels, [7] the merge's time
+ * beside group 2.  *valid = 0 when the last call did not complete a split
+ * exchange. */
 int shd_round_exchange_phases(double* ms, int n, int* valid);
 
 /* Unit strings as the GML loader reads them (replace parse_time_nanosec /

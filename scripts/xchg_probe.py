@@ -75,9 +75,9 @@ def local_ranks(N):
                                                    b["fin"].data_ptr(), b["fin_off"].data_ptr())
             # this thread's last split exchange (HIP events): decide, counts,
             # group 1, group 2, merge, whole call, transfer beside the decide
-            ph = (C.c_double * 7)()
+            ph = (C.c_double * 8)()
             ok = C.c_int()
-            _lib.check(_lib.lib().shd_round_exchange_phases(ph, 7, C.byref(ok)))
+            _lib.check(_lib.lib().shd_round_exchange_phases(ph, 8, C.byref(ok)))
             phases[r] = list(ph) if ok.value else None
         except BaseException as e:
             errs.append(e)
@@ -119,7 +119,8 @@ def local_ranks(N):
                 if phases[r]:
                     p = phases[r]
                     print(f"  rank {r}: decide {p[0]:.3f} counts {p[1]:.3f} group1 {p[2]:.3f} group2 {p[3]:.3f} "
-                          f"merge {p[4]:.3f} call {p[5]:.3f} transfer beside decide {p[6]:.3f} ms", flush=True)
+                          f"merge {p[4]:.3f} call {p[5]:.3f} transfer beside decide {p[6]:.3f} "
+                          f"merge beside group2 {p[7]:.3f} ms", flush=True)
             outs[v] = union()
         if not knob:
             print("sorted and unsorted wire unions identical:",

@@ -618,10 +618,10 @@ int exchange_runs_core(void* ws, const ShdTransport* x, const void* d_events, si
 //      group 1 (G1) | wait B | slices B, group 2 (G2)
 // Phase times of the last split round of this thread, from HIP events
 // (shd_round_exchange_phases): decide (the sender's kernels), counts (the
-// matrix all-gather), group 1, group 2, merge, whole call, and the time the
+// matrix all-gather), group 1, group 2, merge, whole call, the time the
 // transfers ran beside the sender's sort (group 1's start to the end of
-// the sender's kernels).
-constexpr int kPhases = 7;
+// the sender's kernels) and the merge's time beside group 2.
+constexpr int kPhases = 8;
 thread_local double t_phase[kPhases];
 thread_local int t_phase_valid = 0;
 
@@ -845,6 +845,11 @@ int exchange_split(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_re
     t_phase[5] = ev_ms(ev[kEv0], ev[kEvEnd]);
     const float ov = ev_ms(ev[kEvG1s], ev[kEvB]);
     t_phase[6] = ov > 0.f ? ov : 0.0;
+    // the merge's time beside group 2 (the intervals' intersection)
+    const float ms0 = ev_ms(ev[kEv0], ev[kEvMs]), me0 = ev_ms(ev[kEv0], ev[kEvMe]);
+    const float gs0 = ev_ms(ev[kEv0], ev[kEvG2s]), ge0 = ev_ms(ev[kEv0], ev[kEvG2]);
+    const float mo = (me0 < ge0 ? me0 : ge0) - (ms0 > gs0 ? ms0 : gs0);
+    t_phase[7] = mo > 0.f ? mo : 0.0;
     t_phase_valid = 1;
     *n_out = nrecv;
     return 0;

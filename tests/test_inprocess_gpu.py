@@ -204,8 +204,8 @@ def test_threads_as_ranks(kind, world, fused, split, monkeypatch):
             import ctypes as C
 
             from shadow_amd import _lib
-            ph, ok = (C.c_double * 7)(), C.c_int()
-            _lib.check(_lib.lib().shd_round_exchange_phases(ph, 7, C.byref(ok)))
+            ph, ok = (C.c_double * 8)(), C.c_int()
+            _lib.check(_lib.lib().shd_round_exchange_phases(ph, 8, C.byref(ok)))
             split_ran = split == "1" and world >= 2 and kind == "local"
             assert ok.value == (1 if split_ran else 0)
             if split_ran:  # decide, counts, group 1, group 2, merge, call, overlap
