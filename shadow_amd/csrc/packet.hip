@@ -950,9 +950,9 @@ __device__ void wave_rank_segment(Load load, uint32_t n, uint32_t d, ShdDeliv* _
 #pragma unroll
         for (int e = 0; e < E; e++) lk[e * 64 + lane] = key[e]; // (padding lanes hold ~0ull)
         if (lane < 8) lk[64 * E + lane] = ~0ull;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         const ulonglong2* lk2 = reinterpret_cast<const ulonglong2*>(lk);
         for (uint32_t j = 0; j < n; j += 8) {
             ulonglong2 kk[4];
@@ -2915,10 +2915,10 @@ struct BucketRankLds {
     uint8_t m[128];     // the events of each bucket, at its first rank
 };
 static_assert(sizeof(BucketRankLds) <= 8 * (64 * 2 + 8), "fits a wave's LDS key array (kKeyE >= 2)");
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+__device__ __forceinline__ void wave_lds_sync() { // (LDS only: in-flight global stores stay in flight)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off));
@@ -2989,6 +2989,86 @@ __device__ __forceinline__ bool wave_bucket_rank(const uint4* lev, uint32_t o, u
     return true;
 }
 
+// The part sort's rank of one destination segment lev[o, o + n) (n <= 64 E,
+// LDS stage records {time - tbase, seq, pkt_index, src << shift | dl}) by
+// event_compare, with 31-bit keys: key = time offset - the destination's
+// earliest (the caller checks the span fits), so kj < key is the sign bit of
+// kj - key -- a subtract and a shift per pair on plain VGPRs, independent of
+// each other, where a 64-bit compare writes an SGPR pair that the next
+// instruction must wait for.  Keys come four at a time by LDS broadcast.
+// Equal times (rare: 3 of C3's 100,000 segments hold a pair) are ranked
+// among themselves by (src, srcHostEventID) in a second pass.  Each event is
+// stored at out + its rank (kOut 1: the 32-B event, 2: the 24-B wire record).
+template <int E, int kOut>
+__device__ __forceinline__ void wave_rank_x31(const uint4* lev, uint32_t o, uint32_t n, uint32_t tmin, uint32_t shift,
+                                              unsigned long long tbase, uint32_t dh, ShdDeliv* __restrict__ out,
+                                              uint32_t ob, int lane, uint32_t* lk32) {
+    uint4 r[E];
+    uint32_t key[E], rank[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        r[e] = i < n ? lev[o + i] : make_uint4(0u, 0u, 0u, 0u);
+        key[e] = i < n ? r[e].x - tmin : 0x7FFFFFFFu; // (padding: above every key)
+        rank[e] = 0;
+        lk32[e * 64 + lane] = key[e];
+    }
+    if (lane < 16) lk32[64 * E + lane] = 0x7FFFFFFFu;
+    wave_lds_sync();
+    const uint4* lk4 = reinterpret_cast<const uint4*>(lk32);
+    for (uint32_t j = 0; j < n; j += 16) {
+        uint4 kk[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) kk[u] = lk4[(j >> 2) + u];
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            uint32_t a = 0, c = 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                a += ((kk[u].x - key[e]) >> 31) + ((kk[u].y - key[e]) >> 31);
+                c += ((kk[u].z - key[e]) >> 31) + ((kk[u].w - key[e]) >> 31);
+            }
+            rank[e] += a + c;
+        }
+    }
+    // ties (equal keys share their lowest rank: the ranks' sum falls short)
+    uint32_t rsum = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) rsum += (e * 64 + lane < (int)n) ? rank[e] : 0u;
+    for (int off = 32; off > 0; off >>= 1) rsum += (uint32_t)__shfl_xor((int)rsum, off);
+    if (rsum != n * (n - 1) / 2) {
+#pragma unroll
+        for (int ej = 0; ej < E; ej++) {
+            const int lim = (int)n - ej * 64 < 64 ? (int)n - ej * 64 : 64;
+            for (int l = 0; l < lim; l++) {
+                const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key[ej], l);
+                const uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)(r[ej].w >> shift), l);
+                const uint32_t qj = (uint32_t)__builtin_amdgcn_readlane((int)r[ej].y, l);
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const uint32_t se = r[e].w >> shift;
+                    rank[e] += (uint32_t)((kj == key[e]) & ((sj < se) | ((sj == se) & (qj < r[e].y))));
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        if ((uint32_t)(e * 64 + lane) >= n) continue;
+        const unsigned long long t = tbase + r[e].x;
+        const uint32_t src = r[e].w >> shift;
+        if (kOut == 2) {
+            st_wire(reinterpret_cast<Wire*>(out) + ob + rank[e], t, (unsigned long long)r[e].y, src, r[e].z);
+        } else {
+            shd_v4u* q = reinterpret_cast<shd_v4u*>(&out[ob + rank[e]]);
+            const shd_v4u a = {(uint32_t)t, (uint32_t)(t >> 32), r[e].y, 0u};
+            const shd_v4u c2 = {src, dh, r[e].z, 0u};
+            __builtin_nontemporal_store(a, q);
+            __builtin_nontemporal_store(c2, q + 1);
+        }
+    }
+}
+
 template <int kWG, int kCap, int kKeyE, bool kWire>
 __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restrict__ stage,
                                                           const uint32_t* __restrict__ gcnt,
@@ -2998,7 +3078,8 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                                                           uint32_t* __restrict__ offsets, ShdDeliv* __restrict__ out,
                                                           ShdDeliv* __restrict__ scr, uint32_t* __restrict__ big,
                                                           uint32_t* __restrict__ nbig,
-                                                          unsigned long long* __restrict__ counters, uint32_t lds_keys) {
+                                                          unsigned long long* __restrict__ counters, uint32_t lds_keys,
+                                                          const uint32_t b) {
     // perm: the segments' ranks go to an LDS permutation and the bucket is
     // written in order afterwards -- consecutive lanes, consecutive 16-B (8-B
     // for wire records) pieces of the output, whole lines per instruction
@@ -3011,15 +3092,15 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     const bool perm = kPermOk && (lds_keys & 2u);
     __shared__ unsigned long long keys[kWG / 64][kKeyE ? 64 * kKeyE + 8 : 1];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
+    __shared__ uint32_t xmn[kPartMaxDst], xmx[kPartMaxDst]; // each destination's time-offset range
     const bool brank = kKeyE >= 2 && (lds_keys & 4u);
-    const uint32_t b = g.b0 + blockIdx.x;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t d0 = b << g.shift;
     const uint32_t nd = min(1u << g.shift, g.H - d0);
     const uint32_t mask = (1u << g.shift) - 1u;
     const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
     const bool listed = tot > (uint32_t)kCap || nw > 0; // (block-uniform)
-    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
+    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = xmx[j] = 0, xmn[j] = ~0u;
     const uint4* sb = stage + (size_t)b * g.cap;
     uint4 e[kCap / kWG];
     if (!listed) { // the bucket's records
@@ -3038,11 +3119,15 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     const uint32_t* bpre = gcnt + 3 * (size_t)g.nb;
     const uint32_t obase = bpre[b];
     const ShdDeliv* wb = wide + (nw ? bpre[g.nb + 1 + b] : 0u); // this bucket's wide events (k_wide_group)
-    __syncthreads(); // (orders the cnt reset)
+    lds_barrier(); // (orders the cnt reset)
     if (!listed) {
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++)
-            if ((uint32_t)k * kWG + threadIdx.x < ns) atomicAdd(&cnt[e[k].w & mask], 1u);
+            if ((uint32_t)k * kWG + threadIdx.x < ns) {
+                const uint32_t dl = e[k].w & mask;
+                atomicAdd(&cnt[dl], 1u);
+                if (kKeyE >= 2) atomicMin(&xmn[dl], e[k].x), atomicMax(&xmx[dl], e[k].x);
+            }
     } else {
         for (uint32_t i = threadIdx.x; i < ns; i += kWG) atomicAdd(&cnt[sb[i].w & mask], 1u);
         const uint32_t m = *nwide;
@@ -3052,7 +3137,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
             for (uint32_t i = threadIdx.x; i < nw; i += kWG) atomicAdd(&cnt[(wb[i].dst_host - g.host_lo) & mask], 1u);
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x < 64) { // destination offsets (nd <= 64: one wave)
         const uint32_t v = threadIdx.x < nd ? cnt[threadIdx.x] : 0u;
         const uint32_t inc = wave_incl_scan(v, lane);
@@ -3066,7 +3151,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
         offsets[g.H] = obase + tot;
         counters[0] = obase + tot; // the round's delivered count
     }
-    __syncthreads();
+    lds_barrier();
     if (!listed) {
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++) {
@@ -3076,7 +3161,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                 lev[loc[dl] + atomicAdd(&cur[dl], 1u)] = e[k];
             }
         }
-        __syncthreads();
+        lds_barrier();
         // segments of at most kTinySeg events (many destinations per bucket,
         // few events each: C4's rounds): one thread per event, its rank the
         // count of its segment's events before it in event_compare order
@@ -3143,6 +3228,18 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                     continue;
                 }
             }
+            // 31-bit keys (the time offset from the destination's earliest):
+            // the signed difference's sign bit is the compare, no SGPR carry
+            // chain (SHD_SORT_X31=0: the packed 64-bit keys)
+            if (kKeyE >= 2 && lk && !perm && !(lds_keys & 64u) && nj <= 128 && xmx[j] - xmn[j] < 0x7FFFFFFFu) {
+                if (nj <= 64)
+                    wave_rank_x31<1, kOut>(lev, o, nj, xmn[j], g.shift, g.tbase, dh, out, obase + o, lane,
+                                           reinterpret_cast<uint32_t*>(lk));
+                else
+                    wave_rank_x31<2, kOut>(lev, o, nj, xmn[j], g.shift, g.tbase, dh, out, obase + o, lane,
+                                           reinterpret_cast<uint32_t*>(lk));
+                continue;
+            }
             if (nj <= 64) {
                 if (perm) wave_rank_segment<1, 3>(load, nj, dh, wo, o, lane, lk);
                 else wave_rank_segment<1, kOut>(load, nj, dh, out, obase + o, lane, lk);
@@ -3166,7 +3263,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
             }
         }
         if (perm) { // the bucket in output order
-            __syncthreads();
+            lds_barrier();
             if (kWire) {
                 uint2* ob = reinterpret_cast<uint2*>(reinterpret_cast<Wire*>(out) + obase);
                 for (uint32_t u = threadIdx.x; u < 3 * ns; u += kWG) {
@@ -3209,7 +3306,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
             r.pad = 0;
             st_ev(&scr[obase + loc[dl] + atomicAdd(&cur[dl], 1u)], r);
         }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t j = threadIdx.x; j < nd; j += kWG)
         if (cnt[j] > 0) {
             const uint32_t k = atomicAdd(nbig, 1u);
@@ -3233,7 +3330,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kMinW, 8)))
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
     part_sort_body<kWG, kCap, kKeyE, kWire>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig,
-                                           counters, lds_keys);
+                                           counters, lds_keys, g.b0 + blockIdx.x);
 }
 template <int kWG, int kCap, int kKeyE, int kOcc>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc, kOcc))) void k_part_sort_occ(PartGeo g, const uint4* __restrict__ stage,
@@ -3246,7 +3343,7 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc, kOcc)
                                                           uint32_t* __restrict__ nbig,
                                                           unsigned long long* __restrict__ counters, uint32_t lds_keys) {
     part_sort_body<kWG, kCap, kKeyE, false>(g, stage, gcnt, wcnt, wide, nwide, wide_cap, offsets, out, scr, big, nbig,
-                                           counters, lds_keys);
+                                           counters, lds_keys, g.b0 + blockIdx.x);
 }
 
 // The sorted wire's listed segments: the listed kernels sorted them as
@@ -3749,7 +3846,9 @@ uint32_t lds_keys() {
 uint32_t part_sort_flags() {
     const char* v = getenv("SHD_PART_PERM");
     const char* bk = getenv("SHD_SORT_BUCKET");
-    return lds_keys() | (v && strcmp(v, "1") == 0 ? 2u : 0u) | (bk && strcmp(bk, "1") == 0 ? 4u : 0u);
+    const char* x31 = getenv("SHD_SORT_X31");
+    return lds_keys() | (v && strcmp(v, "1") == 0 ? 2u : 0u) | (bk && strcmp(bk, "1") == 0 ? 4u : 0u) |
+           (x31 && strcmp(x31, "0") == 0 ? 64u : 0u);
 }
 // Compact 16-B slab records (CSlab) with the rank sort; SHD_SLAB_COMPACT=0
 // (or the bitonic segment sort) keeps the 32-B slab
