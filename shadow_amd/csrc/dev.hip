@@ -73,6 +73,27 @@ extern "C" int shd_dev_d2h_async(void* h, const void* d, size_t bytes, void* s) 
     return bytes ? hip_err(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, (hipStream_t)s), "hipMemcpyAsync D2H") : 0;
 }
 
+extern "C" int shd_dev_d2d_async(void* d, const void* src, size_t bytes, void* s) {
+    return bytes ? hip_err(hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)s), "hipMemcpyAsync D2D")
+                 : 0;
+}
+
+// events that order one stream after another (no timing)
+extern "C" int shd_dev_event_new(void** e) {
+    hipEvent_t h = nullptr;
+    const int rc = hip_err(hipEventCreateWithFlags(&h, hipEventDisableTiming), "hipEventCreate");
+    *e = rc ? nullptr : (void*)h;
+    return rc;
+}
+extern "C" void shd_dev_event_free(void* e) {
+    if (e) (void)hipEventDestroy((hipEvent_t)e);
+}
+// `waiter` waits (on the device) for what `after` has enqueued so far
+extern "C" int shd_dev_stream_after(void* waiter, void* after, void* e) {
+    int rc = hip_err(hipEventRecord((hipEvent_t)e, (hipStream_t)after), "hipEventRecord");
+    return rc ? rc : hip_err(hipStreamWaitEvent((hipStream_t)waiter, (hipEvent_t)e, 0), "hipStreamWaitEvent");
+}
+
 // Pinned (page-locked) host memory: the round's staging buffers, so their
 // copies run at the link's rate and asynchronously on the round's stream.
 extern "C" int shd_host_alloc(void** p, size_t bytes) {

@@ -32,7 +32,7 @@ int shd_round_set_workers(ShdTopology* t, int nworkers) {
         ShdWorkerBuf* nb = (ShdWorkerBuf*)calloc((size_t)nworkers, sizeof(ShdWorkerBuf));
         if (!nb) rc = -ENOMEM;
         else {
-            for (int w = 0; w < t->nworkers; w++) shd_host_free(t->wbuf[w].recs);
+            for (int w = 0; w < t->nworkers; w++) shd_wbuf_release(&t->wbuf[w]);
             free(t->wbuf);
             t->wbuf = nb;
             t->nworkers = nworkers;
@@ -48,9 +48,26 @@ int shd_round_begin(ShdTopology* t, uint64_t barrier, uint64_t end_time, uint64_
     t->barrier = barrier;
     t->end_time = end_time;
     t->bootstrap_end = bootstrap_end;
-    for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0;
+    int rc = 0;
+    for (int w = 0; w < t->nworkers; w++) {
+        ShdWorkerBuf* b = &t->wbuf[w];
+        if (b->stream && b->up) { /* (a round dropped without a collect: its uploads finish first) */
+            const int r = shd_dev_stream_sync(b->stream);
+            if (!rc) rc = r;
+        }
+        b->n = b->up = 0;
+    }
     pthread_mutex_unlock(&t->round_mu);
-    return 0;
+    return rc;
+}
+
+void shd_wbuf_release(ShdWorkerBuf* b) {
+    if (b->stream) (void)shd_dev_stream_sync(b->stream);
+    shd_host_free(b->recs);
+    shd_dev_free(b->d_recs);
+    shd_dev_event_free(b->ev);
+    shd_dev_stream_free(b->stream);
+    memset(b, 0, sizeof *b);
 }
 
 /* Slots of a record's endpoints, or -ENOENT (no side effect). */
@@ -70,13 +87,41 @@ static int wbuf_reserve(ShdWorkerBuf* b, size_t need) {
     size_t nc = b->cap ? b->cap : 4096;
     while (nc < need) nc *= 2;
     ShdPkt* s = NULL;
-    int rc = shd_host_alloc((void**)&s, sizeof(ShdPkt) * nc);
-    if (rc) return rc;
+    int rc = 0;
+    if (b->stream && b->up && (rc = shd_dev_stream_sync(b->stream))) return rc; /* (uploads read the old buffer) */
+    if ((rc = shd_host_alloc((void**)&s, sizeof(ShdPkt) * nc))) return rc;
     if (b->n) memcpy(s, b->recs, sizeof(ShdPkt) * b->n);
     shd_host_free(b->recs);
     b->recs = s;
     b->cap = nc;
     return 0;
+}
+
+/* Uploads worker buffer b's records [up, n) to its device mirror on the
+ * worker's own stream (the link copies while the round's sends go on).  Not
+ * for multi-shard tables (their collect partitions on the host).  A failure
+ * here is not the append's: the collect copies whatever was not uploaded. */
+static void wbuf_upload(ShdTopology* t, ShdWorkerBuf* b) {
+    if (t->nshards > 1 || b->n == b->up) return;
+    const char* v = getenv("SHD_APPEND_UPLOAD");
+    if (v && strcmp(v, "0") == 0) return;
+    if (shd_dev_init(t->device)) return;
+    if (!b->stream && shd_dev_stream_new(&b->stream)) return;
+    if (!b->ev && shd_dev_event_new(&b->ev)) return;
+    if (b->n > b->dcap) { /* grow the mirror, keeping the uploaded prefix */
+        ShdPkt* d = NULL;
+        if (shd_dev_malloc((void**)&d, sizeof(ShdPkt) * b->cap)) return;
+        if (b->up && (shd_dev_d2d_async(d, b->d_recs, sizeof(ShdPkt) * b->up, b->stream) ||
+                      shd_dev_stream_sync(b->stream))) {
+            shd_dev_free(d);
+            return;
+        }
+        shd_dev_free(b->d_recs);
+        b->d_recs = d;
+        b->dcap = b->cap;
+    }
+    if (!shd_dev_h2d_async(b->d_recs + b->up, b->recs + b->up, sizeof(ShdPkt) * (b->n - b->up), b->stream))
+        b->up = b->n;
 }
 
 int shd_round_append_worker(ShdTopology* t, int worker, const ShdPkt* recs, size_t n) {
@@ -100,9 +145,14 @@ int shd_round_append_worker(ShdTopology* t, int worker, const ShdPkt* recs, size
     }
     ShdWorkerBuf* b = &t->wbuf[worker];
     if ((rc = wbuf_reserve(b, b->n + n))) return rc;
-    if (!pending) {
-        if (n) memcpy(b->recs + b->n, recs, sizeof(ShdPkt) * n);
-        b->n += n;
+    if (!pending) { /* in pieces of 4 MB, each uploaded while the next is copied */
+        const size_t kPiece = 131072;
+        for (size_t i = 0; i < n; i += kPiece) {
+            const size_t m = n - i < kPiece ? n - i : kPiece;
+            memcpy(b->recs + b->n, recs + i, sizeof(ShdPkt) * m);
+            b->n += m;
+            wbuf_upload(t, b);
+        }
         return 0;
     }
     for (size_t i = 0; i < n && !rc; i++) {
@@ -112,6 +162,7 @@ int shd_round_append_worker(ShdTopology* t, int worker, const ShdPkt* recs, size
             rc = shd_resolve(t, si, di, &oi, &oj); /* topology_getReliability's lookup, at send time */
         if (!rc) b->recs[b->n++] = recs[i];
     }
+    wbuf_upload(t, b);
     /* device-resident rows first touched here are queued; launched in batches
      * (never waited for at send time), folded in touch order at the boundary */
     const int rcf = shd_release_kick(t);
@@ -204,10 +255,19 @@ static int collect_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_o
     void* s = t->cstream;
     size_t at = 0;
     for (int w = 0; w < t->nworkers && !rc; w++) {
-        rc = shd_dev_h2d_async(t->d_crecs + at, t->wbuf[w].recs, sizeof(ShdPkt) * t->wbuf[w].n, s);
-        at += t->wbuf[w].n;
+        ShdWorkerBuf* b = &t->wbuf[w];
+        /* uploaded at append time: after the worker's stream, device to
+         * device; the rest from the pinned buffer */
+        if (b->up && !(rc = shd_dev_stream_after(s, b->stream, b->ev)))
+            rc = shd_dev_d2d_async(t->d_crecs + at, b->d_recs, sizeof(ShdPkt) * b->up, s);
+        if (!rc && b->n > b->up)
+            rc = shd_dev_h2d_async(t->d_crecs + at + b->up, b->recs + b->up, sizeof(ShdPkt) * (b->n - b->up), s);
+        at += b->n;
     }
-    if (rc) return rc;
+    if (rc) {
+        (void)shd_dev_stream_sync(s);
+        return rc;
+    }
     if ((rc = shd_sync_touch(t)) || (rc = shd_pcnt_ensure(t, &t->pcnt, t->tab_row_lo, t->tab_row_hi, n)) ||
         (rc = shd_ensure_ptab(t)))
         return rc;
@@ -230,7 +290,7 @@ static int collect_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size_t* n_o
     /* the round is decided and counted: its records leave the staging
      * buffers whatever happens below (a retried collect must not count them
      * twice) */
-    for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0;
+    for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = t->wbuf[w].up = 0;
     const uint64_t nev = t->h_ccnt[0], mt = t->h_ccnt[1];
     if (out && nev) rc = shd_dev_d2h_async(out, t->d_cout, sizeof(ShdDeliv) * (size_t)nev, s);
     if (!rc && dst_offsets)
@@ -442,7 +502,7 @@ static int collect_shards_locked(ShdTopology* t, ShdDeliv* out, size_t cap, size
         for (size_t i = 0; i < obase; i++) out[i].pkt_index = perm[out[i].pkt_index];
     if (status)
         for (size_t q = 0; q < n; q++) status[perm[q]] = pst[q]; /* partition order -> record order */
-    for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = 0; /* decided and counted (see collect_locked) */
+    for (int w = 0; w < t->nworkers; w++) t->wbuf[w].n = t->wbuf[w].up = 0; /* decided and counted (see collect_locked) */
 done:
     free(perm);
     free(owner);

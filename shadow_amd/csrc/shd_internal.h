@@ -98,6 +98,12 @@ int shd_dev_memset(void* d, int v, size_t bytes);
  * should be pinned (shd_host_alloc) for them to be asynchronous */
 int shd_dev_h2d_async(void* d, const void* h, size_t bytes, void* stream);
 int shd_dev_d2h_async(void* h, const void* d, size_t bytes, void* stream);
+int shd_dev_d2d_async(void* d, const void* s, size_t bytes, void* stream);
+/* an event (hipEvent_t behind void*, no timing); shd_dev_stream_after:
+ * `waiter` waits on the device for everything enqueued on `after` so far */
+int shd_dev_event_new(void** e);
+void shd_dev_event_free(void* e);
+int shd_dev_stream_after(void* waiter, void* after, void* e);
 /* pinned host memory */
 int shd_host_alloc(void** p, size_t bytes);
 void shd_host_free(void* p);

@@ -501,7 +501,7 @@ void shd_topology_free(ShdTopology* t) {
     shd_dev_free(t->d_ccnt);
     shd_host_free(t->h_ccnt);
     shd_dev_stream_free(t->cstream);
-    for (int w = 0; w < t->nworkers; w++) shd_host_free(t->wbuf[w].recs);
+    for (int w = 0; w < t->nworkers; w++) shd_wbuf_release(&t->wbuf[w]);
     free(t->wbuf);
     pthread_mutex_destroy(&t->setup_mu);
     pthread_mutex_destroy(&t->touch_mu);

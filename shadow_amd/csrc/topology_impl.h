@@ -25,13 +25,21 @@
 
 #define SHD_UNTOUCHED 0xffffffffu
 
-/* One worker's staged sends for the current round (cache-line padded: each
- * worker writes only its own). */
+/* One worker's staged sends for the current round (one cache line: each
+ * worker writes only its own).  recs: pinned host buffer; d_recs: its
+ * device mirror, records [0, up) already copied there -- each append is
+ * uploaded on the worker's own stream while the round's sends go on, so the
+ * collect finds them on the device. */
 typedef struct {
     ShdPkt* recs;
     size_t n, cap;
-    char pad[40];
+    ShdPkt* d_recs;
+    size_t dcap, up;
+    void* stream; /* the worker's upload stream (hipStream_t) and its event */
+    void* ev;
 } ShdWorkerBuf;
+/* frees a worker buffer's host and device sides (its uploads finished) */
+void shd_wbuf_release(ShdWorkerBuf* b);
 
 typedef struct {
     uint32_t ip;

@@ -208,6 +208,13 @@ int shd_dev_gather_entries(const ShdEntry* tab, const uint64_t* d_idx, size_t n,
 
 int shd_dev_h2d_async(void* d, const void* h, size_t bytes, void* stream) { return shd_dev_h2d(d, h, bytes); }
 int shd_dev_d2h_async(void* h, const void* d, size_t bytes, void* stream) { return shd_dev_d2h(h, d, bytes); }
+int shd_dev_d2d_async(void* d, const void* s, size_t bytes, void* stream) { return shd_dev_d2d(d, s, bytes); }
+int shd_dev_event_new(void** e) {
+    *e = malloc(1);
+    return *e ? 0 : -ENOMEM;
+}
+void shd_dev_event_free(void* e) { free(e); }
+int shd_dev_stream_after(void* waiter, void* after, void* e) { return 0; }
 int shd_host_alloc(void** p, size_t bytes) {
     *p = malloc(bytes ? bytes : 4);
     return *p ? 0 : -ENOMEM;
