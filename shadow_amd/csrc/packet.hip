@@ -2333,6 +2333,7 @@ struct PartGeo {
     uint32_t cap;        // stage records per bucket
     unsigned long long tbase;
     uint32_t b0 = 0;     // the sorts: first bucket of the launch (blockIdx.x + b0)
+    uint32_t xbar = 0x80000000u; // the barrier's time offset (barrier - tbase)
 };
 
 __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* total, uint32_t* ws) {
@@ -2991,25 +2992,36 @@ __device__ __forceinline__ bool wave_bucket_rank(const uint4* lev, uint32_t o, u
 
 // The part sort's rank of one destination segment lev[o, o + n) (n <= 64 E,
 // LDS stage records {time - tbase, seq, pkt_index, src << shift | dl}) by
-// event_compare, with 31-bit keys: key = time offset - the destination's
-// earliest (the caller checks the span fits), so kj < key is the sign bit of
-// kj - key -- a subtract and a shift per pair on plain VGPRs, independent of
-// each other, where a 64-bit compare writes an SGPR pair that the next
-// instruction must wait for.  Keys come four at a time by LDS broadcast.
+// event_compare, with 31-bit keys: key = time - barrier (xbar: the
+// barrier's offset from tbase), which every inter-host delivery (clamped to
+// the barrier) has in [0, 2^31 - 1) unless it lands 2.1 s or more after the
+// barrier; kj < key is then the sign bit of kj - key -- a subtract and a shift
+// per pair on plain VGPRs, independent of each other, where a 64-bit compare
+// writes an SGPR pair that the next instruction must wait for.  Keys come
+// four at a time by LDS broadcast.  Returns false (wave-uniform, before any
+// output) when an event precedes the barrier (a host's packet to itself) or
+// lies that far past it: the caller ranks that segment on 64-bit keys.
 // Equal times (rare: 3 of C3's 100,000 segments hold a pair) are ranked
 // among themselves by (src, srcHostEventID) in a second pass.  Each event is
 // stored at out + its rank (kOut 1: the 32-B event, 2: the 24-B wire record).
 template <int E, int kOut>
-__device__ __forceinline__ void wave_rank_x31(const uint4* lev, uint32_t o, uint32_t n, uint32_t tmin, uint32_t shift,
+__device__ __forceinline__ bool wave_rank_x31(const uint4* lev, uint32_t o, uint32_t n, uint32_t xbar, uint32_t shift,
                                               unsigned long long tbase, uint32_t dh, ShdDeliv* __restrict__ out,
                                               uint32_t ob, int lane, uint32_t* lk32) {
     uint4 r[E];
     uint32_t key[E], rank[E];
+    bool early = false;
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)(e * 64 + lane);
-        r[e] = i < n ? lev[o + i] : make_uint4(0u, 0u, 0u, 0u);
-        key[e] = i < n ? r[e].x - tmin : 0x7FFFFFFFu; // (padding: above every key)
+        r[e] = i < n ? lev[o + i] : make_uint4(xbar, 0u, 0u, 0u);
+        early |= r[e].x < xbar || r[e].x - xbar >= 0x7FFFFFFFu;
+    }
+    if (__ballot(early)) return false;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * 64 + lane);
+        key[e] = i < n ? r[e].x - xbar : 0x7FFFFFFFu; // (padding: above every key)
         rank[e] = 0;
         lk32[e * 64 + lane] = key[e];
     }
@@ -3067,6 +3079,7 @@ __device__ __forceinline__ void wave_rank_x31(const uint4* lev, uint32_t o, uint
             __builtin_nontemporal_store(c2, q + 1);
         }
     }
+    return true;
 }
 
 template <int kWG, int kCap, int kKeyE, bool kWire>
@@ -3092,7 +3105,6 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     const bool perm = kPermOk && (lds_keys & 2u);
     __shared__ unsigned long long keys[kWG / 64][kKeyE ? 64 * kKeyE + 8 : 1];
     __shared__ uint32_t cnt[kPartMaxDst], loc[kPartMaxDst + 1], cur[kPartMaxDst];
-    __shared__ uint32_t xmn[kPartMaxDst], xmx[kPartMaxDst]; // each destination's time-offset range
     const bool brank = kKeyE >= 2 && (lds_keys & 4u);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t d0 = b << g.shift;
@@ -3100,7 +3112,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     const uint32_t mask = (1u << g.shift) - 1u;
     const uint32_t ns = min(gcnt[b], g.cap), nw = wcnt[b], tot = ns + nw;
     const bool listed = tot > (uint32_t)kCap || nw > 0; // (block-uniform)
-    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = xmx[j] = 0, xmn[j] = ~0u;
+    for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
     const uint4* sb = stage + (size_t)b * g.cap;
     uint4 e[kCap / kWG];
     if (!listed) { // the bucket's records
@@ -3123,11 +3135,7 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     if (!listed) {
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++)
-            if ((uint32_t)k * kWG + threadIdx.x < ns) {
-                const uint32_t dl = e[k].w & mask;
-                atomicAdd(&cnt[dl], 1u);
-                if (kKeyE >= 2) atomicMin(&xmn[dl], e[k].x), atomicMax(&xmx[dl], e[k].x);
-            }
+            if ((uint32_t)k * kWG + threadIdx.x < ns) atomicAdd(&cnt[e[k].w & mask], 1u);
     } else {
         for (uint32_t i = threadIdx.x; i < ns; i += kWG) atomicAdd(&cnt[sb[i].w & mask], 1u);
         const uint32_t m = *nwide;
@@ -3231,14 +3239,13 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
             // 31-bit keys (the time offset from the destination's earliest):
             // the signed difference's sign bit is the compare, no SGPR carry
             // chain (SHD_SORT_X31=0: the packed 64-bit keys)
-            if (kKeyE >= 2 && lk && !perm && !(lds_keys & 64u) && nj <= 128 && xmx[j] - xmn[j] < 0x7FFFFFFFu) {
-                if (nj <= 64)
-                    wave_rank_x31<1, kOut>(lev, o, nj, xmn[j], g.shift, g.tbase, dh, out, obase + o, lane,
-                                           reinterpret_cast<uint32_t*>(lk));
-                else
-                    wave_rank_x31<2, kOut>(lev, o, nj, xmn[j], g.shift, g.tbase, dh, out, obase + o, lane,
-                                           reinterpret_cast<uint32_t*>(lk));
-                continue;
+            if (kKeyE >= 2 && lk && !perm && !(lds_keys & 64u) && nj <= 128) {
+                const bool done =
+                    nj <= 64 ? wave_rank_x31<1, kOut>(lev, o, nj, g.xbar, g.shift, g.tbase, dh, out, obase + o, lane,
+                                                      reinterpret_cast<uint32_t*>(lk))
+                             : wave_rank_x31<2, kOut>(lev, o, nj, g.xbar, g.shift, g.tbase, dh, out, obase + o, lane,
+                                                      reinterpret_cast<uint32_t*>(lk));
+                if (done) continue;
             }
             if (nj <= 64) {
                 if (perm) wave_rank_segment<1, 3>(load, nj, dh, wo, o, lane, lk);
@@ -4097,7 +4104,8 @@ constexpr int kPartSortCap[5] = {7168, 3584, 1792, 2304, 2304};
 // widest buckets (shift <= 6) whose expected load stays within the LDS sort's
 // capacity with room for the spread of a uniform load (6/7 of it); false
 // when the buckets would be too many for the scatter's LDS histogram.
-bool part_geometry(uint32_t host_lo, uint32_t H, size_t n, unsigned long long tbase, PartGeo* g) {
+bool part_geometry(uint32_t host_lo, uint32_t H, size_t n, unsigned long long tbase, PartGeo* g,
+                   unsigned long long barrier) {
     if (!H) return false;
     const double target = kPartSortCap[part_sort_cfg()] * 6.0 / 7.0;
     uint32_t shift = 6;
@@ -4110,6 +4118,7 @@ bool part_geometry(uint32_t host_lo, uint32_t H, size_t n, unsigned long long tb
     g->nb = nb;
     g->cap = (uint32_t)((double)n * (double)(1u << shift) / (double)H * 1.25) + 256u;
     g->tbase = tbase;
+    g->xbar = (uint32_t)(barrier - tbase); // (tbase = barrier - 2^31, or 0 below 2^31: <= 2^31)
     return true;
 }
 
@@ -4858,7 +4867,7 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     int pipe = pipeline_for(H, true, true);
     if (pipe == kPartPipe) {
         PartGeo g;
-        if (part_geometry(0, H, n, barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull, &g)) {
+        if (part_geometry(0, H, n, barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull, &g, barrier)) {
             int rc = part_round(w, c, d_recs, n, barrier, end_time, bootstrap_end, g, d_out, d_dst_offsets, d_status,
                                 d_counters, s);
             if (rc || stream) return rc;
@@ -4951,7 +4960,7 @@ extern "C" int shd_round_pipeline_of(uint32_t nhosts, size_t n, int* pipe) {
     if (!pipe) return -EINVAL;
     int p = pipeline_for(nhosts, true, true);
     PartGeo g;
-    if (p == kPartPipe && !part_geometry(0, nhosts, n, 0, &g)) p = pipeline_for(nhosts, true);
+    if (p == kPartPipe && !part_geometry(0, nhosts, n, 0, &g, 0)) p = pipeline_for(nhosts, true);
     *pipe = p;
     return 0;
 }
@@ -5145,7 +5154,7 @@ extern "C" int shd_dev_packet_round_grouped(const ShdPktCtx* c, const ShdPkt* d_
     const uint32_t H = c->nhosts;
     const unsigned long long tb = barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull;
     PartGeo pg;
-    if (pipeline_for(H, true, true) == kPartPipe && part_geometry(0, H, n, tb, &pg)) {
+    if (pipeline_for(H, true, true) == kPartPipe && part_geometry(0, H, n, tb, &pg, barrier)) {
         // the part scatter, then the bucket's events grouped by destination
         // straight into the wire array (k_part_wire)
         unsigned long long* counters = (unsigned long long*)d_counters;
@@ -5222,7 +5231,7 @@ extern "C" int shd_dev_packet_round_grouped_split(const ShdPktCtx* c, const ShdP
     for (int r = 0; r <= W; r++) ca.b[r] = bounds[r];
     int rc;
     PartGeo pg;
-    if (!(pipeline_for(H, true, true) == kPartPipe && part_geometry(0, H, n, tb, &pg))) {
+    if (!(pipeline_for(H, true, true) == kPartPipe && part_geometry(0, H, n, tb, &pg, barrier))) {
         // the slab sender: the whole round, then its cuts and both hooks
         int sorted = 0;
         if ((rc = shd_dev_packet_round_grouped(c, d_recs, n, barrier, end_time, bootstrap_end, d_wire, d_off, d_status,
