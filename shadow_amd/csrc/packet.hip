@@ -3547,6 +3547,7 @@ struct Ws {
     size_t cap_xhost = 0;
     uint64_t* xmat = nullptr;  // the exchange's count matrix (kXmatWords u64), device and pinned host
     uint64_t* hxmat = nullptr;
+    bool done_pending = false; // the last use's w.done not recorded yet (done_flush)
     hipStream_t xs = nullptr;  // the split exchange's transfer stream (non-blocking) and its events
     hipEvent_t xev[kXchgEvents] = {};
 };
@@ -3556,10 +3557,22 @@ int hip_status(hipError_t e, const char* what) {
     return shd_fail(e == hipErrorOutOfMemory ? -ENOMEM : -EIO, "%s: %s", what, hipGetErrorString(e));
 }
 
+// w.done is recorded lazily on the null stream: ws_end only notes the use,
+// and the first reader records the event there, behind everything it launched.
+// A synchronous call that waits for that stream itself never records it
+// (ws_sync): an event record holds the stream's next command back ~5 us
+// (profiles/r05z_round_trace_gaps.log).
+int done_flush(Ws& w) {
+    if (!w.done_pending) return 0;
+    w.done_pending = false;
+    return hip_status(hipEventRecord(w.done, w.last), "hipEventRecord ws");
+}
+
 // Before buffers are freed or regrown, the last launch that used them (on
 // whatever stream) must have finished.
 int ws_quiesce(Ws& w) {
     if (!w.used) return 0;
+    if (int rc = done_flush(w)) return rc;
     return hip_status(hipEventSynchronize(w.done), "hipEventSynchronize ws");
 }
 
@@ -3753,6 +3766,7 @@ int fault_word_buf(Ws& w) {
 int fault_report(Ws& w, hipStream_t s);
 int ws_faults(Ws& w, bool completed, hipStream_t s) {
     if (!w.used || !w.meta || w.checked) return 0;
+    if (int rc = done_flush(w)) return rc;
     if (!completed && hipEventQuery(w.done) != hipSuccess) return 0;
     // the word, read on a stream of the workspace's own (it waits for nothing
     // else: the use it reports on has completed)
@@ -3788,10 +3802,12 @@ int ws_sync(Ws& w, hipStream_t s, const char* what) {
             while ((e = hipEventQuery(w.fin)) == hipErrorNotReady) {
             }
             if (int rc = hip_status(e, what)) return rc;
+            if (s == w.last) w.done_pending = false; // (the last use has finished: nothing to record)
             return fault_report(w, s);
         }
     }
     if (int rc = hip_status(hipStreamSynchronize(s), what)) return rc;
+    if (s == w.last) w.done_pending = false;
     return fault_report(w, s);
 }
 // *w.fault holds the word of the workspace's last, completed use
@@ -4142,6 +4158,7 @@ int ws_begin(Ws& w, hipStream_t s) {
     if (w.device >= 0 && w.device != dev) return shd_fail(-EINVAL, "workspace of device %d used on device %d", w.device, dev);
     w.device = dev;
     if ((rc = ws_faults(w, false, s))) return rc;
+    if ((rc = done_flush(w))) return rc;
     if (!w.done && (rc = hip_status(hipEventCreateWithFlags(&w.done, hipEventDisableTiming), "hipEventCreate ws")))
         return rc;
     if (w.used && w.last != s) return hip_status(hipStreamWaitEvent(s, w.done, 0), "hipStreamWaitEvent ws");
@@ -4151,7 +4168,13 @@ int ws_end(Ws& w, hipStream_t s) {
     w.last = s;
     w.used = true;
     w.checked = false;
-    return hip_status(hipEventRecord(w.done, s), "hipEventRecord ws");
+    // deferred on the null stream only (the synchronous calls' stream, which
+    // outlives the workspace; a caller's stream could be destroyed before a
+    // deferred record); SHD_WS_LAZY=0: record at once
+    const char* e = getenv("SHD_WS_LAZY");
+    if (s || (e && strcmp(e, "0") == 0)) return hip_status(hipEventRecord(w.done, s), "hipEventRecord ws");
+    w.done_pending = true;
+    return 0;
 }
 
 } // namespace
@@ -4167,6 +4190,7 @@ extern "C" int shd_dev_ws_check_faults(void* ws) {
     if (!ws) return 0;
     Ws& w = *static_cast<Ws*>(ws);
     if (!w.used) return 0;
+    if (int rc = done_flush(w)) return rc;
     if (int rc = hip_status(hipEventSynchronize(w.done), "hipEventSynchronize ws")) return rc;
     return ws_faults(w, true, nullptr);
 }
@@ -4179,7 +4203,10 @@ extern "C" int shd_dev_ws_new(void** ws) {
 extern "C" void shd_dev_ws_free(void* p) {
     if (!p) return;
     Ws* w = static_cast<Ws*>(p);
-    if (w->used) (void)hipEventSynchronize(w->done);
+    if (w->used) {
+        (void)done_flush(*w);
+        (void)hipEventSynchronize(w->done);
+    }
     (void)hipFree(w->tmp);
     (void)hipFree(w->st1);
     (void)hipFree(w->rnk);

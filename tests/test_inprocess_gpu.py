@@ -104,7 +104,7 @@ def _run_ranks(world, fn):
     return res, errs
 
 
-def _setup(world, hot=0):
+def _setup(world, hot=0, host_bounds=None):
     import torch
 
     from shadow_amd import Topology, scenario
@@ -115,7 +115,7 @@ def _setup(world, hot=0):
         ips, st, verts = scenario.register_hosts(top, H, seed=1)
         tops.append((top, st))
     A = tops[0][0].slot_count()
-    host_bounds = [r * H // world for r in range(world + 1)]
+    host_bounds = host_bounds or [r * H // world for r in range(world + 1)]
     bufs = []
     for r in range(world):
         cap = NPK * world
@@ -260,6 +260,41 @@ def test_exchange_long_segments(world, hot, wire_sorted, split, monkeypatch):
     finally:
         xps.close()
     _, ref, mt = _oracle_round(gml, world, hot)
+    _check_union(bufs, res, world, host_bounds, ref, mt)
+    _check_counts(tops)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("bounds", [[0, 1, 64, 200, H], [0, 150, 150, 151, H], [0, 0, 0, 0, H], [0, H, H, H, H],
+                                    [0, 37, 38, 299, H]], ids=["ragged", "empty_mid", "last_owns_all",
+                                                               "first_owns_all", "singletons"])
+@pytest.mark.parametrize("split", ["1", "0"], ids=["split", "one_group"])
+def test_uneven_owner_bounds(bounds, split, monkeypatch):
+    """Owner ranges of every shape on 4 ranks: single hosts, empty ranges,
+    one rank owning every destination.  The split exchange cuts each
+    sender's sorted events at these bounds before the sort (k_part_cuts) and
+    sends owners below W/2 first; the union must still equal the oracle."""
+    monkeypatch.setenv("SHD_XCHG_SPLIT", split)
+    world = 4
+    gml, tops, A, host_bounds, bufs = _setup(world, host_bounds=bounds)
+    xps = _transports("local", world)
+
+    def rank_main(r):
+        top, _ = tops[r]
+        b, xp = bufs[r], xps.ranks[r]
+        top.build_rows_device(0, A, b["tab"].data_ptr())
+        top.adopt_table_device(b["tab"].data_ptr())
+        top.touch_all()
+        return top.process_exchange(xp, b["recs"].data_ptr(), NPK, BARRIER, END, 0, host_bounds,
+                                    b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
+                                    b["recv"].data_ptr(), NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+
+    try:
+        res, errs = _run_ranks(world, rank_main)
+        assert not any(errs), [e for e in errs if e]
+    finally:
+        xps.close()
+    _, ref, mt = _oracle_round(gml, world)
     _check_union(bufs, res, world, host_bounds, ref, mt)
     _check_counts(tops)
 
