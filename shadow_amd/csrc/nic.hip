@@ -45,7 +45,7 @@ constexpr uint64_t kRefillInterval = 1000000ull; // _networkinterface_getRefillI
 constexpr uint64_t kMtu = shd_codel::kMtu;
 constexpr uint64_t kNever = ~0ull;
 
-enum { kErrRing = 1, kErrOrder = 2, kErrHost = 4, kErrId = 8, kErrWindow = 16, kErrAssert = 32 };
+enum { kErrRing = 1, kErrOrder = 2, kErrHost = 4, kErrId = 8, kErrWindow = 16, kErrAssert = 32, kErrArgs = 64 };
 
 // A lane's packet fates (receive time, status) go out in runs: the ids a
 // router pops are consecutive (FIFO over the carried run, then over the
@@ -219,6 +219,26 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
     __shared__ uint64_t stage_t[kStage * 64];
     __shared__ uint8_t stage_s[kStage * 64];
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    // The window's arrivals start as queued (~0, SHD_NIC_QUEUED) and its send
+    // requests unsent (~0): the wave's hosts' segments are one contiguous id
+    // range, filled by the whole wave in coalesced strides (no offsets read
+    // back to the host, no memsets before the launch); the fence orders these
+    // stores before any lane's fates to the same ids.
+    // (inputs every lane checks alike, so that no host runs when they fail)
+    const uint32_t all0 = eoff[0], all1 = eoff[n];
+    const int bad_all = ((uint64_t)id_base + all1 > fate_cap ? kErrId : 0) |
+                        (all1 > all0 && (!ev || !elen) ? kErrArgs : 0);
+    if (!bad_all) {
+        const uint32_t h0 = blockIdx.x * blockDim.x, h1 = h0 + 64 < n ? h0 + 64 : n;
+        const uint32_t w0 = eoff[h0], w1 = eoff[h1];
+        for (uint32_t k = w0 + threadIdx.x; k < w1; k += 64) {
+            rtime[id_base + k] = ~0ull;
+            rstat[id_base + k] = SHD_NIC_QUEUED;
+        }
+        if (soff)
+            for (uint32_t k = soff[h0] + threadIdx.x; k < soff[h1]; k += 64) stime[k] = ~0ull;
+    }
+    __threadfence_block();
     if (h >= n) return;
     const uint32_t self = host_base + h;
     FateStage out{rtime, rstat, stage_t + threadIdx.x, stage_s + threadIdx.x, 0u, 0u};
@@ -233,8 +253,7 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
     const uint32_t kend = soff ? soff[h + 1] : 0;
     H.stime = stime;
     H.boot_end = boot_end;
-    int bad = 0;
-    if ((uint64_t)id_base + iend > fate_cap) bad |= kErrId;
+    int bad = bad_all;
     uint64_t last = 0;
     // every lane ends: at most this many events (a host whose bucket refills
     // by 0 bytes per ms schedules a refill every ms for ever, as the reference)
@@ -371,34 +390,16 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
         return shd_fail(-EINVAL, "missing buffer");
     if (d_send_offsets && (!d_sends || !d_send_time)) return shd_fail(-EINVAL, "send offsets without sends");
     hipStream_t s = (hipStream_t)stream;
-    uint32_t range[2];
-    int rc = hip_status(hipMemcpyAsync(range, d_event_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
-    if (!rc) rc = hip_status(hipMemcpyAsync(range + 1, d_event_offsets + nhosts, sizeof(uint32_t),
-                                            hipMemcpyDeviceToHost, s), "D2H");
-    uint32_t srange[2] = {0, 0};
-    if (!rc && d_send_offsets) {
-        rc = hip_status(hipMemcpyAsync(srange, d_send_offsets, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H");
-        if (!rc) rc = hip_status(hipMemcpyAsync(srange + 1, d_send_offsets + nhosts, sizeof(uint32_t),
-                                                hipMemcpyDeviceToHost, s), "D2H");
-    }
-    if (!rc) rc = hip_status(hipStreamSynchronize(s), "offsets");
+    // the error word: one per thread and device, kept (a round allocates nothing)
+    static thread_local int* t_err[64];
+    int dev = 0;
+    int rc = hip_status(hipGetDevice(&dev), "hipGetDevice");
     if (rc) return rc;
-    if (range[1] > range[0] && (!d_events || !d_event_lengths)) return shd_fail(-EINVAL, "events without lengths");
-    if ((uint64_t)id_base + range[1] > fate_cap) return shd_fail(-ERANGE, "packet ids exceed the fate arrays");
-    int* d_err = nullptr;
-    if ((rc = hip_status(hipMalloc((void**)&d_err, sizeof(int)), "hipMalloc nic"))) return rc;
+    if (dev < 0 || dev >= 64) return shd_fail(-EINVAL, "device %d", dev);
+    if (!t_err[dev] && (rc = hip_status(hipMalloc((void**)&t_err[dev], sizeof(int)), "hipMalloc nic"))) return rc;
+    int* d_err = t_err[dev];
     int h_err = 0;
-    // the window's arrivals start as "queued"; unsent requests keep ~0
     rc = hip_status(hipMemsetAsync(d_err, 0, sizeof(int), s), "memset");
-    if (!rc && range[1] > range[0])
-        rc = hip_status(hipMemsetAsync(d_recv_status + id_base + range[0], SHD_NIC_QUEUED, range[1] - range[0], s),
-                        "memset");
-    if (!rc && range[1] > range[0])
-        rc = hip_status(hipMemsetAsync(d_recv_time + id_base + range[0], 0xff,
-                                       sizeof(uint64_t) * (range[1] - range[0]), s), "memset");
-    if (!rc && srange[1] > srange[0])
-        rc = hip_status(hipMemsetAsync(d_send_time + srange[0], 0xff, sizeof(uint64_t) * (srange[1] - srange[0]), s),
-                        "memset");
     if (!rc) {
         const char* mv = getenv("SHD_NIC_MERGED");
         if (mv && strcmp(mv, "0") == 0)
@@ -415,7 +416,6 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
     }
     if (!rc) rc = hip_status(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s), "D2H");
     if (!rc) rc = hip_status(hipStreamSynchronize(s), "k_nic_run");
-    (void)hipFree(d_err);
     if (rc) return rc;
     if (h_err & kErrRing) return shd_fail(-ENOSPC, "a router queue outgrew its ring (capacity %u)", ring_cap);
     if (h_err & kErrHost) return shd_fail(-EINVAL, "an event in a host's segment is addressed to another host");
@@ -425,5 +425,6 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
                                  "in one window");
     if (h_err & kErrId) return shd_fail(-ERANGE, "packet ids exceed the fate arrays");
     if (h_err & kErrAssert) return shd_fail(-EINVAL, "router dequeue before an entry's enqueue time");
+    if (h_err & kErrArgs) return shd_fail(-EINVAL, "events without lengths");
     return 0;
 }
