@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
-"""In-process A/B of a knob of the interface engine (shd_nic_run) on the C3
-round's output, as bench.py's nic leg runs it: alternating blocks of 10
-windows, HIP events on the launch stream, fates compared between arms.
-Usage: nic_probe.py ENV_NAME VALUE VALUE ...  (VALUE "-": unset)."""
+"""In-process A/B of an interface-engine knob (the bench's nic leg: the C3
+round's delivered events through every host's router + receive bucket),
+alternating arms, outputs compared.  Usage: nic_probe.py ENV V1 V2 ..."""
 import os
 import sys
 
@@ -13,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     import torch
-    from shadow_amd import Topology, scenario, synth, _lib
+    from shadow_amd import Topology, _lib, scenario, synth
     from shadow_amd.router import HEADER_UDP, Interfaces
     H, V, P = 100_000, 20_000, 10_000_000
     dev = torch.device("cuda", 0)
@@ -32,22 +31,18 @@ def main():
     d_cnt = torch.empty(2, dtype=torch.int64, device=dev)
     top.process_device(d_recs.data_ptr(), P, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
                        d_status.data_ptr(), d_cnt.data_ptr(), 0)
-    torch.cuda.synchronize()
-    delivered = int(d_off[H].item())
+    n = int(d_off[-1].item())
     lib = _lib.lib()
-    stream = torch.cuda.Stream(dev)
-    sptr = stream.cuda_stream
-    d_len = torch.empty(max(delivered, 1), dtype=torch.int32, device=dev)
-    _lib.check(lib.shd_event_lengths(d_out.data_ptr(), delivered, d_recs.data_ptr(), HEADER_UDP, d_len.data_ptr(),
-                                     sptr))
-    tmax = int(d_out.view(torch.int64).view(-1, 4)[:delivered, 0].max().item())
+    d_len = torch.empty(n, dtype=torch.int32, device=dev)
+    _lib.check(lib.shd_event_lengths(d_out.data_ptr(), n, d_recs.data_ptr(), HEADER_UDP, d_len.data_ptr(), None))
+    tmax = int(d_out.view(torch.int64).view(-1, 4)[:n, 0].max().item())
     gbit = 1_000_000_000 // 8 // 1024
     bw = np.full(H, gbit, dtype=np.uint64)
-    nic = Interfaces(H, bw, bw, 100_000_000, 4096, max(delivered, 1), device=dev)
-    states0 = nic.states.clone()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    nic = Interfaces(H, bw, bw, 100_000_000, 4096, n, device=dev)
+    s0 = nic.states.clone()
     name, vals = sys.argv[1], sys.argv[2:]
-    fates = {}
+    outs = {}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rep in range(3):
         for v in vals:
             if v == "-":
@@ -55,25 +50,19 @@ def main():
             else:
                 os.environ[name] = v
             ms = []
-            for r in range(11):
-                nic.states.copy_(states0)
-                torch.cuda.synchronize(dev)
-                ev0.record(stream)
-                nic.run_device(d_out.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), tmax + 1, 0, 0, stream=sptr)
-                ev1.record(stream)
-                torch.cuda.synchronize(dev)
+            for r in range(6):
+                nic.states.copy_(s0)
+                torch.cuda.synchronize()
+                e0.record()
+                nic.run_device(d_out.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), tmax + 1)
+                e1.record()
+                torch.cuda.synchronize()
                 if r:
-                    ms.append(ev0.elapsed_time(ev1))
-            t, st = nic.fates()
-            fates[v] = (t.clone() if hasattr(t, "clone") else np.copy(t), st.clone() if hasattr(st, "clone") else
-                        np.copy(st), nic.states.clone(), nic.rings.clone())
-            print(f"{name}={v} rep {rep}: window {np.mean(ms):.4f} ms (min {min(ms):.4f})", flush=True)
-    ref = fates[vals[0]]
-    same = True
-    for v in vals[1:]:
-        for a, b in zip(ref, fates[v]):
-            same &= bool((a == b).all()) if hasattr(a, "all") else a == b
-    print(f"fates and states identical: {same}", flush=True)
+                    ms.append(e0.elapsed_time(e1))
+            print(f"{name}={v} rep {rep}: shd_nic_run {np.median(ms):.4f} ms (median of 5)", flush=True)
+            outs[v] = (nic.recv_time.clone(), nic.recv_status.clone(), nic.states.clone(), nic.rings.clone())
+    same = all(all(torch.equal(a, b) for a, b in zip(outs[vals[0]], outs[v])) for v in vals[1:])
+    print(f"outputs identical: {same}", flush=True)
 
 
 if __name__ == "__main__":

@@ -215,7 +215,8 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
                                                 ShdCodelEntry* __restrict__ rings, uint32_t ring_cap,
                                                 uint32_t id_base, uint64_t* __restrict__ rtime,
                                                 uint8_t* __restrict__ rstat, uint64_t fate_cap,
-                                                uint64_t* __restrict__ stime, int* __restrict__ err) {
+                                                uint64_t* __restrict__ stime, int* __restrict__ err,
+                                                uint32_t flush_at, uint32_t inline_refill) {
     __shared__ uint64_t stage_t[kStage * 64];
     __shared__ uint8_t stage_s[kStage * 64];
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
@@ -270,6 +271,24 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
         l_nxt = elen[i + 1];
     }
     while (!bad) {
+        // A refill that comes next in the host's order while its router queue
+        // is empty (the common case: the queue drains at each arrival) runs
+        // here, in a loop of its own -- the same call, in the same order --
+        // so that a wave whose lanes reach their refills at different
+        // iterations does not run the whole merged body (arrival, CoDel
+        // dequeue, send) once more per lane's refill.
+        if (kMerged && inline_refill)
+            while (H.s.refill_pending && H.s.refill_time < window_end && H.q.empty()) {
+                const uint64_t tr = H.s.refill_time;
+                if (H.sk < kend && sends[H.sk].ready <= tr) break; // a send request first
+                if (i < iend && (a_cur.time < tr || (a_cur.time == tr && a_cur.src_host < self))) break; // an arrival
+                if (budget-- == 0) {
+                    bad |= kErrWindow;
+                    break;
+                }
+                H.refill(tr);
+            }
+        if (bad) break;
         if (budget-- == 0) {
             bad |= kErrWindow;
             break;
@@ -329,6 +348,10 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
             if (do_sched) schedule_if_needed(H.s, now);
         }
         if (H.q.bad) bad |= kErrAssert;
+        // the wave's lanes flush their staged fates together once one of them
+        // holds flush_at: a lane flushing alone (its stage full) makes the
+        // whole wave run the store loop for it, 64 times as often
+        if (__any(out.n >= flush_at)) out.flush();
     }
     // the window's arrivals still queued move to the ring
     while (!bad && H.q.qhead < H.q.qtail) {
@@ -400,18 +423,25 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
     int* d_err = t_err[dev];
     int h_err = 0;
     rc = hip_status(hipMemsetAsync(d_err, 0, sizeof(int), s), "memset");
+    // SHD_NIC_FLUSH: the staged-fate count at which a wave flushes together
+    // (kStage + 1: each lane on its own when its stage fills)
+    const char* fv = getenv("SHD_NIC_FLUSH");
+    const uint32_t flush_at = fv ? (uint32_t)atoi(fv) : 12;
+    // SHD_NIC_INLINE_REFILL=0: refills only as iterations of the merged loop
+    const char* iv = getenv("SHD_NIC_INLINE_REFILL");
+    const uint32_t inline_refill = !(iv && strcmp(iv, "0") == 0);
     if (!rc) {
         const char* mv = getenv("SHD_NIC_MERGED");
         if (mv && strcmp(mv, "0") == 0)
             hipLaunchKernelGGL(k_nic_run<false>, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base,
                                d_events, d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end,
                                bootstrap_end, d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status,
-                               fate_cap, d_send_time, d_err);
+                               fate_cap, d_send_time, d_err, flush_at, inline_refill);
         else
             hipLaunchKernelGGL(k_nic_run<true>, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base,
                                d_events, d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end,
                                bootstrap_end, d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status,
-                               fate_cap, d_send_time, d_err);
+                               fate_cap, d_send_time, d_err, flush_at, inline_refill);
         rc = hip_status(hipGetLastError(), "k_nic_run launch");
     }
     if (!rc) rc = hip_status(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s), "D2H");
