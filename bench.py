@@ -843,7 +843,7 @@ def nic_leg(lib, top, d_recs, d_out, d_off, delivered, H, dev, stream, reps=5):
                   "arrival" % (delivered, H),
         "ms_per_round": t, "events_per_s": delivered / (t * 1e-3),
         "received": int((stat[:delivered] == 1).sum()), "router_dropped": int((stat[:delivered] == 2).sum()),
-        "kernel": "k_nic_run (one lane per host; shd_nic_run incl. its memsets and offset reads)",
+        "kernel": "k_nic_run (one lane per host; shd_nic_run incl. its error-word memset and read-back)",
         "roofline": {"bound": "hbm", "achieved": alg / (t * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
                      "alg_bytes": "45 B per event (32 record + 4 length in, 8 time + 1 status out) + 256 B per host"},

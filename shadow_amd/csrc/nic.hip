@@ -216,7 +216,8 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
                                                 uint32_t id_base, uint64_t* __restrict__ rtime,
                                                 uint8_t* __restrict__ rstat, uint64_t fate_cap,
                                                 uint64_t* __restrict__ stime, int* __restrict__ err,
-                                                uint32_t flush_at, uint32_t inline_refill) {
+                                                uint32_t flush_at, uint32_t opts) {
+    const bool inline_refill = opts & 1u, fast_arrival = opts & 2u;
     __shared__ uint64_t stage_t[kStage * 64];
     __shared__ uint8_t stage_s[kStage * 64];
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
@@ -320,14 +321,31 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
             H.q.clen = l_cur;
             H.q.qtail = ++i;
             H.s.router.total_size += l_cur; // _routerqueuecodel_enqueue (:113-136)
+            const uint32_t l_prev = l_cur;
             a_cur = a_nxt;
             l_cur = l_nxt;
             if (i + 1 < iend) {
                 a_nxt = ev[i + 1];
                 l_nxt = elen[i + 1];
             }
-            if (kMerged) now = ta, do_recv = !buffered;
-            else if (!buffered) H.receive(ta);
+            if (kMerged && fast_arrival && !buffered && ta >= boot_end && H.s.recv_remaining >= kMtu &&
+                H.s.router.mode == 0) {
+                // the common arrival: the queue held nothing before it, the
+                // bucket has a packet's tokens and CoDel is not dropping, so
+                // receivePackets dequeues exactly this packet (sojourn 0:
+                // below target) and then finds the queue empty -- its
+                // effects, without the dequeue's general code
+                H.q.qhead++;
+                H.s.router.total_size -= l_prev;
+                H.s.router.interval_expire = 0;
+                out.put(id_base + i - 1, ta, SHD_NIC_RECEIVED);
+                consume(H.s.recv_remaining, l_prev);
+                schedule_if_needed(H.s, ta);
+            } else if (kMerged) {
+                now = ta, do_recv = !buffered;
+            } else if (!buffered) {
+                H.receive(ta);
+            }
         } else if (own_is_send) {
             if (ts >= window_end) {
                 bad |= kErrWindow;
@@ -427,21 +445,23 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
     // (kStage + 1: each lane on its own when its stage fills)
     const char* fv = getenv("SHD_NIC_FLUSH");
     const uint32_t flush_at = fv ? (uint32_t)atoi(fv) : 12;
-    // SHD_NIC_INLINE_REFILL=0: refills only as iterations of the merged loop
+    // SHD_NIC_INLINE_REFILL=0: refills only as iterations of the merged loop;
+    // SHD_NIC_FAST=0: every arrival's receive through the CoDel dequeue
     const char* iv = getenv("SHD_NIC_INLINE_REFILL");
-    const uint32_t inline_refill = !(iv && strcmp(iv, "0") == 0);
+    const char* fa = getenv("SHD_NIC_FAST");
+    const uint32_t opts = (iv && strcmp(iv, "0") == 0 ? 0u : 1u) | (fa && strcmp(fa, "0") == 0 ? 0u : 2u);
     if (!rc) {
         const char* mv = getenv("SHD_NIC_MERGED");
         if (mv && strcmp(mv, "0") == 0)
             hipLaunchKernelGGL(k_nic_run<false>, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base,
                                d_events, d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end,
                                bootstrap_end, d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status,
-                               fate_cap, d_send_time, d_err, flush_at, inline_refill);
+                               fate_cap, d_send_time, d_err, flush_at, opts);
         else
             hipLaunchKernelGGL(k_nic_run<true>, dim3((nhosts + 63) / 64), dim3(64), 0, s, nhosts, host_base,
                                d_events, d_event_offsets, d_event_lengths, d_sends, d_send_offsets, window_end,
                                bootstrap_end, d_states, d_rings, ring_cap, id_base, d_recv_time, d_recv_status,
-                               fate_cap, d_send_time, d_err, flush_at, inline_refill);
+                               fate_cap, d_send_time, d_err, flush_at, opts);
         rc = hip_status(hipGetLastError(), "k_nic_run launch");
     }
     if (!rc) rc = hip_status(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s), "D2H");
