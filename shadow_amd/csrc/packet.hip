@@ -4479,6 +4479,11 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_part2(const uint32_t* __restri
 }
 
 // region r = c * 128 + f: its keys are [M2 index (c, f, 0), (c, f + 1, 0))
+// kVec: the region's counters zeroed and read-modify-written 16 B per lane,
+// eight loads in flight per lane before the stores (the scalar form waits
+// on each counter's load before its store: latency-bound at one workgroup
+// per CU); the dense table 16-B aligned (the caller checks)
+template <bool kVec>
 __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ M1,
                                                       uint32_t C, uint32_t nt1, const uint32_t* __restrict__ M2,
                                                       uint32_t* __restrict__ dense, unsigned long long N) {
@@ -4492,7 +4497,10 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict
     const uint32_t beg = M2[mb + (size_t)f * ntc], end = M2[mb + (size_t)(f + 1) * ntc];
     if (beg == end) return;
     constexpr uint32_t R = 1u << kFoldRegionBits;
-    for (uint32_t j = threadIdx.x; j < R; j += kFoldWG) fc[j] = 0u;
+    if (kVec)
+        for (uint32_t j = threadIdx.x; j < R / 4; j += kFoldWG) reinterpret_cast<uint4*>(fc)[j] = uint4{0u, 0u, 0u, 0u};
+    else
+        for (uint32_t j = threadIdx.x; j < R; j += kFoldWG) fc[j] = 0u;
     __syncthreads();
     for (uint32_t i0 = beg + threadIdx.x; i0 < end; i0 += kFoldWG * 4) {
         uint32_t k[4];
@@ -4505,7 +4513,32 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict
     __syncthreads();
     const unsigned long long rb = (unsigned long long)r << kFoldRegionBits;
     const uint32_t lim = N - rb < R ? (uint32_t)(N - rb) : R;
-    for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
+    uint32_t j0 = 0;
+    if (kVec) {
+        constexpr int kU = R / 4 / kFoldWG; // 8: the whole region in one pass
+        const uint32_t lim4 = lim / 4;
+        const uint4* f4 = reinterpret_cast<const uint4*>(fc);
+        uint4* d4 = reinterpret_cast<uint4*>(dense + rb);
+        uint4 v[kU], d[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            v[u] = q < lim4 ? f4[q] : uint4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            if (q < lim4 && (v[u].x | v[u].y | v[u].z | v[u].w)) d[u] = d4[q];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            if (q < lim4 && (v[u].x | v[u].y | v[u].z | v[u].w))
+                d4[q] = uint4{d[u].x + v[u].x, d[u].y + v[u].y, d[u].z + v[u].z, d[u].w + v[u].w};
+        }
+        j0 = lim4 * 4; // (a partial last region's tail: one counter per lane)
+    }
+    for (uint32_t j = j0 + threadIdx.x; j < lim; j += kFoldWG) {
         const uint32_t v = fc[j];
         if (v) dense[rb + j] += v;
     }
@@ -4554,10 +4587,11 @@ int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, unsigned long long N, Fo
     if (int rc = fold_reserve(f, L)) return rc;
     static bool attr = false;
     if (!attr) {
-        if (int rc = hip_status(hipFuncSetAttribute((const void*)k_fold_add, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    4 << kFoldRegionBits),
-                                "hipFuncSetAttribute k_fold_add"))
-            return rc;
+        for (const void* fn : {(const void*)k_fold_add<true>, (const void*)k_fold_add<false>})
+            if (int rc = hip_status(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        4 << kFoldRegionBits),
+                                    "hipFuncSetAttribute k_fold_add"))
+                return rc;
         attr = true;
     }
     const uint32_t R = (uint32_t)(((N - 1) >> kFoldRegionBits) + 1);
@@ -4576,8 +4610,14 @@ int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, unsigned long long N, Fo
     hipLaunchKernelGGL(k_fold_hist2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2);
     scan_counts(f.M2, m2, f.M2, f.bsum, nullptr, s);
     hipLaunchKernelGGL(k_fold_part2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2, log);
-    hipLaunchKernelGGL(k_fold_add, dim3(R), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, f.M1, C, nt1, f.M2,
-                       dense, N);
+    // SHD_FOLD_VEC=0: the scalar read-modify-write
+    const char* fv = getenv("SHD_FOLD_VEC");
+    if (((uintptr_t)dense & 15u) == 0 && !(fv && strcmp(fv, "0") == 0))
+        hipLaunchKernelGGL(k_fold_add<true>, dim3(R), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, f.M1, C, nt1,
+                           f.M2, dense, N);
+    else
+        hipLaunchKernelGGL(k_fold_add<false>, dim3(R), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, f.M1, C,
+                           nt1, f.M2, dense, N);
     return hip_status(hipGetLastError(), "pcnt fold launch");
 }
 
