@@ -39,6 +39,7 @@ BYTES_MOVE_PER_EVENT = 32 + 32
 # and adds it into the u32 counters (PCNT_FOLD_BYTES per kept packet + the
 # counter lines it touches)
 PCNT_LOG_BYTES = 4
+TIMING_EVERY = 4  # the timed steps whose stages carry HIP events: one in TIMING_EVERY
 STAGES = ["packet_scatter", "scan", "place", "segment_sort"]
 
 
@@ -336,7 +337,10 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     xph["on"] = True
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        # stage events on every TIMING_EVERY-th timed step (each event record
+        # holds the next kernel back ~5 us, profiles/r05z_round_trace_gaps.log)
+        _lib.check(lib.shd_round_timing_pause(int(k % TIMING_EVERY != 0)))
         step()
     xph["on"] = False
     torch.cuda.synchronize(dev)
@@ -431,7 +435,8 @@ def main():
             "per_stage_kernels": dict(zip(STAGES, kernels)),
             "per_stage_GBps": dict(zip(STAGES, achieved)),
             "alg_bytes_per_launch": dict(zip(STAGES, alg_bytes)),
-            "timing": "HIP events on the launch stream, averaged over the timed steps",
+            "timing": "HIP events on the launch stream, averaged over the timed steps that carry them "
+                      "(every %d-th: an event record holds the next kernel back ~5 us)" % TIMING_EVERY,
             # the scatter's irreducible random requests: one table gather per
             # packet (3.16 GB table), against the measured rate of independent
             # 8-B gathers from a table of that size (scripts/ubench_fetch.hip)

@@ -575,6 +575,10 @@ int shd_memcpy(void* dst, const void* src, size_t bytes);
  * per-destination count), 1 scan, 2 place, 3 segment sort.  enable resets
  * the record; read sums the elapsed ms per stage over recorded launches. */
 int shd_round_timing_enable(int enable);
+/* Pauses (paused != 0) or resumes the recording without resetting it: a
+ * benchmark times only some rounds' stages (each event record holds the
+ * stream's next kernel back a few microseconds). */
+int shd_round_timing_pause(int paused);
 /* The grouping pipeline a round of n records over nhosts destinations runs
  * (SHD_PACKET_PIPELINE or the default): 0 bucket, 1 rank, 2 slab, 3 part. */
 int shd_round_pipeline_of(uint32_t nhosts, size_t n, int* pipe);

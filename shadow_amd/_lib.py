@@ -81,6 +81,7 @@ PROTOS = {
                                            _P]),
     "shd_deliv_sort_device": (C.c_int, [_P, _P, C.c_size_t, C.c_uint32, C.c_uint32, _P, _P, _P]),
     "shd_round_timing_enable": (C.c_int, [C.c_int]),
+    "shd_round_timing_pause": (C.c_int, [C.c_int]),
     "shd_round_timing_read": (C.c_int, [_dp, C.c_int, _ip]),
     "shd_round_exchange_phases": (C.c_int, [_dp, C.c_int, _ip]),
     "shd_round_pipeline_of": (C.c_int, [C.c_uint32, C.c_size_t, _ip]),

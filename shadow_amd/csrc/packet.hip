@@ -4003,6 +4003,7 @@ struct Timing {
     hipEvent_t ev[kMaxTimed][kStages + 1];
     int8_t at[kMaxTimed][kStages + 1]; // the event a boundary reads (a stage with no kernels: the previous one)
     bool created = false;
+    bool enabled = false; // (on: enabled and not paused)
 };
 Timing g_tm;
 
@@ -5039,8 +5040,13 @@ extern "C" int shd_round_timing_enable(int enable) {
                 if (hipEventCreate(&g_tm.ev[i][k]) != hipSuccess) return shd_fail(-EIO, "hipEventCreate");
         g_tm.created = true;
     }
-    g_tm.on = enable != 0;
+    g_tm.on = g_tm.enabled = enable != 0;
     g_tm.n = 0;
+    return 0;
+}
+
+extern "C" int shd_round_timing_pause(int paused) {
+    g_tm.on = g_tm.enabled && paused == 0;
     return 0;
 }
 

@@ -41,14 +41,15 @@ def test_stage_timing(ext, monkeypatch):
     torch.cuda.synchronize()
     _lib.check(lib.shd_round_timing_enable(1))
     t0 = time.perf_counter()
-    for _ in range(K):
+    for k in range(K + 2):  # (two more rounds with the recording paused: not counted)
+        _lib.check(lib.shd_round_timing_pause(int(k >= K)))
         rnd()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) * 1e3
     st, nl = (C.c_double * 4)(), C.c_int()
     _lib.check(lib.shd_round_timing_read(st, 4, C.byref(nl)))
     _lib.check(lib.shd_round_timing_enable(0))
-    assert nl.value == K
+    assert nl.value == K  # the paused rounds left no record
     assert st[0] > 0 and st[3] > 0, list(st)  # packet scatter, sort (the part pipeline: no scan / place)
     assert sum(st) <= wall, (list(st), wall)
     assert torch.equal(d_out, want)
