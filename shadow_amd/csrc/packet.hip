@@ -3578,6 +3578,17 @@ int ws_quiesce(Ws& w) {
 
 int ws_faults(Ws& w, bool completed, hipStream_t s);
 
+// SHD_DEBUG_WS_OOM=<tag>: the first growth of the per-bucket counters after
+// the tag changes fails with -ENOMEM, once, after the old buffers are freed
+// (tests of the callers' retry without the 8-B table, routes.c)
+bool dbg_oom_once() {
+    static char last[64];
+    const char* e = getenv("SHD_DEBUG_WS_OOM");
+    if (!e || !*e || strncmp(e, last, sizeof last - 1) == 0) return false;
+    strncpy(last, e, sizeof last - 1);
+    return true;
+}
+
 int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
     int rc = 0;
     if ((n > w.cap_n || m + 1 > w.cap_m || H + 1 > w.cap_h) && (rc = ws_quiesce(w))) return rc;
@@ -3623,6 +3634,7 @@ int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
         w.cnt1 = w.off1 = w.bsum = w.poff = w.cursor = nullptr;
         w.cap_m = 0;
         const size_t cap = m + 1 + (m >> 3) + 4096;
+        if (dbg_oom_once()) return shd_fail(-ENOMEM, "hipMalloc ws.cnt1: injected (SHD_DEBUG_WS_OOM)");
         if ((rc = hip_status(hipMalloc((void**)&w.cnt1, 4 * cap), "hipMalloc ws.cnt1")) ||
             (rc = hip_status(hipMalloc((void**)&w.off1, 4 * cap), "hipMalloc ws.off1")) ||
             (rc = hip_status(hipMalloc((void**)&w.bsum, 4 * (cap / kScanTile + 2)), "hipMalloc ws.bsum")) ||

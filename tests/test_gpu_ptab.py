@@ -131,3 +131,44 @@ def test_table_refused_when_it_does_not_fit(monkeypatch):
     oout, ostatus, omt = orc.round(ips2, pk, 110_000_000, 10**15)
     assert np.array_equal(d_status.cpu().numpy(), ostatus) and int(cnt[1]) == omt
     assert np.array_equal(d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]], oout)
+
+
+def test_round_retried_without_the_table_after_oom(monkeypatch):
+    """A round whose workspace does not fit beside the 8-B table
+    (SHD_DEBUG_WS_OOM: the per-bucket counters' allocation fails once, after
+    the old buffers were freed) drops the table and runs again from the f64
+    entries (shd_ptab_release_for_retry): the same results as the oracle's,
+    no stale buffer freed twice, and the next round runs clean."""
+    import uuid
+
+    import torch
+
+    from shadow_amd import Topology
+    from test_gpu_parity import GRAPHS
+    gml, H = GRAPHS["sparse300_ns"]
+    top = Topology(gml)
+    ips, st, verts = scenario.register_hosts(top, H, 1)
+    orc = O.OracleTopology(gml)
+    ips2, _, _ = scenario.register_hosts(orc, H, 1)
+    top.touch_all()
+    lat, rel, sv = top.table()
+    orc.preload(sv, lat, rel)
+    pk = synth.packet_batch(30000, H, 0x5EED0A04, 100_000_000, 10_000_000, st)
+    n = len(pk)
+    d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    oout, ostatus, omt = orc.round(ips2, pk, 110_000_000, 10**15)
+    monkeypatch.setenv("SHD_DEBUG_WS_OOM", uuid.uuid4().hex[:16])
+    for k in range(2):  # the retried round, then a clean one on the same workspace
+        top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                           d_status.data_ptr(), d_cnt.data_ptr(), 0)
+        torch.cuda.synchronize()
+        if k == 0:  # (the injected failure happened: its message is the thread's last error)
+            assert b"injected" in (_lib.lib().shd_last_error() or b"")
+        cnt = d_cnt.cpu().numpy().view(np.uint64)
+        assert np.array_equal(d_status.cpu().numpy(), ostatus) and int(cnt[1]) == omt
+        assert np.array_equal(d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]], oout)
