@@ -263,11 +263,11 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
     // the next arrival and its length in registers, the one after it in flight
     ShdDeliv a_cur{}, a_nxt{};
     uint32_t l_cur = 0, l_nxt = 0;
-    if (i < iend) {
+    if (!bad && i < iend) { // (bad: e.g. events without an event array -- nothing is read)
         a_cur = ev[i];
         l_cur = elen[i];
     }
-    if (i + 1 < iend) {
+    if (!bad && i + 1 < iend) {
         a_nxt = ev[i + 1];
         l_nxt = elen[i + 1];
     }

@@ -139,3 +139,18 @@ def test_errors_fail_loudly():
     with pytest.raises(ShdError) as e:
         G.run(ev, [0, 8], [1500] * 8, MS // 2)
     assert e.value.code == -28
+    # inputs every lane checks before anything runs: packet ids past the fate
+    # arrays (-ERANGE) and events without their lengths (-EINVAL); no host's
+    # state, fate or ring moves
+    ev = _events([(k * 10, 0) for k in range(4)], 1)
+    G = Interfaces(1, [1000], [1000], 0, 4, 4, host_base=1)
+    st0, t0 = G.state().copy(), G.fates()[0].copy()
+    with pytest.raises(ShdError) as e:
+        G.run(ev, [0, 4], [100] * 4, MS, id_base=1)
+    assert e.value.code == -34
+    d_ev = torch.from_numpy(ev.view(np.uint8)).cuda()
+    d_off = torch.from_numpy(np.array([0, 4], np.uint32).view(np.int32)).cuda()
+    with pytest.raises(ShdError) as e:
+        G.run_device(d_ev.data_ptr(), d_off.data_ptr(), 0, MS)
+    assert e.value.code == -22 and "lengths" in str(e.value)
+    assert G.state().tobytes() == st0.tobytes() and np.array_equal(G.fates()[0], t0)
