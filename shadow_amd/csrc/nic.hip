@@ -431,16 +431,23 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
         return shd_fail(-EINVAL, "missing buffer");
     if (d_send_offsets && (!d_sends || !d_send_time)) return shd_fail(-EINVAL, "send offsets without sends");
     hipStream_t s = (hipStream_t)stream;
-    // the error word: one per thread and device, kept (a round allocates nothing)
+    // the error word: one per thread and device, kept (a call allocates
+    // nothing), zero between calls (only a call that read a nonzero word
+    // clears it), read back into pinned memory
     static thread_local int* t_err[64];
+    static thread_local int* t_herr;
     int dev = 0;
     int rc = hip_status(hipGetDevice(&dev), "hipGetDevice");
     if (rc) return rc;
     if (dev < 0 || dev >= 64) return shd_fail(-EINVAL, "device %d", dev);
-    if (!t_err[dev] && (rc = hip_status(hipMalloc((void**)&t_err[dev], sizeof(int)), "hipMalloc nic"))) return rc;
+    if (!t_herr && (rc = hip_status(hipHostMalloc((void**)&t_herr, sizeof(int), hipHostMallocDefault), "hipHostMalloc nic")))
+        return rc;
+    if (!t_err[dev]) {
+        if ((rc = hip_status(hipMalloc((void**)&t_err[dev], sizeof(int)), "hipMalloc nic")) ||
+            (rc = hip_status(hipMemset(t_err[dev], 0, sizeof(int)), "memset nic")))
+            return rc;
+    }
     int* d_err = t_err[dev];
-    int h_err = 0;
-    rc = hip_status(hipMemsetAsync(d_err, 0, sizeof(int), s), "memset");
     // SHD_NIC_FLUSH: the staged-fate count at which a wave flushes together
     // (kStage + 1: each lane on its own when its stage fills)
     const char* fv = getenv("SHD_NIC_FLUSH");
@@ -464,9 +471,14 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
                                fate_cap, d_send_time, d_err, flush_at, opts);
         rc = hip_status(hipGetLastError(), "k_nic_run launch");
     }
-    if (!rc) rc = hip_status(hipMemcpyAsync(&h_err, d_err, sizeof(int), hipMemcpyDeviceToHost, s), "D2H");
+    if (!rc) rc = hip_status(hipMemcpyAsync(t_herr, d_err, sizeof(int), hipMemcpyDeviceToHost, s), "D2H");
     if (!rc) rc = hip_status(hipStreamSynchronize(s), "k_nic_run");
-    if (rc) return rc;
+    if (rc) {
+        (void)hipMemset(d_err, 0, sizeof(int)); // (whatever failed: the next call starts from zero)
+        return rc;
+    }
+    const int h_err = *t_herr;
+    if (h_err && (rc = hip_status(hipMemset(d_err, 0, sizeof(int)), "memset nic"))) return rc;
     if (h_err & kErrRing) return shd_fail(-ENOSPC, "a router queue outgrew its ring (capacity %u)", ring_cap);
     if (h_err & kErrHost) return shd_fail(-EINVAL, "an event in a host's segment is addressed to another host");
     if (h_err & kErrOrder) return shd_fail(-EINVAL, "a host's events are not in time order");
