@@ -30,10 +30,10 @@ for step in "$@"; do
     test)
         L=$D/pytest$i.log
         if [ -n "$arg" ]; then
-            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread -k "${arg//,/ }" \
+            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --durations=0 --timeout 1100 --timeout-method thread -k "${arg//,/ }" \
                 > $L 2>&1 || { tail -60 $L; exit 1; }
         else
-            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --timeout 1100 --timeout-method thread \
+            timeout -k 10 1150 python -u -m pytest $R/tests -m gpu -x -v -s --durations=0 --timeout 1100 --timeout-method thread \
                 > $L 2>&1 || { tail -60 $L; exit 1; }
         fi
         tail -3 $L ;;

@@ -55,18 +55,14 @@ class _UidTransport:
     """shd_transport_rccl_new over a world-1 torch.distributed group."""
 
     def __init__(self):
-        import os
-        import socket
+        import datetime
 
         import torch.distributed as dist
 
         from shadow_amd.transport import RcclTransport
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        dist.init_process_group("gloo", rank=0, world_size=1)
+        # an in-process store: no port to race for (world 1, this process only)
+        dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1,
+                                timeout=datetime.timedelta(seconds=60))
         self.x = RcclTransport(0)
         self.ranks = [self.x]
 

@@ -7,21 +7,13 @@ one all_gather; unequal or empty blocks: one broadcast per rank).
 The GPU side (kernels, regroup, row routing) runs in test_multirank_gpu.py."""
 import ctypes as C
 import os
-import socket
+import time
 
 import numpy as np
 import pytest
 import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+from rank_procs import RankFailed, run_ranks
 
 
 def _blocks(rank, world):
@@ -32,10 +24,8 @@ def _blocks(rank, world):
     return sizes, data
 
 
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, world):
     from shadow_amd.transport import TorchTransport
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     xp = TorchTransport(device=torch.device("cpu"))
     st = xp.struct
     assert st.rank == rank and st.world == world
@@ -60,8 +50,7 @@ def _worker(rank, world, port, q):
         offs = (C.c_uint64 * (world + 1))(*[b * 48 for b in bounds])
         assert st.allgatherv(None, tab.data_ptr(), offs, None) == 0, xp.error
         gathered.append(tab.numpy().tobytes())
-    q.put((rank, rsizes, dst[:sum(rsizes) * 32].numpy().tobytes(), gathered))
-    dist.destroy_process_group()
+    return rank, rsizes, dst[:sum(rsizes) * 32].numpy().tobytes(), gathered
 
 
 def _row_bounds(world, equal):
@@ -78,17 +67,8 @@ def _rows(rank, bounds):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_transport_collectives_gloo(world):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=240) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+def test_transport_collectives_gloo(world, tmp_path):
+    res = run_ranks(_worker, world, tmp_path, deadline=120)
     sent = [_blocks(r, world) for r in range(world)]
     for k, equal in enumerate((True, False)):
         bounds = _row_bounds(world, equal)
@@ -104,3 +84,46 @@ def test_transport_collectives_gloo(world):
             want.append(data[off:off + sizes[rank] * 32])
             assert rsizes[r] == sizes[rank]
         assert got == np.concatenate(want).tobytes()
+
+
+def _worker_or_die(rank, world):
+    return rank
+
+
+@pytest.mark.timeout(90)
+def test_rank_dying_before_rendezvous_fails_fast(tmp_path):
+    """One rank exits before it reaches init_process_group: the harness must
+    fail within seconds (not the 60 s init timeout, not a queue wait) and
+    leave no live child process behind."""
+    import multiprocessing
+    import psutil
+    before = {c.pid for c in psutil.Process().children(recursive=True)}
+    t0 = time.monotonic()
+    with pytest.raises(RankFailed, match="rank 1 exited with code 3"):
+        run_ranks(_worker_or_die, 2, tmp_path, env={"SHD_TEST_DIE_RANK": "1"}, deadline=60)
+    assert time.monotonic() - t0 < 45
+    left = [c for c in psutil.Process().children(recursive=True) if c.pid not in before and c.is_running()
+            and c.status() != psutil.STATUS_ZOMBIE]
+    assert not left, left
+    assert not [p for p in multiprocessing.active_children()]
+
+
+def _worker_hang(rank, world):
+    if rank == 0:
+        time.sleep(600)
+    return rank
+
+
+@pytest.mark.timeout(90)
+def test_rank_hanging_hits_the_deadline(tmp_path):
+    """A rank that never reports fails the test at the parent's deadline and
+    is killed, not joined forever."""
+    import psutil
+    before = {c.pid for c in psutil.Process().children(recursive=True)}
+    t0 = time.monotonic()
+    with pytest.raises(RankFailed, match="did not report"):
+        run_ranks(_worker_hang, 2, tmp_path, deadline=10)
+    assert time.monotonic() - t0 < 60
+    left = [c for c in psutil.Process().children(recursive=True) if c.pid not in before and c.is_running()
+            and c.status() != psutil.STATUS_ZOMBIE]
+    assert not left, left

@@ -19,11 +19,10 @@ Either way the union over ranks must equal the oracle's single round over
 all ranks' packets: the same events, per destination in event_compare order,
 and the same min delivered time.
 """
-import os
-import socket
-
 import numpy as np
 import pytest
+
+from rank_procs import run_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -36,146 +35,115 @@ def _gml():
     return synth.sparse_graph_gml(250, 0x5EED0801, ns_variant=True)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def _packets(rank, world, st):
     from shadow_amd import synth
     lo, hi = rank * H // world, (rank + 1) * H // world
     return synth.packet_batch(4000, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, hosts_lo=lo, hosts_hi=hi)
 
 
-def _worker(rank, world, port, mode, q, runs="1"):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SHD_XCHG_RUNS=runs)
+def _worker(rank, world, mode):
     import torch
     import torch.distributed as dist
 
     from shadow_amd import Topology, scenario, synth
     from shadow_amd.transport import TorchTransport
-    try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(0)
-        top = Topology(_gml())
-        ips, st, verts = scenario.register_hosts(top, H, seed=1)
-        A = top.slot_count()
-        row_bounds = [r * A // world for r in range(world + 1)]
-        host_bounds = [r * H // world for r in range(world + 1)]
-        pk = _packets(rank, world, st)
-        xp = TorchTransport(device=torch.device("cuda", 0))
-        table = b""
-        if mode in ("replicated", "fused"):
-            lo, hi = row_bounds[rank], row_bounds[rank + 1]
-            tab = torch.zeros(A * A * 2, dtype=torch.float64, device="cuda")
-            if hi > lo:
-                top.build_rows_device(lo, hi, tab.data_ptr())
-            torch.cuda.synchronize()
-            xp.register(tab)
-            top.allgather_rows(xp, tab.data_ptr(), row_bounds)
-            table = tab.cpu().numpy().tobytes()
-            top.adopt_table_device(tab.data_ptr())
-            top.touch_all()
-            recs = torch.from_numpy(pk.view(np.uint8)).cuda()
-            n = len(pk)
-        else:
-            lo, hi = row_bounds[rank], row_bounds[rank + 1]
-            shard = torch.empty(max(hi - lo, 1) * A * 2, dtype=torch.float64, device="cuda")
-            if hi > lo:
-                top.build_rows_device(lo, hi, shard.data_ptr() - lo * A * 16)
-            torch.cuda.synchronize()
-            mn = torch.tensor([top.shard_min_latency(shard.data_ptr(), lo, hi)], dtype=torch.float64)
-            mn[mn < 0] = float("inf")
-            dist.all_reduce(mn, op=dist.ReduceOp.MIN)
-            top.adopt_table_shard_device_resident(shard.data_ptr(), lo, hi, float(mn.item()))
-            src = torch.from_numpy(pk.view(np.uint8)).cuda()
-            scratch = torch.empty_like(src)
-            cap = 4000 * world
-            recs = torch.empty(cap * 32, dtype=torch.uint8, device="cuda")
-            xp.register(scratch, recs)
-            n = top.route_records(xp, src.data_ptr(), len(pk), row_bounds, scratch.data_ptr(), recs.data_ptr(), cap)
-        if mode == "fused":  # decide + group + exchange + merge in one call (24-B wire records)
-            cap = 4000 * world
-            d_send = torch.empty(max(n, 1) * 24, dtype=torch.uint8, device="cuda")
-            d_wrecv = torch.empty(cap * 24, dtype=torch.uint8, device="cuda")
-            d_final = torch.empty(cap * 32, dtype=torch.uint8, device="cuda")
-            d_status = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
-            d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
-            mine = host_bounds[rank + 1] - host_bounds[rank]
-            d_final_off = torch.empty(mine + 1, dtype=torch.int32, device="cuda")
-            xp.register(d_send, d_wrecv)
-            nrecv = top.process_exchange(xp, recs.data_ptr(), n, BARRIER, END, 0, host_bounds, d_send.data_ptr(),
-                                         d_status.data_ptr(), d_cnt.data_ptr(), d_wrecv.data_ptr(), cap,
-                                         d_final.data_ptr(), d_final_off.data_ptr())
-            status = d_status.cpu().numpy()[:n]
-            got = d_final.cpu().numpy().view(synth.DELIV_DTYPE)[:nrecv].copy()
-            offs = d_final_off.cpu().numpy()
-            assert offs[-1] == nrecv
-            assert np.array_equal(np.diff(offs), np.bincount(got["dst_host"] - host_bounds[rank], minlength=mine))
-            mt = torch.tensor([int(d_cnt.cpu().numpy().view(np.uint64)[1])], dtype=torch.float64)
-            dist.all_reduce(mt, op=dist.ReduceOp.MIN)
-            q.put((rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), table, None))
-            dist.destroy_process_group()
-            return
-        cap = max(n, 1) * world
-        d_out = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device="cuda")
-        d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    torch.cuda.set_device(0)
+    top = Topology(_gml())
+    ips, st, verts = scenario.register_hosts(top, H, seed=1)
+    A = top.slot_count()
+    row_bounds = [r * A // world for r in range(world + 1)]
+    host_bounds = [r * H // world for r in range(world + 1)]
+    pk = _packets(rank, world, st)
+    xp = TorchTransport(device=torch.device("cuda", 0))
+    table = b""
+    if mode in ("replicated", "fused"):
+        lo, hi = row_bounds[rank], row_bounds[rank + 1]
+        tab = torch.zeros(A * A * 2, dtype=torch.float64, device="cuda")
+        if hi > lo:
+            top.build_rows_device(lo, hi, tab.data_ptr())
+        torch.cuda.synchronize()
+        xp.register(tab)
+        top.allgather_rows(xp, tab.data_ptr(), row_bounds)
+        table = tab.cpu().numpy().tobytes()
+        top.adopt_table_device(tab.data_ptr())
+        top.touch_all()
+        recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+        n = len(pk)
+    else:
+        lo, hi = row_bounds[rank], row_bounds[rank + 1]
+        shard = torch.empty(max(hi - lo, 1) * A * 2, dtype=torch.float64, device="cuda")
+        if hi > lo:
+            top.build_rows_device(lo, hi, shard.data_ptr() - lo * A * 16)
+        torch.cuda.synchronize()
+        mn = torch.tensor([top.shard_min_latency(shard.data_ptr(), lo, hi)], dtype=torch.float64)
+        mn[mn < 0] = float("inf")
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        top.adopt_table_shard_device_resident(shard.data_ptr(), lo, hi, float(mn.item()))
+        src = torch.from_numpy(pk.view(np.uint8)).cuda()
+        scratch = torch.empty_like(src)
+        cap = 4000 * world
+        recs = torch.empty(cap * 32, dtype=torch.uint8, device="cuda")
+        xp.register(scratch, recs)
+        n = top.route_records(xp, src.data_ptr(), len(pk), row_bounds, scratch.data_ptr(), recs.data_ptr(), cap)
+    if mode == "fused":  # decide + group + exchange + merge in one call (24-B wire records)
+        cap = 4000 * world
+        d_send = torch.empty(max(n, 1) * 24, dtype=torch.uint8, device="cuda")
+        d_wrecv = torch.empty(cap * 24, dtype=torch.uint8, device="cuda")
+        d_final = torch.empty(cap * 32, dtype=torch.uint8, device="cuda")
         d_status = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
         d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
-        torch.cuda.synchronize()
-        top.process_device(recs.data_ptr(), n, BARRIER, END, 0, d_out.data_ptr(), d_off.data_ptr(),
-                           d_status.data_ptr(), d_cnt.data_ptr(), 0)
-        torch.cuda.synchronize()
-        status = d_status.cpu().numpy()[:n]
-        assert (status != 0xFF).all(), "a record reached a rank without its answering row"
-        d_recv = torch.empty(4000 * world * 32, dtype=torch.uint8, device="cuda")
-        d_final = torch.empty_like(d_recv)
         mine = host_bounds[rank + 1] - host_bounds[rank]
         d_final_off = torch.empty(mine + 1, dtype=torch.int32, device="cuda")
-        xp.register(d_out, d_recv)
-        nrecv = top.exchange(xp, d_out.data_ptr(), d_off.data_ptr(), host_bounds, d_recv.data_ptr(), 4000 * world,
-                             d_final.data_ptr(), d_final_off.data_ptr())
+        xp.register(d_send, d_wrecv)
+        nrecv = top.process_exchange(xp, recs.data_ptr(), n, BARRIER, END, 0, host_bounds, d_send.data_ptr(),
+                                     d_status.data_ptr(), d_cnt.data_ptr(), d_wrecv.data_ptr(), cap,
+                                     d_final.data_ptr(), d_final_off.data_ptr())
+        status = d_status.cpu().numpy()[:n]
         got = d_final.cpu().numpy().view(synth.DELIV_DTYPE)[:nrecv].copy()
         offs = d_final_off.cpu().numpy()
         assert offs[-1] == nrecv
         assert np.array_equal(np.diff(offs), np.bincount(got["dst_host"] - host_bounds[rank], minlength=mine))
         mt = torch.tensor([int(d_cnt.cpu().numpy().view(np.uint64)[1])], dtype=torch.float64)
         dist.all_reduce(mt, op=dist.ReduceOp.MIN)
-        q.put((rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), table, None))
-        dist.destroy_process_group()
-    except BaseException as e:  # report, then fail the process
-        import traceback
-        q.put((rank, b"", 0.0, 0, b"", traceback.format_exc()))
-        raise
+        return rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), table
+    cap = max(n, 1) * world
+    d_out = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device="cuda")
+    d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    d_status = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    top.process_device(recs.data_ptr(), n, BARRIER, END, 0, d_out.data_ptr(), d_off.data_ptr(),
+                       d_status.data_ptr(), d_cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    status = d_status.cpu().numpy()[:n]
+    assert (status != 0xFF).all(), "a record reached a rank without its answering row"
+    d_recv = torch.empty(4000 * world * 32, dtype=torch.uint8, device="cuda")
+    d_final = torch.empty_like(d_recv)
+    mine = host_bounds[rank + 1] - host_bounds[rank]
+    d_final_off = torch.empty(mine + 1, dtype=torch.int32, device="cuda")
+    xp.register(d_out, d_recv)
+    nrecv = top.exchange(xp, d_out.data_ptr(), d_off.data_ptr(), host_bounds, d_recv.data_ptr(), 4000 * world,
+                         d_final.data_ptr(), d_final_off.data_ptr())
+    got = d_final.cpu().numpy().view(synth.DELIV_DTYPE)[:nrecv].copy()
+    offs = d_final_off.cpu().numpy()
+    assert offs[-1] == nrecv
+    assert np.array_equal(np.diff(offs), np.bincount(got["dst_host"] - host_bounds[rank], minlength=mine))
+    mt = torch.tensor([int(d_cnt.cpu().numpy().view(np.uint64)[1])], dtype=torch.float64)
+    dist.all_reduce(mt, op=dist.ReduceOp.MIN)
+    return rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), table
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(200)
 @pytest.mark.parametrize("mode,world,runs", [("replicated", 2, "1"), ("replicated", 3, "1"), ("sharded", 2, "1"),
                                              ("sharded", 3, "1"), ("replicated", 3, "0"), ("sharded", 2, "0"),
                                              ("fused", 2, "1"), ("fused", 3, "1")])
-def test_multirank_round_through_c_abi(world, mode, runs):
+def test_multirank_round_through_c_abi(world, mode, runs, tmp_path):
     """runs "1": the owner merges the W received destination-sorted runs in
     place (default); "0": it re-scatters them into destination slabs (the
     round-2 regroup, SHD_XCHG_RUNS=0)."""
-    import torch.multiprocessing as mp
-
     import oracle_ctypes as O
     from shadow_amd import scenario, synth
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q, runs)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted(q.get(timeout=240) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-    errs = [e for *_, e in res if e]
-    assert not errs, errs[0]
-    assert all(p.exitcode == 0 for p in procs)
+    res = run_ranks(_worker, world, tmp_path, args=(mode,), env={"SHD_XCHG_RUNS": runs}, deadline=150)
     merged = np.concatenate([np.frombuffer(b, dtype=synth.DELIV_DTYPE) for _, b, *_ in res])
     orc = O.OracleTopology(_gml())
     ips, st, verts = scenario.register_hosts(orc, H, 1)
