@@ -62,6 +62,11 @@ def parse():
     ap.add_argument("--c4-hosts", type=int, default=200_000)
     ap.add_argument("--c4-rounds", type=int, default=1000, help="C4 packet rounds on the full table (N=1)")
     ap.add_argument("--c4-packets", type=int, default=1_000_000, help="packets per C4 round")
+    ap.add_argument("--batches", type=int, default=4,
+                    help="distinct packet batches resident in HBM, rotated so no round re-gathers the previous one's "
+                         "table lines (fresh inputs per step)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the §8d variant legs (ns-resolution C2 build and C3 round, C1 direct paths, Zipf C3)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05t_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
@@ -277,7 +282,14 @@ def main():
     hlo, hhi = rank * H // world, (rank + 1) * H // world
     pk = synth.packet_batch(P, H, 0x5EED0003 + rank, 100_000_000, 10_000_000, states, hosts_lo=hlo, hosts_hi=hhi)
     barrier_t, end_t = 110_000_000, 10**15
-    d_recs = torch.from_numpy(pk.view(np.uint8)).to(dev)
+    # fresh inputs per step: NB distinct batches (the same senders with new
+    # destinations, synth.redraw_destinations) resident in HBM and rotated,
+    # so no round gathers the table lines the previous round gathered (they
+    # cannot sit in the 256 MB Infinity Cache from the step before)
+    NB = max(1, args.batches)
+    pks = [pk] + [synth.redraw_destinations(pk, H, 0x5EED0030 + 64 * rank + k) for k in range(1, NB)]
+    d_recs_l = [torch.from_numpy(b.view(np.uint8)).to(dev) for b in pks]
+    rot = {"i": 0, "fixed": None}
     d_out = torch.empty(P * 32, dtype=torch.uint8, device=dev)
     d_off = torch.empty(H + 1, dtype=torch.int32, device=dev)
     d_status = torch.empty(P, dtype=torch.uint8, device=dev)
@@ -307,6 +319,10 @@ def main():
     ph_buf, ph_ok = (C.c_double * 8)(), C.c_int()
 
     def step():
+        bi = rot["fixed"] if rot["fixed"] is not None else rot["i"] % NB
+        rot["i"] += 1
+        last["batch"] = bi
+        d_recs = d_recs_l[bi]
         if world > 1 and not split:
             last["nrecv"] = top.process_exchange(xport, d_recs.data_ptr(), P, barrier_t, end_t, 0, own_lo,
                                                  d_send.data_ptr(), d_status.data_ptr(), d_cnt.data_ptr(),
@@ -357,6 +373,23 @@ def main():
     nl = C.c_int()
     _lib.check(lib.shd_round_timing_read(stage_ms, 4, C.byref(nl)))
     _lib.check(lib.shd_round_timing_enable(0))
+    lb = last["batch"]  # the batch of the last timed round (the legs below read its outputs)
+    pk, d_recs = pks[lb], d_recs_l[lb]
+    # beside it: the same K rounds replaying ONE batch (the rounds before
+    # round 6 timed this form; its lines can stay cache-resident across steps)
+    rep_ms = None
+    if NB > 1:
+        rot["fixed"] = lb
+        barrier()
+        torch.cuda.synchronize(dev)
+        r0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        top.path_counts_sync()
+        barrier()
+        rep_ms = max_over_ranks(time.perf_counter() - r0) / args.steps * 1e3
+        rot["fixed"] = None
     cnt = d_cnt.cpu().numpy().view(np.uint64)
     delivered = int(cnt[0])
     overflow = 0
@@ -416,6 +449,13 @@ def main():
         "vs_baseline": None,
         "dtype": "u64+f64",
         "data": "synthetic (seeded splitmix64 graph, hosts, packets; no datasets)",
+        "inputs": "fresh per step" if NB > 1 else "one batch replayed every step",
+        "input_batches": {"batches": NB, "rotation": "round k reads batch k mod %d (resident in HBM, %.2f GB)"
+                                                       % (NB, NB * P * 32 / 1e9),
+                          "what": "batch 0 = synth.packet_batch; batches 1.. = the same senders, send times and "
+                                  "rand_r pre-states with new uniform destinations (synth.redraw_destinations)",
+                          "fresh_ms_per_step": dt / args.steps * 1e3, "replayed_ms_per_step": rep_ms,
+                          "headline": "fresh"},
         "config": {
             "workload": f"C3 per-round packet hand-off: {P / 1e6:g}M packets/round/GPU over {H / 1e3:g}k hosts on "
                         f"the C2 sparse graph (V={V / 1e3:g}k); dst-sharded with RCCL all-to-all at N>1",
@@ -490,6 +530,12 @@ def main():
     if world == 1 and not args.no_host_api:
         result["host_api"] = host_api_leg(lib, top, pk, H, barrier_t, end_t, d_out, d_off, delivered,
                                           args.host_workers)
+
+    # ------------------------------- §8d variant legs (N=1): ns, direct, Zipf
+    if world == 1 and not args.no_variants:
+        result["variants"] = variant_legs(args, lib, top, gml, states, pks, d_recs_l, d_out, d_off, d_status, d_cnt,
+                                          dev, stream, tj)
+        torch.cuda.empty_cache()
 
     # ------------------------------------------------------------ C1 routing
     if not args.no_routing:
@@ -805,6 +851,210 @@ def main():
         if hasattr(xport, "close"):
             xport.close()
         dist.destroy_process_group()
+
+
+def timed_rounds(lib, top, recs, P, steps, warmup, dev, stream, d_out, d_off, d_status, d_cnt):
+    """K device rounds (shd_round_process_device) over the resident batches
+    `recs`, rotated (round k reads recs[k mod len]), timed like the headline:
+    synchronize on both sides, the path-counter fold inside, HIP-event stage
+    times on every TIMING_EVERY-th round.  Returns the leg's numbers and the
+    scatter kernel's roofline (the same algorithmic bytes as the headline's)."""
+    import torch
+
+    from shadow_amd import _lib
+    sptr = stream.cuda_stream
+    it = [0]
+
+    def one():
+        top.process_device(recs[it[0] % len(recs)].data_ptr(), P, 110_000_000, 10**15, 0, d_out.data_ptr(),
+                           d_off.data_ptr(), d_status.data_ptr(), d_cnt.data_ptr(), sptr)
+        it[0] += 1
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize(dev)
+    top.path_counts_sync()
+    _lib.check(lib.shd_round_timing_enable(1))
+    t0 = time.perf_counter()
+    for k in range(steps):
+        _lib.check(lib.shd_round_timing_pause(int(k % TIMING_EVERY != 0)))
+        one()
+    torch.cuda.synchronize(dev)
+    top.path_counts_sync()
+    dt = time.perf_counter() - t0
+    st = (C.c_double * 4)()
+    nl = C.c_int()
+    _lib.check(lib.shd_round_timing_read(st, 4, C.byref(nl)))
+    _lib.check(lib.shd_round_timing_enable(0))
+    per = [st[k] / max(nl.value, 1) for k in range(4)]
+    delivered = int(d_cnt.cpu().numpy().view(np.uint64)[0])
+    alg = (32 + 2 * 4 + 16 + 1 + PCNT_LOG_BYTES) * P + 16.0 * delivered
+    ach = alg / (per[0] * 1e-3) / 1e9 if per[0] > 0 else 0.0
+    return {
+        "rounds": steps, "batches": len(recs), "inputs": "fresh per step" if len(recs) > 1 else "one batch",
+        "ms_per_step": dt / steps * 1e3, "packets_per_s": P * steps / dt, "delivered_last_round": delivered,
+        "per_stage_ms": dict(zip(STAGES, per)),
+        "roofline": {"kernel": "k_part_scatter", "bound": "hbm", "alg_bytes_per_launch": alg, "achieved": ach,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                     "request_roofline": request_roofline(float(P), per[0] * 1e-3, "gath8_3160MB",
+                                                          "one 8-B table gather per packet") if per[0] > 0 else None,
+                     "attainable": attainable(P, delivered, per[0]) if per[0] > 0 else None},
+    }
+
+
+def variant_legs(args, lib, top, gml, states, pks, d_recs_l, d_out, d_off, d_status, d_cnt, dev, stream, tj):
+    """SURVEY.md §8d's variants beside the headline, each with its roofline
+    and the CPU oracle timed on a bounded sample (cores stated):
+      c2_ns_build  -- C2 (V=20k, H=50k) on the ns-resolution graph: fractional
+                      ms latencies (topology.c:290-295), the f64 kernel;
+      c3_ns_round  -- the C3 round on the ns-resolution graph's 100k-host table
+                      (ceil(lat * 1e6) at worker.c:548 on non-integer ms);
+      c1_direct    -- C1 with use_shortest_path=false: every pair's direct
+                      edge (topology.c:1816-1858);
+      c3_zipf      -- the C3 round with Zipf(1.1) senders (one host sends ~10%)."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from shadow_amd import Topology, scenario, synth
+    H, V, P = args.hosts, args.vertices, args.packets
+    cpu = not args.no_cpu_baseline
+    if cpu:
+        import oracle_ctypes as O  # checker/baseline only
+    threads = cpu_share()["threads_used"]
+    out = {}
+    K, W = args.steps, args.warmup
+    gml_ns = synth.sparse_graph_gml(V, 0x5EED0002, ns_variant=True)
+
+    # ---- C2 ns-variant build (f64 kernel)
+    H2 = args.c2_hosts
+    t2 = Topology(gml_ns, device=dev.index)
+    scenario.register_hosts(t2, H2, seed=1)
+    A2 = t2.slot_count()
+    tab2 = torch.empty(A2 * A2 * 2, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize(dev)
+    s0 = time.perf_counter()
+    t2.build_rows_device(0, A2, tab2.data_ptr())
+    torch.cuda.synchronize(dev)
+    tb2 = time.perf_counter() - s0
+    e2 = t2.info()["edges"]
+    leg = {"config": f"C2 ns variant: V={V} sparse graph, fractional-ms latencies, H={H2} hosts, A={A2}",
+           "build_s": tb2, "value": float(H2) ** 2 / tb2, "unit": "routed host-pairs/s",
+           "kernel": "k_sssp_slab (igraph-exact Dijkstra, f64 keys: the latencies are not whole ms)",
+           "roofline": routing_roofline(A2, tb2, 20.0 * 2 * e2 + 4 * (V + 1), A2, V, tj.get("routing_slab_c2_ns"))}
+    del tab2
+    if cpu:
+        o2 = O.OracleTopology(gml_ns)
+        _, _, v2 = scenario.register_hosts(o2, H2, seed=1)
+        sv2 = np.unique(v2).astype(np.int32)
+        k2 = 1024
+        per = cpu_rows_parallel(o2, sv2[:: max(1, len(sv2) // k2)][:k2], sv2, threads)
+        leg["cpu_baseline"] = {"value": float(H2) ** 2 / (per * len(sv2)), "unit": "routed host-pairs/s",
+                               "cores": threads, "kind": "port", "build_s_extrapolated": per * len(sv2),
+                               "sample": f"{k2} of {len(sv2)} source rows (evenly spaced), {threads} threads, "
+                                         "extrapolated to the full table"}
+        del o2
+    out["c2_ns_build"] = leg
+    del t2
+    log(f"variant C2 ns build: {tb2:.3f}s")
+
+    # ---- C3 round on the ns-variant table
+    tn = Topology(gml_ns, device=dev.index)
+    ips_n, st_n, verts_n = scenario.register_hosts(tn, H, seed=1)
+    assert np.array_equal(st_n, states), "host rand_r seeds differ between the graphs"
+    An = tn.slot_count()
+    tabn = tn.alloc_table(An * An * 16)
+    torch.cuda.synchronize(dev)
+    s0 = time.perf_counter()
+    tn.build_rows_device(0, An, tabn.ptr)
+    torch.cuda.synchronize(dev)
+    tbn = time.perf_counter() - s0
+    tn.adopt_table_device(tabn.ptr)
+    tn.touch_all()
+    leg = timed_rounds(lib, tn, d_recs_l, P, K, W, dev, stream, d_out, d_off, d_status, d_cnt)
+    leg.update({"config": f"C3 round on the ns-variant table: {P / 1e6:g}M packets over {H / 1e3:g}k hosts, "
+                          f"V={V} fractional-ms graph (A={An})", "table_build_s": tbn})
+    if cpu:
+        n_s = 2_000_000
+        pk_s = pks[0][:n_s]
+        orc = O.OracleTopology(gml_ns)
+        ipo, _, _ = scenario.register_hosts(orc, H, seed=1)
+        lat, rel, sv = tn.table()
+        orc.preload(sv, lat, rel)
+        del lat, rel
+        s0 = time.perf_counter()
+        orc.round(ipo, pk_s, 110_000_000, 10**15)
+        dtc = time.perf_counter() - s0
+        leg["cpu_baseline"] = {"value": n_s / dtc, "unit": "packets/s", "cores": 1, "kind": "port",
+                               "sample": f"the first {n_s} packets of batch 0 on the full ns-variant table "
+                                         f"(preloaded; routing excluded): {dtc:.2f}s"}
+        del orc
+    out["c3_ns_round"] = leg
+    del tn, tabn
+    log(f"variant C3 ns round: {leg['ms_per_step']:.3f} ms")
+
+    # ---- C1 with use_shortest_path=false (direct paths, R-10)
+    g1 = synth.complete_graph_gml(1000, 0x5EED0001)
+    t1 = Topology(g1, use_shortest_path=False, device=dev.index)
+    _, _, v1 = scenario.register_hosts(t1, 5000, seed=1)
+    A1 = t1.slot_count()
+    tab1 = torch.empty(A1 * A1 * 2, dtype=torch.float64, device=dev)
+    t1.build_rows_device(0, A1, tab1.data_ptr())  # warm
+    reps = 10
+    torch.cuda.synchronize(dev)
+    s0 = time.perf_counter()
+    for _ in range(reps):
+        t1.build_rows_device(0, A1, tab1.data_ptr())
+    torch.cuda.synchronize(dev)
+    td = (time.perf_counter() - s0) / reps
+    # per pair: the 16-B entry written; the edge id found in the source's
+    # incidence list and the edge's weight and reliability read
+    alg1 = 16.0 * A1 * A1 + 20.0 * 2 * t1.info()["edges"]
+    leg = {"config": f"C1 complete graph V=1000, H=5000 hosts, A={A1}, use_shortest_path=false",
+           "ms_per_table": td * 1e3, "value": 5000.0 ** 2 / td, "unit": "routed host-pairs/s",
+           "kernel": "direct-path gather (shd_dev_build_rows, use_sp=0)",
+           "roofline": {"bound": "hbm", "alg_bytes": alg1, "achieved": alg1 / td / 1e9, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": alg1 / td / 1e9 / HBM_PEAK_GBS}}
+    if cpu:
+        o1 = O.OracleTopology(g1, use_shortest_path=False)
+        _, _, vo = scenario.register_hosts(o1, 5000, seed=1)
+        svo = np.unique(vo).astype(np.int32)
+        s0 = time.perf_counter()
+        for s in svo:
+            o1.direct_row(int(s), svo)
+        tc = time.perf_counter() - s0
+        leg["cpu_baseline"] = {"value": 5000.0 ** 2 / tc, "unit": "routed host-pairs/s", "cores": 1, "kind": "port",
+                               "sample": f"all {len(svo)} rows of direct paths (orc_direct_row): {tc:.2f}s"}
+        del o1
+    out["c1_direct"] = leg
+    del t1, tab1
+    log(f"variant C1 direct: {td * 1e3:.3f} ms")
+
+    # ---- C3 with Zipf(1.1) senders, on the headline's table
+    pz = synth.packet_batch(P, H, 0x5EED0005, 100_000_000, 10_000_000, states, zipf=1.1)
+    pzs = [pz] + [synth.redraw_destinations(pz, H, 0x5EED0050 + k) for k in range(1, len(d_recs_l))]
+    dz = [torch.from_numpy(b.view(np.uint8)).to(dev) for b in pzs]
+    leg = timed_rounds(lib, top, dz, P, K, W, dev, stream, d_out, d_off, d_status, d_cnt)
+    top_share = float(np.bincount(pz["src_host"], minlength=H).max()) / P
+    leg.update({"config": f"C3 with Zipf(1.1) senders: {P / 1e6:g}M packets over {H / 1e3:g}k hosts, the top "
+                          f"sender {top_share:.1%} of them; destinations uniform"})
+    if cpu:
+        n_s = 2_000_000
+        lat, rel, sv = top.table()
+        orc = O.OracleTopology(gml)
+        ipo, _, _ = scenario.register_hosts(orc, H, seed=1)
+        orc.preload(sv, lat, rel)
+        del lat, rel
+        s0 = time.perf_counter()
+        orc.round(ipo, pz[:n_s], 110_000_000, 10**15)
+        dtc = time.perf_counter() - s0
+        leg["cpu_baseline"] = {"value": n_s / dtc, "unit": "packets/s", "cores": 1, "kind": "port",
+                               "sample": f"the first {n_s} packets of the Zipf batch on the full table (preloaded): "
+                                         f"{dtc:.2f}s"}
+        del orc
+    out["c3_zipf"] = leg
+    del dz
+    log(f"variant C3 zipf: {leg['ms_per_step']:.3f} ms")
+    return out
 
 
 BYTES_NIC_PER_EVENT = 32 + 4 + 8 + 1  # event record + length in; receive time + status out

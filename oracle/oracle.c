@@ -1152,6 +1152,13 @@ int orc_direct_path(OrcTopo* t, int s, int d, double* lat, double* rel) {
     return 0;
 }
 
+/* A row of direct paths (use_shortest_path=false, topology.c:1816-1858):
+ * orc_direct_path for every target; -1 / -1 where no edge joins them. */
+void orc_direct_row(OrcTopo* t, int src, const int* targets, int ntargets, double* lat, double* rel) {
+    for (int i = 0; i < ntargets; i++)
+        if (orc_direct_path(t, src, targets[i], &lat[i], &rel[i]) != 0) lat[i] = rel[i] = -1.0;
+}
+
 int orc_compute_row(OrcTopo* t, int src, const int* targets, int ntargets, double* lat, double* rel) {
     int V = t->V;
     unsigned char* is_t = (unsigned char*)calloc((size_t)V, 1);

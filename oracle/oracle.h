@@ -79,6 +79,7 @@ int orc_compute_row(OrcTopo* t, int src, const int* targets, int ntargets, doubl
                     double* rel);
 /* use_shortest_path=false value of (src,dst) (topology.c:1816-1858). */
 int orc_direct_path(OrcTopo* t, int src, int dst, double* lat, double* rel);
+void orc_direct_row(OrcTopo* t, int src, const int* targets, int ntargets, double* lat, double* rel);
 int orc_vertex_of_ip(OrcTopo* t, uint32_t ip_net);
 
 /* Seed the cache with a precomputed row table (for CPU baseline timing of the

@@ -224,8 +224,10 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
     // The window's arrivals start as queued (~0, SHD_NIC_QUEUED) and its send
     // requests unsent (~0): the wave's hosts' segments are one contiguous id
     // range, filled by the whole wave in coalesced strides (no offsets read
-    // back to the host, no memsets before the launch); the fence orders these
-    // stores before any lane's fates to the same ids.
+    // back to the host, no memsets before the launch); the barrier orders
+    // these stores before any lane's fates to the same ids (one wave per
+    // block: it costs nothing, and unlike a thread-scope fence it is a
+    // release/acquire pair under the HIP memory model).
     // (inputs every lane checks alike, so that no host runs when they fail)
     const uint32_t all0 = eoff[0], all1 = eoff[n];
     const int bad_all = ((uint64_t)id_base + all1 > fate_cap ? kErrId : 0) |
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(64) void k_nic_run(uint32_t n, uint32_t host_base, 
         if (soff)
             for (uint32_t k = soff[h0] + threadIdx.x; k < soff[h1]; k += 64) stime[k] = ~0ull;
     }
-    __threadfence_block();
+    __syncthreads();
     if (h >= n) return;
     const uint32_t self = host_base + h;
     FateStage out{rtime, rstat, stage_t + threadIdx.x, stage_s + threadIdx.x, 0u, 0u};
@@ -420,6 +422,38 @@ extern "C" int shd_event_lengths(const ShdDeliv* d_events, size_t n, const ShdPk
     return hip_status(hipGetLastError(), "k_event_lengths launch");
 }
 
+namespace {
+// Per-thread error words (device words per device, one pinned host word).
+// A word whose allocation no longer exists (a hipDeviceReset since) is
+// allocated again.
+struct NicErrWords {
+    int* d[64] = {};
+    int* h = nullptr;
+    ~NicErrWords() {
+        for (int* p : d)
+            if (p) (void)hipFree(p);
+        if (h) (void)hipHostFree(h);
+    }
+};
+thread_local NicErrWords t_nic_err;
+
+int nic_err_words(int dev, int** d_err) {
+    int rc = 0;
+    hipPointerAttribute_t at;
+    if (t_nic_err.h && hipPointerGetAttributes(&at, t_nic_err.h) != hipSuccess) t_nic_err.h = nullptr;
+    if (!t_nic_err.h &&
+        (rc = hip_status(hipHostMalloc((void**)&t_nic_err.h, sizeof(int), hipHostMallocDefault), "hipHostMalloc nic")))
+        return rc;
+    int*& w = t_nic_err.d[dev];
+    if (w && hipPointerGetAttributes(&at, w) != hipSuccess) w = nullptr;
+    if (!w && ((rc = hip_status(hipMalloc((void**)&w, sizeof(int)), "hipMalloc nic")) ||
+               (rc = hip_status(hipMemset(w, 0, sizeof(int)), "memset nic"))))
+        return rc;
+    *d_err = w;
+    return 0;
+}
+} // namespace
+
 extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* d_events,
                            const uint32_t* d_event_offsets, const uint32_t* d_event_lengths, const ShdNicSend* d_sends,
                            const uint32_t* d_send_offsets, uint64_t window_end, uint64_t bootstrap_end,
@@ -433,21 +467,17 @@ extern "C" int shd_nic_run(uint32_t nhosts, uint32_t host_base, const ShdDeliv* 
     hipStream_t s = (hipStream_t)stream;
     // the error word: one per thread and device, kept (a call allocates
     // nothing), zero between calls (only a call that read a nonzero word
-    // clears it), read back into pinned memory
-    static thread_local int* t_err[64];
-    static thread_local int* t_herr;
-    int dev = 0;
+    // clears it), read back into pinned memory; freed when the thread ends.
+    // The stream must belong to the calling thread's current device.
+    int dev = 0, sdev = 0;
     int rc = hip_status(hipGetDevice(&dev), "hipGetDevice");
     if (rc) return rc;
     if (dev < 0 || dev >= 64) return shd_fail(-EINVAL, "device %d", dev);
-    if (!t_herr && (rc = hip_status(hipHostMalloc((void**)&t_herr, sizeof(int), hipHostMallocDefault), "hipHostMalloc nic")))
-        return rc;
-    if (!t_err[dev]) {
-        if ((rc = hip_status(hipMalloc((void**)&t_err[dev], sizeof(int)), "hipMalloc nic")) ||
-            (rc = hip_status(hipMemset(t_err[dev], 0, sizeof(int)), "memset nic")))
-            return rc;
-    }
-    int* d_err = t_err[dev];
+    if (s && (rc = hip_status(hipStreamGetDevice(s, &sdev), "hipStreamGetDevice"))) return rc;
+    if (s && sdev != dev) return shd_fail(-EINVAL, "stream of device %d used on device %d", sdev, dev);
+    int* d_err = nullptr;
+    if ((rc = nic_err_words(dev, &d_err))) return rc;
+    int* t_herr = t_nic_err.h;
     // SHD_NIC_FLUSH: the staged-fate count at which a wave flushes together
     // (kStage + 1: each lane on its own when its stage fills)
     const char* fv = getenv("SHD_NIC_FLUSH");

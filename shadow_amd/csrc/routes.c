@@ -539,9 +539,36 @@ static int pcnt_dev(ShdTopology* t, const ShdPcnt* p) {
     return t->device;
 }
 
+/* Host-log mode: counts every logged key (global row * A + col; all-ones:
+ * not kept) into the host map, in chunks of at most 2^22 records. */
+static int pcnt_drain_host(ShdTopology* t, ShdPcnt* p) {
+    if (!p->log_fill) return 0;
+    int rc = shd_dev_init(p->device);
+    if (!rc) rc = shd_dev_sync(); /* every round that wrote the log has finished */
+    const size_t ksz = p->log64 ? 8 : 4, chunk = (size_t)1 << 22, A = (size_t)t->A;
+    void* h = malloc(ksz * (p->log_fill < chunk ? p->log_fill : chunk));
+    if (!h && !rc) rc = -ENOMEM;
+    for (size_t off = 0; !rc && off < p->log_fill; off += chunk) {
+        const size_t m = p->log_fill - off < chunk ? p->log_fill - off : chunk;
+        if ((rc = shd_dev_d2h(h, (const char*)p->log + off * ksz, m * ksz))) break;
+        pthread_mutex_lock(&t->pkt_mu);
+        for (size_t k = 0; k < m && !rc; k++) {
+            const uint64_t key = p->log64 ? ((const uint64_t*)h)[k] : ((const uint32_t*)h)[k];
+            if (key == (p->log64 ? UINT64_MAX : (uint64_t)UINT32_MAX)) continue;
+            rc = shd_count_packet_locked(t, (int)(key / A), (int)(key % A), 1);
+        }
+        pthread_mutex_unlock(&t->pkt_mu);
+    }
+    free(h);
+    if (!rc) p->log_fill = 0;
+    shd_dev_init(t->device);
+    return rc;
+}
+
 /* Adds the log into the counters (synchronous: every round that wrote it
  * has finished -- they may have run on any stream). */
 static int pcnt_fold(ShdTopology* t, ShdPcnt* p) {
+    if (p->hostlog) return pcnt_drain_host(t, p);
     if (!p->alloc || !p->log_fill) return 0;
     int rc = shd_dev_init(p->device);
     if (!rc) rc = shd_dev_sync();
@@ -594,23 +621,57 @@ int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
     int rc = 0;
     if (p->alloc && (p->lo != lo || p->hi != hi) && (rc = shd_pcnt_drop(t, p))) return rc;
     const int dev = pcnt_dev(t, p);
-    if (!p->alloc) {
+    /* SHD_DEBUG_PCNT_OOM (tests): "1" the dense counters' allocation fails as
+     * on a full device; "64" also with u64 log keys */
+    const char* oom = getenv("SHD_DEBUG_PCNT_OOM");
+    if (!p->alloc && !p->hostlog) {
         const size_t bytes = (size_t)(hi - lo) * (size_t)t->A * 4;
         void* d = NULL;
-        rc = shd_dev_malloc(&d, bytes);
-        if (rc == -ENOMEM && t->d_ptab_alloc) { /* the counters are not optional, the 8-B table is */
+        rc = oom && *oom && strcmp(oom, "0") ? -ENOMEM : shd_dev_malloc(&d, bytes);
+        if (rc == -ENOMEM && !oom && t->d_ptab_alloc) { /* the counters are worth more than the 8-B table */
             shd_ptab_drop(t);
             t->ptab_unavailable = 1;
             rc = shd_dev_malloc(&d, bytes);
         }
         if (!rc && ((rc = shd_dev_memset(d, 0, bytes)) || (rc = shd_dev_sync()))) shd_dev_free(d);
-        if (rc) return rc;
-        p->alloc = (uint32_t*)d;
-        p->base = p->alloc - (ptrdiff_t)lo * (ptrdiff_t)t->A;
-        p->lo = lo;
+        if (rc == -ENOMEM) { /* bounded fallback: log on the device, count on the host */
+            p->hostlog = 1;
+            p->device = dev;
+            p->log_fill = 0;
+            rc = 0;
+        } else if (rc) {
+            return rc;
+        } else {
+            p->alloc = (uint32_t*)d;
+            p->base = p->alloc - (ptrdiff_t)lo * (ptrdiff_t)t->A;
+            p->lo = lo;
+            p->hi = hi;
+            p->device = dev;
+            p->budget = 0;
+        }
+    }
+    if (p->hostlog) {
+        const int log64 = ((uint64_t)hi * (uint64_t)t->A > (uint64_t)UINT32_MAX) || (oom && !strcmp(oom, "64"));
+        if (log64 != p->log64 || p->log_fill + n > p->log_cap) { /* drain, then re-size when needed */
+            if ((rc = pcnt_drain_host(t, p))) return rc;
+            if (log64 != p->log64 || n > p->log_cap || !p->log) {
+                shd_dev_init(dev);
+                shd_dev_free(p->log);
+                p->log = NULL;
+                p->log_cap = 0;
+                p->log64 = log64;
+                size_t cap = pcnt_log_cap(n);
+                if (cap > ((size_t)1 << 26) && n <= ((size_t)1 << 26)) cap = (size_t)1 << 26; /* <= 512 MB */
+                if ((rc = shd_dev_malloc(&p->log, cap * (log64 ? 8 : 4)))) return rc;
+                p->log_cap = cap;
+            }
+        }
+        p->lo = lo; /* (keys are global: a new row range needs no drain) */
         p->hi = hi;
-        p->device = dev;
-        p->budget = 0;
+        p->mode = 1;
+        p->cur = (char*)p->log + p->log_fill * (p->log64 ? 8 : 4);
+        p->cur_n = n;
+        return shd_dev_init(dev);
     }
     const uint64_t T = pcnt_spill_at();
     if (p->budget + n >= T) { /* a counter below T could otherwise pass 2^32 - 1 */
@@ -644,7 +705,7 @@ int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
 
 void shd_pcnt_ctx(const ShdPcnt* p, ShdPktCtx* c) {
     c->plog = p->cur;
-    c->plog64 = 0;
+    c->plog64 = p->cur ? (uint32_t)p->log64 : 0u;
     c->pcnt = p->mode == 2 ? p->base : NULL;
 }
 
@@ -654,11 +715,17 @@ void shd_pcnt_commit(ShdPcnt* p, int rc) {
     p->cur_n = 0;
 }
 
-int shd_pcnt_sync(ShdTopology* t) {
-    int rc = 0;
-    pthread_mutex_lock(&t->round_mu);
-    rc = pcnt_fold(t, &t->pcnt);
+/* caller holds round_mu -- and keeps it across its reads of the counters,
+ * so no re-adoption (shd_shards_clear) can free them in between */
+int shd_pcnt_sync_locked(ShdTopology* t) {
+    int rc = pcnt_fold(t, &t->pcnt);
     for (int k = 0; k < t->nshards && !rc; k++) rc = pcnt_fold(t, &t->shards[k].pcnt);
+    return rc;
+}
+
+int shd_pcnt_sync(ShdTopology* t) {
+    pthread_mutex_lock(&t->round_mu);
+    int rc = shd_pcnt_sync_locked(t);
     pthread_mutex_unlock(&t->round_mu);
     return rc;
 }
@@ -669,8 +736,8 @@ int shd_topology_path_counts_sync(ShdTopology* t) {
 }
 
 int shd_pcnt_drop(ShdTopology* t, ShdPcnt* p) {
-    if (!p->alloc) return 0;
-    int rc = pcnt_spill(t, p, 1u); /* (folds the log first) */
+    if (!p->alloc && !p->hostlog) return 0;
+    int rc = p->hostlog ? pcnt_drain_host(t, p) : pcnt_spill(t, p, 1u); /* (folds the log first) */
     shd_dev_init(p->device);
     shd_dev_free(p->alloc);
     shd_dev_free(p->log);
@@ -686,7 +753,7 @@ void shd_pcnt_discard(ShdTopology* t) {
     ps[n++] = &t->pcnt;
     for (int k = 0; k < t->nshards; k++) ps[n++] = &t->shards[k].pcnt;
     for (int k = 0; k < n; k++)
-        if (ps[k]->alloc) {
+        if (ps[k]->alloc || ps[k]->hostlog) {
             shd_dev_init(ps[k]->device);
             shd_dev_free(ps[k]->alloc);
             shd_dev_free(ps[k]->log);

@@ -1309,7 +1309,8 @@ int shd_topology_copy_path_packet_counts(ShdTopology* t, int lo, int hi, uint64_
     if (lo < 0 || hi > t->A || lo > hi) return shd_fail(-EINVAL, "row range out of bounds");
     const size_t A = (size_t)t->A;
     memset(out, 0, sizeof(uint64_t) * (size_t)(hi - lo) * A);
-    int rc = shd_pcnt_sync(t); /* the rounds' logged counts folded in first */
+    pthread_mutex_lock(&t->round_mu);
+    int rc = shd_pcnt_sync_locked(t); /* the rounds' logged counts folded in first */
     if (!rc) rc = shd_pcnt_read_rows(t, lo, hi, out);
     pthread_mutex_lock(&t->pkt_mu);
     for (uint64_t h = 0; !rc && h < t->pkt_cap; h++)
@@ -1318,6 +1319,7 @@ int shd_topology_copy_path_packet_counts(ShdTopology* t, int lo, int hi, uint64_
             if (i >= lo && i < hi) out[(size_t)(i - lo) * A + (size_t)j] += t->pkt_vals[h];
         }
     pthread_mutex_unlock(&t->pkt_mu);
+    pthread_mutex_unlock(&t->round_mu);
     return rc;
 }
 
@@ -1333,7 +1335,8 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
      * keys is its count -- host map (explicit increments, spilled counters)
      * plus the rounds' device counters */
     uint64_t dv = 0, tot = 0;
-    int rc = shd_pcnt_sync(t); /* the rounds' logged counts folded in first */
+    pthread_mutex_lock(&t->round_mu);
+    int rc = shd_pcnt_sync_locked(t); /* the rounds' logged counts folded in first */
     for (int pass = 0; pass < (si == di ? 1 : 2) && !rc; pass++) {
         const int i = pass ? di : si, j = pass ? si : di;
         if (!(rc = shd_pcnt_read(t, i, j, &dv))) tot += dv;
@@ -1342,6 +1345,7 @@ int shd_topology_get_path_packet_count(ShdTopology* t, uint32_t s, uint32_t d, u
     tot += pkt_count_of(t, si, di);
     if (si != di) tot += pkt_count_of(t, di, si);
     pthread_mutex_unlock(&t->pkt_mu);
+    pthread_mutex_unlock(&t->round_mu);
     *out = tot;
     return rc;
 }
@@ -1398,14 +1402,26 @@ static void log_line(ShdTopology* t, ShdPathLogFn fn, void* user, int i, int j, 
  * released self paths, and stored direct pairs.  Lines come in (source,
  * destination) vertex order; the reference walks glib hash tables, whose
  * order is unspecified. */
+static int log_cached_paths_locked(ShdTopology* t, ShdPathLogFn fn, void* user, uint64_t* nout);
+
 int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, uint64_t* nlines) {
     if (!t || !fn) return -EINVAL;
     uint64_t n = 0;
     if (nlines) *nlines = 0;
     if (!__atomic_load_n(&t->ready, __ATOMIC_ACQUIRE)) return 0;
     int rc = shd_release_sync(t, 1); /* (topology_free's log follows every release) */
-    if (!rc) rc = shd_pcnt_sync(t); /* and every round's path packet counts */
     if (rc) return rc;
+    pthread_mutex_lock(&t->round_mu); /* (held across the counter reads: see shd_pcnt_sync_locked) */
+    rc = shd_pcnt_sync_locked(t); /* and every round's path packet counts */
+    if (!rc) rc = log_cached_paths_locked(t, fn, user, &n);
+    pthread_mutex_unlock(&t->round_mu);
+    if (nlines) *nlines = n;
+    return rc;
+}
+
+static int log_cached_paths_locked(ShdTopology* t, ShdPathLogFn fn, void* user, uint64_t* nout) {
+    int rc = 0;
+    uint64_t n = 0;
     const int A = t->A;
     ShdEntry* row = NULL;
     if (!t->h_tab) {
@@ -1454,7 +1470,7 @@ int shd_topology_log_cached_paths(ShdTopology* t, ShdPathLogFn fn, void* user, u
     pthread_mutex_unlock(&t->pkt_mu);
     free(row);
     free(prow);
-    if (nlines) *nlines = n;
+    *nout = n;
     return rc;
 }
 
@@ -1467,8 +1483,10 @@ void shd_shards_clear(ShdTopology* t) {
     (void)shd_release_sync(t, 0); /* nothing of the old table stays queued or in flight */
     /* the old table's path packet counts stay, in the host map (teardown:
      * already discarded) */
+    pthread_mutex_lock(&t->round_mu); /* (the counter readers hold it across their reads) */
     (void)shd_pcnt_drop(t, &t->pcnt);
     for (int k = 0; k < t->nshards; k++) (void)shd_pcnt_drop(t, &t->shards[k].pcnt);
+    pthread_mutex_unlock(&t->round_mu);
     shd_rel_list_free(&t->relq);
     shd_rel_list_free(&t->relself);
     for (int k = 0; k < t->nshards; k++) {

@@ -85,8 +85,13 @@ typedef struct {
      * cur_n: the slice reserved for the round being launched */
     void* log;
     size_t log_cap, log_fill;
-    int log64; /* (always 0: the fold takes u32 keys) */
+    int log64; /* u64 keys (host-log mode on tables of 2^32 entries or more; the fold takes u32) */
     int mode;  /* this round's: 0 none, 1 log, 2 atomic */
+    /* host-log mode: the dense counters did not fit on the device (-ENOMEM
+     * even with the 8-B table dropped), so alloc stays NULL and the rounds
+     * only log; the log is drained into the host map (u64 counters) when it
+     * is full and before every read -- bounded device memory, slower reads */
+    int hostlog;
     void* cur;
     size_t cur_n;
     void* fold; /* shd_dev_pcnt_fold scratch */
@@ -259,6 +264,7 @@ void shd_pcnt_ctx(const ShdPcnt* p, ShdPktCtx* c);
 /* folds every log of the topology into its counters (takes round_mu; the
  * readers call it before reading) */
 int shd_pcnt_sync(ShdTopology* t);
+int shd_pcnt_sync_locked(ShdTopology* t); /* (caller holds round_mu) */
 int shd_pcnt_drop(ShdTopology* t, ShdPcnt* p);
 /* frees every device counter without folding (topology teardown) */
 void shd_pcnt_discard(ShdTopology* t);

@@ -756,7 +756,11 @@ int exchange_split(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_re
         return local_rc ? local_rc : rc2;
     }
     // (the matrix went out saying this rank is fine: a later failure still
-    // takes part in both groups below, then reports)
+    // takes part in both groups below and in the closing status agreement)
+    if (!local_rc) { // SHD_DEBUG_FAIL_LATE_RANK=r: rank r fails after its matrix row went out
+        const char* f = getenv("SHD_DEBUG_FAIL_LATE_RANK");
+        if (f && atoi(f) == me) local_rc = shd_fail(-EIO, "debug: injected late failure of rank %d", me);
+    }
     if (!k.mid_done && (rc = split_mid(&k))) return rc;
     (void)hipEventRecord(ev[kEvB], s);
     if ((rc = hip_status(hipEventSynchronize(ev[kEvE]), "exchange counts"))) return rc;
@@ -832,11 +836,28 @@ int exchange_split(const ShdPktCtx* c, const ShdTransport* x, const ShdPkt* d_re
     (void)hipEventRecord(ev[kEvEnd], s);
     rc = shd_dev_ws_sync(c->ws, (void*)s);
     if (!rc) rc = hip_status(hipStreamSynchronize(xs), "transfer stream");
-    if (local_rc) return local_rc;
-    if (g1) return g1;
-    if (g2) return g2;
-    if (mg) return mg;
-    if (rc) return rc;
+    // closing agreement: a rank that failed after its matrix row said it was
+    // fine has still sent (possibly half-written) blocks in both groups, so
+    // every rank learns every rank's final status before any returns, and
+    // all of them fail together -- the rule the front all-gather keeps for
+    // failures before the exchange
+    const int mine_rc = local_rc ? local_rc : g1 ? g1 : g2 ? g2 : mg ? mg : rc;
+    int failed_rank = -1;
+    {
+        std::vector<uint64_t> moff(W + 1);
+        for (int r = 0; r <= W; r++) moff[r] = 8ull * rw * (uint64_t)r;
+        h_mat[(size_t)me * rw] = mine_rc ? 1ull : 0ull;
+        int a = hip_status(hipMemcpyAsync(d_mat + (size_t)me * rw, h_mat + (size_t)me * rw, 8, hipMemcpyHostToDevice, s),
+                           "status H2D");
+        if (!a) a = x->allgatherv(x->user, d_mat, moff.data(), (void*)s);
+        if (!a) a = hip_status(hipMemcpyAsync(h_mat, d_mat, 8 * rw * (size_t)W, hipMemcpyDeviceToHost, s), "status D2H");
+        if (!a) a = hip_status(hipStreamSynchronize(s), "status sync");
+        if (a) return mine_rc ? mine_rc : (a < 0 ? a : -EIO);
+        for (int r = 0; r < W && failed_rank < 0; r++)
+            if (h_mat[(size_t)r * rw]) failed_rank = r;
+    }
+    if (mine_rc) return mine_rc;
+    if (failed_rank >= 0) return shd_fail(-EIO, "rank %d failed during the exchange", failed_rank);
     t_phase[0] = ev_ms(ev[kEv0], ev[kEvFront]) + ev_ms(ev[kEvCounts], ev[kEvB]);
     t_phase[1] = ev_ms(ev[kEvFront], ev[kEvCounts]);
     t_phase[2] = ev_ms(ev[kEvG1s], ev[kEvG1]);

@@ -62,6 +62,8 @@ lib.orc_controller_next_min_jump_ns.argtypes = [C.c_void_p]
 lib.orc_compute_row.restype = C.c_int
 lib.orc_compute_row.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
 lib.orc_direct_path.restype = C.c_int
+lib.orc_direct_row.restype = None
+lib.orc_direct_row.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
 lib.orc_direct_path.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 lib.orc_vertex_of_ip.restype = C.c_int
 lib.orc_vertex_of_ip.argtypes = [C.c_void_p, C.c_uint32]
@@ -168,6 +170,14 @@ class OracleTopology:
         lat = np.empty(len(targets), dtype=np.float64)
         rel = np.empty(len(targets), dtype=np.float64)
         lib.orc_compute_row(self.h, int(src), targets.ctypes.data, len(targets), lat.ctypes.data, rel.ctypes.data)
+        return lat, rel
+
+    def direct_row(self, src, targets):
+        """orc_direct_row: the direct paths from src to every target (-1: no edge)."""
+        targets = np.ascontiguousarray(targets, dtype=np.int32)
+        lat = np.empty(len(targets), dtype=np.float64)
+        rel = np.empty(len(targets), dtype=np.float64)
+        lib.orc_direct_row(self.h, int(src), targets.ctypes.data, len(targets), lat.ctypes.data, rel.ctypes.data)
         return lat, rel
 
     def direct(self, s, d):

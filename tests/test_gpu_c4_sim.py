@@ -33,7 +33,7 @@ def progress(t0, *a):
     print(f"[c4sim {time.perf_counter() - t0:7.1f}s]", *a, flush=True)
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(60)
 def test_c4_three_simulated_rounds():
     import torch
     t_start = time.perf_counter()

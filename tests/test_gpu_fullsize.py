@@ -46,7 +46,7 @@ def device_round(top, pk, H, barrier=BARRIER, end=END, boot=0):
     return out, d_off.cpu().numpy().astype(np.int64), d_status.cpu().numpy(), int(cnt[1])
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("ns", [False, True], ids=["ms", "ns"])
 def test_c1_full_table_bit_exact(ns):
     """configs[1]: every row of the V=1000 / H=5000 complete-graph table (the
@@ -69,7 +69,7 @@ def test_c1_full_table_bit_exact(ns):
         assert np.array_equal(bits(d.cpu().numpy().reshape(996, 996)), bits(olat))
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("ns", [False, True], ids=["ms", "ns"])
 def test_c2_full_table_bit_exact(ns):
     """configs[2]: the V = 20k sparse graph with 50k hosts; every one of the
@@ -112,7 +112,7 @@ def test_c2_full_table_bit_exact(ns):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.timeout(500)
+@pytest.mark.timeout(60)
 def test_c3_uniform_unrestricted_round_bit_exact(monkeypatch):
     """configs[3] at full size with the bench's own distribution: 10M packets,
     senders and destinations uniform over all 100k hosts (segments of ~92
@@ -204,7 +204,7 @@ def c4():
     torch.cuda.empty_cache()
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(90)
 def test_c4_sampled_rows_bit_exact(c4):
     """1,027 full-length rows (first, second, last and 1,024 evenly spaced) of
     the 86k x 86k slab-kernel table against the oracle's Dijkstra."""
@@ -216,7 +216,7 @@ def test_c4_sampled_rows_bit_exact(c4):
     assert not bad, f"rows differ: {bad[:8]}"
 
 
-@pytest.mark.timeout(900)
+@pytest.mark.timeout(250)
 def test_c4_all_rows_bit_exact(c4):
     """Every one of the 86,603 rows of the C4 table -- latencies AND
     reliabilities (the tie-dependent half, topology.c:1578-1814) -- against the
@@ -244,7 +244,7 @@ def test_c4_all_rows_bit_exact(c4):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(60)
 def test_c4_frontier_latencies_all_rows(c4):
     """The frontier SSSP's latencies for all 86,603 rows of C4 against the
     heap kernel's table (an independent algorithm: Dial's buckets vs igraph's
@@ -265,7 +265,7 @@ def test_c4_frontier_latencies_all_rows(c4):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.timeout(400)
+@pytest.mark.timeout(60)
 def test_c4_round_all_hosts_bit_exact(c4):
     """A device-resident C4 round (1M packets) whose packets involve all 200k
     hosts: every pair's owner row (the lower slot: rows released in slot

@@ -330,19 +330,25 @@ def test_device_api_matches_oracle_after_touch_all(pipeline):
                                      a.ravel(), b.ravel())
 
 
-@pytest.mark.parametrize("mode", ["log", "log_small", "atomic"])
+@pytest.mark.parametrize("mode", ["log", "log_small", "atomic", "oom", "oom64_small"])
 @pytest.mark.parametrize("api", ["host", "device"])
 def test_path_counters_spill_to_host(api, mode, monkeypatch):
     """The device counters move to the host map before any could wrap
     (SHD_PCNT_SPILL_AT lowers the 2^31 threshold to 3): five rounds, every
     cached path's count equal to the oracle's after each.  Modes: the log
     (folded at each read), a log of 4,000 records (each round but the first
-    folds the previous one first: SHD_PCNT_LOG) and the per-packet atomic."""
+    folds the previous one first: SHD_PCNT_LOG) and the per-packet atomic.
+    oom: the dense counters' allocation fails (SHD_DEBUG_PCNT_OOM), so the
+    rounds only log and the log drains into the host map -- with u32 keys,
+    and with u64 keys (the form of tables of 2^32 entries or more) in a log
+    of 4,000 records that drains before each round."""
     import torch
     monkeypatch.setenv("SHD_PCNT_SPILL_AT", "3")
     monkeypatch.setenv("SHD_PCNT", "atomic" if mode == "atomic" else "log")
-    if mode == "log_small":
+    if mode.endswith("_small"):
         monkeypatch.setenv("SHD_PCNT_LOG", "4000")
+    if mode.startswith("oom"):
+        monkeypatch.setenv("SHD_DEBUG_PCNT_OOM", "64" if "64" in mode else "1")
     gml, H = GRAPHS["complete30_ms"]
     top, orc, ips, st = make_pair(gml, H)
     if api == "device":
@@ -932,7 +938,7 @@ def test_minplus_needs_whole_ms():
     assert ei.value.code == -95  # ENOTSUP
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(60)
 def test_large_complete_graph_list_handles():
     """A complete graph with more than 2^23 incidence entries (V = 3,000: 9M):
     list starts above 2^23 in the 24-bit handles (read unsigned); sampled

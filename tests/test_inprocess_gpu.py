@@ -170,7 +170,7 @@ def _check_union(bufs, res, world, host_bounds, ref, mt, nrec=None):
                                                          minlength=host_bounds[r + 1] - host_bounds[r]))
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("kind,world", [("local", 2), ("local", 3), ("rccl_all", 1), ("rccl_uid", 1)])
 @pytest.mark.parametrize("fused", [True, False], ids=["process_exchange", "device+exchange"])
 @pytest.mark.parametrize("split", ["1", "0"], ids=["split", "one_group"])
@@ -224,7 +224,7 @@ def test_threads_as_ranks(kind, world, fused, split, monkeypatch):
     _check_counts(tops)
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("hot", [1, 2, 6])
 @pytest.mark.parametrize("wire_sorted", ["1", "0"], ids=["sorted_wire", "unsorted_wire"])
@@ -260,7 +260,7 @@ def test_exchange_long_segments(world, hot, wire_sorted, split, monkeypatch):
     _check_counts(tops)
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("bounds", [[0, 1, 64, 200, H], [0, 150, 150, 151, H], [0, 0, 0, 0, H], [0, H, H, H, H],
                                     [0, 37, 38, 299, H]], ids=["ragged", "empty_mid", "last_owns_all",
                                                                "first_owns_all", "singletons"])
@@ -295,7 +295,7 @@ def test_uneven_owner_bounds(bounds, split, monkeypatch):
     _check_counts(tops)
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("kind,world", [("local", 2), ("rccl_all", 1)])
 def test_row_sharded_route_decide_exchange(kind, world):
     """C4 at N>1: the rows stay sharded (no all-gather); every record goes to
@@ -332,7 +332,7 @@ def test_row_sharded_route_decide_exchange(kind, world):
     _check_counts(tops)  # (each record counted on the rank holding its answering row)
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("kind,world", [("local", 2), ("local", 3)])
 @pytest.mark.parametrize("split", ["1", "0"], ids=["split", "one_group"])
 def test_one_rank_failing_fails_every_rank(kind, world, split, monkeypatch):
@@ -363,3 +363,38 @@ def test_one_rank_failing_fails_every_rank(kind, world, split, monkeypatch):
         xps.close()
     assert all(isinstance(e, ShdError) and e.code == -errno.EIO for e in errs), errs
     assert "injected" in str(errs[1]) and all("rank 1 failed" in str(errs[r]) for r in range(world) if r != 1)
+
+
+@pytest.mark.timeout(60)
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank_failing_after_its_counts_fails_every_rank(world, monkeypatch):
+    """The split exchange's late failure (SHD_DEBUG_FAIL_LATE_RANK): the rank's
+    count row already went out saying it was fine, so it still sends in both
+    groups; the closing status all-gather then makes every rank fail
+    together (-EIO), instead of the peers merging its half-written blocks
+    and returning 0."""
+    import errno
+
+    from shadow_amd._lib import ShdError
+    gml, tops, A, host_bounds, bufs = _setup(world)
+    xps = _transports("local", world)
+    monkeypatch.setenv("SHD_DEBUG_FAIL_LATE_RANK", "1")
+    monkeypatch.setenv("SHD_XCHG_SPLIT", "1")
+
+    def rank_main(r):
+        top, _ = tops[r]
+        b, xp = bufs[r], xps.ranks[r]
+        top.build_rows_device(0, A, b["tab"].data_ptr())
+        top.adopt_table_device(b["tab"].data_ptr())
+        top.touch_all()
+        return top.process_exchange(xp, b["recs"].data_ptr(), NPK, BARRIER, END, 0, host_bounds,
+                                    b["send"].data_ptr(), b["status"].data_ptr(), b["cnt"].data_ptr(),
+                                    b["recv"].data_ptr(), NPK * world, b["fin"].data_ptr(), b["fin_off"].data_ptr())
+
+    try:
+        res, errs = _run_ranks(world, rank_main)
+    finally:
+        xps.close()
+    assert all(isinstance(e, ShdError) and e.code == -errno.EIO for e in errs), errs
+    assert "injected late" in str(errs[1])
+    assert all("rank 1 failed during the exchange" in str(errs[r]) for r in range(world) if r != 1), errs

@@ -133,7 +133,7 @@ def _worker(rank, world, mode):
     return rank, got.tobytes(), float(mt.item()), int((status == 1).sum()), table
 
 
-@pytest.mark.timeout(200)
+@pytest.mark.timeout(60)
 @pytest.mark.parametrize("mode,world,runs", [("replicated", 2, "1"), ("replicated", 3, "1"), ("sharded", 2, "1"),
                                              ("sharded", 3, "1"), ("replicated", 3, "0"), ("sharded", 2, "0"),
                                              ("fused", 2, "1"), ("fused", 3, "1")])
@@ -143,7 +143,7 @@ def test_multirank_round_through_c_abi(world, mode, runs, tmp_path):
     round-2 regroup, SHD_XCHG_RUNS=0)."""
     import oracle_ctypes as O
     from shadow_amd import scenario, synth
-    res = run_ranks(_worker, world, tmp_path, args=(mode,), env={"SHD_XCHG_RUNS": runs}, deadline=150)
+    res = run_ranks(_worker, world, tmp_path, args=(mode,), env={"SHD_XCHG_RUNS": runs}, deadline=45)
     merged = np.concatenate([np.frombuffer(b, dtype=synth.DELIV_DTYPE) for _, b, *_ in res])
     orc = O.OracleTopology(_gml())
     ips, st, verts = scenario.register_hosts(orc, H, 1)

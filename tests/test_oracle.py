@@ -234,3 +234,17 @@ def test_teardown_log_known_answer_1_gbit_switch():
     assert t.cached_paths_log() == [
         "Found path 0<->0 in cache: SourceIndex=0 DestinationIndex=0 Latency=1.000000 Reliability=1.000000 "
         "PacketCount=3 isDirect=True"]
+
+
+@pytest.mark.parametrize("directed", [False, True])
+def test_direct_row_equals_direct_paths(directed):
+    """orc_direct_row (the CPU baseline of bench.py's C1 direct-path leg) is
+    orc_direct_path per target, -1 where no edge joins the pair."""
+    gml = synth.complete_graph_gml(40, 0x5EED0D1, directed=directed)  # (direct paths need a complete graph)
+    o = O.OracleTopology(gml, use_shortest_path=False)
+    t = np.arange(40)
+    for s in range(0, 40, 7):
+        lat, rel = o.direct_row(s, t)
+        for j in t:
+            l, r = o.direct(s, int(j))
+            assert (lat[j], rel[j]) == ((-1.0, -1.0) if l is None else (l, r))
