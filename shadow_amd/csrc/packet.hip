@@ -4491,23 +4491,71 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_part2(const uint32_t* __restri
     fold_part_tile<false>(k, h, start, base, stage, out);
 }
 
-// region r = c * 128 + f: its keys are [M2 index (c, f, 0), (c, f + 1, 0))
+// The add's work units: a region's keys in chunks of at most kFoldAddMax,
+// one workgroup per chunk.  A region with one chunk (every region of a
+// uniform round: ~15k keys) is read-modify-written by its workgroup alone; a
+// hot region (Zipf senders: one sender's row takes ~10 % of all keys) is
+// split over many workgroups that add their nonzero counters with device
+// atomics -- instead of one workgroup walking 20M keys while the chip idles
+// (the Zipf C3 fold: ~4 ms per 20 rounds, profiles/r06b_bench_line.json).
+// k_fold_chunks (one workgroup): rbeg[r] = region r's first key (r <= R),
+// the chunks' exclusive prefix over the regions and, per chunk id, its
+// region and index in cmap[id] = r | j << 14.
+constexpr uint32_t kFoldAddMax = 1u << 18;
+constexpr uint32_t kFoldMaxRegions = 1u << 14;
+__global__ __launch_bounds__(kFoldWG) void k_fold_chunks(const uint32_t* __restrict__ M1, uint32_t C, uint32_t nt1,
+                                                         const uint32_t* __restrict__ M2, uint32_t R,
+                                                         uint32_t* __restrict__ rbeg, uint32_t* __restrict__ cmap,
+                                                         uint32_t* __restrict__ nchunks) {
+    __shared__ FoldL2 g;
+    __shared__ uint32_t ws[kFoldWG / 64];
+    const uint32_t* lb = rbeg; // (re-read below by other threads of the block: fenced)
+    fold_l2_geometry(M1, C, nt1, g);
+    for (uint32_t r = threadIdx.x; r <= R; r += kFoldWG) {
+        uint32_t b;
+        if (r == R) {
+            b = g.lo[C];
+        } else {
+            const uint32_t c = r >> kFoldFineBits, f = r & ((1u << kFoldFineBits) - 1u);
+            const uint32_t ntc = g.tb[c + 1] - g.tb[c];
+            b = ntc ? M2[((size_t)g.tb[c] << kFoldFineBits) + (size_t)f * ntc] : g.lo[c];
+        }
+        rbeg[r] = b;
+    }
+    __threadfence_block();
+    __syncthreads();
+    constexpr uint32_t per = kFoldMaxRegions / kFoldWG; // 16 regions per thread
+    const uint32_t r0 = threadIdx.x * per;
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < per && r0 + k < R; k++) sum += (lb[r0 + k + 1] - lb[r0 + k] + kFoldAddMax - 1) / kFoldAddMax;
+    uint32_t tot;
+    uint32_t pre = block_excl_scan_n(sum, &tot, ws);
+    for (uint32_t k = 0; k < per && r0 + k < R; k++) {
+        const uint32_t n = (lb[r0 + k + 1] - lb[r0 + k] + kFoldAddMax - 1) / kFoldAddMax;
+        for (uint32_t j = 0; j < n; j++) cmap[pre + j] = (r0 + k) | (j << 14);
+        pre += n;
+    }
+    if (threadIdx.x == 0) *nchunks = tot;
+}
+
+// chunk blockIdx.x of region r = cmap & 0x3FFF: its keys are [rbeg[r] + j *
+// kFoldAddMax, ...) up to rbeg[r + 1]
 // kVec: the region's counters zeroed and read-modify-written 16 B per lane,
 // eight loads in flight per lane before the stores (the scalar form waits
 // on each counter's load before its store: latency-bound at one workgroup
 // per CU); the dense table 16-B aligned (the caller checks)
 template <bool kVec>
-__global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ M1,
-                                                      uint32_t C, uint32_t nt1, const uint32_t* __restrict__ M2,
+__global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ rbeg,
+                                                      const uint32_t* __restrict__ cmap,
+                                                      const uint32_t* __restrict__ nchunks,
                                                       uint32_t* __restrict__ dense, unsigned long long N) {
     extern __shared__ uint32_t fc[];
-    __shared__ FoldL2 g;
-    fold_l2_geometry(M1, C, nt1, g);
-    const uint32_t r = blockIdx.x, c = r >> kFoldFineBits, f = r & ((1u << kFoldFineBits) - 1u);
-    const uint32_t ntc = g.tb[c + 1] - g.tb[c];
-    if (!ntc) return; // (block-uniform: the coarse bucket is empty)
-    const size_t mb = (size_t)g.tb[c] << kFoldFineBits;
-    const uint32_t beg = M2[mb + (size_t)f * ntc], end = M2[mb + (size_t)(f + 1) * ntc];
+    if (blockIdx.x >= *nchunks) return; // (block-uniform: the grid is the chunks' upper bound)
+    const uint32_t cm = cmap[blockIdx.x], r = cm & 0x3FFFu, jc = cm >> 14;
+    const uint32_t rb0 = rbeg[r], re = rbeg[r + 1];
+    const uint32_t beg = rb0 + jc * kFoldAddMax, end = re - beg > kFoldAddMax ? beg + kFoldAddMax : re;
+    const bool shared_region = re - rb0 > kFoldAddMax; // (block-uniform) other chunks add to it too
     if (beg == end) return;
     constexpr uint32_t R = 1u << kFoldRegionBits;
     if (kVec)
@@ -4527,6 +4575,13 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict
     const unsigned long long rb = (unsigned long long)r << kFoldRegionBits;
     const uint32_t lim = N - rb < R ? (uint32_t)(N - rb) : R;
     uint32_t j0 = 0;
+    if (shared_region) { // a hot region's chunk: device atomics for its nonzero counters
+        for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
+            const uint32_t v = fc[j];
+            if (v) atomicAdd(dense + rb + j, v);
+        }
+        return;
+    }
     if (kVec) {
         constexpr int kU = R / 4 / kFoldWG; // 8: the whole region in one pass
         const uint32_t lim4 = lim / 4;
@@ -4560,6 +4615,8 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict
 struct FoldScratch {
     uint32_t* part = nullptr;
     size_t cap_part = 0; // keys
+    uint32_t* cmap = nullptr; // [rbeg R + 1 | nchunks | cmap]
+    size_t cap_cmap = 0;
     uint32_t* M1 = nullptr;
     size_t cap_M1 = 0; // words
     uint32_t* M2 = nullptr;
@@ -4578,6 +4635,11 @@ int fold_grow(uint32_t** p, size_t* cap, size_t need, const char* what) {
     return 0;
 }
 
+// the add's chunk table: rbeg (R + 1) | nchunks | one entry per chunk (at
+// most one per region plus one per kFoldAddMax keys)
+size_t fold_max_chunks(size_t L) { return kFoldMaxRegions + L / kFoldAddMax + 1; }
+size_t fold_cmap_words(size_t L) { return (kFoldMaxRegions + 1) + 1 + fold_max_chunks(L); }
+
 // buffers for folds of up to L keys (grow-only; reserved with the log so that
 // a fold inside a timed region allocates nothing)
 int fold_reserve(FoldScratch& f, size_t L) {
@@ -4588,7 +4650,8 @@ int fold_reserve(FoldScratch& f, size_t L) {
     if ((rc = fold_grow(&f.part, &f.cap_part, L ? L : 1, "hipMalloc fold part")) ||
         (rc = fold_grow(&f.M1, &f.cap_M1, m1, "hipMalloc fold M1")) ||
         (rc = fold_grow(&f.M2, &f.cap_M2, m2, "hipMalloc fold M2")) ||
-        (rc = fold_grow(&f.bsum, &f.cap_bsum, mb, "hipMalloc fold scan")))
+        (rc = fold_grow(&f.bsum, &f.cap_bsum, mb, "hipMalloc fold scan")) ||
+        (rc = fold_grow(&f.cmap, &f.cap_cmap, fold_cmap_words(L), "hipMalloc fold chunks")))
         return rc;
     return 0;
 }
@@ -4623,14 +4686,19 @@ int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, unsigned long long N, Fo
     hipLaunchKernelGGL(k_fold_hist2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2);
     scan_counts(f.M2, m2, f.M2, f.bsum, nullptr, s);
     hipLaunchKernelGGL(k_fold_part2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2, log);
+    uint32_t* rbeg = f.cmap;
+    uint32_t* nch = rbeg + (kFoldMaxRegions + 1);
+    uint32_t* cmap = nch + 1;
+    hipLaunchKernelGGL(k_fold_chunks, dim3(1), dim3(kFoldWG), 0, s, f.M1, C, nt1, f.M2, R, rbeg, cmap, nch);
+    const uint32_t grid = (uint32_t)(R + L / kFoldAddMax + 1); // (>= the chunks; the rest exit at once)
     // SHD_FOLD_VEC=0: the scalar read-modify-write
     const char* fv = getenv("SHD_FOLD_VEC");
     if (((uintptr_t)dense & 15u) == 0 && !(fv && strcmp(fv, "0") == 0))
-        hipLaunchKernelGGL(k_fold_add<true>, dim3(R), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, f.M1, C, nt1,
-                           f.M2, dense, N);
+        hipLaunchKernelGGL(k_fold_add<true>, dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, rbeg, cmap,
+                           nch, dense, N);
     else
-        hipLaunchKernelGGL(k_fold_add<false>, dim3(R), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, f.M1, C,
-                           nt1, f.M2, dense, N);
+        hipLaunchKernelGGL(k_fold_add<false>, dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, rbeg,
+                           cmap, nch, dense, N);
     return hip_status(hipGetLastError(), "pcnt fold launch");
 }
 
@@ -4655,6 +4723,7 @@ extern "C" void shd_dev_pcnt_scratch_free(void* scratch) {
     (void)hipFree(f->M1);
     (void)hipFree(f->M2);
     (void)hipFree(f->bsum);
+    (void)hipFree(f->cmap);
     delete f;
 }
 

@@ -419,6 +419,48 @@ def test_path_counter_fold_multi_region(log, monkeypatch):
         assert len(bad) == 0, f"round {r}: {len(bad)} counters differ, first {bad[:4].tolist()}"
 
 
+@pytest.mark.parametrize("rounds_per_fold", [1, 2])
+def test_path_counter_fold_hot_region(rounds_per_fold, monkeypatch):
+    """A hot sender (Zipf-like: 450k of 600k packets from one host to uniform
+    destinations) puts more than the add's chunk (2^18 keys) into one 32K
+    counter region: the fold splits that region over several workgroups that
+    add with device atomics.  Every counter against the numpy restatement,
+    folded after each round or after two."""
+    import torch
+    monkeypatch.setenv("SHD_PCNT", "log")
+    gml = synth.sparse_graph_gml(3000, 0x5EED0F21)
+    H = 6_000
+    top = Topology(gml)
+    ips, st, verts = scenario.register_hosts(top, H, seed=1)
+    A = top.slot_count()
+    top.touch_all()
+    hslot = count_check.slot_map(verts)
+    hot = int(np.argmin(hslot))  # (slot 0: its row owns its pairs with every later slot)
+    want = np.zeros((A, A), dtype=np.uint64)
+    n = 600_000
+    for r in range(2):
+        pk = synth.packet_batch(n, H, 0x5EED0F22 + r, 100_000_000, 10_000_000, st)
+        src = np.where(np.arange(n) % 4 != 0, hot, pk["src_host"]).astype(np.uint32)
+        dst = synth.redraw_destinations(pk, H, 0x5EED0F30 + r)["dst_host"]
+        dst = np.where(dst == src, (src + 1) % H, dst).astype(np.uint32)
+        pk = synth.packet_batch(n, H, 0x5EED0F22 + r, 100_000_000, 10_000_000, st, pairs=(src, dst))
+        d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+        d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+        d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+        d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+        d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                           d_status.data_ptr(), d_cnt.data_ptr(), 0)
+        torch.cuda.synchronize()
+        want += count_check.expected_counts(hslot, pk, d_status.cpu().numpy(), A)
+        if (r + 1) % rounds_per_fold == 0:
+            got = top.path_packet_counts()
+            bad = np.argwhere(got != want)
+            assert len(bad) == 0, f"round {r}: {len(bad)} counters differ, first {bad[:4].tolist()}"
+    assert want.max() > 0 and int((want > 0).sum(axis=1).max()) > 1000
+
+
 def test_deliv_sort_device_against_lexsort(pipeline):
     import torch
     top, _, _, _ = make_pair(synth.complete_graph_gml(5, 3), 5)
