@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--batches", type=int, default=4,
                     help="distinct packet batches resident in HBM, rotated so no round re-gathers the previous one's "
                          "table lines (fresh inputs per step)")
+    ap.add_argument("--no-replay", action="store_true",
+                    help="skip the replayed-batch comparison rounds (PMC passes: fresh rounds only)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the §8d variant legs (ns-resolution C2 build and C3 round, C1 direct paths, Zipf C3)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r05t_traffic.json"),
@@ -378,7 +380,7 @@ def main():
     # beside it: the same K rounds replaying ONE batch (the rounds before
     # round 6 timed this form; its lines can stay cache-resident across steps)
     rep_ms = None
-    if NB > 1:
+    if NB > 1 and not args.no_replay:
         rot["fixed"] = lb
         barrier()
         torch.cuda.synchronize(dev)

@@ -24,12 +24,12 @@ run_passes() { # NAME LIMIT CMD...
 # C3_ONLY=FILE: only the C3 passes, merged into a copy of an earlier traffic.json
 if [ -n "$C3_ONLY" ]; then
     cp $C3_ONLY $O/traffic.json &&
-    run_passes c3 150 python3 $R/bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline --no-nic &&
+    run_passes c3 150 python3 $R/bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline --no-nic --no-host-api --no-variants --no-replay &&
     python3 $R/scripts/traffic.py $O/traffic.json $(find $O/c3 -name "*counter_collection.csv") &&
     echo "traffic: $O/traffic.json"
     exit $?
 fi
-run_passes c3 150 python3 $R/bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline --no-nic &&
+run_passes c3 150 python3 $R/bench.py --steps 3 --warmup 1 --no-routing --no-cpu-baseline --no-nic --no-host-api --no-variants --no-replay &&
 run_passes c1 100 python3 $R/scripts/build_c4.py complete 1000 5000 0x5EED0001 &&
 run_passes c2 150 python3 $R/scripts/build_c4.py 20000 50000 0x5EED0002 &&
 run_passes c4 200 python3 $R/scripts/build_c4.py || exit 1

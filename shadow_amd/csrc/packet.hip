@@ -2584,6 +2584,196 @@ __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(kOcc ? kOcc
     }
 }
 
+// The split scatter (SHD_PART_SCATTER=10): the decision and the partition
+// as two kernels.  k_part_decide makes the decision of k_part_scatter
+// (identical code path: gathers, rand_r, drop, ceil delay, end-time drop,
+// barrier clamp, status, counter log, wide list, min time) in small
+// workgroups with no LDS and few registers, so that many waves per SIMD keep
+// the table gathers and the record stream in flight together, and writes
+// each record's 16-B stage form {time - tbase, seq, src, dst} (w = ~0: not
+// staged) in record order -- coalesced.  k_part_place then reads those in
+// chunks of kCH and does k_part_scatter's bucket counting, run reservation
+// and run stores.  (The one-kernel form waits for each workgroup's gathers
+// and then does everything else, one 1,024-thread workgroup per CU: the
+// probes add up, profiles/r05g_part_scatter_probe_bits.log.)
+template <int kWG, int kB>
+__global__ __launch_bounds__(kWG) void k_part_decide(ShdPktCtx c, const ShdPkt* __restrict__ recs, size_t n,
+                                                     uint64_t barrier, uint64_t end_time, uint64_t boot_end, PartGeo g,
+                                                     uint4* __restrict__ dec, uint32_t* __restrict__ wcnt,
+                                                     uint8_t* __restrict__ status, unsigned long long* counters,
+                                                     ShdDeliv* __restrict__ wide, uint32_t* __restrict__ nwide) {
+    __shared__ unsigned long long wmin[kWG / 64];
+    const int lane = threadIdx.x & 63;
+    const size_t base = (size_t)blockIdx.x * (kWG * kB);
+    const size_t A = (size_t)c.A;
+    const uint2* __restrict__ host_info = reinterpret_cast<const uint2*>(c.host_info);
+    const uint2* __restrict__ ptab = reinterpret_cast<const uint2*>(c.ptab);
+    const uint32_t smax = g.shift ? (0xFFFFFFFFu >> g.shift) : 0xFFFFFFFFu;
+    unsigned long long mn = ~0ull;
+    ShdPkt p[kB];
+    bool live[kB];
+#pragma unroll
+    for (int k = 0; k < kB; k++) {
+        const size_t i = base + (size_t)k * kWG + threadIdx.x;
+        live[k] = i < n;
+        if (live[k]) p[k] = ld_pkt(&recs[i]);
+    }
+    int si[kB], di[kB];
+    uint32_t ts[kB], td[kB];
+#pragma unroll
+    for (int k = 0; k < kB; k++) {
+        const bool known = live[k] && p[k].src_host < c.nhosts && p[k].dst_host < c.nhosts;
+        uint2 hs = make_uint2(~0u, ~0u), hd = make_uint2(~0u, ~0u);
+        if (known) {
+            hs = host_info[p[k].src_host];
+            hd = host_info[p[k].dst_host];
+        }
+        si[k] = hs.x == ~0u ? -1 : (int)hs.x;
+        di[k] = hd.x == ~0u ? -1 : (int)hd.x;
+        ts[k] = hs.y;
+        td[k] = hd.y;
+    }
+    size_t ei[kB];
+#pragma unroll
+    for (int k = 0; k < kB; k++) {
+        int oi = si[k], oj = di[k];
+        if (oi >= 0 && oj >= 0) {
+            if (c.mode == 0) {
+                if (oi != oj && td[k] < ts[k]) oi = di[k], oj = si[k]; // owner: row touched first
+            } else if (c.mode == 2) {
+                const size_t b = (size_t)oi * A + (size_t)oj;
+                if (!((c.pair_bits[b >> 5] >> (b & 31)) & 1u)) oi = di[k], oj = si[k];
+            }
+        }
+        if (oi < c.row_lo || oi >= c.row_hi) si[k] = -1; // another rank's row: not decided here
+        ei[k] = (size_t)(oi < 0 ? 0 : oi) * A + (size_t)(oj < 0 ? 0 : oj);
+    }
+    ShdEntry e[kB];
+    uint2 q[kB];
+#pragma unroll
+    for (int k = 0; k < kB; k++) {
+        q[k] = make_uint2(kPtabFallback, 0u);
+        if (ptab && si[k] >= 0 && di[k] >= 0) {
+            const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(ptab) + ei[k]);
+            q[k] = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kB; k++)
+        if (si[k] >= 0 && di[k] >= 0 && q[k].x == kPtabFallback) e[k] = c.tab[ei[k]];
+#pragma unroll
+    for (int k = 0; k < kB; k++) {
+        const size_t i = base + (size_t)k * kWG + threadIdx.x;
+        uint8_t st = 0xff; // unregistered host: not delivered
+        uint64_t t = 0;
+        if (live[k] && si[k] >= 0 && di[k] >= 0) {
+            uint32_t rs = p[k].rng_state;
+            const uint32_t r = (uint32_t)glibc_rand_r(&rs);
+            bool keep;
+            uint64_t delay;
+            if (q[k].x != kPtabFallback) {
+                keep = r <= q[k].y; // == (chance <= rel), see kPtabFallback
+                delay = q[k].x;
+            } else {
+                keep = (double)r / 2147483647.0 <= e[k].rel; // random_nextDouble, worker.c:545
+                delay = (uint64_t)ceil(e[k].lat * 1000000.0);
+            }
+            st = SHD_DROPPED_LOSS;
+            if (p[k].now < boot_end || keep || p[k].payload_len == 0) {
+                t = p[k].now + delay;                                   // worker.c:548-549
+                if (t >= end_time) st = SHD_DROPPED_END;                // scheduler.c:236-239
+                else {
+                    if (p[k].src_host != p[k].dst_host && t < barrier) t = barrier; // host_single.c:187-192
+                    st = SHD_DELIVERED;
+                }
+                if (c.pcnt) atomicAdd(c.pcnt + ei[k], 1u); // (SHD_PCNT=atomic) worker.c:551
+            }
+        }
+        if (live[k]) pcnt_log(c, i, st == SHD_DELIVERED || st == SHD_DROPPED_END, ei[k]);
+        const bool dl = st == SHD_DELIVERED;
+        const uint32_t dr = p[k].dst_host - g.host_lo;
+        const bool fits = dl && c_fits(t, g.tbase, p[k].seq) && p[k].src_host <= smax && dr < g.H;
+        if (live[k]) {
+            const shd_v4u sv = fits ? shd_v4u{(uint32_t)(t - g.tbase), (uint32_t)p[k].seq, p[k].src_host, p[k].dst_host}
+                                    : shd_v4u{0u, 0u, 0u, ~0u};
+            *reinterpret_cast<shd_v4u*>(dec + i) = sv;
+        }
+        const uint32_t ws = wave_alloc(dl && !fits, nwide, lane); // (every lane: ballot)
+        if (dl && !fits) {
+            st_ev(&wide[ws], ShdDeliv{t, p[k].seq, p[k].src_host, p[k].dst_host, (uint32_t)i + c.idx_base, 0u});
+            if (dr < g.H) atomicAdd(&wcnt[dr >> g.shift], 1u);
+        }
+        if (dl && t >= barrier && t < mn) mn = t; // worker.c:350-363
+        if (live[k]) status[i] = st;
+    }
+    mn = wave_min_u64(mn);
+    if (lane == 0) wmin[threadIdx.x >> 6] = mn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = wmin[0];
+        for (int k = 1; k < kWG / 64; k++) m = wmin[k] < m ? wmin[k] : m;
+        if (m != ~0ull) atomicMin(&counters[1], m);
+    }
+}
+
+// the split scatter's partition: records [blockIdx.x * ch, + ch) of dec
+// counted per bucket (LDS), one run per nonempty bucket reserved, each
+// staged record stored at its run position -- k_part_scatter's tail
+template <int kWG, int kCH>
+__global__ __launch_bounds__(kWG) void k_part_place(const uint4* __restrict__ dec, size_t n, uint32_t idx_base,
+                                                    PartGeo g, uint4* __restrict__ stage, uint32_t* __restrict__ gcnt,
+                                                    uint32_t* __restrict__ wcnt, ShdDeliv* __restrict__ wide,
+                                                    uint32_t* __restrict__ nwide, uint32_t ch) {
+    constexpr int kR = kCH / kWG;
+    extern __shared__ uint4 part_smem[];
+    uint32_t* hist = reinterpret_cast<uint32_t*>(part_smem);
+    uint32_t* gb = hist + g.nb;
+    const int lane = threadIdx.x & 63;
+    for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) hist[b] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * ch;
+    const uint32_t mask = (1u << g.shift) - 1u;
+    uint4 rv[kR];
+    uint32_t rr[kR];
+#pragma unroll
+    for (int k = 0; k < kR; k++) {
+        const uint32_t li = (uint32_t)(k * kWG + threadIdx.x);
+        const size_t i = base + li;
+        rv[k] = make_uint4(0u, 0u, 0u, ~0u);
+        if (li < ch && i < n) {
+            const shd_v4u v = __builtin_nontemporal_load(reinterpret_cast<const shd_v4u*>(dec) + i);
+            rv[k] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kR; k++) rr[k] = rv[k].w != ~0u ? atomicAdd(&hist[(rv[k].w - g.host_lo) >> g.shift], 1u) : 0u;
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < g.nb; b += kWG) {
+        const uint32_t h = hist[b];
+        gb[b] = h ? atomicAdd(&gcnt[b], h) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kR; k++) {
+        const uint4 e = rv[k];
+        const bool valid = e.w != ~0u;
+        const uint32_t b = valid ? (e.w - g.host_lo) >> g.shift : 0u;
+        const size_t j = valid ? (size_t)gb[b] + rr[k] : 0;
+        const uint32_t li = (uint32_t)(k * kWG + threadIdx.x);
+        const bool in = valid && j < g.cap;
+        if (in)
+            stage[(size_t)b * g.cap + j] =
+                make_uint4(e.x, e.y, (uint32_t)(base + li) + idx_base, (e.z << g.shift) | ((e.w - g.host_lo) & mask));
+        const bool full = valid && !in; // the bucket's region is full: whole event to the wide list
+        const uint32_t ws = wave_alloc(full, nwide, lane);
+        if (full) {
+            st_ev(&wide[ws], ShdDeliv{g.tbase + e.x, (unsigned long long)e.y, e.z, e.w, (uint32_t)(base + li) + idx_base,
+                                      0u});
+            atomicAdd(&wcnt[b], 1u);
+        }
+    }
+}
+
 // The software-pipelined scatter (SHD_PART_SCATTER=7): the same decisions,
 // runs and outputs as k_part_scatter, but one persistent workgroup per CU
 // walks its chunks with the NEXT chunk's table gathers in flight while the
@@ -4831,6 +5021,7 @@ struct PartCfg {
     int wg, ch;
     bool lds;
     int pipe = 0; // k_part_scatter_pipe: persistent workgroups per CU
+    int split = 0; // k_part_decide (records per thread) + k_part_place
 };
 int part_probe() {
     const char* v = getenv("SHD_PART_PROBE");
@@ -4847,6 +5038,7 @@ PartCfg part_cfg(uint32_t nb) {
     if (k == 4) return {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false};
     if (k == 5) return {(const void*)k_part_scatter<512, 4096, false>, 512, 4096, false};
     if (k == 6) return {(const void*)k_part_scatter<1024, 8192, false>, 1024, 8192, false};
+    if (k == 10 || k == 11) return {(const void*)k_part_place<1024, 4096>, 1024, 4096, false, 0, k == 10 ? 4 : 2};
     if ((k == 7 || k == 8 || k == 9) && nb > kPartPipeMaxBuckets) k = 1;
     if (k == 7) return {(const void*)k_part_scatter_pipe<1024, 2048>, 1024, 2048, false, 1};
     if (k == 8) return {(const void*)k_part_scatter_pipe<512, 1024>, 512, 1024, false, 2};
@@ -4876,7 +5068,8 @@ int part_attr() {
                             {(const void*)k_part_scatter<1024, 4096, false, 15>, 1024, 4096, false},
                             {(const void*)k_part_scatter_pipe<1024, 2048>, 1024, 2048, false},
                             {(const void*)k_part_scatter_pipe<512, 1024>, 512, 1024, false},
-                            {(const void*)k_part_scatter_pipe<256, 512>, 256, 512, false}};
+                            {(const void*)k_part_scatter_pipe<256, 512>, 256, 512, false},
+                            {(const void*)k_part_place<1024, 4096>, 1024, 4096, false}};
     if (int rc = hip_status(hipFuncSetAttribute((const void*)k_wide_group, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                 (int)(4 * kPartMaxBuckets)),
                             "hipFuncSetAttribute k_wide_group"))
@@ -4923,7 +5116,20 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         }
         const dim3 grid((unsigned)((n + ch - 1) / ch)), blk(f.wg);
         const size_t lds = part_lds(f, g.nb);
-        if (f.pipe) {
+        if (f.split) {
+            // (dec: w.st1, free until the sort's listed segments)
+            uint4* dec = reinterpret_cast<uint4*>(w.st1);
+            if (f.split == 4)
+                hipLaunchKernelGGL((k_part_decide<256, 4>), dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, s, *c,
+                                   d_recs, n, barrier, end_time, bootstrap_end, g, dec, wcnt, d_status, counters, w.st2,
+                                   w.nbig + 1);
+            else
+                hipLaunchKernelGGL((k_part_decide<256, 2>), dim3((unsigned)((n + 511) / 512)), dim3(256), 0, s, *c,
+                                   d_recs, n, barrier, end_time, bootstrap_end, g, dec, wcnt, d_status, counters, w.st2,
+                                   w.nbig + 1);
+            hipLaunchKernelGGL((k_part_place<1024, 4096>), grid, blk, lds, s, dec, n, c->idx_base, g, w.pstage, gcnt, wcnt,
+                               w.st2, w.nbig + 1, ch);
+        } else if (f.pipe) {
             const char* pg = getenv("SHD_PART_PIPE_GRID");
             const unsigned nch = grid.x,
                            nwg = pg && atoi(pg) > 0 ? (unsigned)atoi(pg) : (unsigned)ncu * (unsigned)f.pipe,

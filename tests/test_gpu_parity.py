@@ -186,7 +186,7 @@ def test_unattached_address():
 
 @pytest.fixture(params=["bucket", "rank", "slab", "slab_rankmajor", "slab_readlane", "slab_noagg", "rank_noagg",
                         "slab_unfused", "slab_wide", "part", "part_readlane", "part_lds", "part_s1", "part_s2", "part_s3", "part_s4",
-                        "part_s3perm", "part_x5", "part_x6", "part_x7", "part_x8", "part_x9", "part_x7g3", "part_x8g5", "part_x9g7"])
+                        "part_s3perm", "part_x5", "part_x6", "part_x7", "part_x8", "part_x9", "part_x7g3", "part_x8g5", "part_x9g7", "part_x10", "part_x11"])
 def pipeline(request, monkeypatch):
     """The grouping pipelines of packet.hip (SHD_PACKET_PIPELINE: bucket,
     rank, slab, part -- the LDS-staged bucket partition + per-bucket LDS sort;
@@ -203,7 +203,9 @@ def pipeline(request, monkeypatch):
     # part: the scatter's LDS-staged form and other instances (_xK), the
     # bucket sort's other instances (_sK), its in-order write (perm)
     p = request.param
-    monkeypatch.setenv("SHD_PART_SCATTER", "0" if p.endswith("lds") else p.split("_x")[1][0] if "_x" in p else "1")
+    import re
+    monkeypatch.setenv("SHD_PART_SCATTER", "0" if p.endswith("lds") else
+                       re.match(r"\d+", p.split("_x")[1]).group(0) if "_x" in p else "1")
     # the pipelined scatter (_x7 / _x8) on a few workgroups (_gK): many
     # chunks per workgroup even on these small batches
     if "_x" in p and "g" in p.split("_x")[1]:
