@@ -500,8 +500,10 @@ def main():
         "path_counts": {
             "what": "topology_incrementPathPacketCounter of every kept packet (worker.c:551) inside the timed "
                     "region: k_part_scatter logs each record's answering pair (4 B, coalesced); at the end of "
-                    "the K timed rounds shd_topology_path_counts_sync adds the K logs into the u32 counters "
-                    "(bucket partition + LDS accumulation, shd_dev_pcnt_fold)",
+                    "the K timed rounds shd_topology_path_counts_sync adds the K logs into the counters "
+                    "(bucket partition + LDS accumulation, shd_dev_pcnt_fold; a pair's count is its u32 counter "
+                    "plus its byte of the u8 delta layer the fold writes, a byte past 255 moved into the u32 "
+                    "counter by the fold itself -- every count exact after the fold, no deferred merge)",
             "mode": os.environ.get("SHD_PCNT", "log"), "counted_per_round_rank0": kept,
             "fold_ms_total": t_fold * 1e3, "fold_ms_per_round": t_fold * 1e3 / args.steps,
             "rounds_per_fold": args.steps,

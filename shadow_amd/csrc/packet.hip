@@ -4461,21 +4461,23 @@ __global__ __launch_bounds__(256) void k_ptab_build(const ShdEntry* __restrict__
 
 // Path packet counters >= thr move to a list (see shd_dev_pcnt_spill): one
 // wave-aggregated slot reservation per wave, the appended entries zeroed.
-__global__ __launch_bounds__(256) void k_pcnt_spill(uint32_t* __restrict__ cnt, size_t n, uint32_t thr,
-                                                    unsigned long long* __restrict__ list, uint32_t cap,
+// (d8: the u8 delta layer, NULL: none; a count is cnt + d8, below 2^32)
+__global__ __launch_bounds__(256) void k_pcnt_spill(uint32_t* __restrict__ cnt, uint8_t* __restrict__ d8, size_t n,
+                                                    uint32_t thr, unsigned long long* __restrict__ list, uint32_t cap,
                                                     uint32_t* __restrict__ nlist) {
     const int lane = threadIdx.x & 63;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     // (uniform trip count over the wave: wave_alloc ballots)
     for (size_t i0 = (size_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
         const size_t i = i0 + threadIdx.x;
-        const uint32_t v = i < n ? cnt[i] : 0u;
+        const uint32_t v = i < n ? cnt[i] + (d8 ? (uint32_t)d8[i] : 0u) : 0u;
         const bool hit = i < n && v >= thr && v != 0u;
         const uint32_t slot = wave_alloc(hit, nlist, lane);
         if (hit && slot < cap) {
             list[2 * (size_t)slot] = i;
             list[2 * (size_t)slot + 1] = v;
             cnt[i] = 0u;
+            if (d8) d8[i] = 0u;
         }
     }
 }
@@ -4734,12 +4736,18 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_chunks(const uint32_t* __restr
 // eight loads in flight per lane before the stores (the scalar form waits
 // on each counter's load before its store: latency-bound at one workgroup
 // per CU); the dense table 16-B aligned (the caller checks)
-template <bool kVec>
+// kD8: the counts go to the u8 delta layer d8 (16-B aligned at index 0,
+// readable up to N rounded up to 16): 16 counters per lane-step, one 16-B
+// load and store of their delta bytes; a byte whose sum passes 255 moves the
+// whole sum into dense (a device atomic) and restarts at 0 -- the region's
+// HBM traffic is its 32 KB of deltas, not its 128 KB of u32 counters
+template <bool kVec, bool kD8 = false>
 __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ rbeg,
                                                       const uint32_t* __restrict__ cmap,
                                                       const uint32_t* __restrict__ nchunks,
-                                                      uint32_t* __restrict__ dense, unsigned long long N) {
+                                                      uint32_t* __restrict__ dense, unsigned long long N,
+                                                      uint8_t* __restrict__ d8 = nullptr) {
     extern __shared__ uint32_t fc[];
     if (blockIdx.x >= *nchunks) return; // (block-uniform: the grid is the chunks' upper bound)
     const uint32_t cm = cmap[blockIdx.x], r = cm & 0x3FFFu, jc = cm >> 14;
@@ -4772,6 +4780,49 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict
         }
         return;
     }
+    if (kD8) {
+        constexpr int kU = R / 16 / kFoldWG; // 2: the whole region in one pass
+        const uint32_t lim16 = (lim + 15u) / 16u;
+        const uint4* f4 = reinterpret_cast<const uint4*>(fc);
+        uint4* d16 = reinterpret_cast<uint4*>(d8 + rb);
+        uint4 v[kU][4], dv[kU];
+        bool any[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            uint32_t o = 0u;
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                v[u][w] = q < lim16 ? f4[4 * q + w] : uint4{0u, 0u, 0u, 0u};
+                o |= v[u][w].x | v[u][w].y | v[u][w].z | v[u][w].w;
+            }
+            any[u] = o != 0u;
+            if (any[u]) dv[u] = d16[q];
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            if (!any[u]) continue;
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            uint32_t dw[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint32_t c[4] = {v[u][w].x, v[u][w].y, v[u][w].z, v[u][w].w};
+                uint32_t nw = 0u;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    uint32_t s = ((dw[w] >> (8 * b)) & 0xFFu) + c[b];
+                    if (s > 0xFFu) { // (rare: a pair past 255 since its last move)
+                        atomicAdd(dense + rb + 16u * q + 4u * w + b, s);
+                        s = 0u;
+                    }
+                    nw |= s << (8 * b);
+                }
+                dw[w] = nw;
+            }
+            d16[q] = uint4{dw[0], dw[1], dw[2], dw[3]};
+        }
+        return;
+    }
     if (kVec) {
         constexpr int kU = R / 4 / kFoldWG; // 8: the whole region in one pass
         const uint32_t lim4 = lim / 4;
@@ -4799,6 +4850,102 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict
     for (uint32_t j = j0 + threadIdx.x; j < lim; j += kFoldWG) {
         const uint32_t v = fc[j];
         if (v) dense[rb + j] += v;
+    }
+}
+
+// The add into the u8 delta layer (k_fold_add<_, true>'s arithmetic) with
+// one memory round trip per workgroup: the chunk's first kFoldAddK keys per
+// thread and the region's 32 KB of delta bytes are loaded first, the LDS
+// counters zeroed while they are in flight (an LDS-only barrier keeps them
+// in flight), then the LDS adds, then every 16-counter group combined and
+// stored.  (The phased form waits on its keys, then on its deltas, one
+// 1,024-thread workgroup per CU: 0.41 ms of a 1.6 ms fold of 20 C3 rounds,
+// profiles/r06f.)
+constexpr int kFoldAddK = 16;
+__global__ __launch_bounds__(kFoldWG) void k_fold_add8(const uint32_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ rbeg,
+                                                       const uint32_t* __restrict__ cmap,
+                                                       const uint32_t* __restrict__ nchunks,
+                                                       uint32_t* __restrict__ dense, unsigned long long N,
+                                                       uint8_t* __restrict__ d8) {
+    extern __shared__ uint32_t fc[];
+    if (blockIdx.x >= *nchunks) return; // (block-uniform)
+    const uint32_t cm = cmap[blockIdx.x], r = cm & 0x3FFFu, jc = cm >> 14;
+    const uint32_t rb0 = rbeg[r], re = rbeg[r + 1];
+    const uint32_t beg = rb0 + jc * kFoldAddMax, end = re - beg > kFoldAddMax ? beg + kFoldAddMax : re;
+    const bool shared_region = re - rb0 > kFoldAddMax; // (block-uniform)
+    if (beg == end) return;
+    constexpr uint32_t R = 1u << kFoldRegionBits;
+    constexpr int kU = R / 16 / kFoldWG; // 2: 16 counters per lane-step, the whole region
+    const unsigned long long rb = (unsigned long long)r << kFoldRegionBits;
+    const uint32_t lim = N - rb < R ? (uint32_t)(N - rb) : R;
+    const uint32_t lim16 = (lim + 15u) / 16u;
+    uint32_t k[kFoldAddK];
+#pragma unroll
+    for (int u = 0; u < kFoldAddK; u++) {
+        const uint32_t i = beg + (uint32_t)u * kFoldWG + threadIdx.x;
+        k[u] = i < end ? keys[i] : kFoldSent;
+    }
+    uint4* d16 = reinterpret_cast<uint4*>(d8 + rb);
+    uint4 dv[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+        dv[u] = !shared_region && q < lim16 ? d16[q] : uint4{0u, 0u, 0u, 0u};
+    }
+    for (uint32_t j = threadIdx.x; j < R / 4; j += kFoldWG) reinterpret_cast<uint4*>(fc)[j] = uint4{0u, 0u, 0u, 0u};
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < kFoldAddK; u++)
+        if (k[u] != kFoldSent) atomicAdd(&fc[k[u] & (R - 1u)], 1u);
+    for (uint32_t i0 = beg + kFoldAddK * kFoldWG; i0 < end; i0 += kFoldAddK * kFoldWG) { // (chunks past 16K keys)
+#pragma unroll
+        for (int u = 0; u < kFoldAddK; u++) {
+            const uint32_t i = i0 + (uint32_t)u * kFoldWG + threadIdx.x;
+            k[u] = i < end ? keys[i] : kFoldSent;
+        }
+#pragma unroll
+        for (int u = 0; u < kFoldAddK; u++)
+            if (k[u] != kFoldSent) atomicAdd(&fc[k[u] & (R - 1u)], 1u);
+    }
+    __syncthreads();
+    if (shared_region) { // a hot region's chunk: device atomics for its nonzero counters
+        for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
+            const uint32_t v = fc[j];
+            if (v) atomicAdd(dense + rb + j, v);
+        }
+        return;
+    }
+    const uint4* f4 = reinterpret_cast<const uint4*>(fc);
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+        if (q >= lim16) continue;
+        uint4 v[4];
+        uint32_t o = 0u;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            v[w] = f4[4 * q + w];
+            o |= v[w].x | v[w].y | v[w].z | v[w].w;
+        }
+        if (!o) continue;
+        uint32_t dw[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint32_t c[4] = {v[w].x, v[w].y, v[w].z, v[w].w};
+            uint32_t nw = 0u;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                uint32_t x = ((dw[w] >> (8 * b)) & 0xFFu) + c[b];
+                if (x > 0xFFu) { // (rare: a pair past 255 since its last move)
+                    atomicAdd(dense + rb + 16u * q + 4u * w + b, x);
+                    x = 0u;
+                }
+                nw |= x << (8 * b);
+            }
+            dw[w] = nw;
+        }
+        d16[q] = uint4{dw[0], dw[1], dw[2], dw[3]};
     }
 }
 
@@ -4848,12 +4995,15 @@ int fold_reserve(FoldScratch& f, size_t L) {
 
 // (log: both the input and, after the level-1 pass has read it, the level-2
 // output -- one scratch array of L keys besides it)
-int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, unsigned long long N, FoldScratch& f, hipStream_t s) {
+int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, uint8_t* d8, unsigned long long N, FoldScratch& f,
+              hipStream_t s) {
     if (N > kFoldMaxN) return shd_fail(-EINVAL, "fold: %llu counters exceed the fold's %llu", N, kFoldMaxN);
+    if (d8 && ((uintptr_t)d8 & 15u)) return shd_fail(-EINVAL, "fold: the delta layer is not 16-B aligned");
     if (int rc = fold_reserve(f, L)) return rc;
     static bool attr = false;
     if (!attr) {
-        for (const void* fn : {(const void*)k_fold_add<true>, (const void*)k_fold_add<false>})
+        for (const void* fn : {(const void*)k_fold_add<true>, (const void*)k_fold_add<false>,
+                               (const void*)k_fold_add<false, true>, (const void*)k_fold_add8})
             if (int rc = hip_status(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                         4 << kFoldRegionBits),
                                     "hipFuncSetAttribute k_fold_add"))
@@ -4883,7 +5033,15 @@ int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, unsigned long long N, Fo
     const uint32_t grid = (uint32_t)(R + L / kFoldAddMax + 1); // (>= the chunks; the rest exit at once)
     // SHD_FOLD_VEC=0: the scalar read-modify-write
     const char* fv = getenv("SHD_FOLD_VEC");
-    if (((uintptr_t)dense & 15u) == 0 && !(fv && strcmp(fv, "0") == 0))
+    // SHD_FOLD_ADD=phased: the delta add in phases (A/B)
+    const char* fa = getenv("SHD_FOLD_ADD");
+    if (d8 && fa && strcmp(fa, "phased") == 0)
+        hipLaunchKernelGGL((k_fold_add<false, true>), dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log,
+                           rbeg, cmap, nch, dense, N, d8);
+    else if (d8)
+        hipLaunchKernelGGL(k_fold_add8, dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, rbeg, cmap,
+                           nch, dense, N, d8);
+    else if (((uintptr_t)dense & 15u) == 0 && !(fv && strcmp(fv, "0") == 0))
         hipLaunchKernelGGL(k_fold_add<true>, dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, rbeg, cmap,
                            nch, dense, N);
     else
@@ -4899,10 +5057,11 @@ extern "C" int shd_dev_pcnt_fold_reserve(size_t L, void** scratch) {
     return fold_reserve(*static_cast<FoldScratch*>(*scratch), L);
 }
 
-extern "C" int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream) {
+extern "C" int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t N, void** scratch,
+                                 void* stream) {
     if (!L || !N) return 0;
     if (!*scratch && !(*scratch = new (std::nothrow) FoldScratch())) return shd_fail(-ENOMEM, "fold scratch");
-    return pcnt_fold(static_cast<uint32_t*>(log), L, dense, N, *static_cast<FoldScratch*>(*scratch),
+    return pcnt_fold(static_cast<uint32_t*>(log), L, dense, d8, N, *static_cast<FoldScratch*>(*scratch),
                      (hipStream_t)stream);
 }
 
@@ -4917,14 +5076,14 @@ extern "C" void shd_dev_pcnt_scratch_free(void* scratch) {
     delete f;
 }
 
-extern "C" int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, size_t cap,
+extern "C" int shd_dev_pcnt_spill(uint32_t* cnt, uint8_t* d8, size_t n, uint32_t thr, uint64_t* d_list, size_t cap,
                                   uint32_t* d_nlist, size_t* appended) {
     *appended = 0;
     if (!n) return 0;
     if (cap > 0xFFFFFFFFull) cap = 0xFFFFFFFFull;
     int rc = hip_status(hipMemset(d_nlist, 0, 4), "hipMemset spill count");
     if (rc) return rc;
-    hipLaunchKernelGGL(k_pcnt_spill, dim3(grid_for(n, 256, 8192)), dim3(256), 0, nullptr, cnt, n, thr,
+    hipLaunchKernelGGL(k_pcnt_spill, dim3(grid_for(n, 256, 8192)), dim3(256), 0, nullptr, cnt, d8, n, thr,
                        (unsigned long long*)d_list, (uint32_t)cap, d_nlist);
     if ((rc = hip_status(hipGetLastError(), "k_pcnt_spill launch"))) return rc;
     uint32_t m = 0;

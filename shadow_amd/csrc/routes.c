@@ -572,8 +572,12 @@ static int pcnt_fold(ShdTopology* t, ShdPcnt* p) {
     if (!p->alloc || !p->log_fill) return 0;
     int rc = shd_dev_init(p->device);
     if (!rc) rc = shd_dev_sync();
+    /* SHD_FOLD_D8=0 (A/B): this fold adds into the u32 counters (the deltas
+     * already held stay counted: reads sum both) */
+    const char* d8v = getenv("SHD_FOLD_D8");
+    uint8_t* d8 = d8v && !strcmp(d8v, "0") ? NULL : p->d8;
     if (!rc)
-        rc = shd_dev_pcnt_fold(p->log, p->log_fill, p->base, (uint64_t)(p->hi) * (uint64_t)t->A, &p->fold, NULL);
+        rc = shd_dev_pcnt_fold(p->log, p->log_fill, p->base, d8, (uint64_t)(p->hi) * (uint64_t)t->A, &p->fold, NULL);
     if (!rc) rc = shd_dev_sync();
     if (!rc) p->log_fill = 0;
     shd_dev_init(t->device);
@@ -595,7 +599,10 @@ static int pcnt_spill(ShdTopology* t, ShdPcnt* p, uint32_t thr) {
     if (!h) rc = -ENOMEM;
     if (!rc && !(rc = shd_dev_malloc((void**)&d_list, 16 * cap))) rc = shd_dev_malloc((void**)&d_n, 4);
     for (size_t got = cap; !rc && got == cap;) {
-        if ((rc = shd_dev_pcnt_spill(p->alloc, n, thr, d_list, cap, d_n, &got)) || !got) break;
+        if ((rc = shd_dev_pcnt_spill(p->alloc, p->d8 ? p->d8 + (size_t)p->lo * A : NULL, n, thr, d_list, cap, d_n,
+                                     &got)) ||
+            !got)
+            break;
         if ((rc = shd_dev_d2h(h, d_list, 16 * got))) break;
         pthread_mutex_lock(&t->pkt_mu);
         if (!(rc = shd_count_reserve_locked(t, got)))
@@ -648,6 +655,22 @@ int shd_pcnt_ensure(ShdTopology* t, ShdPcnt* p, int lo, int hi, size_t n) {
             p->hi = hi;
             p->device = dev;
             p->budget = 0;
+            /* the fold's u8 delta layer (log-mode tables only; without it --
+             * no memory -- the fold adds into the u32 counters) */
+            size_t fr = 0, tot = 0;
+            if ((uint64_t)hi * (uint64_t)t->A <= SHD_PCNT_FOLD_MAX_N && !shd_dev_mem_info(&fr, &tot) &&
+                fr > bytes / 4 + ((size_t)1 << 30)) { /* (headroom: no failed allocation left behind) */
+                const size_t first = (size_t)lo * (size_t)t->A, off = first & 15u;
+                void* d8 = NULL;
+                if (!shd_dev_malloc(&d8, bytes / 4 + 32)) {
+                    if (shd_dev_memset(d8, 0, bytes / 4 + 32) || shd_dev_sync()) {
+                        shd_dev_free(d8);
+                    } else {
+                        p->d8_alloc = (uint8_t*)d8;
+                        p->d8 = p->d8_alloc + off - first; /* (16-B aligned: hipMalloc is) */
+                    }
+                }
+            }
         }
     }
     if (p->hostlog) {
@@ -740,6 +763,7 @@ int shd_pcnt_drop(ShdTopology* t, ShdPcnt* p) {
     int rc = p->hostlog ? pcnt_drain_host(t, p) : pcnt_spill(t, p, 1u); /* (folds the log first) */
     shd_dev_init(p->device);
     shd_dev_free(p->alloc);
+    shd_dev_free(p->d8_alloc);
     shd_dev_free(p->log);
     shd_dev_pcnt_scratch_free(p->fold);
     memset(p, 0, sizeof *p);
@@ -756,6 +780,7 @@ void shd_pcnt_discard(ShdTopology* t) {
         if (ps[k]->alloc || ps[k]->hostlog) {
             shd_dev_init(ps[k]->device);
             shd_dev_free(ps[k]->alloc);
+            shd_dev_free(ps[k]->d8_alloc);
             shd_dev_free(ps[k]->log);
             shd_dev_pcnt_scratch_free(ps[k]->fold);
             memset(ps[k], 0, sizeof *ps[k]);
@@ -778,10 +803,13 @@ int shd_pcnt_read(ShdTopology* t, int row, int col, uint64_t* v) {
     ShdPcnt* p = pcnt_of(t, row);
     if (!p) return 0;
     uint32_t x = 0;
+    uint8_t y = 0;
+    const size_t k = (size_t)row * (size_t)t->A + (size_t)col;
     int rc = shd_dev_init(p->device);
     if (!rc) rc = shd_dev_sync();
-    if (!rc) rc = shd_dev_d2h(&x, p->base + (size_t)row * (size_t)t->A + (size_t)col, 4);
-    *v = x;
+    if (!rc) rc = shd_dev_d2h(&x, p->base + k, 4);
+    if (!rc && p->d8) rc = shd_dev_d2h(&y, p->d8 + k, 1); /* (the fold's delta layer) */
+    *v = (uint64_t)x + y;
     shd_dev_init(t->device);
     return rc;
 }
@@ -792,6 +820,7 @@ int shd_pcnt_read_rows(ShdTopology* t, int lo, int hi, uint64_t* out) {
     const size_t A = (size_t)t->A;
     const size_t chunk_rows = A ? ((size_t)1 << 24) / A + 1 : 1; /* ~64 MB of u32 per copy */
     uint32_t* x = NULL;
+    uint8_t* y = NULL;
     int rc = 0;
     for (int i = lo; i < hi && !rc;) {
         ShdPcnt* p = pcnt_of(t, i);
@@ -804,13 +833,19 @@ int shd_pcnt_read_rows(ShdTopology* t, int lo, int hi, uint64_t* out) {
         const size_t m = (size_t)(e - i) * A;
         if (!x && !(x = (uint32_t*)malloc(4 * (chunk_rows < (size_t)(hi - lo) ? chunk_rows : (size_t)(hi - lo)) * A)))
             return -ENOMEM;
+        if (p->d8 && !y && !(y = (uint8_t*)malloc((chunk_rows < (size_t)(hi - lo) ? chunk_rows : (size_t)(hi - lo)) * A))) {
+            free(x);
+            return -ENOMEM;
+        }
         if (!(rc = shd_dev_init(p->device)) && !(rc = shd_dev_sync()))
             rc = shd_dev_d2h(x, p->base + (size_t)i * A, 4 * m);
+        if (!rc && p->d8) rc = shd_dev_d2h(y, p->d8 + (size_t)i * A, m); /* (the fold's delta layer) */
         uint64_t* o = out + (size_t)(i - lo) * A;
-        for (size_t k = 0; !rc && k < m; k++) o[k] += x[k];
+        for (size_t k = 0; !rc && k < m; k++) o[k] += (uint64_t)x[k] + (p->d8 ? y[k] : 0u);
         i = e;
     }
     free(x);
+    free(y);
     shd_dev_init(t->device);
     return rc;
 }

@@ -176,23 +176,28 @@ typedef struct {
     uint32_t* pcnt;
 } ShdPktCtx;
 
-/* Path packet counter spill (packet.hip): every entry of cnt[0, n) that is
+/* Path packet counter spill (packet.hip): every entry of cnt[0, n) whose
+ * count -- cnt[i], plus d8[i] when the u8 delta layer d8 is not NULL -- is
  * >= thr is appended to list as {index (u64), value (u64)} (at most cap
- * entries; *d_nlist, device, counts all that qualified) and zeroed -- only
- * the appended ones.  Synchronous on the calling thread's device.  Returns
- * the number of entries appended in *appended (host). */
-int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, size_t cap, uint32_t* d_nlist,
-                       size_t* appended);
+ * entries; *d_nlist, device, counts all that qualified) and zeroed (both
+ * layers) -- only the appended ones.  Synchronous on the calling thread's
+ * device.  Returns the number of entries appended in *appended (host). */
+int shd_dev_pcnt_spill(uint32_t* cnt, uint8_t* d8, size_t n, uint32_t thr, uint64_t* d_list, size_t cap,
+                       uint32_t* d_nlist, size_t* appended);
 /* Adds the L logged keys of `log` (u32 flat entry indices below N <=
- * SHD_PCNT_FOLD_MAX_N, all-ones = nothing) into the dense counters (N u32):
- * a two-level partition of the keys into 32K-counter regions and one
- * workgroup per region that accumulates its keys in LDS and adds its
- * counters to the dense table.  The log's buffer is overwritten (it holds
- * the second level's output).  Enqueued on stream; *scratch: grow-only
- * buffers (NULL the first time; shd_dev_pcnt_fold_reserve sizes them for L
- * keys ahead), freed with shd_dev_pcnt_scratch_free. */
+ * SHD_PCNT_FOLD_MAX_N, all-ones = nothing) into the counters: a two-level
+ * partition of the keys into 32K-counter regions and one workgroup per
+ * region that accumulates its keys in LDS and adds its counters to the
+ * table.  With d8 (NULL: none) the counts go to the u8 delta layer d8[N]
+ * (16-B aligned at index 0; a pair's count is dense + d8): a byte that would
+ * pass 255 moves its whole value into dense with one device atomic and
+ * restarts at 0, so the fold streams N bytes of deltas instead of 4N of
+ * counters.  The log's buffer is overwritten (it holds the second level's
+ * output).  Enqueued on stream; *scratch: grow-only buffers (NULL the first
+ * time; shd_dev_pcnt_fold_reserve sizes them for L keys ahead), freed with
+ * shd_dev_pcnt_scratch_free. */
 #define SHD_PCNT_FOLD_MAX_N (1ull << 29)
-int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream);
+int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t N, void** scratch, void* stream);
 int shd_dev_pcnt_fold_reserve(size_t L, void** scratch);
 void shd_dev_pcnt_scratch_free(void* scratch);
 

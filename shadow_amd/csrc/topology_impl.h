@@ -77,6 +77,11 @@ void shd_rel_list_free(ShdRelList* q);
 typedef struct {
     uint32_t* alloc;
     uint32_t* base;
+    /* the u8 delta layer of the log mode's fold (NULL: none): a pair's count
+     * is base[k] + d8[k]; d8 is 16-B aligned at index 0 (d8_alloc holds
+     * rows [lo, hi) plus 32 B of padding) */
+    uint8_t* d8_alloc;
+    uint8_t* d8;
     int lo, hi;
     int device;
     uint64_t budget;

@@ -220,24 +220,35 @@ int shd_host_alloc(void** p, size_t bytes) {
     return *p ? 0 : -ENOMEM;
 }
 void shd_host_free(void* p) { free(p); }
-int shd_dev_pcnt_spill(uint32_t* cnt, size_t n, uint32_t thr, uint64_t* d_list, size_t cap, uint32_t* d_nlist,
-                       size_t* appended) {
+int shd_dev_pcnt_spill(uint32_t* cnt, uint8_t* d8, size_t n, uint32_t thr, uint64_t* d_list, size_t cap,
+                       uint32_t* d_nlist, size_t* appended) {
     size_t k = 0;
-    for (size_t i = 0; i < n && k < cap; i++)
-        if (cnt[i] && cnt[i] >= thr) {
+    for (size_t i = 0; i < n && k < cap; i++) {
+        const uint32_t v = cnt[i] + (d8 ? d8[i] : 0u);
+        if (v && v >= thr) {
             d_list[2 * k] = i;
-            d_list[2 * k + 1] = cnt[i];
+            d_list[2 * k + 1] = v;
             cnt[i] = 0;
+            if (d8) d8[i] = 0;
             k++;
         }
+    }
     *d_nlist = (uint32_t)k;
     *appended = k;
     return 0;
 }
-int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint64_t N, void** scratch, void* stream) {
+int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t N, void** scratch, void* stream) {
     for (size_t i = 0; i < L; i++) {
         const uint32_t k = ((const uint32_t*)log)[i];
-        if (k != UINT32_MAX) dense[k]++;
+        if (k == UINT32_MAX) continue;
+        if (!d8) {
+            dense[k]++;
+        } else if (d8[k] == 255) { /* (the device fold moves a byte past 255 into the u32 counter) */
+            dense[k] += 256;
+            d8[k] = 0;
+        } else {
+            d8[k]++;
+        }
     }
     return 0;
 }

@@ -381,13 +381,18 @@ def test_path_counters_spill_to_host(api, mode, monkeypatch):
     assert max(int(x.split("PacketCount=")[1].split()[0]) for x in orc.cached_paths_log()) > 3  # spilled
 
 
+@pytest.mark.parametrize("fold", ["d8", "u32", "mixed"])
 @pytest.mark.parametrize("log", ["250000", "-"])
-def test_path_counter_fold_multi_region(log, monkeypatch):
+def test_path_counter_fold_multi_region(log, fold, monkeypatch):
     """The counter log's fold over several coarse buckets and hundreds of
     32K-counter regions (A ~ 5,600 slots: 31M counters), three device rounds
     of 200k packets: every counter against the numpy restatement after each
     round.  SHD_PCNT_LOG=250000 makes the second and third round fold the
-    logs before them first; "-" folds only at each read."""
+    logs before them first; "-" folds only at each read.  fold: into the u8
+    delta layer (default; two hot pairs take 200 / 5,000 / 200 and 200 /
+    200 / 200 counts, so bytes pass 255 within one fold and across folds and
+    move into the u32 counters), into the u32 counters alone (SHD_FOLD_D8=0),
+    or alternating per round (both layers hold counts)."""
     import torch
     if log != "-":
         monkeypatch.setenv("SHD_PCNT_LOG", log)
@@ -404,8 +409,14 @@ def test_path_counter_fold_multi_region(log, monkeypatch):
     n = 200_000
     for r in range(3):
         pk = synth.packet_batch(n, H, 0x5EED0F12 + r, 100_000_000, 10_000_000, st)
-        if r == 1:  # a hot pair: many counts on one counter
-            pk["src_host"][:5000], pk["dst_host"][:5000] = 3, 7
+        # hot pairs: many counts on one counter
+        k = 5000 if r == 1 else 200
+        pk["src_host"][:k], pk["dst_host"][:k] = 3, 7
+        pk["src_host"][k:k + 200], pk["dst_host"][k:k + 200] = 5, 9
+        if fold == "u32" or (fold == "mixed" and r == 1):
+            monkeypatch.setenv("SHD_FOLD_D8", "0")
+        else:
+            monkeypatch.delenv("SHD_FOLD_D8", raising=False)
         d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
         d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
         d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
