@@ -4484,26 +4484,36 @@ __global__ __launch_bounds__(256) void k_pcnt_spill(uint32_t* __restrict__ cnt, 
 
 // ---- the counter log's fold (shd_dev_pcnt_fold) ----
 // The logged keys (u32 flat entry indices < N <= kFoldMaxN, all-ones = not
-// kept) are added into the dense counters by a two-level partition and one
-// LDS accumulation per 32K-counter region:
+// kept) are added into the counters by a two-level partition and one LDS
+// accumulation per 32K-counter region:
 //   key -> region r = key >> 15 (at most 16,384), coarse c = r >> 7 (<= 128),
 //   fine f = r & 127.
-// 1. k_fold_hist1: per tile of kFoldT log entries, the count per coarse
-//    bucket -> M1[c * nt1 + t]; scan -> every (c, t) run's start;
-// 2. k_fold_part1: each tile's kept keys counting-sorted by coarse bucket in
-//    LDS and written in that order (a run per coarse bucket: consecutive
-//    lanes, consecutive addresses) -> part;
-// 3. k_fold_hist2 / k_fold_part2: the same within each coarse bucket's
-//    contiguous range of part, by fine bucket, over tiles of that range
-//    alone; M2 is laid out (c, f, t), so its scan is the global order of the
-//    regions -> back into the log's buffer;
-// 4. k_fold_add: one workgroup per region adds its keys into LDS counters and
-//    each nonzero one into the dense table (the region's counters belong to
-//    this workgroup alone: plain read-modify-write, only the lines that hold a
-//    nonzero counter move).
-// Every pass streams the keys with whole-line writes; the single-level
-// partition over 12k regions (runs of < 1 key per tile) wrote every key as
-// its own store: 2.1 ms of a 3.1 ms fold of 184M keys (profiles/r05d_fold_kernel_stats.csv).
+// Both levels sort tile-locally -- no histogram pass over the keys and no
+// global scan of per-tile counts: each level writes its tiles' digit
+// prefixes, and the next level reads runs out of the tiles.
+// 1. k_fold_p1: a tile of kFoldT log entries counting-sorted by coarse
+//    digit in LDS, written back at the tile's own offset of `part` (kept
+//    keys only), with its prefix P1[t][0..128] (P1[t][128]: kept keys).
+// 2. k_fold_units: unit (c, g) = coarse digit c over the group g of kFoldG
+//    consecutive level-1 tiles; its key count from P1 and the level-2 tiles
+//    it needs (ceil(count / kFoldT)); two small scans place every unit's keys
+//    (c-major: a coarse digit's units are contiguous) and level-2 tiles.
+// 3. k_fold_p2: one workgroup per unit gathers its runs (coarse c of each of
+//    its kFoldG tiles, ~60 keys each) in batches of kFoldT, counting-sorts a
+//    batch by fine digit in LDS and writes it as u16 region offsets (the
+//    coarse and fine digits are implied from here on) at the unit's place,
+//    with the level-2 tile's fine prefix F[tile][0..128] and start S[tile].
+// 4. k_fold_rn: region r's keys = its fine run in each of its coarse
+//    digit's level-2 tiles; rn[r] = its chunks (at most kFoldAddMax keys
+//    each, by tile ranges); k_fold_chunks: the chunk list.
+// 5. k_fold_add: one workgroup per chunk gathers the region's runs, adds
+//    them into LDS counters and the LDS counters into the table: the u8
+//    delta layer d8 (a byte past 255 moves into the u32 counter) or the u32
+//    counters themselves; a region of several chunks adds with device atomics.
+// Every pass streams the keys in whole-line runs; the single-level partition
+// over 12k regions (runs of < 1 key per tile) wrote every key as its own
+// store: 2.1 ms of a 3.1 ms fold of 184M keys (profiles/r05d_fold_kernel_stats.csv);
+// the histogram passes of round 5's two levels took 0.42 of 1.6 ms (r06f).
 constexpr uint32_t kFoldRegionBits = 15;          // 32K u32 counters = 128 KB of LDS
 constexpr uint32_t kFoldFineBits = 7;              // 128 regions per coarse bucket
 constexpr uint32_t kFoldCoarse = 128;              // at most
@@ -4511,405 +4521,327 @@ constexpr unsigned long long kFoldMaxN = 1ull << (kFoldRegionBits + kFoldFineBit
 constexpr int kFoldWG = 1024;
 constexpr int kFoldPer = 8;                        // keys per thread per tile
 constexpr uint32_t kFoldT = kFoldWG * kFoldPer;    // 8,192 keys per tile
+constexpr uint32_t kFoldG = 128;                   // level-1 tiles per level-2 unit
+constexpr uint32_t kFoldP = kFoldCoarse + 1;       // prefix words per tile
 constexpr uint32_t kFoldSent = 0xFFFFFFFFu;
+constexpr uint32_t kFoldAddMax = 1u << 18;         // keys per add chunk of a big region (about)
+constexpr uint32_t kFoldSmallMax = 65535;          // a small region's keys: its u16 LDS counters cannot wrap
+constexpr uint32_t kFoldBig = 0x80000000u;         // rn flag: a big region
+constexpr uint32_t kFoldMaxRegions = 1u << 14;
 
 __device__ __forceinline__ uint32_t fold_coarse(uint32_t k) { return k >> (kFoldRegionBits + kFoldFineBits); }
 __device__ __forceinline__ uint32_t fold_fine(uint32_t k) { return (k >> kFoldRegionBits) & ((1u << kFoldFineBits) - 1u); }
 
-// one tile's keys into registers (sentinel past the end)
-__device__ __forceinline__ void fold_load(const uint32_t* __restrict__ keys, size_t beg, size_t end,
-                                          uint32_t (&k)[kFoldPer]) {
-#pragma unroll
-    for (int u = 0; u < kFoldPer; u++) {
-        const size_t i = beg + (size_t)u * kFoldWG + threadIdx.x;
-        k[u] = i < end ? __builtin_nontemporal_load(keys + i) : kFoldSent;
-    }
-}
-
-// the digit counts of a tile in LDS h[128] (zeroed by the caller, synced after)
-template <bool kCoarse>
-__device__ __forceinline__ void fold_count(const uint32_t (&k)[kFoldPer], uint32_t* h) {
-#pragma unroll
-    for (int u = 0; u < kFoldPer; u++)
-        if (k[u] != kFoldSent) atomicAdd(&h[kCoarse ? fold_coarse(k[u]) : fold_fine(k[u])], 1u);
-}
-
-__global__ __launch_bounds__(kFoldWG) void k_fold_hist1(const uint32_t* __restrict__ log, size_t L, uint32_t C,
-                                                        uint32_t nt1, uint32_t* __restrict__ M1) {
-    __shared__ uint32_t h[kFoldCoarse];
-    if (threadIdx.x < kFoldCoarse) h[threadIdx.x] = 0u;
-    __syncthreads();
-    uint32_t k[kFoldPer];
-    const size_t beg = (size_t)blockIdx.x * kFoldT;
-    fold_load(log, beg, beg + kFoldT < L ? beg + kFoldT : L, k);
-    fold_count<true>(k, h);
-    __syncthreads();
-    if (threadIdx.x < C) M1[(size_t)threadIdx.x * nt1 + blockIdx.x] = h[threadIdx.x];
-}
-
-// counting sort of the tile's keys by digit in LDS, then written in that
-// order: element j of the sorted tile (digit d, the d-run's j - start[d]-th)
-// goes to base[d] + j - start[d] (base: this tile's run starts, LDS)
-template <bool kCoarse>
-__device__ __forceinline__ void fold_part_tile(const uint32_t (&k)[kFoldPer], uint32_t* h, uint32_t* start,
-                                               const uint32_t* base, uint32_t* stage, uint32_t* __restrict__ out) {
-    uint32_t rk[kFoldPer];
-#pragma unroll
-    for (int u = 0; u < kFoldPer; u++)
-        rk[u] = k[u] != kFoldSent ? atomicAdd(&h[kCoarse ? fold_coarse(k[u]) : fold_fine(k[u])], 1u) : 0u;
-    __syncthreads();
-    __shared__ uint32_t tot;
-    if (threadIdx.x < 64) { // exclusive scan of the 128 counts (two per lane)
+// the 128 counts h[] of a tile -> exclusive prefix start[] and *tot (64
+// threads, two digits per lane; the caller syncs)
+__device__ __forceinline__ void fold_prefix128(const uint32_t* h, uint32_t* start, uint32_t* tot) {
+    if (threadIdx.x < 64) {
         const uint32_t a = h[2 * threadIdx.x], b = h[2 * threadIdx.x + 1];
         const uint32_t inc = wave_incl_scan(a + b, (int)threadIdx.x);
         start[2 * threadIdx.x] = inc - a - b;
         start[2 * threadIdx.x + 1] = inc - b;
-        if (threadIdx.x == 63) tot = inc;
+        if (threadIdx.x == 63) *tot = inc;
     }
+}
+
+__global__ __launch_bounds__(kFoldWG) void k_fold_p1(const uint32_t* __restrict__ log, size_t L,
+                                                     uint32_t* __restrict__ part, uint32_t* __restrict__ P1) {
+    __shared__ uint32_t h[kFoldCoarse], start[kFoldCoarse], tot;
+    __shared__ uint32_t stage[kFoldT];
+    if (threadIdx.x < kFoldCoarse) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const size_t beg = (size_t)blockIdx.x * kFoldT, end = beg + kFoldT < L ? beg + kFoldT : L;
+    uint32_t k[kFoldPer], rk[kFoldPer];
+#pragma unroll
+    for (int u = 0; u < kFoldPer; u++) {
+        const size_t i = beg + (size_t)u * kFoldWG + threadIdx.x;
+        k[u] = i < end ? __builtin_nontemporal_load(log + i) : kFoldSent;
+    }
+#pragma unroll
+    for (int u = 0; u < kFoldPer; u++) rk[u] = k[u] != kFoldSent ? atomicAdd(&h[fold_coarse(k[u])], 1u) : 0u;
+    __syncthreads();
+    fold_prefix128(h, start, &tot);
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kFoldPer; u++)
-        if (k[u] != kFoldSent) stage[start[kCoarse ? fold_coarse(k[u]) : fold_fine(k[u])] + rk[u]] = k[u];
+        if (k[u] != kFoldSent) stage[start[fold_coarse(k[u])] + rk[u]] = k[u];
+    if (threadIdx.x < kFoldP) P1[(size_t)blockIdx.x * kFoldP + threadIdx.x] = threadIdx.x < kFoldCoarse ? start[threadIdx.x] : tot;
     __syncthreads();
     const uint32_t n = tot;
-    for (uint32_t j = threadIdx.x; j < n; j += kFoldWG) {
-        const uint32_t key = stage[j], d = kCoarse ? fold_coarse(key) : fold_fine(key);
-        out[base[d] + (j - start[d])] = key;
-    }
+    for (uint32_t j = threadIdx.x; j < n; j += kFoldWG) part[beg + j] = stage[j];
 }
 
-__global__ __launch_bounds__(kFoldWG) void k_fold_part1(const uint32_t* __restrict__ log, size_t L, uint32_t C,
-                                                        uint32_t nt1, const uint32_t* __restrict__ M1,
-                                                        uint32_t* __restrict__ part) {
-    __shared__ uint32_t h[kFoldCoarse], start[kFoldCoarse], base[kFoldCoarse];
-    __shared__ uint32_t stage[kFoldT];
-    if (threadIdx.x < kFoldCoarse) {
-        h[threadIdx.x] = 0u;
-        base[threadIdx.x] = threadIdx.x < C ? M1[(size_t)threadIdx.x * nt1 + blockIdx.x] : 0u;
+// Group g of kFoldG level-1 tiles (one workgroup): its prefixes through LDS
+// (coalesced both ways) into every unit (c, g)'s run table RT[u][i] = {start
+// in part, length} of tile g kFoldG + i, and the unit's keys U[u] and level-2
+// tiles T2[u] (u = c * ng + g: c-major)
+constexpr int kFoldUnitsWG = 1024;
+__global__ __launch_bounds__(kFoldUnitsWG) void k_fold_units(const uint32_t* __restrict__ P1, uint32_t nt1, uint32_t C,
+                                                             uint32_t ng, uint2* __restrict__ RT,
+                                                             uint32_t* __restrict__ U, uint32_t* __restrict__ T2) {
+    __shared__ uint32_t P[kFoldG * kFoldP];
+    __shared__ uint32_t us[kFoldCoarse];
+    const uint32_t g = blockIdx.x, t0 = g * kFoldG, nt = t0 + kFoldG < nt1 ? kFoldG : nt1 - t0;
+    for (uint32_t j = threadIdx.x; j < nt * kFoldP; j += kFoldUnitsWG) P[j] = P1[(size_t)t0 * kFoldP + j];
+    if (threadIdx.x < kFoldCoarse) us[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < C * kFoldG; j += kFoldUnitsWG) { // (c, i): i fastest
+        const uint32_t c = j / kFoldG, i = j - c * kFoldG;
+        uint2 e = make_uint2(0u, 0u);
+        if (i < nt) {
+            const uint32_t a = P[i * kFoldP + c], b = P[i * kFoldP + c + 1];
+            e = make_uint2((t0 + i) * kFoldT + a, b - a);
+        }
+        RT[((size_t)c * ng + g) * kFoldG + i] = e;
+        const uint32_t w = wave_incl_scan(e.y, (int)(threadIdx.x & 63)); // (64 i of one c per wave)
+        if ((threadIdx.x & 63) == 63) atomicAdd(&us[c], w);
     }
     __syncthreads();
-    uint32_t k[kFoldPer];
-    const size_t beg = (size_t)blockIdx.x * kFoldT;
-    fold_load(log, beg, beg + kFoldT < L ? beg + kFoldT : L, k);
-    fold_part_tile<true>(k, h, start, base, stage, part);
+    if (threadIdx.x < C) {
+        const uint32_t v = us[threadIdx.x];
+        U[(size_t)threadIdx.x * ng + g] = v;
+        T2[(size_t)threadIdx.x * ng + g] = (v + kFoldT - 1) / kFoldT;
+    }
 }
 
-// the level-2 tiles: coarse bucket c's range of part is [M1[c * nt1],
-// M1[(c + 1) * nt1]) and holds tiles_c = ceil(size / kFoldT) tiles; tbase[c]
-// = the tiles before c.  Every workgroup derives them from M1 (LDS).
-struct FoldL2 {
-    uint32_t lo[kFoldCoarse + 1]; // range starts (lo[C] = total)
-    uint32_t tb[kFoldCoarse + 1]; // tile bases (tb[C] = all tiles)
-};
-__device__ __forceinline__ void fold_l2_geometry(const uint32_t* __restrict__ M1, uint32_t C, uint32_t nt1, FoldL2& g) {
-    if (threadIdx.x < 64) {
-        uint32_t lo[2], nt[2];
+// units blockIdx.x, + gridDim.x, ... (u = (c, g): runs of c out of tiles [g
+// kFoldG, ...), RT), each in batches of kFoldT keys (virtual position v: run
+// i holds [vs[i], vs[i + 1])).  Persistent, two workgroups per CU: the next
+// unit's run table and places are loaded while this one's keys are (one
+// unit per workgroup waits for them first: 0.51 ms of a 1.2 ms fold, r06j).
+constexpr int kFoldP2WG = 512;
+constexpr int kFoldP2Per = kFoldT / kFoldP2WG; // 16 keys per thread per batch
+__global__ __launch_bounds__(kFoldP2WG) void k_fold_p2(const uint32_t* __restrict__ part, const uint2* __restrict__ RT,
+                                                       uint32_t units, const uint32_t* __restrict__ Uoff,
+                                                       const uint32_t* __restrict__ L2b, uint16_t* __restrict__ out16,
+                                                       uint32_t* __restrict__ F, uint32_t* __restrict__ S) {
+    __shared__ uint32_t rs[kFoldG], vs[kFoldG + 1], pl[2];
+    __shared__ uint32_t h[kFoldCoarse], start[kFoldCoarse], tot;
+    __shared__ __attribute__((aligned(16))) uint16_t stage[kFoldT];
+    uint2 n0 = make_uint2(0u, 0u), n1 = make_uint2(0u, 0u);
+    uint32_t np = 0;
+    auto fetch = [&](uint32_t u) { // (threads < 64: two runs each; threads 64, 65: the places)
+        if (u >= units) return;
+        if (threadIdx.x < 64) {
+            n0 = RT[(size_t)u * kFoldG + 2 * threadIdx.x];
+            n1 = RT[(size_t)u * kFoldG + 2 * threadIdx.x + 1];
+        } else if (threadIdx.x == 64) {
+            np = Uoff[u];
+        } else if (threadIdx.x == 65) {
+            np = L2b[u];
+        }
+    };
+    fetch(blockIdx.x);
+    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) { // (block-uniform)
+        if (threadIdx.x < 64) { // this unit's runs and their exclusive prefix
+            rs[2 * threadIdx.x] = n0.x;
+            rs[2 * threadIdx.x + 1] = n1.x;
+            const uint32_t inc = wave_incl_scan(n0.y + n1.y, (int)threadIdx.x);
+            vs[2 * threadIdx.x] = inc - n0.y - n1.y;
+            vs[2 * threadIdx.x + 1] = inc - n1.y;
+            if (threadIdx.x == 63) vs[kFoldG] = inc;
+        } else if (threadIdx.x < 66) {
+            pl[threadIdx.x - 64] = np;
+        }
+        __syncthreads();
+        fetch(u + gridDim.x); // (in flight behind this unit's keys)
+        const uint32_t U = vs[kFoldG];
+        const uint32_t pos0 = pl[0], tile0 = pl[1];
+        for (uint32_t b0 = 0; b0 < U; b0 += kFoldT) { // (block-uniform)
+            if (threadIdx.x < kFoldCoarse) h[threadIdx.x] = 0u;
+            uint32_t k[kFoldP2Per], rk[kFoldP2Per];
 #pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const uint32_t c = 2 * threadIdx.x + e;
-            lo[e] = c <= C ? M1[(size_t)c * nt1] : 0u;
-        }
-        // (tile counts need the next range start: lo of c + 1)
-        const uint32_t next1 = (2 * threadIdx.x + 2 <= C) ? M1[(size_t)(2 * threadIdx.x + 2) * nt1] : 0u;
+            for (int e = 0; e < kFoldP2Per; e++) {
+                const uint32_t v = b0 + (uint32_t)e * kFoldP2WG + threadIdx.x;
+                k[e] = kFoldSent;
+                if (v < U) {
+                    uint32_t lo = 0, hi = kFoldG; // the run holding v: largest i with vs[i] <= v
 #pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const uint32_t c = 2 * threadIdx.x + e;
-            const uint32_t hi = e == 0 ? lo[1] : next1;
-            nt[e] = c < C ? (hi - lo[e] + kFoldT - 1) / kFoldT : 0u;
-            if (c <= C) g.lo[c] = lo[e];
+                    for (int it = 0; it < 7; it++) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (vs[m] <= v) lo = m;
+                        else hi = m;
+                    }
+                    k[e] = part[rs[lo] + (v - vs[lo])];
+                }
+            }
+            lds_barrier(); // (the h reset; the key loads stay in flight)
+#pragma unroll
+            for (int e = 0; e < kFoldP2Per; e++) rk[e] = k[e] != kFoldSent ? atomicAdd(&h[fold_fine(k[e])], 1u) : 0u;
+            __syncthreads();
+            fold_prefix128(h, start, &tot);
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < kFoldP2Per; e++)
+                if (k[e] != kFoldSent)
+                    stage[start[fold_fine(k[e])] + rk[e]] = (uint16_t)(k[e] & ((1u << kFoldRegionBits) - 1u));
+            const uint32_t tile = tile0 + b0 / kFoldT, p0 = pos0 + b0;
+            if (threadIdx.x < kFoldP) F[(size_t)tile * kFoldP + threadIdx.x] = threadIdx.x < kFoldCoarse ? start[threadIdx.x] : tot;
+            if (threadIdx.x == 0) S[tile] = p0;
+            __syncthreads();
+            const uint32_t n = tot;
+            // (u16 pairs where the batch starts at an even position: kFoldT is even)
+            if ((p0 & 1u) == 0u) {
+                const uint32_t* st2 = reinterpret_cast<const uint32_t*>(stage);
+                uint32_t* o2 = reinterpret_cast<uint32_t*>(out16 + p0);
+                for (uint32_t j = threadIdx.x; j < n / 2; j += kFoldP2WG) o2[j] = st2[j];
+                if ((n & 1u) && threadIdx.x == 0) out16[p0 + n - 1] = stage[n - 1];
+            } else {
+                for (uint32_t j = threadIdx.x; j < n; j += kFoldP2WG) out16[p0 + j] = stage[j];
+            }
+            __syncthreads();
         }
-        const uint32_t inc = wave_incl_scan(nt[0] + nt[1], (int)threadIdx.x);
-        if (2 * threadIdx.x <= C) g.tb[2 * threadIdx.x] = inc - nt[0] - nt[1];
-        if (2 * threadIdx.x + 1 <= C) g.tb[2 * threadIdx.x + 1] = inc - nt[1];
-        if (threadIdx.x == 63) { // (C = 128: entry C lies past the 64 lanes' pairs)
-            g.tb[C] = inc;
-            g.lo[C] = M1[(size_t)C * nt1];
-        }
     }
-    __syncthreads();
-}
-// the (coarse, tile) of level-2 tile number `gt` (false: past the last tile)
-__device__ __forceinline__ bool fold_l2_tile(const FoldL2& g, uint32_t C, uint32_t gt, uint32_t* c, uint32_t* t) {
-    if (gt >= g.tb[C]) return false;
-    uint32_t a = 0, b = C; // largest c with tb[c] <= gt and a tile of its own
-    while (b - a > 1) {
-        const uint32_t m = (a + b) >> 1;
-        if (g.tb[m] <= gt) a = m;
-        else b = m;
-    }
-    while (g.tb[a + 1] <= gt) a++; // (skips empty buckets: tb[a + 1] == tb[a])
-    *c = a;
-    *t = gt - g.tb[a];
-    return true;
 }
 
-__global__ __launch_bounds__(kFoldWG) void k_fold_hist2(const uint32_t* __restrict__ part, const uint32_t* __restrict__ M1,
-                                                        uint32_t C, uint32_t nt1, uint32_t* __restrict__ M2) {
-    __shared__ FoldL2 g;
-    __shared__ uint32_t h[1u << kFoldFineBits];
-    fold_l2_geometry(M1, C, nt1, g);
-    uint32_t c, t;
-    if (!fold_l2_tile(g, C, blockIdx.x, &c, &t)) return; // (block-uniform)
-    if (threadIdx.x < (1u << kFoldFineBits)) h[threadIdx.x] = 0u;
-    __syncthreads();
-    const uint32_t ntc = g.tb[c + 1] - g.tb[c];
-    const size_t beg = (size_t)g.lo[c] + (size_t)t * kFoldT, end = beg + kFoldT < g.lo[c + 1] ? beg + kFoldT : g.lo[c + 1];
-    uint32_t k[kFoldPer];
-    fold_load(part, beg, end, k);
-    fold_count<false>(k, h);
-    __syncthreads();
-    if (threadIdx.x < (1u << kFoldFineBits))
-        M2[((size_t)g.tb[c] << kFoldFineBits) + (size_t)threadIdx.x * ntc + t] = h[threadIdx.x];
-}
-
-__global__ __launch_bounds__(kFoldWG) void k_fold_part2(const uint32_t* __restrict__ part, const uint32_t* __restrict__ M1,
-                                                        uint32_t C, uint32_t nt1, const uint32_t* __restrict__ M2,
-                                                        uint32_t* __restrict__ out) {
-    __shared__ FoldL2 g;
-    __shared__ uint32_t h[1u << kFoldFineBits], start[1u << kFoldFineBits], base[1u << kFoldFineBits];
-    __shared__ uint32_t stage[kFoldT];
-    fold_l2_geometry(M1, C, nt1, g);
-    uint32_t c, t;
-    if (!fold_l2_tile(g, C, blockIdx.x, &c, &t)) return;
-    const uint32_t ntc = g.tb[c + 1] - g.tb[c];
-    if (threadIdx.x < (1u << kFoldFineBits)) {
-        h[threadIdx.x] = 0u;
-        base[threadIdx.x] = M2[((size_t)g.tb[c] << kFoldFineBits) + (size_t)threadIdx.x * ntc + t];
+// coarse digit blockIdx.x: each of its regions' keys over its level-2 tiles
+// [L2b[c ng], L2b[(c + 1) ng]) (8 slices of tiles per fine digit, summed in
+// LDS) and its chunk count rn[r]
+__global__ __launch_bounds__(1024) void k_fold_rn(const uint32_t* __restrict__ F, const uint32_t* __restrict__ L2b,
+                                                  uint32_t ng, uint32_t R, uint32_t* __restrict__ rn) {
+    __shared__ uint32_t sum[8][kFoldCoarse];
+    const uint32_t c = blockIdx.x, f = threadIdx.x & (kFoldCoarse - 1), sl = threadIdx.x >> 7;
+    const uint32_t ta = L2b[(size_t)c * ng], tb = L2b[(size_t)(c + 1) * ng];
+    uint32_t s = 0;
+#pragma unroll 4
+    for (uint32_t t = ta + sl; t < tb; t += 8) {
+        const uint32_t* p = F + (size_t)t * kFoldP;
+        s += p[f + 1] - p[f];
     }
+    sum[sl][f] = s;
     __syncthreads();
-    const size_t beg = (size_t)g.lo[c] + (size_t)t * kFoldT, end = beg + kFoldT < g.lo[c + 1] ? beg + kFoldT : g.lo[c + 1];
-    uint32_t k[kFoldPer];
-    fold_load(part, beg, end, k);
-    fold_part_tile<false>(k, h, start, base, stage, out);
+    const uint32_t r = c * kFoldCoarse + threadIdx.x;
+    if (threadIdx.x < kFoldCoarse && r < R) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) tot += sum[k][threadIdx.x];
+        // small: one chunk counted in u16 LDS counters (no count can pass
+        // 65,535); else chunks of about kFoldAddMax keys, flagged
+        rn[r] = tot <= kFoldSmallMax ? (tot ? 1u : 0u) : ((tot + kFoldAddMax - 1) / kFoldAddMax) | kFoldBig;
+    }
 }
 
-// The add's work units: a region's keys in chunks of at most kFoldAddMax,
-// one workgroup per chunk.  A region with one chunk (every region of a
-// uniform round: ~15k keys) is read-modify-written by its workgroup alone; a
-// hot region (Zipf senders: one sender's row takes ~10 % of all keys) is
-// split over many workgroups that add their nonzero counters with device
-// atomics -- instead of one workgroup walking 20M keys while the chip idles
-// (the Zipf C3 fold: ~4 ms per 20 rounds, profiles/r06b_bench_line.json).
-// k_fold_chunks (one workgroup): rbeg[r] = region r's first key (r <= R),
-// the chunks' exclusive prefix over the regions and, per chunk id, its
-// region and index in cmap[id] = r | j << 14.
-constexpr uint32_t kFoldAddMax = 1u << 18;
-constexpr uint32_t kFoldMaxRegions = 1u << 14;
-__global__ __launch_bounds__(kFoldWG) void k_fold_chunks(const uint32_t* __restrict__ M1, uint32_t C, uint32_t nt1,
-                                                         const uint32_t* __restrict__ M2, uint32_t R,
-                                                         uint32_t* __restrict__ rbeg, uint32_t* __restrict__ cmap,
-                                                         uint32_t* __restrict__ nchunks) {
-    __shared__ FoldL2 g;
+// The add's work units.  A small region (at most kFoldSmallMax keys: every
+// region of a uniform fold of ~20 C3 rounds, ~15k keys) is one chunk of
+// list A, counted in u16 LDS counters (64 KB: two workgroups per CU); a big
+// region's level-2 tiles go to list B in rn[r] chunks of equal tile ranges,
+// counted in u32 LDS counters (a hot region -- Zipf senders, one sender's
+// row takes ~10 % of all keys -- spreads over many workgroups that add with
+// device atomics instead of one workgroup walking 20M keys while the chip
+// idles, the Zipf C3 fold ~4 ms per 20 rounds, profiles/r06b_bench_line.json).
+// One workgroup: both lists' exclusive prefixes over the regions; cA[id] =
+// r, cB[id] = r | j << 14; n2 = {|A|, |B|}.
+__global__ __launch_bounds__(kFoldWG) void k_fold_chunks(const uint32_t* __restrict__ rn, uint32_t R,
+                                                         uint32_t* __restrict__ cA, uint32_t* __restrict__ cB,
+                                                         uint32_t* __restrict__ n2) {
     __shared__ uint32_t ws[kFoldWG / 64];
-    const uint32_t* lb = rbeg; // (re-read below by other threads of the block: fenced)
-    fold_l2_geometry(M1, C, nt1, g);
-    for (uint32_t r = threadIdx.x; r <= R; r += kFoldWG) {
-        uint32_t b;
-        if (r == R) {
-            b = g.lo[C];
-        } else {
-            const uint32_t c = r >> kFoldFineBits, f = r & ((1u << kFoldFineBits) - 1u);
-            const uint32_t ntc = g.tb[c + 1] - g.tb[c];
-            b = ntc ? M2[((size_t)g.tb[c] << kFoldFineBits) + (size_t)f * ntc] : g.lo[c];
-        }
-        rbeg[r] = b;
-    }
-    __threadfence_block();
-    __syncthreads();
     constexpr uint32_t per = kFoldMaxRegions / kFoldWG; // 16 regions per thread
     const uint32_t r0 = threadIdx.x * per;
-    uint32_t sum = 0;
-    for (uint32_t k = 0; k < per && r0 + k < R; k++) sum += (lb[r0 + k + 1] - lb[r0 + k] + kFoldAddMax - 1) / kFoldAddMax;
-    uint32_t tot;
-    uint32_t pre = block_excl_scan_n(sum, &tot, ws);
+    uint32_t sa = 0, sb = 0;
     for (uint32_t k = 0; k < per && r0 + k < R; k++) {
-        const uint32_t n = (lb[r0 + k + 1] - lb[r0 + k] + kFoldAddMax - 1) / kFoldAddMax;
-        for (uint32_t j = 0; j < n; j++) cmap[pre + j] = (r0 + k) | (j << 14);
-        pre += n;
+        const uint32_t v = rn[r0 + k];
+        if (v & kFoldBig) sb += v & ~kFoldBig;
+        else sa += v;
     }
-    if (threadIdx.x == 0) *nchunks = tot;
+    uint32_t ta, tb;
+    uint32_t pa = block_excl_scan_n(sa, &ta, ws);
+    uint32_t pb = block_excl_scan_n(sb, &tb, ws);
+    for (uint32_t k = 0; k < per && r0 + k < R; k++) {
+        const uint32_t v = rn[r0 + k];
+        if (v & kFoldBig) {
+            for (uint32_t j = 0; j < (v & ~kFoldBig); j++) cB[pb++] = (r0 + k) | (j << 14);
+        } else if (v) {
+            cA[pa++] = r0 + k;
+        }
+    }
+    if (threadIdx.x == 0) n2[0] = ta, n2[1] = tb;
 }
 
-// chunk blockIdx.x of region r = cmap & 0x3FFF: its keys are [rbeg[r] + j *
-// kFoldAddMax, ...) up to rbeg[r + 1]
-// kVec: the region's counters zeroed and read-modify-written 16 B per lane,
-// eight loads in flight per lane before the stores (the scalar form waits
-// on each counter's load before its store: latency-bound at one workgroup
-// per CU); the dense table 16-B aligned (the caller checks)
+// chunk blockIdx.x of list A (kSmall: region r, all its level-2 tiles) or
+// B (region r, tiles [ta + j nt / n, ta + (j + 1) nt / n) of coarse c's
+// level-2 tiles).  The region's runs are gathered a tile per thread (start,
+// length), each wave walking its threads' runs 8 at a time (two keys per
+// lane per run in flight; longer runs loop); the keys are region offsets
+// (u16).  kSmall: u16 counters packed in pairs (the chunk's keys are at most
+// 65,535), 64 KB of LDS.
 // kD8: the counts go to the u8 delta layer d8 (16-B aligned at index 0,
 // readable up to N rounded up to 16): 16 counters per lane-step, one 16-B
-// load and store of their delta bytes; a byte whose sum passes 255 moves the
-// whole sum into dense (a device atomic) and restarts at 0 -- the region's
-// HBM traffic is its 32 KB of deltas, not its 128 KB of u32 counters
-template <bool kVec, bool kD8 = false>
-__global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint32_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ rbeg,
-                                                      const uint32_t* __restrict__ cmap,
-                                                      const uint32_t* __restrict__ nchunks,
-                                                      uint32_t* __restrict__ dense, unsigned long long N,
-                                                      uint8_t* __restrict__ d8 = nullptr) {
-    extern __shared__ uint32_t fc[];
-    if (blockIdx.x >= *nchunks) return; // (block-uniform: the grid is the chunks' upper bound)
-    const uint32_t cm = cmap[blockIdx.x], r = cm & 0x3FFFu, jc = cm >> 14;
-    const uint32_t rb0 = rbeg[r], re = rbeg[r + 1];
-    const uint32_t beg = rb0 + jc * kFoldAddMax, end = re - beg > kFoldAddMax ? beg + kFoldAddMax : re;
-    const bool shared_region = re - rb0 > kFoldAddMax; // (block-uniform) other chunks add to it too
-    if (beg == end) return;
-    constexpr uint32_t R = 1u << kFoldRegionBits;
-    if (kVec)
-        for (uint32_t j = threadIdx.x; j < R / 4; j += kFoldWG) reinterpret_cast<uint4*>(fc)[j] = uint4{0u, 0u, 0u, 0u};
-    else
-        for (uint32_t j = threadIdx.x; j < R; j += kFoldWG) fc[j] = 0u;
-    __syncthreads();
-    for (uint32_t i0 = beg + threadIdx.x; i0 < end; i0 += kFoldWG * 4) {
-        uint32_t k[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) k[u] = i0 + u * kFoldWG < end ? keys[i0 + u * kFoldWG] : kFoldSent;
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (k[u] != kFoldSent) atomicAdd(&fc[k[u] & (R - 1u)], 1u);
-    }
-    __syncthreads();
-    const unsigned long long rb = (unsigned long long)r << kFoldRegionBits;
-    const uint32_t lim = N - rb < R ? (uint32_t)(N - rb) : R;
-    uint32_t j0 = 0;
-    if (shared_region) { // a hot region's chunk: device atomics for its nonzero counters
-        for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
-            const uint32_t v = fc[j];
-            if (v) atomicAdd(dense + rb + j, v);
-        }
-        return;
-    }
-    if (kD8) {
-        constexpr int kU = R / 16 / kFoldWG; // 2: the whole region in one pass
-        const uint32_t lim16 = (lim + 15u) / 16u;
-        const uint4* f4 = reinterpret_cast<const uint4*>(fc);
-        uint4* d16 = reinterpret_cast<uint4*>(d8 + rb);
-        uint4 v[kU][4], dv[kU];
-        bool any[kU];
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-            uint32_t o = 0u;
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                v[u][w] = q < lim16 ? f4[4 * q + w] : uint4{0u, 0u, 0u, 0u};
-                o |= v[u][w].x | v[u][w].y | v[u][w].z | v[u][w].w;
-            }
-            any[u] = o != 0u;
-            if (any[u]) dv[u] = d16[q];
-        }
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            if (!any[u]) continue;
-            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-            uint32_t dw[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-                const uint32_t c[4] = {v[u][w].x, v[u][w].y, v[u][w].z, v[u][w].w};
-                uint32_t nw = 0u;
-#pragma unroll
-                for (int b = 0; b < 4; b++) {
-                    uint32_t s = ((dw[w] >> (8 * b)) & 0xFFu) + c[b];
-                    if (s > 0xFFu) { // (rare: a pair past 255 since its last move)
-                        atomicAdd(dense + rb + 16u * q + 4u * w + b, s);
-                        s = 0u;
-                    }
-                    nw |= s << (8 * b);
-                }
-                dw[w] = nw;
-            }
-            d16[q] = uint4{dw[0], dw[1], dw[2], dw[3]};
-        }
-        return;
-    }
-    if (kVec) {
-        constexpr int kU = R / 4 / kFoldWG; // 8: the whole region in one pass
-        const uint32_t lim4 = lim / 4;
-        const uint4* f4 = reinterpret_cast<const uint4*>(fc);
-        uint4* d4 = reinterpret_cast<uint4*>(dense + rb);
-        uint4 v[kU], d[kU];
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-            v[u] = q < lim4 ? f4[q] : uint4{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-            if (q < lim4 && (v[u].x | v[u].y | v[u].z | v[u].w)) d[u] = d4[q];
-        }
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-            if (q < lim4 && (v[u].x | v[u].y | v[u].z | v[u].w))
-                d4[q] = uint4{d[u].x + v[u].x, d[u].y + v[u].y, d[u].z + v[u].z, d[u].w + v[u].w};
-        }
-        j0 = lim4 * 4; // (a partial last region's tail: one counter per lane)
-    }
-    for (uint32_t j = j0 + threadIdx.x; j < lim; j += kFoldWG) {
-        const uint32_t v = fc[j];
-        if (v) dense[rb + j] += v;
-    }
-}
-
-// The add into the u8 delta layer (k_fold_add<_, true>'s arithmetic) with
-// one memory round trip per workgroup: the chunk's first kFoldAddK keys per
-// thread and the region's 32 KB of delta bytes are loaded first, the LDS
-// counters zeroed while they are in flight (an LDS-only barrier keeps them
-// in flight), then the LDS adds, then every 16-counter group combined and
-// stored.  (The phased form waits on its keys, then on its deltas, one
-// 1,024-thread workgroup per CU: 0.41 ms of a 1.6 ms fold of 20 C3 rounds,
-// profiles/r06f.)
-constexpr int kFoldAddK = 16;
-__global__ __launch_bounds__(kFoldWG) void k_fold_add8(const uint32_t* __restrict__ keys,
-                                                       const uint32_t* __restrict__ rbeg,
-                                                       const uint32_t* __restrict__ cmap,
-                                                       const uint32_t* __restrict__ nchunks,
-                                                       uint32_t* __restrict__ dense, unsigned long long N,
-                                                       uint8_t* __restrict__ d8) {
-    extern __shared__ uint32_t fc[];
-    if (blockIdx.x >= *nchunks) return; // (block-uniform)
-    const uint32_t cm = cmap[blockIdx.x], r = cm & 0x3FFFu, jc = cm >> 14;
-    const uint32_t rb0 = rbeg[r], re = rbeg[r + 1];
-    const uint32_t beg = rb0 + jc * kFoldAddMax, end = re - beg > kFoldAddMax ? beg + kFoldAddMax : re;
-    const bool shared_region = re - rb0 > kFoldAddMax; // (block-uniform)
-    if (beg == end) return;
+// load (issued before the gathers) and store of their delta bytes; a byte
+// whose sum passes 255 moves the whole sum into dense (a device atomic) and
+// restarts at 0 -- the region's HBM traffic is its 32 KB of deltas, not its
+// 128 KB of u32 counters.  Else the u32 counters are read-modify-written 16 B
+// per lane (dense 16-B aligned, the caller checks) or one per lane.
+template <bool kD8, bool kVec, bool kSmall>
+__device__ __forceinline__ void fold_add_chunk(uint32_t id, const uint16_t* __restrict__ keys,
+                                               const uint32_t* __restrict__ F, const uint32_t* __restrict__ S,
+                                               const uint32_t* __restrict__ L2b, uint32_t ng,
+                                               const uint32_t* __restrict__ rn, const uint32_t* __restrict__ cmap,
+                                               uint32_t* __restrict__ dense, unsigned long long N,
+                                               uint8_t* __restrict__ d8, uint32_t* fc) {
+    const uint32_t cm = cmap[id], r = cm & 0x3FFFu, jc = kSmall ? 0u : cm >> 14;
+    const uint32_t c = r >> kFoldFineBits, f = r & ((1u << kFoldFineBits) - 1u);
+    const uint32_t ta = L2b[(size_t)c * ng], ntl = L2b[(size_t)(c + 1) * ng] - ta, n = kSmall ? 1u : rn[r] & ~kFoldBig;
+    const uint32_t t0 = ta + (uint32_t)((unsigned long long)jc * ntl / n),
+                   t1 = ta + (uint32_t)((unsigned long long)(jc + 1) * ntl / n);
+    const bool shared_region = n > 1; // (block-uniform) other chunks add to it too
     constexpr uint32_t R = 1u << kFoldRegionBits;
     constexpr int kU = R / 16 / kFoldWG; // 2: 16 counters per lane-step, the whole region
     const unsigned long long rb = (unsigned long long)r << kFoldRegionBits;
     const uint32_t lim = N - rb < R ? (uint32_t)(N - rb) : R;
     const uint32_t lim16 = (lim + 15u) / 16u;
-    uint32_t k[kFoldAddK];
-#pragma unroll
-    for (int u = 0; u < kFoldAddK; u++) {
-        const uint32_t i = beg + (uint32_t)u * kFoldWG + threadIdx.x;
-        k[u] = i < end ? keys[i] : kFoldSent;
-    }
+    const int lane = threadIdx.x & 63;
     uint4* d16 = reinterpret_cast<uint4*>(d8 + rb);
     uint4 dv[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
         const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-        dv[u] = !shared_region && q < lim16 ? d16[q] : uint4{0u, 0u, 0u, 0u};
+        dv[u] = kD8 && !shared_region && q < lim16 ? d16[q] : uint4{0u, 0u, 0u, 0u};
     }
-    for (uint32_t j = threadIdx.x; j < R / 4; j += kFoldWG) reinterpret_cast<uint4*>(fc)[j] = uint4{0u, 0u, 0u, 0u};
-    lds_barrier();
-#pragma unroll
-    for (int u = 0; u < kFoldAddK; u++)
-        if (k[u] != kFoldSent) atomicAdd(&fc[k[u] & (R - 1u)], 1u);
-    for (uint32_t i0 = beg + kFoldAddK * kFoldWG; i0 < end; i0 += kFoldAddK * kFoldWG) { // (chunks past 16K keys)
-#pragma unroll
-        for (int u = 0; u < kFoldAddK; u++) {
-            const uint32_t i = i0 + (uint32_t)u * kFoldWG + threadIdx.x;
-            k[u] = i < end ? keys[i] : kFoldSent;
+    constexpr uint32_t kWords = kSmall ? R / 2 : R;
+    for (uint32_t j = threadIdx.x; j < kWords / 4; j += kFoldWG) reinterpret_cast<uint4*>(fc)[j] = uint4{0u, 0u, 0u, 0u};
+    lds_barrier(); // (LDS only: the delta loads stay in flight)
+    // one key into the LDS counters
+    auto count = [&](uint32_t k) {
+        if (kSmall) atomicAdd(&fc[k >> 1], 1u << ((k & 1u) << 4));
+        else atomicAdd(&fc[k], 1u);
+    };
+    const int wv = threadIdx.x >> 6;
+    for (uint32_t tb0 = t0; tb0 < t1; tb0 += kFoldWG) { // (block-uniform)
+        // tile tb0 + wv + 16 lane: every wave holds ~1/16 of the runs in its low lanes
+        const uint32_t t = tb0 + (uint32_t)wv + 16u * (uint32_t)lane;
+        uint32_t rs = 0, rl = 0;
+        if (t < t1) {
+            const uint32_t* p = F + (size_t)t * kFoldP;
+            const uint32_t a = p[f];
+            rs = S[t] + a;
+            rl = p[f + 1] - a;
         }
+        const unsigned long long live = __ballot(t < t1);
+        const int nl = live ? 64 - __builtin_clzll(live) : 0; // (wave-uniform)
+        for (int l0 = 0; l0 < nl; l0 += 8) { // this wave's runs, 8 at a time
+            uint32_t k0[8], k1[8];
 #pragma unroll
-        for (int u = 0; u < kFoldAddK; u++)
-            if (k[u] != kFoldSent) atomicAdd(&fc[k[u] & (R - 1u)], 1u);
+            for (int e = 0; e < 8; e++) {
+                const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)rs, l0 + e);
+                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)rl, l0 + e);
+                k0[e] = (uint32_t)lane < m ? keys[s + lane] : kFoldSent;
+                k1[e] = (uint32_t)lane + 64u < m ? keys[s + 64 + lane] : kFoldSent;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                if (k0[e] != kFoldSent) count(k0[e]);
+                if (k1[e] != kFoldSent) count(k1[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; e++) { // (runs past 128 keys: hot regions)
+                const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)rs, l0 + e);
+                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)rl, l0 + e);
+                for (uint32_t i = 128u + (uint32_t)lane; i < m; i += 64u) count(keys[s + i]);
+            }
+        }
     }
     __syncthreads();
-    if (shared_region) { // a hot region's chunk: device atomics for its nonzero counters
+    if (!kSmall && shared_region) { // a hot region's chunk: device atomics for its nonzero counters
         for (uint32_t j = threadIdx.x; j < lim; j += kFoldWG) {
             const uint32_t v = fc[j];
             if (v) atomicAdd(dense + rb + j, v);
@@ -4917,47 +4849,107 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add8(const uint32_t* __restric
         return;
     }
     const uint4* f4 = reinterpret_cast<const uint4*>(fc);
+    // counters [4 i, 4 i + 4) of the LDS counters
+    auto four = [&](uint32_t i) -> uint4 {
+        if (!kSmall) return f4[i];
+        const uint2 w = reinterpret_cast<const uint2*>(fc)[i];
+        return uint4{w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16};
+    };
+    if (kD8) {
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
-        const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-        if (q >= lim16) continue;
-        uint4 v[4];
-        uint32_t o = 0u;
+        for (int u = 0; u < kU; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            if (q >= lim16) continue;
+            uint4 v[4];
+            uint32_t o = 0u;
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
-            v[w] = f4[4 * q + w];
-            o |= v[w].x | v[w].y | v[w].z | v[w].w;
-        }
-        if (!o) continue;
-        uint32_t dw[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            const uint32_t c[4] = {v[w].x, v[w].y, v[w].z, v[w].w};
-            uint32_t nw = 0u;
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                uint32_t x = ((dw[w] >> (8 * b)) & 0xFFu) + c[b];
-                if (x > 0xFFu) { // (rare: a pair past 255 since its last move)
-                    atomicAdd(dense + rb + 16u * q + 4u * w + b, x);
-                    x = 0u;
-                }
-                nw |= x << (8 * b);
+            for (int w = 0; w < 4; w++) {
+                v[w] = four(4 * q + w);
+                o |= v[w].x | v[w].y | v[w].z | v[w].w;
             }
-            dw[w] = nw;
+            if (!o) continue;
+            uint32_t dw[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint32_t cc[4] = {v[w].x, v[w].y, v[w].z, v[w].w};
+                uint32_t nw = 0u;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    uint32_t x = ((dw[w] >> (8 * b)) & 0xFFu) + cc[b];
+                    if (x > 0xFFu) { // (rare: a pair past 255 since its last move)
+                        atomicAdd(dense + rb + 16u * q + 4u * w + b, x);
+                        x = 0u;
+                    }
+                    nw |= x << (8 * b);
+                }
+                dw[w] = nw;
+            }
+            d16[q] = uint4{dw[0], dw[1], dw[2], dw[3]};
         }
-        d16[q] = uint4{dw[0], dw[1], dw[2], dw[3]};
+        return;
+    }
+    uint32_t j0 = 0;
+    if (kVec) { // eight loads in flight per lane before the stores
+        constexpr int kV = R / 4 / kFoldWG; // 8: the whole region in one pass
+        const uint32_t lim4 = lim / 4;
+        uint4* dd4 = reinterpret_cast<uint4*>(dense + rb);
+        uint4 v[kV], d[kV];
+#pragma unroll
+        for (int u = 0; u < kV; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            v[u] = q < lim4 ? four(q) : uint4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < kV; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            if (q < lim4 && (v[u].x | v[u].y | v[u].z | v[u].w)) d[u] = dd4[q];
+        }
+#pragma unroll
+        for (int u = 0; u < kV; u++) {
+            const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
+            if (q < lim4 && (v[u].x | v[u].y | v[u].z | v[u].w))
+                dd4[q] = uint4{d[u].x + v[u].x, d[u].y + v[u].y, d[u].z + v[u].z, d[u].w + v[u].w};
+        }
+        j0 = lim4 * 4; // (a partial last region's tail: one counter per lane)
+    }
+    for (uint32_t j = j0 + threadIdx.x; j < lim; j += kFoldWG) {
+        const uint32_t v = kSmall ? (fc[j >> 1] >> ((j & 1u) << 4)) & 0xFFFFu : fc[j];
+        if (v) dense[rb + j] += v;
+    }
+}
+
+// chunks blockIdx.x, + gridDim.x, ... of the list (list B's grid is a few
+// per CU: its length is known on the device only)
+template <bool kD8, bool kVec, bool kSmall>
+__global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint16_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ F, const uint32_t* __restrict__ S,
+                                                      const uint32_t* __restrict__ L2b, uint32_t ng,
+                                                      const uint32_t* __restrict__ rn,
+                                                      const uint32_t* __restrict__ cmap,
+                                                      const uint32_t* __restrict__ nchunks,
+                                                      uint32_t* __restrict__ dense, unsigned long long N,
+                                                      uint8_t* __restrict__ d8) {
+    extern __shared__ uint32_t fc[];
+    const uint32_t nc = *nchunks;
+    for (uint32_t id = blockIdx.x; id < nc; id += gridDim.x) { // (block-uniform)
+        if (id != blockIdx.x) __syncthreads(); // (the last chunk's LDS reads before the reset)
+        fold_add_chunk<kD8, kVec, kSmall>(id, keys, F, S, L2b, ng, rn, cmap, dense, N, d8, fc);
     }
 }
 
 struct FoldScratch {
-    uint32_t* part = nullptr;
-    size_t cap_part = 0; // keys
-    uint32_t* cmap = nullptr; // [rbeg R + 1 | nchunks | cmap]
+    uint32_t* part = nullptr; // level-1 output (L keys)
+    size_t cap_part = 0;
+    uint32_t* P1 = nullptr; // level-1 prefixes (nt1 x 129)
+    size_t cap_P1 = 0;
+    uint32_t* un = nullptr; // U | Uoff | T2 | L2b (4 x (units + 1))
+    size_t cap_un = 0;
+    uint32_t* RT = nullptr; // the units' run tables (units x kFoldG uint2)
+    size_t cap_RT = 0;
+    uint32_t* F = nullptr; // level-2 prefixes (tiles x 129) | S (tiles)
+    size_t cap_F = 0;
+    uint32_t* cmap = nullptr; // rn (kFoldMaxRegions) | nchunks | cmap
     size_t cap_cmap = 0;
-    uint32_t* M1 = nullptr;
-    size_t cap_M1 = 0; // words
-    uint32_t* M2 = nullptr;
-    size_t cap_M2 = 0;
     uint32_t* bsum = nullptr;
     size_t cap_bsum = 0;
 };
@@ -4972,29 +4964,40 @@ int fold_grow(uint32_t** p, size_t* cap, size_t need, const char* what) {
     return 0;
 }
 
-// the add's chunk table: rbeg (R + 1) | nchunks | one entry per chunk (at
-// most one per region plus one per kFoldAddMax keys)
-size_t fold_max_chunks(size_t L) { return kFoldMaxRegions + L / kFoldAddMax + 1; }
-size_t fold_cmap_words(size_t L) { return (kFoldMaxRegions + 1) + 1 + fold_max_chunks(L); }
+struct FoldGeo {
+    size_t nt1, ng, units, tiles2; // level-1 tiles, unit groups, units (at most), level-2 tiles (at most)
+};
+FoldGeo fold_geo(size_t L, uint32_t C) {
+    FoldGeo q;
+    q.nt1 = (L + kFoldT - 1) / kFoldT;
+    q.ng = (q.nt1 + kFoldG - 1) / kFoldG;
+    q.units = (size_t)C * q.ng;
+    q.tiles2 = q.units + L / kFoldT + 1;
+    return q;
+}
+// the add's chunk list: at most one per region plus one per kFoldAddMax keys
+// list B's chunks: at most one per kFoldAddMax keys plus one per big region
+size_t fold_max_chunks(size_t L) { return L / kFoldAddMax + L / (kFoldSmallMax + 1) + 1; }
 
 // buffers for folds of up to L keys (grow-only; reserved with the log so that
 // a fold inside a timed region allocates nothing)
 int fold_reserve(FoldScratch& f, size_t L) {
-    const size_t nt1 = (L + kFoldT - 1) / kFoldT;
-    const size_t m1 = kFoldCoarse * nt1 + 1, m2 = ((nt1 + kFoldCoarse) << kFoldFineBits) + 1;
-    const size_t mb = (m1 > m2 ? m1 : m2) / kScanTile + 2;
+    const FoldGeo q = fold_geo(L, kFoldCoarse);
+    const size_t mb = (q.units + 1) / kScanTile + 2;
     int rc;
     if ((rc = fold_grow(&f.part, &f.cap_part, L ? L : 1, "hipMalloc fold part")) ||
-        (rc = fold_grow(&f.M1, &f.cap_M1, m1, "hipMalloc fold M1")) ||
-        (rc = fold_grow(&f.M2, &f.cap_M2, m2, "hipMalloc fold M2")) ||
+        (rc = fold_grow(&f.P1, &f.cap_P1, q.nt1 * kFoldP + 1, "hipMalloc fold P1")) ||
+        (rc = fold_grow(&f.un, &f.cap_un, 4 * (q.units + 1), "hipMalloc fold units")) ||
+        (rc = fold_grow(&f.RT, &f.cap_RT, 2 * q.units * kFoldG, "hipMalloc fold runs")) ||
+        (rc = fold_grow(&f.F, &f.cap_F, q.tiles2 * (kFoldP + 1), "hipMalloc fold F")) ||
         (rc = fold_grow(&f.bsum, &f.cap_bsum, mb, "hipMalloc fold scan")) ||
-        (rc = fold_grow(&f.cmap, &f.cap_cmap, fold_cmap_words(L), "hipMalloc fold chunks")))
+        (rc = fold_grow(&f.cmap, &f.cap_cmap, 2 * kFoldMaxRegions + 2 + fold_max_chunks(L), "hipMalloc fold chunks")))
         return rc;
     return 0;
 }
 
-// (log: both the input and, after the level-1 pass has read it, the level-2
-// output -- one scratch array of L keys besides it)
+// (log: the input and, as u16, the level-2 output -- one scratch array of L
+// keys besides it)
 int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, uint8_t* d8, unsigned long long N, FoldScratch& f,
               hipStream_t s) {
     if (N > kFoldMaxN) return shd_fail(-EINVAL, "fold: %llu counters exceed the fold's %llu", N, kFoldMaxN);
@@ -5002,8 +5005,9 @@ int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, uint8_t* d8, unsigned lo
     if (int rc = fold_reserve(f, L)) return rc;
     static bool attr = false;
     if (!attr) {
-        for (const void* fn : {(const void*)k_fold_add<true>, (const void*)k_fold_add<false>,
-                               (const void*)k_fold_add<false, true>, (const void*)k_fold_add8})
+        for (const void* fn : {(const void*)k_fold_add<true, false, false>, (const void*)k_fold_add<false, true, false>,
+                               (const void*)k_fold_add<false, false, false>, (const void*)k_fold_add<true, false, true>,
+                               (const void*)k_fold_add<false, true, true>, (const void*)k_fold_add<false, false, true>})
             if (int rc = hip_status(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                         4 << kFoldRegionBits),
                                     "hipFuncSetAttribute k_fold_add"))
@@ -5012,41 +5016,46 @@ int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, uint8_t* d8, unsigned lo
     }
     const uint32_t R = (uint32_t)(((N - 1) >> kFoldRegionBits) + 1);
     const uint32_t C = ((R - 1) >> kFoldFineBits) + 1;
-    const uint32_t nt1 = (uint32_t)((L + kFoldT - 1) / kFoldT);
-    const size_t m1 = (size_t)C * nt1;
-    hipLaunchKernelGGL(k_fold_hist1, dim3(nt1), dim3(kFoldWG), 0, s, log, L, C, nt1, f.M1);
-    scan_counts(f.M1, m1, f.M1, f.bsum, nullptr, s);
-    hipLaunchKernelGGL(k_fold_part1, dim3(nt1), dim3(kFoldWG), 0, s, log, L, C, nt1, f.M1, f.part);
-    const uint32_t nt2 = nt1 + C; // level-2 tiles: at most one partial tile per coarse bucket more
-    const size_t m2 = (size_t)nt2 << kFoldFineBits;
-    // (M2 past the last tile stays unused; its scan covers the whole
-    // reservation's head: entries never written are read as left by the
-    // previous fold, so zero them)
-    if (int rc = hip_status(hipMemsetAsync(f.M2, 0, 4 * m2, s), "memset fold M2")) return rc;
-    hipLaunchKernelGGL(k_fold_hist2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2);
-    scan_counts(f.M2, m2, f.M2, f.bsum, nullptr, s);
-    hipLaunchKernelGGL(k_fold_part2, dim3(nt2), dim3(kFoldWG), 0, s, f.part, f.M1, C, nt1, f.M2, log);
-    uint32_t* rbeg = f.cmap;
-    uint32_t* nch = rbeg + (kFoldMaxRegions + 1);
-    uint32_t* cmap = nch + 1;
-    hipLaunchKernelGGL(k_fold_chunks, dim3(1), dim3(kFoldWG), 0, s, f.M1, C, nt1, f.M2, R, rbeg, cmap, nch);
-    const uint32_t grid = (uint32_t)(R + L / kFoldAddMax + 1); // (>= the chunks; the rest exit at once)
-    // SHD_FOLD_VEC=0: the scalar read-modify-write
+    const FoldGeo q = fold_geo(L, C);
+    const uint32_t units = (uint32_t)q.units, ng = (uint32_t)q.ng;
+    uint32_t* U = f.un;
+    uint32_t* Uoff = U + (units + 1);
+    uint32_t* T2 = Uoff + (units + 1);
+    uint32_t* L2b = T2 + (units + 1);
+    uint2* RT = reinterpret_cast<uint2*>(f.RT);
+    uint32_t* F = f.F;
+    uint32_t* S = F + q.tiles2 * kFoldP;
+    uint32_t* rn = f.cmap;
+    uint32_t* n2 = rn + kFoldMaxRegions;
+    uint32_t* cA = n2 + 2;
+    uint32_t* cB = cA + kFoldMaxRegions;
+    uint16_t* out16 = reinterpret_cast<uint16_t*>(log);
+    hipLaunchKernelGGL(k_fold_p1, dim3((unsigned)q.nt1), dim3(kFoldWG), 0, s, log, L, f.part, f.P1);
+    hipLaunchKernelGGL(k_fold_units, dim3(ng), dim3(kFoldUnitsWG), 0, s, f.P1, (uint32_t)q.nt1, C, ng, RT, U, T2);
+    scan_counts(U, units, Uoff, f.bsum, nullptr, s);
+    scan_counts(T2, units, L2b, f.bsum, nullptr, s);
+    // SHD_FOLD_P2_GRID: the persistent grid (default two workgroups per CU)
+    const char* pg = getenv("SHD_FOLD_P2_GRID");
+    const uint32_t g2 = pg && atoi(pg) > 0 ? (uint32_t)atoi(pg) : 2u * (uint32_t)dev_cus();
+    hipLaunchKernelGGL(k_fold_p2, dim3(units < g2 ? units : g2), dim3(kFoldP2WG), 0, s, f.part, RT, units, Uoff, L2b,
+                       out16, F, S);
+    hipLaunchKernelGGL(k_fold_rn, dim3(C), dim3(1024), 0, s, F, L2b, ng, R, rn);
+    hipLaunchKernelGGL(k_fold_chunks, dim3(1), dim3(kFoldWG), 0, s, rn, R, cA, cB, n2);
+    // (grids: the lists' upper bounds; the rest exit at once)
+    const uint32_t gA = R, gB = (uint32_t)(fold_max_chunks(L) < 128 ? fold_max_chunks(L) : 128);
+    // SHD_FOLD_VEC=0: the scalar read-modify-write of the u32 counters
     const char* fv = getenv("SHD_FOLD_VEC");
-    // SHD_FOLD_ADD=phased: the delta add in phases (A/B)
-    const char* fa = getenv("SHD_FOLD_ADD");
-    if (d8 && fa && strcmp(fa, "phased") == 0)
-        hipLaunchKernelGGL((k_fold_add<false, true>), dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log,
-                           rbeg, cmap, nch, dense, N, d8);
-    else if (d8)
-        hipLaunchKernelGGL(k_fold_add8, dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, rbeg, cmap,
-                           nch, dense, N, d8);
-    else if (((uintptr_t)dense & 15u) == 0 && !(fv && strcmp(fv, "0") == 0))
-        hipLaunchKernelGGL(k_fold_add<true>, dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, rbeg, cmap,
-                           nch, dense, N);
-    else
-        hipLaunchKernelGGL(k_fold_add<false>, dim3(grid), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s, log, rbeg,
-                           cmap, nch, dense, N);
+#define SHD_FOLD_ADD(D8, VEC)                                                                                         \
+    do {                                                                                                              \
+        hipLaunchKernelGGL((k_fold_add<D8, VEC, true>), dim3(gA), dim3(kFoldWG), (size_t)2 << kFoldRegionBits, s,     \
+                           out16, F, S, L2b, ng, rn, cA, n2, dense, N, d8);                                           \
+        hipLaunchKernelGGL((k_fold_add<D8, VEC, false>), dim3(gB), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s,    \
+                           out16, F, S, L2b, ng, rn, cB, n2 + 1, dense, N, d8);                                       \
+    } while (0)
+    if (d8) SHD_FOLD_ADD(true, false);
+    else if (((uintptr_t)dense & 15u) == 0 && !(fv && strcmp(fv, "0") == 0)) SHD_FOLD_ADD(false, true);
+    else SHD_FOLD_ADD(false, false);
+#undef SHD_FOLD_ADD
     return hip_status(hipGetLastError(), "pcnt fold launch");
 }
 
@@ -5069,8 +5078,10 @@ extern "C" void shd_dev_pcnt_scratch_free(void* scratch) {
     if (!scratch) return;
     FoldScratch* f = static_cast<FoldScratch*>(scratch);
     (void)hipFree(f->part);
-    (void)hipFree(f->M1);
-    (void)hipFree(f->M2);
+    (void)hipFree(f->P1);
+    (void)hipFree(f->un);
+    (void)hipFree(f->RT);
+    (void)hipFree(f->F);
     (void)hipFree(f->bsum);
     (void)hipFree(f->cmap);
     delete f;
@@ -5197,6 +5208,7 @@ PartCfg part_cfg(uint32_t nb) {
     if (k == 4) return {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false};
     if (k == 5) return {(const void*)k_part_scatter<512, 4096, false>, 512, 4096, false};
     if (k == 6) return {(const void*)k_part_scatter<1024, 8192, false>, 1024, 8192, false};
+    if (k == 12) return {(const void*)k_part_scatter<1024, 16384, false>, 1024, 16384, false};
     if (k == 10 || k == 11) return {(const void*)k_part_place<1024, 4096>, 1024, 4096, false, 0, k == 10 ? 4 : 2};
     if ((k == 7 || k == 8 || k == 9) && nb > kPartPipeMaxBuckets) k = 1;
     if (k == 7) return {(const void*)k_part_scatter_pipe<1024, 2048>, 1024, 2048, false, 1};
@@ -5217,6 +5229,7 @@ int part_attr() {
                             {(const void*)k_part_scatter<1024, 4096, false, 0, 8>, 1024, 4096, false},
                             {(const void*)k_part_scatter<512, 4096, false>, 512, 4096, false},
                             {(const void*)k_part_scatter<1024, 8192, false>, 1024, 8192, false},
+                            {(const void*)k_part_scatter<1024, 16384, false>, 1024, 16384, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 1>, 1024, 4096, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 2>, 1024, 4096, false},
                             {(const void*)k_part_scatter<1024, 4096, false, 4>, 1024, 4096, false},
@@ -5317,6 +5330,7 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
         } else if (f.lds) SHD_PART_LAUNCH(1024, 4096, true);
         else if (f.fn == (const void*)k_part_scatter<1024, 4096, false, 0, 8>) SHD_PART_LAUNCH(1024, 4096, false, 0, 8);
         else if (f.wg == 1024 && f.ch == 8192) SHD_PART_LAUNCH(1024, 8192, false);
+        else if (f.wg == 1024 && f.ch == 16384) SHD_PART_LAUNCH(1024, 16384, false);
         else if (f.wg == 1024) SHD_PART_LAUNCH(1024, 4096, false);
         else if (f.wg == 512 && f.ch == 4096) SHD_PART_LAUNCH(512, 4096, false);
         else if (f.wg == 512) SHD_PART_LAUNCH(512, 2048, false);

@@ -432,13 +432,18 @@ def test_path_counter_fold_multi_region(log, fold, monkeypatch):
         assert len(bad) == 0, f"round {r}: {len(bad)} counters differ, first {bad[:4].tolist()}"
 
 
+@pytest.mark.parametrize("hot_every", [4, 6])
 @pytest.mark.parametrize("rounds_per_fold", [1, 2])
-def test_path_counter_fold_hot_region(rounds_per_fold, monkeypatch):
+def test_path_counter_fold_hot_region(rounds_per_fold, hot_every, monkeypatch):
     """A hot sender (Zipf-like: 450k of 600k packets from one host to uniform
-    destinations) puts more than the add's chunk (2^18 keys) into one 32K
-    counter region: the fold splits that region over several workgroups that
-    add with device atomics.  Every counter against the numpy restatement,
-    folded after each round or after two."""
+    destinations -- every packet but each hot_every-th) puts more than the
+    add's chunk (2^18 keys) into one 32K counter region: the fold splits that
+    region over several workgroups that add with device atomics.  hot_every
+    6, folded each round: the 100k packets of every sixth one go to the hot
+    sender's region alone with the rest uniform (a big region of one chunk:
+    more keys than the u16 LDS counters of the small regions hold, less than
+    a chunk).  Every counter against the numpy restatement, folded after each
+    round or after two."""
     import torch
     monkeypatch.setenv("SHD_PCNT", "log")
     gml = synth.sparse_graph_gml(3000, 0x5EED0F21)
@@ -453,7 +458,8 @@ def test_path_counter_fold_hot_region(rounds_per_fold, monkeypatch):
     n = 600_000
     for r in range(2):
         pk = synth.packet_batch(n, H, 0x5EED0F22 + r, 100_000_000, 10_000_000, st)
-        src = np.where(np.arange(n) % 4 != 0, hot, pk["src_host"]).astype(np.uint32)
+        src = (np.where(np.arange(n) % 4 != 0, hot, pk["src_host"]) if hot_every == 4 else
+               np.where(np.arange(n) % 6 == 0, hot, pk["src_host"])).astype(np.uint32)
         dst = synth.redraw_destinations(pk, H, 0x5EED0F30 + r)["dst_host"]
         dst = np.where(dst == src, (src + 1) % H, dst).astype(np.uint32)
         pk = synth.packet_batch(n, H, 0x5EED0F22 + r, 100_000_000, 10_000_000, st, pairs=(src, dst))
