@@ -4777,7 +4777,7 @@ __device__ __forceinline__ void fold_add_chunk(uint32_t id, const uint16_t* __re
                                                const uint32_t* __restrict__ L2b, uint32_t ng,
                                                const uint32_t* __restrict__ rn, const uint32_t* __restrict__ cmap,
                                                uint32_t* __restrict__ dense, unsigned long long N,
-                                               uint8_t* __restrict__ d8, uint32_t* fc) {
+                                               unsigned long long n0, uint8_t* __restrict__ d8, uint32_t* fc) {
     const uint32_t cm = cmap[id], r = cm & 0x3FFFu, jc = kSmall ? 0u : cm >> 14;
     const uint32_t c = r >> kFoldFineBits, f = r & ((1u << kFoldFineBits) - 1u);
     const uint32_t ta = L2b[(size_t)c * ng], ntl = L2b[(size_t)(c + 1) * ng] - ta, n = kSmall ? 1u : rn[r] & ~kFoldBig;
@@ -4795,7 +4795,9 @@ __device__ __forceinline__ void fold_add_chunk(uint32_t id, const uint16_t* __re
 #pragma unroll
     for (int u = 0; u < kU; u++) {
         const uint32_t q = threadIdx.x + (uint32_t)u * kFoldWG;
-        dv[u] = kD8 && !shared_region && q < lim16 ? d16[q] : uint4{0u, 0u, 0u, 0u};
+        // (only groups at or past the first counter's: a shard's first region
+        // starts below its rows, where no delta byte is allocated)
+        dv[u] = kD8 && !shared_region && q < lim16 && rb + 16u * q >= (n0 & ~15ull) ? d16[q] : uint4{0u, 0u, 0u, 0u};
     }
     constexpr uint32_t kWords = kSmall ? R / 2 : R;
     for (uint32_t j = threadIdx.x; j < kWords / 4; j += kFoldWG) reinterpret_cast<uint4*>(fc)[j] = uint4{0u, 0u, 0u, 0u};
@@ -4928,12 +4930,12 @@ __global__ __launch_bounds__(kFoldWG) void k_fold_add(const uint16_t* __restrict
                                                       const uint32_t* __restrict__ cmap,
                                                       const uint32_t* __restrict__ nchunks,
                                                       uint32_t* __restrict__ dense, unsigned long long N,
-                                                      uint8_t* __restrict__ d8) {
+                                                      unsigned long long n0, uint8_t* __restrict__ d8) {
     extern __shared__ uint32_t fc[];
     const uint32_t nc = *nchunks;
     for (uint32_t id = blockIdx.x; id < nc; id += gridDim.x) { // (block-uniform)
         if (id != blockIdx.x) __syncthreads(); // (the last chunk's LDS reads before the reset)
-        fold_add_chunk<kD8, kVec, kSmall>(id, keys, F, S, L2b, ng, rn, cmap, dense, N, d8, fc);
+        fold_add_chunk<kD8, kVec, kSmall>(id, keys, F, S, L2b, ng, rn, cmap, dense, N, n0, d8, fc);
     }
 }
 
@@ -4998,8 +5000,8 @@ int fold_reserve(FoldScratch& f, size_t L) {
 
 // (log: the input and, as u16, the level-2 output -- one scratch array of L
 // keys besides it)
-int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, uint8_t* d8, unsigned long long N, FoldScratch& f,
-              hipStream_t s) {
+int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, uint8_t* d8, unsigned long long n0, unsigned long long N,
+              FoldScratch& f, hipStream_t s) {
     if (N > kFoldMaxN) return shd_fail(-EINVAL, "fold: %llu counters exceed the fold's %llu", N, kFoldMaxN);
     if (d8 && ((uintptr_t)d8 & 15u)) return shd_fail(-EINVAL, "fold: the delta layer is not 16-B aligned");
     if (int rc = fold_reserve(f, L)) return rc;
@@ -5048,9 +5050,9 @@ int pcnt_fold(uint32_t* log, size_t L, uint32_t* dense, uint8_t* d8, unsigned lo
 #define SHD_FOLD_ADD(D8, VEC)                                                                                         \
     do {                                                                                                              \
         hipLaunchKernelGGL((k_fold_add<D8, VEC, true>), dim3(gA), dim3(kFoldWG), (size_t)2 << kFoldRegionBits, s,     \
-                           out16, F, S, L2b, ng, rn, cA, n2, dense, N, d8);                                           \
+                           out16, F, S, L2b, ng, rn, cA, n2, dense, N, n0, d8);                                       \
         hipLaunchKernelGGL((k_fold_add<D8, VEC, false>), dim3(gB), dim3(kFoldWG), (size_t)4 << kFoldRegionBits, s,    \
-                           out16, F, S, L2b, ng, rn, cB, n2 + 1, dense, N, d8);                                       \
+                           out16, F, S, L2b, ng, rn, cB, n2 + 1, dense, N, n0, d8);                                   \
     } while (0)
     if (d8) SHD_FOLD_ADD(true, false);
     else if (((uintptr_t)dense & 15u) == 0 && !(fv && strcmp(fv, "0") == 0)) SHD_FOLD_ADD(false, true);
@@ -5066,11 +5068,11 @@ extern "C" int shd_dev_pcnt_fold_reserve(size_t L, void** scratch) {
     return fold_reserve(*static_cast<FoldScratch*>(*scratch), L);
 }
 
-extern "C" int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t N, void** scratch,
-                                 void* stream) {
+extern "C" int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t n0, uint64_t N,
+                                 void** scratch, void* stream) {
     if (!L || !N) return 0;
     if (!*scratch && !(*scratch = new (std::nothrow) FoldScratch())) return shd_fail(-ENOMEM, "fold scratch");
-    return pcnt_fold(static_cast<uint32_t*>(log), L, dense, d8, N, *static_cast<FoldScratch*>(*scratch),
+    return pcnt_fold(static_cast<uint32_t*>(log), L, dense, d8, n0, N, *static_cast<FoldScratch*>(*scratch),
                      (hipStream_t)stream);
 }
 

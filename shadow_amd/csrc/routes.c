@@ -577,7 +577,8 @@ static int pcnt_fold(ShdTopology* t, ShdPcnt* p) {
     const char* d8v = getenv("SHD_FOLD_D8");
     uint8_t* d8 = d8v && !strcmp(d8v, "0") ? NULL : p->d8;
     if (!rc)
-        rc = shd_dev_pcnt_fold(p->log, p->log_fill, p->base, d8, (uint64_t)(p->hi) * (uint64_t)t->A, &p->fold, NULL);
+        rc = shd_dev_pcnt_fold(p->log, p->log_fill, p->base, d8, (uint64_t)(p->lo) * (uint64_t)t->A,
+                               (uint64_t)(p->hi) * (uint64_t)t->A, &p->fold, NULL);
     if (!rc) rc = shd_dev_sync();
     if (!rc) p->log_fill = 0;
     shd_dev_init(t->device);

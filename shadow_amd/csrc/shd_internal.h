@@ -185,7 +185,8 @@ typedef struct {
 int shd_dev_pcnt_spill(uint32_t* cnt, uint8_t* d8, size_t n, uint32_t thr, uint64_t* d_list, size_t cap,
                        uint32_t* d_nlist, size_t* appended);
 /* Adds the L logged keys of `log` (u32 flat entry indices below N <=
- * SHD_PCNT_FOLD_MAX_N, all-ones = nothing) into the counters: a two-level
+ * SHD_PCNT_FOLD_MAX_N, all-ones = nothing; the counters of keys [n0, N)
+ * exist, n0 = a shard's first row times A) into the counters: a two-level
  * partition of the keys into 32K-counter regions and one workgroup per
  * region that accumulates its keys in LDS and adds its counters to the
  * table.  With d8 (NULL: none) the counts go to the u8 delta layer d8[N]
@@ -197,7 +198,8 @@ int shd_dev_pcnt_spill(uint32_t* cnt, uint8_t* d8, size_t n, uint32_t thr, uint6
  * time; shd_dev_pcnt_fold_reserve sizes them for L keys ahead), freed with
  * shd_dev_pcnt_scratch_free. */
 #define SHD_PCNT_FOLD_MAX_N (1ull << 29)
-int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t N, void** scratch, void* stream);
+int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t n0, uint64_t N, void** scratch,
+                      void* stream);
 int shd_dev_pcnt_fold_reserve(size_t L, void** scratch);
 void shd_dev_pcnt_scratch_free(void* scratch);
 

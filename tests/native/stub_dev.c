@@ -237,7 +237,8 @@ int shd_dev_pcnt_spill(uint32_t* cnt, uint8_t* d8, size_t n, uint32_t thr, uint6
     *appended = k;
     return 0;
 }
-int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t N, void** scratch, void* stream) {
+int shd_dev_pcnt_fold(void* log, size_t L, uint32_t* dense, uint8_t* d8, uint64_t n0, uint64_t N, void** scratch,
+                      void* stream) {
     for (size_t i = 0; i < L; i++) {
         const uint32_t k = ((const uint32_t*)log)[i];
         if (k == UINT32_MAX) continue;
