@@ -23,6 +23,9 @@ STAGE = {"k_pkt_scatter": "packet_scatter", "k_part_scatter": "packet_scatter", 
          "k_place_rank": "place", "k_place_bucket": "place", "k_segsort_dst": "segment_sort", "k_place_ovf": "place_ovf",
          "k_sssp_slab": "routing_slab", "k_sssp_islab": "routing_islab", "k_sssp_ilds": "routing_ilds",
          "k_sssp_lds": "routing_lds", "k_scan_one": "scan"}
+# the path-counter fold's kernels: per fold (the add runs twice per fold, its
+# small- and big-region lists: summed), folds = launches of k_fold_p1
+FOLD = {"k_fold_p1": "fold_p1", "k_fold_p2": "fold_p2", "k_fold_add": "fold_add"}
 
 
 def kname(n):
@@ -59,6 +62,15 @@ def main():
         res[key] = {"kernel": k, "bytes": rd + wr, "read_bytes": rd, "write_bytes": wr,
                    "rd_requests": sum(rq) / len(rq) if rq else None,
                    "wr_requests": sum(wq) / len(wq) if wq else None}
+    nf = len(agg.get(("k_fold_p1", "FETCH_SIZE"), []))
+    for k, st in FOLD.items():
+        f, w = agg.get((k, "FETCH_SIZE")), agg.get((k, "WRITE_SIZE"))
+        if not f or not w or not nf:
+            continue
+        rq, wq = agg.get((k, "TCC_EA0_RDREQ_sum")), agg.get((k, "TCC_EA0_WRREQ_sum"))
+        res[st] = {"kernel": k, "per": "fold", "folds": nf, "bytes": (2 * 1024 * sum(f) + 1024 * sum(w)) / nf,
+                   "read_bytes": 2 * 1024 * sum(f) / nf, "write_bytes": 1024 * sum(w) / nf,
+                   "rd_requests": sum(rq) / nf if rq else None, "wr_requests": sum(wq) / nf if wq else None}
     if suffix:
         try:
             base = json.load(open(out))
