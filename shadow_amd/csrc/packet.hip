@@ -4606,21 +4606,55 @@ __global__ __launch_bounds__(kFoldUnitsWG) void k_fold_units(const uint32_t* __r
 
 // units blockIdx.x, + gridDim.x, ... (u = (c, g): runs of c out of tiles [g
 // kFoldG, ...), RT), each in batches of kFoldT keys (virtual position v: run
-// i holds [vs[i], vs[i + 1])).  Persistent, two workgroups per CU: the next
-// unit's run table and places are loaded while this one's keys are (one
-// unit per workgroup waits for them first: 0.51 ms of a 1.2 ms fold, r06j).
+// i holds [vs[i], vs[i + 1])).  Persistent, two workgroups per CU, software
+// pipelined over its units: while unit i's keys are ranked, sorted and
+// written, unit i + 1's keys and unit i + 2's run table are in flight (two
+// LDS run tables and two key sets, used in turn; every barrier of the
+// processing orders LDS only, so those loads stay in flight).  (One unit at
+// a time, waiting on its run table and then its keys: 0.52 ms of a 1.17 ms
+// fold, profiles/r06l_fold_timeline.log.)
 constexpr int kFoldP2WG = 512;
 constexpr int kFoldP2Per = kFoldT / kFoldP2WG; // 16 keys per thread per batch
-__global__ __launch_bounds__(kFoldP2WG) void k_fold_p2(const uint32_t* __restrict__ part, const uint2* __restrict__ RT,
+// a unit's run table in LDS: dl[i] = run i's start in part minus its first
+// virtual position, vs[i] = that position (vs[kFoldG] = the unit's keys), pl
+// = {key place, first level-2 tile}, map[v - b0] = the run holding virtual
+// position v of the batch at b0 (the waves write it run by run: two LDS reads
+// per key instead of a binary search's seven)
+struct FoldP2Lds {
+    uint32_t dl[kFoldG], vs[kFoldG + 1], pl[2];
+    uint8_t map[kFoldT];
+};
+__device__ __forceinline__ void fold_p2_map(FoldP2Lds& L, uint32_t b0) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int i = wv; i < (int)kFoldG; i += kFoldP2WG / 64) {
+        const uint32_t lo = L.vs[i] > b0 ? L.vs[i] : b0, e = b0 + kFoldT, hi = L.vs[i + 1] < e ? L.vs[i + 1] : e;
+        for (uint32_t v = lo + (uint32_t)lane; v < hi; v += 64u) L.map[v - b0] = (uint8_t)i;
+    }
+    lds_barrier();
+}
+// the keys of batch b0 of the unit whose run table is L, map built for b0
+// (sentinel past the unit's keys)
+__device__ __forceinline__ void fold_p2_keys(const FoldP2Lds& L, const uint32_t* __restrict__ part, uint32_t b0,
+                                             uint32_t (&k)[kFoldP2Per]) {
+    const uint32_t U = L.vs[kFoldG];
+#pragma unroll
+    for (int e = 0; e < kFoldP2Per; e++) {
+        const uint32_t j = (uint32_t)e * kFoldP2WG + threadIdx.x, v = b0 + j;
+        k[e] = v < U ? part[L.dl[L.map[j]] + v] : kFoldSent;
+    }
+}
+__global__ __launch_bounds__(kFoldP2WG) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_fold_p2(
+    const uint32_t* __restrict__ part, const uint2* __restrict__ RT,
                                                        uint32_t units, const uint32_t* __restrict__ Uoff,
                                                        const uint32_t* __restrict__ L2b, uint16_t* __restrict__ out16,
                                                        uint32_t* __restrict__ F, uint32_t* __restrict__ S) {
-    __shared__ uint32_t rs[kFoldG], vs[kFoldG + 1], pl[2];
+    __shared__ FoldP2Lds lt[2];
     __shared__ uint32_t h[kFoldCoarse], start[kFoldCoarse], tot;
     __shared__ __attribute__((aligned(16))) uint16_t stage[kFoldT];
+    const uint32_t G = gridDim.x;
     uint2 n0 = make_uint2(0u, 0u), n1 = make_uint2(0u, 0u);
     uint32_t np = 0;
-    auto fetch = [&](uint32_t u) { // (threads < 64: two runs each; threads 64, 65: the places)
+    auto fetch = [&](uint32_t u) { // a run table into registers (threads < 64: two runs each; 64, 65: the places)
         if (u >= units) return;
         if (threadIdx.x < 64) {
             n0 = RT[(size_t)u * kFoldG + 2 * threadIdx.x];
@@ -4631,66 +4665,82 @@ __global__ __launch_bounds__(kFoldP2WG) void k_fold_p2(const uint32_t* __restric
             np = L2b[u];
         }
     };
-    fetch(blockIdx.x);
-    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) { // (block-uniform)
-        if (threadIdx.x < 64) { // this unit's runs and their exclusive prefix
-            rs[2 * threadIdx.x] = n0.x;
-            rs[2 * threadIdx.x + 1] = n1.x;
+    auto put = [&](FoldP2Lds& L) { // the fetched run table into LDS: runs and their exclusive prefix
+        if (threadIdx.x < 64) {
             const uint32_t inc = wave_incl_scan(n0.y + n1.y, (int)threadIdx.x);
-            vs[2 * threadIdx.x] = inc - n0.y - n1.y;
-            vs[2 * threadIdx.x + 1] = inc - n1.y;
-            if (threadIdx.x == 63) vs[kFoldG] = inc;
+            const uint32_t v0 = inc - n0.y - n1.y, v1 = inc - n1.y;
+            L.dl[2 * threadIdx.x] = n0.x - v0;
+            L.dl[2 * threadIdx.x + 1] = n1.x - v1;
+            L.vs[2 * threadIdx.x] = v0;
+            L.vs[2 * threadIdx.x + 1] = v1;
+            if (threadIdx.x == 63) L.vs[kFoldG] = inc;
         } else if (threadIdx.x < 66) {
-            pl[threadIdx.x - 64] = np;
+            L.pl[threadIdx.x - 64] = np;
         }
-        __syncthreads();
-        fetch(u + gridDim.x); // (in flight behind this unit's keys)
-        const uint32_t U = vs[kFoldG];
-        const uint32_t pos0 = pl[0], tile0 = pl[1];
-        for (uint32_t b0 = 0; b0 < U; b0 += kFoldT) { // (block-uniform)
-            if (threadIdx.x < kFoldCoarse) h[threadIdx.x] = 0u;
-            uint32_t k[kFoldP2Per], rk[kFoldP2Per];
+    };
+    // one batch (keys k) of the unit of L: fine-digit counting sort in LDS,
+    // written as u16 region offsets with its prefix and start
+    auto batch = [&](const FoldP2Lds& L, uint32_t b0, const uint32_t (&k)[kFoldP2Per]) {
+        uint32_t rk[kFoldP2Per];
 #pragma unroll
-            for (int e = 0; e < kFoldP2Per; e++) {
-                const uint32_t v = b0 + (uint32_t)e * kFoldP2WG + threadIdx.x;
-                k[e] = kFoldSent;
-                if (v < U) {
-                    uint32_t lo = 0, hi = kFoldG; // the run holding v: largest i with vs[i] <= v
+        for (int e = 0; e < kFoldP2Per; e++) rk[e] = k[e] != kFoldSent ? atomicAdd(&h[fold_fine(k[e])], 1u) : 0u;
+        lds_barrier();
+        fold_prefix128(h, start, &tot);
+        lds_barrier();
 #pragma unroll
-                    for (int it = 0; it < 7; it++) {
-                        const uint32_t m = (lo + hi) >> 1;
-                        if (vs[m] <= v) lo = m;
-                        else hi = m;
-                    }
-                    k[e] = part[rs[lo] + (v - vs[lo])];
-                }
-            }
-            lds_barrier(); // (the h reset; the key loads stay in flight)
-#pragma unroll
-            for (int e = 0; e < kFoldP2Per; e++) rk[e] = k[e] != kFoldSent ? atomicAdd(&h[fold_fine(k[e])], 1u) : 0u;
-            __syncthreads();
-            fold_prefix128(h, start, &tot);
-            __syncthreads();
-#pragma unroll
-            for (int e = 0; e < kFoldP2Per; e++)
-                if (k[e] != kFoldSent)
-                    stage[start[fold_fine(k[e])] + rk[e]] = (uint16_t)(k[e] & ((1u << kFoldRegionBits) - 1u));
-            const uint32_t tile = tile0 + b0 / kFoldT, p0 = pos0 + b0;
-            if (threadIdx.x < kFoldP) F[(size_t)tile * kFoldP + threadIdx.x] = threadIdx.x < kFoldCoarse ? start[threadIdx.x] : tot;
-            if (threadIdx.x == 0) S[tile] = p0;
-            __syncthreads();
-            const uint32_t n = tot;
-            // (u16 pairs where the batch starts at an even position: kFoldT is even)
-            if ((p0 & 1u) == 0u) {
-                const uint32_t* st2 = reinterpret_cast<const uint32_t*>(stage);
-                uint32_t* o2 = reinterpret_cast<uint32_t*>(out16 + p0);
-                for (uint32_t j = threadIdx.x; j < n / 2; j += kFoldP2WG) o2[j] = st2[j];
-                if ((n & 1u) && threadIdx.x == 0) out16[p0 + n - 1] = stage[n - 1];
-            } else {
-                for (uint32_t j = threadIdx.x; j < n; j += kFoldP2WG) out16[p0 + j] = stage[j];
-            }
-            __syncthreads();
+        for (int e = 0; e < kFoldP2Per; e++)
+            if (k[e] != kFoldSent)
+                stage[start[fold_fine(k[e])] + rk[e]] = (uint16_t)(k[e] & ((1u << kFoldRegionBits) - 1u));
+        const uint32_t tile = L.pl[1] + b0 / kFoldT, p0 = L.pl[0] + b0;
+        if (threadIdx.x < kFoldP) F[(size_t)tile * kFoldP + threadIdx.x] = threadIdx.x < kFoldCoarse ? start[threadIdx.x] : tot;
+        if (threadIdx.x == 0) S[tile] = p0;
+        lds_barrier();
+        const uint32_t n = tot;
+        // (u16 pairs where the batch starts at an even position: kFoldT is even)
+        if ((p0 & 1u) == 0u) {
+            const uint32_t* st2 = reinterpret_cast<const uint32_t*>(stage);
+            uint32_t* o2 = reinterpret_cast<uint32_t*>(out16 + p0);
+            for (uint32_t j = threadIdx.x; j < n / 2; j += kFoldP2WG) o2[j] = st2[j];
+            if ((n & 1u) && threadIdx.x == 0) out16[p0 + n - 1] = stage[n - 1];
+        } else {
+            for (uint32_t j = threadIdx.x; j < n; j += kFoldP2WG) out16[p0 + j] = stage[j];
         }
+        lds_barrier(); // (stage, h and tot free for the next batch)
+        if (threadIdx.x < kFoldCoarse) h[threadIdx.x] = 0u;
+        lds_barrier();
+    };
+    // unit u (run table in Lc, first batch's keys kc, already loaded or in
+    // flight) while unit u + G's keys go into kn (its table into Ln) and unit
+    // u + 2G's table into registers
+    auto step = [&](uint32_t u, FoldP2Lds& Lc, FoldP2Lds& Ln, uint32_t (&kc)[kFoldP2Per], uint32_t (&kn)[kFoldP2Per]) {
+        put(Ln); // (unit u + G's table, fetched one step ago)
+        lds_barrier();
+        if (u + G < units) {
+            fold_p2_map(Ln, 0u);
+            fold_p2_keys(Ln, part, 0u, kn);
+        }
+        fetch(u + 2 * G);
+        const uint32_t U = Lc.vs[kFoldG];
+        if (U) batch(Lc, 0u, kc); // (an empty unit has no level-2 tile: its place is the next unit's)
+        for (uint32_t b0 = kFoldT; b0 < U; b0 += kFoldT) { // (block-uniform; units past kFoldT keys: Zipf)
+            fold_p2_map(Lc, b0);
+            fold_p2_keys(Lc, part, b0, kc);
+            batch(Lc, b0, kc);
+        }
+    };
+    if (threadIdx.x < kFoldCoarse) h[threadIdx.x] = 0u;
+    uint32_t ka[kFoldP2Per], kb[kFoldP2Per];
+    const uint32_t u0 = blockIdx.x;
+    fetch(u0);
+    put(lt[0]);
+    lds_barrier();
+    fold_p2_map(lt[0], 0u);
+    fold_p2_keys(lt[0], part, 0u, ka);
+    fetch(u0 + G);
+    for (uint32_t u = u0; u < units; u += 2 * G) { // (block-uniform)
+        step(u, lt[0], lt[1], ka, kb);
+        if (u + G >= units) break;
+        step(u + G, lt[1], lt[0], kb, ka);
     }
 }
 
