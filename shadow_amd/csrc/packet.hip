@@ -3959,7 +3959,9 @@ int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDel
 // destination segment may be mis-sorted), the merge metadata overflowed or a
 // stage guard fired.
 int fault_word_buf(Ws& w) {
-    if (!w.fault && hipHostMalloc((void**)&w.fault, 4, hipHostMallocDefault) != hipSuccess) {
+    // (two words: the fault word and, copied with it, meta hdr[kStickyFault +
+    // 1] -- never written, so 0 -- over a host-set marker: ws_sync's end)
+    if (!w.fault && hipHostMalloc((void**)&w.fault, 8, hipHostMallocDefault) != hipSuccess) {
         w.fault = nullptr;
         return shd_fail(-ENOMEM, "hipHostMalloc fault word");
     }
@@ -3989,19 +3991,37 @@ int ws_faults(Ws& w, bool completed, hipStream_t s) {
 int ws_sync(Ws& w, hipStream_t s, const char* what) {
     if (!w.meta) return hip_status(hipStreamSynchronize(s), what);
     if (int rc = fault_word_buf(w)) return rc;
-    if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 4, hipMemcpyDeviceToHost, s),
+    // SHD_SYNC_SPIN (default 1): the calling thread polls instead of
+    // sleeping in hipStreamSynchronize -- the caller waits anyway, and a poll
+    // sees the end sooner than a wake-up does (the gap before the next round's
+    // launches).  It polls the fault word's copy itself: the copy is the
+    // call's last operation on the stream and overwrites a host-set marker
+    // with the device's zero word beside the fault word, so the marker's
+    // change is the end of every earlier operation of the stream (an event
+    // recorded behind it reported the end ~4 us after the copy had landed,
+    // profiles/r06u round trace; the GPU idle between rounds 25.6 -> 9.2 us,
+    // profiles/r06y_round_gaps.log); the event is still queried every 256 polls
+    // so a failed stream ends the wait with its error.  SHD_SYNC_SPIN=event:
+    // poll the event alone.
+    const char* sp = getenv("SHD_SYNC_SPIN");
+    const bool spin = !(sp && strcmp(sp, "0") == 0), marker = !(sp && strcmp(sp, "event") == 0);
+    // (the two words are read as one aligned 8-B load: the copy lands them with
+    // one 8-B store, so a zero marker comes with its fault word)
+    volatile uint64_t* fw = reinterpret_cast<volatile uint64_t*>(w.fault);
+    w.fault[1] = ~0u;
+    if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 8, hipMemcpyDeviceToHost, s),
                             "fault word D2H"))
         return rc;
-    // SHD_SYNC_SPIN (default 1): the calling thread polls an event recorded
-    // behind the call's work instead of sleeping in hipStreamSynchronize --
-    // the caller waits anyway, and the poll sees the end sooner than a
-    // wake-up does (the gap before the next round's launches)
-    const char* sp = getenv("SHD_SYNC_SPIN");
-    if (!(sp && strcmp(sp, "0") == 0)) {
+    if (spin) {
         if (!w.fin && hipEventCreateWithFlags(&w.fin, hipEventDisableTiming) != hipSuccess) w.fin = nullptr;
         if (w.fin && hipEventRecord(w.fin, s) == hipSuccess) {
-            hipError_t e;
-            while ((e = hipEventQuery(w.fin)) == hipErrorNotReady) {
+            hipError_t e = hipErrorNotReady;
+            for (uint32_t k = 1;; k++) {
+                if (marker && (*fw >> 32) == 0u) {
+                    e = hipSuccess;
+                    break;
+                }
+                if ((!marker || (k & 255u) == 0u) && (e = hipEventQuery(w.fin)) != hipErrorNotReady) break;
             }
             if (int rc = hip_status(e, what)) return rc;
             if (s == w.last) w.done_pending = false; // (the last use has finished: nothing to record)
