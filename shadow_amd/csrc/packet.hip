@@ -3985,6 +3985,14 @@ int ws_faults(Ws& w, bool completed, hipStream_t s) {
     if (int rc = hip_status(hipStreamSynchronize(w.rd), "fault word read")) return rc;
     return fault_report(w, s);
 }
+// the synchronous round's last operation: the sticky fault word and the
+// zero word beside it (the end marker, see ws_sync) into pinned host memory
+__global__ __launch_bounds__(64) void k_fault_out(const uint32_t* __restrict__ src, unsigned long long* host) {
+    if (threadIdx.x == 0) {
+        const unsigned long long v = (unsigned long long)src[0] | ((unsigned long long)src[1] << 32);
+        __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 // A synchronous call's end: the fault word copied on the call's own stream
 // behind its launches, one wait for both (not a wait for the round and then
 // another for the word's copy on a side stream)
@@ -4009,9 +4017,18 @@ int ws_sync(Ws& w, hipStream_t s, const char* what) {
     // one 8-B store, so a zero marker comes with its fault word)
     volatile uint64_t* fw = reinterpret_cast<volatile uint64_t*>(w.fault);
     w.fault[1] = ~0u;
-    if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 8, hipMemcpyDeviceToHost, s),
-                            "fault word D2H"))
+    // the copy: one wave storing the 8 B straight into the pinned words (a
+    // system-scope store; SHD_SYNC_COPY=memcpy: hipMemcpyAsync, whose blit
+    // kernel took 3.7-4.3 us per round in the trace)
+    const char* cp = getenv("SHD_SYNC_COPY");
+    if (!(cp && strcmp(cp, "memcpy") == 0)) {
+        hipLaunchKernelGGL(k_fault_out, dim3(1), dim3(64), 0, s, w.meta + kStickyFault,
+                           reinterpret_cast<unsigned long long*>(w.fault));
+        if (int rc = hip_status(hipGetLastError(), "fault word store")) return rc;
+    } else if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 8, hipMemcpyDeviceToHost, s),
+                                   "fault word D2H")) {
         return rc;
+    }
     if (spin) {
         if (!w.fin && hipEventCreateWithFlags(&w.fin, hipEventDisableTiming) != hipSuccess) w.fin = nullptr;
         if (w.fin && hipEventRecord(w.fin, s) == hipSuccess) {
