@@ -453,10 +453,12 @@ __global__ __launch_bounds__(kBlock) void k_pkt_scatter(ShdPktCtx c, const ShdPk
 // The round's resets: nbig[0..2] (big-segment count, overflow count, fault
 // word) = 0, counters[0..1] = ~0 (the min-time slots), cnt1[0..m) = 0.
 __global__ __launch_bounds__(256) void k_round_init(uint32_t* __restrict__ nbig, unsigned long long* __restrict__ counters,
-                                                    uint32_t* __restrict__ cnt1, uint32_t m) {
+                                                    uint32_t* __restrict__ cnt1, uint32_t m,
+                                                    unsigned long long* __restrict__ minw2 = nullptr) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < 3) nbig[t] = 0u;
     else if (t < 5) counters[t - 3] = ~0ull;
+    else if (t == 5 && minw2) minw2[1] = ~0ull;
     for (uint32_t i = t; i < m; i += gridDim.x * blockDim.x) cnt1[i] = 0u;
 }
 
@@ -3020,7 +3022,11 @@ __global__ __launch_bounds__(1024) void k_wide_group(PartGeo g, const ShdDeliv* 
                                                      const uint32_t* __restrict__ nwide, uint32_t wide_cap,
                                                      const uint32_t* __restrict__ gcnt,
                                                      const uint32_t* __restrict__ wcnt, uint32_t* __restrict__ wcur,
-                                                     ShdDeliv* __restrict__ grouped) {
+                                                     ShdDeliv* __restrict__ grouped, unsigned long long* counters,
+                                                     const unsigned long long* __restrict__ minw2) {
+    // the scatter's minimum delivered time (into the workspace's word: it
+    // needs no per-round initialisation of the caller's counters)
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[1] = minw2[1];
     if (blockIdx.x == 0) {
         __shared__ uint32_t ps[16];
         uint32_t* bpre = wcur + g.nb;
@@ -3738,6 +3744,14 @@ struct Ws {
     uint64_t* xmat = nullptr;  // the exchange's count matrix (kXmatWords u64), device and pinned host
     uint64_t* hxmat = nullptr;
     bool done_pending = false; // the last use's w.done not recorded yet (done_flush)
+    // the part pipeline's round state pre-cleared by the last synchronous
+    // round's final kernel (k_fault_out): nbig, cnt1[0, pre_m) and the min
+    // word are zero / all-ones; clean_now: this use may rely on it (set by
+    // ws_begin, dropped by any regrowth); pre_req: the cnt1 words this use
+    // wants cleared at its end (part_front)
+    bool pre_clean = false, clean_now = false;
+    size_t pre_m = 0, pre_req = 0;
+    unsigned long long* minw2 = nullptr; // [1]: the scatter's minimum delivered time (part pipeline)
     hipStream_t xs = nullptr;  // the split exchange's transfer stream (non-blocking) and its events
     hipEvent_t xev[kXchgEvents] = {};
 };
@@ -3781,6 +3795,7 @@ bool dbg_oom_once() {
 
 int ws_reserve(Ws& w, size_t n, size_t m, uint32_t H) {
     int rc = 0;
+    if (m + 1 > w.cap_m || H + 1 > w.cap_h) w.clean_now = false; // (new buffers: not cleared)
     if ((n > w.cap_n || m + 1 > w.cap_m || H + 1 > w.cap_h) && (rc = ws_quiesce(w))) return rc;
     if (n > w.cap_n) {
         (void)hipFree(w.tmp);
@@ -3986,8 +4001,23 @@ int ws_faults(Ws& w, bool completed, hipStream_t s) {
     return fault_report(w, s);
 }
 // the synchronous round's last operation: the sticky fault word and the
-// zero word beside it (the end marker, see ws_sync) into pinned host memory
-__global__ __launch_bounds__(64) void k_fault_out(const uint32_t* __restrict__ src, unsigned long long* host) {
+// zero word beside it (the end marker, see ws_sync) into pinned host memory;
+// before it (m > 0) the next part round's resets -- nbig, cnt1[0, m), the
+// min word -- so that round launches no k_round_init (every store of this
+// workgroup is device-visible before the marker: the host may start the next
+// round on another stream as soon as it sees it)
+__global__ __launch_bounds__(256) void k_fault_out(const uint32_t* __restrict__ src, unsigned long long* host,
+                                                   uint32_t* __restrict__ nbig, uint32_t* __restrict__ cnt1, uint32_t m,
+                                                   unsigned long long* __restrict__ minw2) {
+    if (m) {
+        if (threadIdx.x < 3) nbig[threadIdx.x] = 0u;
+        if (threadIdx.x == 3) minw2[1] = ~0ull;
+        uint4* c4 = reinterpret_cast<uint4*>(cnt1); // (hipMalloc'd: 16-B aligned)
+        for (uint32_t i = threadIdx.x; i < m / 4; i += blockDim.x) c4[i] = uint4{0u, 0u, 0u, 0u};
+        for (uint32_t i = (m / 4) * 4 + threadIdx.x; i < m; i += blockDim.x) cnt1[i] = 0u;
+        __threadfence();
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
         const unsigned long long v = (unsigned long long)src[0] | ((unsigned long long)src[1] << 32);
         __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -4022,9 +4052,13 @@ int ws_sync(Ws& w, hipStream_t s, const char* what) {
     // kernel took 3.7-4.3 us per round in the trace)
     const char* cp = getenv("SHD_SYNC_COPY");
     if (!(cp && strcmp(cp, "memcpy") == 0)) {
-        hipLaunchKernelGGL(k_fault_out, dim3(1), dim3(64), 0, s, w.meta + kStickyFault,
-                           reinterpret_cast<unsigned long long*>(w.fault));
+        const uint32_t m = w.pre_req && w.minw2 && w.pre_req + 1 <= w.cap_m ? (uint32_t)w.pre_req : 0u;
+        hipLaunchKernelGGL(k_fault_out, dim3(1), dim3(256), 0, s, w.meta + kStickyFault,
+                           reinterpret_cast<unsigned long long*>(w.fault), w.nbig, w.cnt1, m, w.minw2);
         if (int rc = hip_status(hipGetLastError(), "fault word store")) return rc;
+        w.pre_clean = m > 0;
+        w.pre_m = m;
+        w.pre_req = 0;
     } else if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 8, hipMemcpyDeviceToHost, s),
                                    "fault word D2H")) {
         return rc;
@@ -4397,6 +4431,9 @@ int ws_begin(Ws& w, hipStream_t s) {
     if (rc) return rc;
     if (w.device >= 0 && w.device != dev) return shd_fail(-EINVAL, "workspace of device %d used on device %d", w.device, dev);
     w.device = dev;
+    w.clean_now = w.pre_clean;
+    w.pre_clean = false;
+    w.pre_req = 0;
     if ((rc = ws_faults(w, false, s))) return rc;
     if ((rc = done_flush(w))) return rc;
     if (!w.done && (rc = hip_status(hipEventCreateWithFlags(&w.done, hipEventDisableTiming), "hipEventCreate ws")))
@@ -4462,6 +4499,7 @@ extern "C" void shd_dev_ws_free(void* p) {
     (void)hipFree(w->cslab);
     (void)hipFree(w->pstage);
     (void)hipFree(w->meta);
+    (void)hipFree(w->minw2);
     if (w->fault) (void)hipHostFree(w->fault);
     if (w->rd) (void)hipStreamDestroy(w->rd);
     (void)hipFree(w->xdev);
@@ -5348,10 +5386,26 @@ int part_attr() {
 int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64_t barrier, uint64_t end_time,
                uint64_t bootstrap_end, const PartGeo& g, uint8_t* d_status, unsigned long long* counters,
                hipStream_t s) {
+    unsigned long long* const ucounters = counters; // (the caller's)
     uint32_t* gcnt = w.cnt1;
     uint32_t* wcnt = w.cnt1 + g.nb;
-    hipLaunchKernelGGL(k_round_init, dim3(grid_for(3 * g.nb, 256, 4096)), dim3(256), 0, s, w.nbig, counters, w.cnt1,
-                       3 * g.nb);
+    if (!w.minw2) {
+        if (int rc = hip_status(hipMalloc((void**)&w.minw2, 16), "hipMalloc ws.minw")) return rc;
+        w.clean_now = false;
+    }
+    // the round's resets: none when the last synchronous round on this
+    // workspace left them done (its final kernel clears them: one launch and
+    // its gap less per round, ws_sync); SHD_ROUND_PRECLEAN=0: always here
+    const char* pcv = getenv("SHD_ROUND_PRECLEAN");
+    const bool pre_ok = !(pcv && strcmp(pcv, "0") == 0);
+    if (!(pre_ok && w.clean_now && w.pre_m >= 3 * (size_t)g.nb))
+        hipLaunchKernelGGL(k_round_init, dim3(grid_for(3 * g.nb, 256, 4096)), dim3(256), 0, s, w.nbig, counters,
+                           w.cnt1, 3 * g.nb, w.minw2);
+    w.clean_now = false;
+    w.pre_req = pre_ok ? 3 * (size_t)g.nb : 0;
+    // (the scatters' minimum goes to the workspace word minw2[1]: they take
+    // minw2 as their counters; k_wide_group hands it to the caller's)
+    counters = w.minw2;
     mark(0, s);
     if (n) {
         const PartCfg f = part_cfg(g.nb);
@@ -5431,7 +5485,7 @@ int part_front(Ws& w, const ShdPktCtx* c, const ShdPkt* d_recs, size_t n, uint64
     }
     // (also with no records: it writes the sort's bucket bases)
     hipLaunchKernelGGL(k_wide_group, dim3(64), dim3(1024), 4 * (size_t)g.nb, s, g, w.st2, w.nbig + 1, (uint32_t)w.cap_n,
-                       gcnt, wcnt, w.cnt1 + 2 * g.nb, w.tmp);
+                       gcnt, wcnt, w.cnt1 + 2 * g.nb, w.tmp, ucounters, w.minw2);
     mark(1, s);
     mark_same(2, 1);
     int rc = hip_status(hipGetLastError(), "k_part_scatter launch");
