@@ -1266,9 +1266,17 @@ struct MergeMeta {
     uint32_t cap_big; // entries of the big-segment list (nbig[0] never exceeds it)
     unsigned long long* flag; // the caller's counters[0] (or null): SHD_ROUND_FAULT set in the faulting round
     uint32_t spin_limit;      // merge waits before a tile gives up (SHD_DEBUG_MERGE_SPIN; 0: every wait faults)
+    // a synchronous part round's end, done by the merge kernel's last
+    // workgroup (fin_host null: none; see fin_body and ws_sync)
+    unsigned long long* fin_host = nullptr;
+    uint32_t* fin_nbig = nullptr;
+    uint32_t* fin_cnt1 = nullptr;
+    uint32_t fin_m = 0;
+    unsigned long long* fin_minw2 = nullptr;
 };
 constexpr uint32_t kMetaHdr = 64;
 constexpr uint32_t kStickyFault = 60;
+constexpr uint32_t kFinCount = 62; // the merge workgroups that finished (the last one ends the round, then resets it)
 
 // A fault of this round: its word into the round's header slot, the sticky
 // word the host reads back, and the caller-visible bit of counters[0]
@@ -1278,6 +1286,30 @@ __device__ __forceinline__ void note_fault(const MergeMeta& mm, uint32_t f) {
     if (!f) return;
     atomicOr(&mm.hdr[kStickyFault], f);
     if (mm.flag) atomicOr(mm.flag, (unsigned long long)SHD_ROUND_FAULT);
+}
+
+// A synchronous round's end (one workgroup, every thread; after all of the
+// round's work): the next part round's resets (m > 0: nbig, cnt1[0, m), the
+// min word), then -- every store of the workgroup device-visible first: the
+// host may start the next round on another stream as soon as it sees it --
+// the sticky fault word and the zero word beside it (the end marker, see
+// ws_sync) into pinned host memory with one system-scope 8-B store
+__device__ __forceinline__ void fin_body(const uint32_t* src, unsigned long long* host, uint32_t* nbig, uint32_t* cnt1,
+                                         uint32_t m, unsigned long long* minw2) {
+    if (m) {
+        if (threadIdx.x < 3) nbig[threadIdx.x] = 0u;
+        if (threadIdx.x == 3) minw2[1] = ~0ull;
+        uint4* c4 = reinterpret_cast<uint4*>(cnt1); // (hipMalloc'd: 16-B aligned)
+        for (uint32_t i = threadIdx.x; i < m / 4; i += blockDim.x) c4[i] = uint4{0u, 0u, 0u, 0u};
+        for (uint32_t i = (m / 4) * 4 + threadIdx.x; i < m; i += blockDim.x) cnt1[i] = 0u;
+    }
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long v = (unsigned long long)__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                                     ((unsigned long long)src[1] << 32);
+        __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // Block-uniform value read from LDS or memory, made wave-uniform for the
@@ -1583,7 +1615,13 @@ __global__ __launch_bounds__(256) void k_segsort_merge(ShdDeliv* out, ShdDeliv* 
     const uint32_t items = bu(mm.hdr[1]);
     // no segment above kChunk (every uniform round): leave without touching
     // the claim counter -- 512 same-address atomics cost more than the launch
-    if (items == 0) return;
+    // (a synchronous round's end then comes from workgroup 0: nothing else
+    // of the round is left)
+    if (items == 0) {
+        if (mm.fin_host && blockIdx.x == 0)
+            fin_body(mm.hdr + kStickyFault, mm.fin_host, mm.fin_nbig, mm.fin_cnt1, mm.fin_m, mm.fin_minw2);
+        return;
+    }
     uint32_t done_slot = ~0u; // the previous tile's (segment, pass) counter, published at the next claim
     for (;;) {
         // one lane: publish the previous tile (its stores were drained before
@@ -1680,6 +1718,21 @@ __global__ __launch_bounds__(256) void k_segsort_merge(ShdDeliv* out, ShdDeliv* 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         done_slot = sgi * kMaxPasses + p;
+    }
+    // a synchronous round's end: the last workgroup to finish (its output
+    // stores drained before the loop's last barrier; a device-scope release
+    // before the count)
+    if (mm.fin_host) {
+        if (tid == 0) {
+            __threadfence();
+            sh[0] = atomicAdd(&mm.hdr[kFinCount], 1u) == gridDim.x - 1 ? 1u : 0u;
+        }
+        __syncthreads();
+        if (sh[0]) {
+            __threadfence();
+            if (tid == 0) mm.hdr[kFinCount] = 0u;
+            fin_body(mm.hdr + kStickyFault, mm.fin_host, mm.fin_nbig, mm.fin_cnt1, mm.fin_m, mm.fin_minw2);
+        }
     }
 }
 
@@ -3752,6 +3805,11 @@ struct Ws {
     bool pre_clean = false, clean_now = false;
     size_t pre_m = 0, pre_req = 0;
     unsigned long long* minw2 = nullptr; // [1]: the scatter's minimum delivered time (part pipeline)
+    // fin_ask: the caller waits for this part round (shd_dev_packet_round on
+    // the null stream): its merge kernel may end it (fin_done, fin_m: the
+    // resets it did) instead of a k_fault_out launch in ws_sync
+    bool fin_ask = false, fin_done = false;
+    uint32_t fin_m = 0;
     hipStream_t xs = nullptr;  // the split exchange's transfer stream (non-blocking) and its events
     hipEvent_t xev[kXchgEvents] = {};
 };
@@ -3944,10 +4002,29 @@ int copy_faults(Ws&, hipStream_t) { return 0; }
 // pass, a metadata overflow, a stage guard) sets SHD_ROUND_FAULT in the
 // caller's counters[0] (flag) during the round and the sticky word, which
 // ws_faults reports.
+int fault_word_buf(Ws& w);
 int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDeliv* out, hipStream_t s,
                 unsigned long long* flag) {
     if (int rc = mid_attr()) return rc;
-    const MergeMeta mm = merge_meta(w, flag);
+    MergeMeta mm = merge_meta(w, flag);
+    // a waited-for part round (w.fin_ask) ends with the merge kernel (see
+    // ws_sync): the end marker is set before that launch; SHD_SYNC_COPY /
+    // SHD_SYNC_SPIN forms other than the default keep the separate end
+    const char* cpv = getenv("SHD_SYNC_COPY");
+    const char* spv = getenv("SHD_SYNC_SPIN");
+    w.fin_done = false;
+    if (w.fin_ask && !(cpv && strcmp(cpv, "memcpy") == 0) && !(spv && (!strcmp(spv, "0") || !strcmp(spv, "event")))) {
+        if (int rc = fault_word_buf(w)) return rc;
+        w.fault[1] = ~0u;
+        mm.fin_host = reinterpret_cast<unsigned long long*>(w.fault);
+        mm.fin_m = w.pre_req && w.minw2 && w.pre_req + 1 <= w.cap_m ? (uint32_t)w.pre_req : 0u;
+        mm.fin_nbig = w.nbig;
+        mm.fin_cnt1 = w.cnt1;
+        mm.fin_minw2 = w.minw2;
+        w.fin_done = true;
+        w.fin_m = mm.fin_m;
+    }
+    w.fin_ask = false;
     const char* mr = getenv("SHD_MID_RANK");
     const char* md = getenv("SHD_MEDIUM_SEG"); // 0: segments up to kMedSeg through k_segsort_mid as before
     const bool med = !(md && strcmp(md, "0") == 0);
@@ -4009,19 +4086,7 @@ int ws_faults(Ws& w, bool completed, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_fault_out(const uint32_t* __restrict__ src, unsigned long long* host,
                                                    uint32_t* __restrict__ nbig, uint32_t* __restrict__ cnt1, uint32_t m,
                                                    unsigned long long* __restrict__ minw2) {
-    if (m) {
-        if (threadIdx.x < 3) nbig[threadIdx.x] = 0u;
-        if (threadIdx.x == 3) minw2[1] = ~0ull;
-        uint4* c4 = reinterpret_cast<uint4*>(cnt1); // (hipMalloc'd: 16-B aligned)
-        for (uint32_t i = threadIdx.x; i < m / 4; i += blockDim.x) c4[i] = uint4{0u, 0u, 0u, 0u};
-        for (uint32_t i = (m / 4) * 4 + threadIdx.x; i < m; i += blockDim.x) cnt1[i] = 0u;
-        __threadfence();
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const unsigned long long v = (unsigned long long)src[0] | ((unsigned long long)src[1] << 32);
-        __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    fin_body(src, host, nbig, cnt1, m, minw2);
 }
 // A synchronous call's end: the fault word copied on the call's own stream
 // behind its launches, one wait for both (not a wait for the round and then
@@ -4046,12 +4111,18 @@ int ws_sync(Ws& w, hipStream_t s, const char* what) {
     // (the two words are read as one aligned 8-B load: the copy lands them with
     // one 8-B store, so a zero marker comes with its fault word)
     volatile uint64_t* fw = reinterpret_cast<volatile uint64_t*>(w.fault);
-    w.fault[1] = ~0u;
     // the copy: one wave storing the 8 B straight into the pinned words (a
     // system-scope store; SHD_SYNC_COPY=memcpy: hipMemcpyAsync, whose blit
-    // kernel took 3.7-4.3 us per round in the trace)
+    // kernel took 3.7-4.3 us per round in the trace) -- or none at all when
+    // the round's merge kernel did that store (fin_done, marker set before
+    // its launch: one launch less per round)
     const char* cp = getenv("SHD_SYNC_COPY");
-    if (!(cp && strcmp(cp, "memcpy") == 0)) {
+    if (w.fin_done) {
+        w.fin_done = false;
+        w.pre_clean = w.fin_m > 0;
+        w.pre_m = w.fin_m;
+        w.pre_req = 0;
+    } else if ((w.fault[1] = ~0u), !(cp && strcmp(cp, "memcpy") == 0)) {
         const uint32_t m = w.pre_req && w.minw2 && w.pre_req + 1 <= w.cap_m ? (uint32_t)w.pre_req : 0u;
         hipLaunchKernelGGL(k_fault_out, dim3(1), dim3(256), 0, s, w.meta + kStickyFault,
                            reinterpret_cast<unsigned long long*>(w.fault), w.nbig, w.cnt1, m, w.minw2);
@@ -5539,8 +5610,11 @@ extern "C" int shd_dev_packet_round(const ShdPktCtx* c, const ShdPkt* d_recs, si
     if (pipe == kPartPipe) {
         PartGeo g;
         if (part_geometry(0, H, n, barrier > (1ull << 31) ? barrier - (1ull << 31) : 0ull, &g, barrier)) {
+            w.fin_ask = stream == nullptr; // (waited for below: its merge kernel may end it)
             int rc = part_round(w, c, d_recs, n, barrier, end_time, bootstrap_end, g, d_out, d_dst_offsets, d_status,
                                 d_counters, s);
+            w.fin_ask = false;
+            if (rc) w.fin_done = false;
             if (rc || stream) return rc;
             return ws_sync(w, s, "packet round");
         }
