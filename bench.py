@@ -69,7 +69,7 @@ def parse():
                     help="skip the replayed-batch comparison rounds (PMC passes: fresh rounds only)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the §8d variant legs (ns-resolution C2 build and C3 round, C1 direct paths, Zipf C3)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06p_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r06ai_traffic.json"),
                     help="JSON with PMC-measured HBM bytes per launch (scripts/traffic.py)")
     return ap.parse_args()
 
