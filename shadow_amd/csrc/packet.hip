@@ -3363,6 +3363,11 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
     const bool listed = tot > (uint32_t)kCap || nw > 0; // (block-uniform)
     for (uint32_t j = threadIdx.x; j < kPartMaxDst; j += kWG) cnt[j] = cur[j] = 0;
     const uint4* sb = stage + (size_t)b * g.cap;
+    // the bucket's records in registers, kCap / kWG per thread; an instance
+    // whose capacity is not a multiple of kWG (512 threads, 2,304 events)
+    // reads its last partial row from the stage twice instead (count, place:
+    // only buckets above kRegEv events)
+    constexpr uint32_t kRegEv = (uint32_t)(kCap / kWG) * kWG;
     uint4 e[kCap / kWG];
     if (!listed) { // the bucket's records
 #pragma unroll
@@ -3385,6 +3390,8 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
 #pragma unroll
         for (int k = 0; k < kCap / kWG; k++)
             if ((uint32_t)k * kWG + threadIdx.x < ns) atomicAdd(&cnt[e[k].w & mask], 1u);
+        if (kRegEv < (uint32_t)kCap)
+            for (uint32_t i = kRegEv + threadIdx.x; i < ns; i += kWG) atomicAdd(&cnt[sb[i].w & mask], 1u);
     } else {
         for (uint32_t i = threadIdx.x; i < ns; i += kWG) atomicAdd(&cnt[sb[i].w & mask], 1u);
         const uint32_t m = *nwide;
@@ -3418,6 +3425,12 @@ __device__ __forceinline__ void part_sort_body(PartGeo g, const uint4* __restric
                 lev[loc[dl] + atomicAdd(&cur[dl], 1u)] = e[k];
             }
         }
+        if (kRegEv < (uint32_t)kCap)
+            for (uint32_t i = kRegEv + threadIdx.x; i < ns; i += kWG) {
+                const uint4 r = sb[i];
+                const uint32_t dl = r.w & mask;
+                lev[loc[dl] + atomicAdd(&cur[dl], 1u)] = r;
+            }
         lds_barrier();
         // segments of at most kTinySeg events (many destinations per bucket,
         // few events each: C4's rounds): one thread per event, its rank the

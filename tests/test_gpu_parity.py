@@ -299,6 +299,38 @@ def test_oversized_bucket_fallback(pipeline):
     assert offs[2] - offs[1] > 16384
 
 
+@pytest.mark.parametrize("inst", ["default", "0", "1", "2", "3", "4"])
+def test_part_sort_bucket_above_register_rows(inst, monkeypatch):
+    """Buckets whose event count lies between a part-sort instance's register
+    rows (kCap / kWG per thread, rounded down: 2,048 events for the 512-thread
+    2,304-event instances) and the bucket cap: every event must still be
+    loaded.  One destination per bucket (the batch's mean load of 1,900
+    events per host sets shift 0 for the 2,304-event instances), destinations
+    1..3 above 2,048 events."""
+    monkeypatch.setenv("SHD_PACKET_PIPELINE", "part")
+    if inst == "default":
+        monkeypatch.delenv("SHD_PART_SORT", raising=False)
+    else:
+        monkeypatch.setenv("SHD_PART_SORT", inst)
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    n = 1900 * H
+    heavy = {1: 2300, 2: 2100, 3: 2049}
+    rest = n - sum(heavy.values())
+    others = [h for h in range(H) if h not in heavy]
+    dst = np.concatenate([np.full(c, h, dtype=np.uint32) for h, c in heavy.items()] +
+                         [np.array(others, dtype=np.uint32)[np.arange(rest) % len(others)]])
+    rng = np.random.default_rng(0x5EED0220)
+    dst = dst[rng.permutation(n)]
+    src = rng.integers(0, H - 1, n).astype(np.uint32)
+    src = np.where(src >= dst, src + 1, src).astype(np.uint32)
+    pk = synth.packet_batch(n, H, 0x5EED0221, 100_000_000, 10_000_000, st, p_payload=0.0, pairs=(src, dst))
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert np.diff(offs)[1] == 2300 and np.diff(offs)[3] == 2049
+
+
 def test_device_api_matches_oracle_after_touch_all(pipeline):
     import torch
     gml, H = GRAPHS["sparse300_ns"]
