@@ -331,6 +331,32 @@ def test_part_sort_bucket_above_register_rows(inst, monkeypatch):
     assert np.diff(offs)[1] == 2300 and np.diff(offs)[3] == 2049
 
 
+SEGMENT_EDGES = [16, 17, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1023, 1024, 1025, 4095, 4096, 4097, 8192, 8193]
+
+
+def test_segment_size_thresholds(pipeline):
+    """Destination segments at every size threshold of the grouping kernels
+    (one thread per event <= 16, wave ranks <= 64 / 128 / 256, the medium
+    bitonic <= 1,024, the chunk sort's 4,096-event runs and the merge passes
+    above), each side of it; the other hosts get a few events each."""
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    loads = {h + 1: c for h, c in enumerate(SEGMENT_EDGES)}
+    others = [h for h in range(H) if h not in loads]
+    n = sum(loads.values()) + 5 * len(others)
+    dst = np.concatenate([np.full(c, h, dtype=np.uint32) for h, c in loads.items()] +
+                         [np.repeat(np.array(others, dtype=np.uint32), 5)])
+    rng = np.random.default_rng(0x5EED0230)
+    dst = dst[rng.permutation(n)]
+    src = rng.integers(0, H - 1, n).astype(np.uint32)
+    src = np.where(src >= dst, src + 1, src).astype(np.uint32)
+    pk = synth.packet_batch(n, H, 0x5EED0231, 100_000_000, 10_000_000, st, p_payload=0.0, pairs=(src, dst))
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert [int(offs[h + 1] - offs[h]) for h in loads] == SEGMENT_EDGES
+
+
 def test_device_api_matches_oracle_after_touch_all(pipeline):
     import torch
     gml, H = GRAPHS["sparse300_ns"]

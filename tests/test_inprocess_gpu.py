@@ -35,11 +35,28 @@ def _gml():
     return synth.sparse_graph_gml(250, 0x5EED0801, ns_variant=True)
 
 
+# owner segment sizes at the grouping and merge thresholds (hot = -1)
+XEDGES = [16, 17, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025]
+
+
 def _packets(rank, world, st, hot=0):
     """hot > 0: every packet goes to one of `hot` destinations spread over
-    the hosts (long destination segments on the sender and the owner)."""
+    the hosts (long destination segments on the sender and the owner);
+    hot = -1: destinations 2, 5, 8, ... receive XEDGES[i] events in all,
+    split over the ranks, the rest of each rank's packets go elsewhere."""
     from shadow_amd import synth
     lo, hi = rank * H // world, (rank + 1) * H // world
+    if hot < 0:
+        rng = np.random.default_rng(0x5EED0830 + rank)
+        edge_hosts = [2 + 3 * i for i in range(len(XEDGES))]
+        d = np.concatenate([np.full(c // world + (1 if rank < c % world else 0), h, dtype=np.int64)
+                            for h, c in zip(edge_hosts, XEDGES)])
+        others = np.setdiff1d(np.arange(H), edge_hosts)
+        dst = np.concatenate([d, rng.choice(others, NPK - len(d))])[rng.permutation(NPK)]
+        src = rng.integers(lo, hi, NPK)
+        src = np.where(src == dst, lo + (src - lo + 1) % (hi - lo), src)
+        return synth.packet_batch(NPK, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, p_payload=0.0,
+                                  pairs=(src.astype(np.uint32), dst.astype(np.uint32)))
     if not hot:
         return synth.packet_batch(NPK, H, 0x5EED0810 + rank, 100_000_000, 10_000_000, st, hosts_lo=lo, hosts_hi=hi)
     rng = np.random.default_rng(0x5EED0820 + rank)
@@ -226,7 +243,7 @@ def test_threads_as_ranks(kind, world, fused, split, monkeypatch):
 
 @pytest.mark.timeout(60)
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("hot", [1, 2, 6])
+@pytest.mark.parametrize("hot", [1, 2, 6, -1], ids=["hot1", "hot2", "hot6", "edges"])
 @pytest.mark.parametrize("wire_sorted", ["1", "0"], ids=["sorted_wire", "unsorted_wire"])
 @pytest.mark.parametrize("split", ["1", "0"], ids=["split", "one_group"])
 def test_exchange_long_segments(world, hot, wire_sorted, split, monkeypatch):
