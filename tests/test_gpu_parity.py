@@ -357,6 +357,27 @@ def test_segment_size_thresholds(pipeline):
     assert [int(offs[h + 1] - offs[h]) for h in loads] == SEGMENT_EDGES
 
 
+@pytest.mark.parametrize("per_dst", [40, 100, 200])
+def test_packets_to_own_host(per_dst, pipeline):
+    """A share of the packets addressed to their own host: no barrier clamp
+    (host_single.c:187-192), so those deliveries land before the barrier and
+    the segment's sort leaves its 31-bit barrier-relative keys for the 64-bit
+    ones (and its time-bucket rank for the all-pairs one)."""
+    gml, H = GRAPHS["sparse300_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    n = per_dst * H
+    rng = np.random.default_rng(0x5EED0240 + per_dst)
+    dst = rng.integers(0, H, n).astype(np.uint32)
+    src = rng.integers(0, H, n).astype(np.uint32)
+    own = rng.random(n) < 0.1
+    src = np.where(own, dst, src).astype(np.uint32)
+    pk = synth.packet_batch(n, H, 0x5EED0241 + per_dst, 100_000_000, 10_000_000, st, p_payload=0.5, pairs=(src, dst))
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    assert (out["time"] < 110_000_000).any()
+
+
 def test_device_api_matches_oracle_after_touch_all(pipeline):
     import torch
     gml, H = GRAPHS["sparse300_ns"]
