@@ -378,6 +378,24 @@ def test_packets_to_own_host(per_dst, pipeline):
     assert (out["time"] < 110_000_000).any()
 
 
+@pytest.mark.parametrize("ns", [False, True], ids=["ms", "ns"])
+def test_long_path_latencies(ns, pipeline):
+    """Path latencies up to 5 s (direct paths of a complete graph,
+    use_shortest_path=false): deliveries 2^31 ns or more past the barrier
+    leave the 16-B stage record and the 31-bit sort keys (wide events), and
+    delays of 2^32 ns or more leave the 8-B packet-path table for the f64
+    entry (kPtabFallback)."""
+    gml = synth.complete_graph_gml(20, 0x5EED0250, ns_variant=ns, max_ms=5000)
+    H = 60
+    top, orc, ips, st = make_pair(gml, H, use_sp=False)
+    pk = synth.packet_batch(30000, H, 0x5EED0251, 100_000_000, 10_000_000, st)
+    out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
+    oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+    assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
+    late = out["time"] - 110_000_000
+    assert (late >= 2**31).sum() > 1000 and (late >= 2**32).sum() > 500
+
+
 def test_device_api_matches_oracle_after_touch_all(pipeline):
     import torch
     gml, H = GRAPHS["sparse300_ns"]
