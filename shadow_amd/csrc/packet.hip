@@ -1296,6 +1296,10 @@ __device__ __forceinline__ void note_fault(const MergeMeta& mm, uint32_t f) {
 // ws_sync) into pinned host memory with one system-scope 8-B store
 __device__ __forceinline__ void fin_body(const uint32_t* src, unsigned long long* host, uint32_t* nbig, uint32_t* cnt1,
                                          uint32_t m, unsigned long long* minw2) {
+    // the segments this round listed, reported in the marker's place (below
+    // the host-set all-ones: ws_sync's end, and k_segsort_medium's launch
+    // decision for the next synchronous round, see sort_listed)
+    const uint32_t nb0 = threadIdx.x == 0 ? nbig[0] : 0u;
     if (m) {
         if (threadIdx.x < 3) nbig[threadIdx.x] = 0u;
         if (threadIdx.x == 3) minw2[1] = ~0ull;
@@ -1307,7 +1311,7 @@ __device__ __forceinline__ void fin_body(const uint32_t* src, unsigned long long
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long v = (unsigned long long)__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-                                     ((unsigned long long)src[1] << 32);
+                                     ((unsigned long long)min(nb0, 0xFFFFFFFEu) << 32);
         __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -3823,6 +3827,9 @@ struct Ws {
     // resets it did) instead of a k_fault_out launch in ws_sync
     bool fin_ask = false, fin_done = false;
     uint32_t fin_m = 0;
+    // the segments the last synchronous round listed (its end word; ~0u:
+    // unknown -- an asynchronous use, or the copy form of the end)
+    uint32_t last_listed = ~0u;
     hipStream_t xs = nullptr;  // the split exchange's transfer stream (non-blocking) and its events
     hipEvent_t xev[kXchgEvents] = {};
 };
@@ -4039,8 +4046,18 @@ int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDel
     }
     w.fin_ask = false;
     const char* mr = getenv("SHD_MID_RANK");
-    const char* md = getenv("SHD_MEDIUM_SEG"); // 0: segments up to kMedSeg through k_segsort_mid as before
-    const bool med = !(md && strcmp(md, "0") == 0);
+    // k_segsort_medium (segments of kSmallSeg < n <= kMedSeg events): launched
+    // unless this round ends synchronously (fin_done) and the synchronous
+    // round before it on this workspace listed no segment at all -- a
+    // uniform load, where the launch finds nothing (~4.6 us per round); a
+    // medium segment that turns up then is k_segsort_mid's (one workgroup's
+    // network per segment, as before the medium kernel), and its round's
+    // count launches the kernel again next round.  SHD_MEDIUM_SEG=0: never,
+    // 1: always.
+    const char* md = getenv("SHD_MEDIUM_SEG");
+    const bool med = md && strcmp(md, "0") == 0   ? false
+                     : md && strcmp(md, "1") == 0 ? true
+                                                  : !(w.fin_done && w.last_listed == 0u);
     if (med) {
         hipLaunchKernelGGL(k_segsort_medium, dim3(2048), dim3(64 * kMedWaves), 0, s, unsorted, offsets, w.big, w.nbig,
                            out, mm.cap_big);
@@ -4064,8 +4081,9 @@ int sort_listed(Ws& w, const ShdDeliv* unsorted, const uint32_t* offsets, ShdDel
 // destination segment may be mis-sorted), the merge metadata overflowed or a
 // stage guard fired.
 int fault_word_buf(Ws& w) {
-    // (two words: the fault word and, copied with it, meta hdr[kStickyFault +
-    // 1] -- never written, so 0 -- over a host-set marker: ws_sync's end)
+    // (two words: the fault word and, over a host-set all-ones marker, the
+    // round's listed-segment count (fin_body) or, in the copy form, meta
+    // hdr[kStickyFault + 1] -- never written, so 0: ws_sync's end)
     if (!w.fault && hipHostMalloc((void**)&w.fault, 8, hipHostMallocDefault) != hipSuccess) {
         w.fault = nullptr;
         return shd_fail(-ENOMEM, "hipHostMalloc fault word");
@@ -4130,6 +4148,7 @@ int ws_sync(Ws& w, hipStream_t s, const char* what) {
     // the round's merge kernel did that store (fin_done, marker set before
     // its launch: one launch less per round)
     const char* cp = getenv("SHD_SYNC_COPY");
+    bool counted = true; // the end word carries the round's listed count (fin_body), not the copy's zero
     if (w.fin_done) {
         w.fin_done = false;
         w.pre_clean = w.fin_m > 0;
@@ -4143,27 +4162,31 @@ int ws_sync(Ws& w, hipStream_t s, const char* what) {
         w.pre_clean = m > 0;
         w.pre_m = m;
         w.pre_req = 0;
-    } else if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 8, hipMemcpyDeviceToHost, s),
-                                   "fault word D2H")) {
-        return rc;
+    } else {
+        counted = false;
+        if (int rc = hip_status(hipMemcpyAsync(w.fault, w.meta + kStickyFault, 8, hipMemcpyDeviceToHost, s),
+                                "fault word D2H"))
+            return rc;
     }
     if (spin) {
         if (!w.fin && hipEventCreateWithFlags(&w.fin, hipEventDisableTiming) != hipSuccess) w.fin = nullptr;
         if (w.fin && hipEventRecord(w.fin, s) == hipSuccess) {
             hipError_t e = hipErrorNotReady;
             for (uint32_t k = 1;; k++) {
-                if (marker && (*fw >> 32) == 0u) {
+                if (marker && (*fw >> 32) != 0xFFFFFFFFu) {
                     e = hipSuccess;
                     break;
                 }
                 if ((!marker || (k & 255u) == 0u) && (e = hipEventQuery(w.fin)) != hipErrorNotReady) break;
             }
             if (int rc = hip_status(e, what)) return rc;
+            w.last_listed = counted ? (uint32_t)(*fw >> 32) : ~0u;
             if (s == w.last) w.done_pending = false; // (the last use has finished: nothing to record)
             return fault_report(w, s);
         }
     }
     if (int rc = hip_status(hipStreamSynchronize(s), what)) return rc;
+    w.last_listed = counted ? (uint32_t)(*fw >> 32) : ~0u;
     if (s == w.last) w.done_pending = false;
     return fault_report(w, s);
 }

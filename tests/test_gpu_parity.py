@@ -342,19 +342,65 @@ def test_segment_size_thresholds(pipeline):
     gml, H = GRAPHS["complete30_ms"]
     top, orc, ips, st = make_pair(gml, H)
     loads = {h + 1: c for h, c in enumerate(SEGMENT_EDGES)}
-    others = [h for h in range(H) if h not in loads]
-    n = sum(loads.values()) + 5 * len(others)
-    dst = np.concatenate([np.full(c, h, dtype=np.uint32) for h, c in loads.items()] +
-                         [np.repeat(np.array(others, dtype=np.uint32), 5)])
-    rng = np.random.default_rng(0x5EED0230)
-    dst = dst[rng.permutation(n)]
-    src = rng.integers(0, H - 1, n).astype(np.uint32)
-    src = np.where(src >= dst, src + 1, src).astype(np.uint32)
-    pk = synth.packet_batch(n, H, 0x5EED0231, 100_000_000, 10_000_000, st, p_payload=0.0, pairs=(src, dst))
+    pk = _edge_batch(H, st, 0x5EED0230)
     out, offs, status, mt = top.round(pk, 110_000_000, 10**15)
     oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
     assert np.array_equal(status, ostatus) and mt == omt and np.array_equal(out, oout)
     assert [int(offs[h + 1] - offs[h]) for h in loads] == SEGMENT_EDGES
+
+
+def _edge_batch(H, st, seed):
+    """SEGMENT_EDGES events to hosts 1.., 5 to every other host, all kept."""
+    loads = {h + 1: c for h, c in enumerate(SEGMENT_EDGES)}
+    others = [h for h in range(H) if h not in loads]
+    n = sum(loads.values()) + 5 * len(others)
+    dst = np.concatenate([np.full(c, h, dtype=np.uint32) for h, c in loads.items()] +
+                         [np.repeat(np.array(others, dtype=np.uint32), 5)])
+    rng = np.random.default_rng(seed)
+    dst = dst[rng.permutation(n)]
+    src = rng.integers(0, H - 1, n).astype(np.uint32)
+    src = np.where(src >= dst, src + 1, src).astype(np.uint32)
+    return synth.packet_batch(n, H, seed + 1, 100_000_000, 10_000_000, st, p_payload=0.0, pairs=(src, dst))
+
+
+@pytest.mark.parametrize("medium", ["auto", "0", "1"])
+def test_sync_rounds_medium_segments_after_uniform(medium, monkeypatch):
+    """Synchronous device rounds (null stream) on one workspace: a uniform
+    round (no listed segment), then two with segments at every grouping
+    threshold.  By default the second runs without k_segsort_medium (its
+    predecessor listed nothing: k_segsort_mid sorts the medium segments) and
+    the third with it again (SHD_MEDIUM_SEG=0 / 1: never / always)."""
+    import torch
+    monkeypatch.setenv("SHD_PACKET_PIPELINE", "part")
+    monkeypatch.delenv("SHD_PART_SORT", raising=False)
+    if medium == "auto":
+        monkeypatch.delenv("SHD_MEDIUM_SEG", raising=False)
+    else:
+        monkeypatch.setenv("SHD_MEDIUM_SEG", medium)
+    gml, H = GRAPHS["complete30_ms"]
+    top, orc, ips, st = make_pair(gml, H)
+    top.touch_all()
+    lat, rel, sv = top.table()
+    orc.preload(sv, lat, rel)
+    batches = [synth.packet_batch(9000, H, 0x5EED0260, 100_000_000, 10_000_000, st, p_payload=0.0),
+               _edge_batch(H, st, 0x5EED0262), _edge_batch(H, st, 0x5EED0264)]
+    for pk in batches:
+        n = len(pk)
+        d_recs = torch.from_numpy(pk.view(np.uint8)).cuda()
+        d_out = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+        d_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+        d_status = torch.empty(n, dtype=torch.uint8, device="cuda")
+        d_cnt = torch.empty(2, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        top.process_device(d_recs.data_ptr(), n, 110_000_000, 10**15, 0, d_out.data_ptr(), d_off.data_ptr(),
+                           d_status.data_ptr(), d_cnt.data_ptr(), 0)
+        cnt = d_cnt.cpu().numpy().view(np.uint64)
+        out = d_out.cpu().numpy().view(synth.DELIV_DTYPE)[:cnt[0]]
+        oout, ostatus, omt = orc.round(ips, pk, 110_000_000, 10**15)
+        assert np.array_equal(d_status.cpu().numpy(), ostatus) and cnt[1] == omt
+        assert np.array_equal(out, oout)
+        offs = d_off.cpu().numpy()
+        assert np.array_equal(np.diff(offs), np.bincount(oout["dst_host"], minlength=H))
 
 
 @pytest.mark.parametrize("per_dst", [40, 100, 200])
